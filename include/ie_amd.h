@@ -1,0 +1,210 @@
+/*
+ * ie_amd.h — C ABI of the MI355X-native `{key}` interpolation resolver (libie_amd.so).
+ *
+ * This is the drop-in boundary for the reference's hot path:
+ *
+ *   Python  src/interpolation_engine/interpolation_engine.py
+ *     interpolate_inserts(inserts, content)        py:497-541   -> ie_interpolate / ie_interpolate_batch
+ *     get_interpdata(inserts, key)                 py:430-467   -> ie_table_build (lookup order baked in)
+ *     get_simple_insertkey(content)                py:477-495   -> ie_simple_insertkey
+ *     recursive_unescape / recursive_escape        py:1436-1460 -> ie_unescape_batch / ie_escape_batch
+ *     InterpolationException / AssertionError      py:426, 519, 530 -> ie_status codes
+ *   Rust    rust-project/src/interp.rs
+ *     interpolate_inserts(&Map, &str, &ctx)        interp.rs:31-89  -> ie_interpolate (dialect IE_DIALECT_RS)
+ *     get_interpdata                               interp.rs:91-137 -> ie_table_build
+ *     get_simple_insertkey                         interp.rs:11-29  -> ie_simple_insertkey
+ *     recursive_unescape / recursive_escape        interp.rs:147-177 -> ie_unescape_batch / ie_escape_batch
+ *
+ * Plain pointers and sizes only; no torch or HIP types appear in a signature (streams are void*).
+ * Every entry point returns 0 (IE_SUCCESS) or a negative IE_ERR_* code; ie_last_error() gives text.
+ * Per-string outcomes are ie_status bytes, one per input string.
+ */
+#ifndef IE_AMD_H
+#define IE_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IE_ABI_VERSION 1
+
+/* ---- dialects: which reference implementation's rules to follow ---- */
+enum ie_dialect {
+  IE_DIALECT_PY = 0, /* interpolation_engine.py (the default parity target) */
+  IE_DIALECT_RS = 1  /* rust-project/src/interp.rs (restated; parity unpinned) */
+};
+
+/* ---- value kinds (the JSON type of an insert value) ---- */
+enum ie_kind {
+  IE_KIND_STR = 0,
+  IE_KIND_INT = 1,
+  IE_KIND_LIST = 2,
+  IE_KIND_FLOAT = 3,
+  IE_KIND_BOOL = 4,
+  IE_KIND_NULL = 5,
+  IE_KIND_DICT = 6
+};
+
+/* ---- per-string status (one byte per input string) ---- */
+enum ie_status {
+  IE_OK_STR = 0,          /* result is the string in the output arena                      */
+  IE_OK_VALUE = 1,        /* whole-string "{key}": result is the raw insert, see value_id   */
+  IE_E_INTERP = 2,        /* InterpolationException: missing key, '' key, missing ARGn      */
+  IE_E_ASSERT_BRACES = 3, /* AssertionError: uneven '{' / '}' count (py:517-519)           */
+  IE_E_ASSERT_TYPE = 4,   /* AssertionError: splice of a non str/int/list (py:530);
+                             Rust: "unsupported type" error (interp.rs:76-79)               */
+  IE_E_UNHASHABLE = 5,    /* TypeError: a list/dict raw value used as a key (py:512, 450)   */
+  IE_E_RS_PANIC = 6,      /* Rust dialect: unwrap() panic on a '}{' leftover (interp.rs:63-66) */
+  IE_NEEDS_HOST = 7,      /* key missing and an --inserts-dir is configured (py:452-461)   */
+  IE_DIVERGED = 8,        /* iteration cap hit: the reference would loop forever           */
+  IE_E_OVERFLOW = 9       /* device scratch too small for this string (host APIs retry)    */
+};
+
+/* ---- API return codes ---- */
+#define IE_SUCCESS 0
+#define IE_ERR_INVALID (-1)
+#define IE_ERR_HIP (-2)
+#define IE_ERR_NOMEM (-3)
+#define IE_ERR_NO_DEVICE (-4)
+#define IE_ERR_TIMEOUT (-5)
+#define IE_ERR_CAPACITY (-6) /* caller-owned output buffer too small: see *total */
+
+/* Divergence caps. The reference loops forever on self-referential inserts (py:516 has no bound)
+ * or grows without limit; both the oracle and the device path stop a string once its working
+ * copy has taken more than IE_ITER_CAP substitutions or grown beyond IE_SIZE_CAP bytes, and report
+ * IE_DIVERGED. `len` is the input string's byte length, `maxtext` the longest splice text in the
+ * table (so any result without re-resolution, at most len/2 refs of maxtext bytes, fits). */
+#define IE_ITER_CAP(len) (4096ull + 8ull * (uint64_t)(len))
+#define IE_SIZE_CAP(len, maxtext) \
+  ((1ull << 20) + 64ull * (uint64_t)(len) + (uint64_t)(maxtext) * ((uint64_t)(len) / 2ull + 1ull))
+
+/* value_id sentinels (value_id is otherwise the index into the ie_kv array given to ie_table_build) */
+#define IE_VID_NONE 0xFFFFFFFFu
+#define IE_VID_CLOCK_HHMM 0xFFFFFFFEu   /* get_interpdata 'HH:MM'    (py:433-434) */
+#define IE_VID_CLOCK_HHMMSS 0xFFFFFFFDu /* get_interpdata 'HH:MM:SS' (py:435-436) */
+
+/* One insert. `text` is the splice rendering the binding computed on the host:
+ *   py: str(v)  (list -> Python repr, int -> decimal; py:531)
+ *   rs: value_to_string(v)  (interp.rs:314-322)
+ * For IE_KIND_STR `text` is the string itself. */
+typedef struct ie_kv {
+  const char* key;
+  uint64_t key_len;
+  const char* text;
+  uint64_t text_len;
+  int32_t kind;
+  uint32_t reserved;
+} ie_kv;
+
+/* Injected wall clock for 'HH:MM' / 'HH:MM:SS' (one clock per table build). */
+typedef struct ie_clock {
+  int32_t hour, minute, second;
+} ie_clock;
+
+#define IE_TABLE_HAS_INSERTS_DIR 1u /* missing keys report IE_NEEDS_HOST instead of IE_E_INTERP */
+
+typedef struct ie_table ie_table; /* immutable after build; read-only on device; thread-safe */
+typedef struct ie_exec ie_exec;   /* one per host thread: device, stream, workspace           */
+
+/* Device-resident output of a batch call. All pointers are DEVICE pointers owned by the caller.
+ * bytes_cap is the capacity of `bytes`. The call writes the required byte count to *total
+ * (a device word); when it exceeds bytes_cap the byte payload is not written and the caller
+ * re-runs with a larger buffer (offsets/status stay valid). value_id[i] is written only
+ * where status[i] == IE_OK_VALUE. */
+typedef struct ie_dev_out {
+  uint8_t* bytes;
+  uint64_t bytes_cap;
+  uint64_t* offsets;  /* n + 1 */
+  uint8_t* status;    /* n     */
+  uint32_t* value_id; /* n     */
+  uint64_t* total;    /* 1     */
+} ie_dev_out;
+
+/* Host-resident result owned by the library (free with ie_batch_free). */
+typedef struct ie_batch {
+  uint8_t* bytes;
+  uint64_t bytes_len;
+  uint64_t* offsets; /* n + 1 */
+  uint8_t* status;   /* n     */
+  uint32_t* value_id;/* n     */
+  uint64_t n;
+} ie_batch;
+
+/* Kernel timing of the last device call on an exec (HIP events on the exec's stream). */
+typedef struct ie_timing {
+  float resolve_ms;  /* the dominant resolve/escape kernel(s) */
+  float complex_ms;  /* literal (complex-string) kernel, 0 if none ran */
+  float total_ms;    /* first to last kernel of the call */
+  uint64_t n_complex;/* strings routed to the literal kernel (valid after ie_exec_sync) */
+} ie_timing;
+
+/* ---- library ---- */
+int32_t ie_abi_version(void);
+const char* ie_last_error(void);
+int32_t ie_device_count(void);
+
+/* ---- table: get_interpdata (py:430-467 / interp.rs:91-137) ---- */
+int ie_table_build(const ie_kv* kv, uint64_t n, int32_t dialect, const ie_clock* now,
+                   uint32_t flags, int32_t device, ie_table** out);
+void ie_table_free(ie_table* t);
+uint64_t ie_table_entries(const ie_table* t);
+int32_t ie_table_dialect(const ie_table* t);
+
+/* ---- exec context ---- */
+int ie_exec_create(int32_t device, void* hip_stream /* NULL: a new non-blocking stream */,
+                   ie_exec** out);
+void ie_exec_destroy(ie_exec* x);
+int ie_exec_sync(ie_exec* x);
+int ie_exec_set_timing(ie_exec* x, int32_t enabled);
+int ie_exec_timing(ie_exec* x, ie_timing* out); /* syncs */
+int ie_exec_set_scratch(ie_exec* x, uint64_t bytes); /* literal-kernel scratch pool size */
+
+/* ---- interpolate_inserts over a packed batch (py:497-541 / interp.rs:31-89) ----
+ * Input: UTF-8 bytes, offsets[n+1] (string i = bytes[offsets[i] .. offsets[i+1])).
+ * _device: all pointers device-resident, asynchronous on the exec's stream.
+ * _batch:  host pointers; H2D + kernels + D2H, synchronous, retries capacity/overflow. */
+int ie_interpolate_device(ie_exec* x, const ie_table* t, const uint8_t* d_bytes,
+                          const uint64_t* d_offsets, uint64_t n, const ie_dev_out* out);
+int ie_interpolate_batch(ie_exec* x, const ie_table* t, const uint8_t* bytes,
+                         const uint64_t* offsets, uint64_t n, ie_batch** out);
+/* scalar drop-in: one string (a batch of one on the device) */
+int ie_interpolate(ie_exec* x, const ie_table* t, const char* s, uint64_t len, ie_batch** out);
+
+/* ---- recursive_unescape / recursive_escape on strings (py:1436-1460 / interp.rs:147-177) ---- */
+int ie_unescape_device(ie_exec* x, const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t n,
+                       const ie_dev_out* out);
+int ie_escape_device(ie_exec* x, const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t n,
+                     const ie_dev_out* out);
+int ie_unescape_batch(ie_exec* x, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                      ie_batch** out);
+int ie_escape_batch(ie_exec* x, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                    ie_batch** out);
+
+void ie_batch_free(ie_batch* b);
+
+/* ---- get_simple_insertkey (py:477-495 / interp.rs:11-29), host-side classifier used by the
+ * callers' control flow (recursive_interpolate, validate_program). Returns 1 when the reference
+ * returns a truthy key (py) / Some (rs), 0 otherwise; *key_off/*key_len locate the key. ---- */
+int ie_simple_insertkey(const char* s, uint64_t len, int32_t dialect, uint64_t* key_off,
+                        uint64_t* key_len);
+
+/* ---- synthetic workloads of SURVEY §8d (configs 2-4): deterministic splitmix64 ---- */
+typedef struct ie_synth ie_synth;
+int ie_synth_create(int32_t config, uint64_t seed, ie_synth** out);
+void ie_synth_free(ie_synth* s);
+uint64_t ie_synth_kv(const ie_synth* s, const ie_kv** kv); /* the inserts, as ie_kv */
+/* Strings [first, first+n). bytes may be NULL (offsets + *total only). offsets are relative
+ * to string `first` (offsets[0] == 0). */
+int ie_synth_strings_host(const ie_synth* s, uint64_t first, uint64_t n, uint8_t* bytes,
+                          uint64_t bytes_cap, uint64_t* offsets, uint64_t* total);
+int ie_synth_strings_device(ie_exec* x, const ie_synth* s, uint64_t first, uint64_t n,
+                            uint8_t* d_bytes, uint64_t bytes_cap, uint64_t* d_offsets,
+                            uint64_t* total /* host */);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IE_AMD_H */
