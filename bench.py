@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""Benchmark of the `{key}` interpolation hot path on MI355X (BASELINE.json metric).
+
+One step = one ie_interpolate_device call over one batch of synthetic strings already resident
+in HBM (SURVEY §8d config 3 by default: 10M strings of 48-80 B, 1-2 nested `{q-{iM}}` refs each,
+100k-entry inserts table). Multi-GPU: one process per GPU, each resolving its own shard of the
+string index space (weak scaling; the table is replicated, no data-path collective — only the
+barrier and the max-over-ranks timing use torch.distributed).
+
+Prints ONE JSON line (rank 0). `value` is interpolated MB/s (input payload, 1 MB = 1e6 B) over all
+ranks; `roofline` prices the resolve pipeline against HBM (algorithmic bytes |in|+|out|+17 per
+string); `cpu_baseline` times the C oracle (a literal restatement of the reference
+algorithm, oracle/ie_oracle.c) on a bounded sample of the same workload on this host.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+CLOCK = (12, 34, 56)
+WORKLOADS = {
+    2: "cfg2: 1M strings/GPU, 48-80 B, 1-3 single-level {kJ} refs, 1k-entry inserts",
+    3: "cfg3: 10M strings/GPU, 48-80 B, 1-2 nested {q-{iM}} refs, 100k-entry inserts",
+}
+DEFAULT_N = {2: 1_000_000, 3: 10_000_000}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", type=int, default=3, choices=[2, 3])
+    ap.add_argument("--n", type=int, default=0, help="strings per GPU (default: the config's size)")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline budget (thread-seconds)")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import __graft_entry__ as G
+    G.build()
+    pkg = G.load_package()
+    N = pkg._native
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.cuda.current_device()
+    stream = torch.cuda.current_stream()
+
+    cfg = args.config
+    n = args.n or DEFAULT_N[cfg]
+    first = rank * n  # this rank's shard of the global string index space
+
+    L = N.lib()
+    synth = ctypes.c_void_p()
+    N.check(L.ie_synth_create(cfg, 0, ctypes.byref(synth)), "ie_synth_create")
+    kvp = ctypes.POINTER(N.KV)()
+    nkv = L.ie_synth_kv(synth, ctypes.byref(kvp))
+    x = N.Exec(dev, stream.cuda_stream)
+    table = ctypes.c_void_p()
+    clk = N.Clock(*CLOCK)
+    N.check(L.ie_table_build(ctypes.cast(kvp, ctypes.c_void_p), nkv, 0, ctypes.byref(clk), 0, dev,
+                             ctypes.byref(table)), "ie_table_build")
+
+    # inputs generated straight into HBM (counter-based splitmix64: rank r owns strings [r*n, (r+1)*n))
+    d_off = torch.zeros(n + 1, dtype=torch.uint64, device="cuda")
+    tot = ctypes.c_uint64()
+    N.check(L.ie_synth_strings_device(x.h, synth, first, n, None, 0, d_off.data_ptr(), ctypes.byref(tot)), "synth")
+    in_bytes = int(tot.value)
+    d_in = torch.empty(in_bytes + 16, dtype=torch.uint8, device="cuda")
+    N.check(L.ie_synth_strings_device(x.h, synth, first, n, d_in.data_ptr(), d_in.numel(), d_off.data_ptr(),
+                                      ctypes.byref(tot)), "synth")
+    out_cap = 2 * in_bytes + (1 << 20)
+    d_out = torch.empty(out_cap, dtype=torch.uint8, device="cuda")
+    d_ooff = torch.empty(n + 1, dtype=torch.uint64, device="cuda")
+    d_st = torch.empty(n, dtype=torch.uint8, device="cuda")
+    d_vid = torch.empty(n, dtype=torch.int32, device="cuda")
+    d_tot = torch.zeros(1, dtype=torch.uint64, device="cuda")
+    o = N.DevOut(d_out.data_ptr(), out_cap, d_ooff.data_ptr(), d_st.data_ptr(), d_vid.data_ptr(), d_tot.data_ptr())
+
+    def step():
+        N.check(L.ie_interpolate_device(x.h, table, d_in.data_ptr(), d_off.data_ptr(), n, ctypes.byref(o)),
+                "ie_interpolate_device")
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    out_bytes = int(d_tot.item())
+    assert out_bytes <= out_cap
+    n_bad = int((d_st != 0).sum().item())
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        step()
+        ev[k][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    step_ms = [a.elapsed_time(b) for a, b in ev]
+    t = torch.tensor([wall], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall_max = float(t.item())
+
+    # one timed call with the library's own HIP events (same stream) for the kernel split
+    x.set_timing(True)
+    step()
+    tm = x.timing()
+    x.set_timing(False)
+
+    gpu_ms = float(np.mean(step_ms))
+    alg_bytes = in_bytes + out_bytes + 17 * n  # |in| + |out| + 16 (offsets) + 1 (status)
+    achieved_gbs = alg_bytes / (gpu_ms * 1e-3) / 1e9
+    total_in = in_bytes * world
+    value = total_in / wall_max * args.steps / 1e6  # MB/s over all ranks
+    strings_per_s = n * world * args.steps / wall_max
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(args, L, N, synth, kvp, nkv, x, table, d_in, d_off, d_ooff, d_out, d_st)
+
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_path):
+        try:
+            pm = json.load(open(pmc_path))
+            if pm.get("config") == cfg and pm.get("n") == n:
+                traffic = pm.get("hbm_bytes_per_step")
+        except Exception:
+            traffic = None
+
+    if rank == 0:
+        line = {
+            "metric": "interpolated MB/s + strings/s on synthetic batches at 1/2/4/8 MI355X",
+            "value": round(value, 1),
+            "unit": "MB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (SURVEY §8d generator, splitmix64 seed 0x1E5EED00+config, generated in HBM)",
+            "config": {"workload": WORKLOADS[cfg], "strings_per_gpu": n, "input_bytes_per_gpu": in_bytes,
+                       "output_bytes_per_gpu": out_bytes, "inserts": int(nkv), "parallelism": "shard%d" % world,
+                       "non_ok_statuses": n_bad},
+            "strings_per_s": round(strings_per_s, 1),
+            "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "resolve pipeline (k_measure + k_literal + k_scan_tiles + k_emit)",
+                         "launch_ms": round(gpu_ms, 4), "alg_bytes_per_launch": alg_bytes,
+                         "split_ms": {"measure+scan+emit": round(tm.resolve_ms, 4),
+                                      "literal": round(tm.complex_ms, 4), "n_literal": int(tm.n_complex)}},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    L.ie_table_free(table)
+    L.ie_synth_free(synth)
+    x.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, L, N, synth, kvp, nkv, x, table, d_in, d_off, d_ooff, d_out, d_st):
+    """The oracle (a literal C restatement of interpolate_inserts) on a bounded sample of the same
+    workload, timed on this host; the sample's GPU results are checked against it."""
+    from oracle import oracle as O
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    ref = O.Oracle.from_kv(ctypes.cast(kvp, ctypes.c_void_p), nkv, "py", clock=CLOCK)
+
+    def host_sample(m):
+        offs = np.zeros(m + 1, np.uint64)
+        tot = ctypes.c_uint64()
+        N.check(L.ie_synth_strings_host(synth, 0, m, None, 0, offs.ctypes.data, ctypes.byref(tot)), "len")
+        buf = np.zeros(int(tot.value) + 1, np.uint8)
+        N.check(L.ie_synth_strings_host(synth, 0, m, buf.ctypes.data, buf.size, offs.ctypes.data,
+                                        ctypes.byref(tot)), "fill")
+        return buf, offs
+
+    buf, offs = host_sample(20000)  # calibrate single-thread speed
+    dt = ref.run_batch(buf, offs, 20000, 1)
+    per_string = max(dt / 20000, 1e-9)
+    m = int(min(args.n or DEFAULT_N[args.config], max(20000, args.cpu_seconds / per_string)))
+    buf, offs = host_sample(m)
+    st = np.zeros(m, np.uint8)
+    ln = np.zeros(m, np.uint64)
+    hs = np.zeros(m, np.uint64)
+    wall = ref.run_batch(buf, offs, m, threads, st, ln, hs, None)
+    sample_bytes = int(offs[m])
+    # parity of the GPU's first m results with the oracle on the same strings
+    gst = d_st[:m].cpu().numpy()
+    goff = d_ooff[:m + 1].cpu().numpy()
+    gout = d_out[:int(goff[m])].cpu().numpy().tobytes()
+    same = bool(np.array_equal(gst, st)) and bool(np.array_equal(np.diff(goff.astype(np.int64)), ln.astype(np.int64)))
+    if same:
+        k = min(m, 20000)
+        gh = np.array([O.fnv1a(gout[int(goff[i]):int(goff[i + 1])]) for i in range(k)], dtype=np.uint64)
+        same = bool(np.array_equal(gh, hs[:k]))
+    return {"value": round(sample_bytes / wall / 1e6, 2), "unit": "MB/s", "cores": threads, "kind": "port",
+            "strings_per_s": round(m / wall, 1),
+            "sample": "first %d strings (%d B) of the same workload; oracle/ie_oracle.c, %d threads, %.2f s wall; "
+                      "GPU output identical on the sample: %s" % (m, sample_bytes, threads, wall, same)}
+
+
+if __name__ == "__main__":
+    main()

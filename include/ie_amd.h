@@ -187,7 +187,7 @@ void ie_batch_free(ie_batch* b);
 
 /* ---- get_simple_insertkey (py:477-495 / interp.rs:11-29), host-side classifier used by the
  * callers' control flow (recursive_interpolate, validate_program). Returns 1 when the reference
- * returns a truthy key (py) / Some (rs), 0 otherwise; *key_off/*key_len locate the key. ---- */
+ * returns a truthy key (py) / Some (rs), 0 otherwise; key_off and key_len locate the key. ---- */
 int ie_simple_insertkey(const char* s, uint64_t len, int32_t dialect, uint64_t* key_off,
                         uint64_t* key_len);
 

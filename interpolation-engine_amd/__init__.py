@@ -1,0 +1,20 @@
+"""interpolation-engine_amd: MI355X-native `{key}` interpolation (the hot path of
+tillfalko/interpolation-engine), HIP kernels behind the C ABI of include/ie_amd.h.
+
+Import this directory as the package `interpolation_engine_amd` (its on-disk name has a hyphen):
+see __graft_entry__.load_package().
+"""
+from . import _native  # noqa: F401
+from .interpolation_engine import (  # noqa: F401
+    InsertsTable,
+    InterpolationException,
+    get_interpdata,
+    get_simple_insertkey,
+    interpolate_batch,
+    interpolate_inserts,
+    recursive_escape,
+    recursive_interpolate,
+    recursive_unescape,
+)
+
+__version__ = "0.1.0"

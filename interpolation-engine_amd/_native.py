@@ -1,0 +1,177 @@
+"""ctypes binding of libie_amd.so (include/ie_amd.h).
+
+The library is the only execution path for the resolver: if it is missing this module raises
+at import-use time, and if no HIP device is visible every compute entry point returns
+IE_ERR_NO_DEVICE, which is raised as RuntimeError here. There is no CPU fallback.
+"""
+import ctypes
+import os
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libie_amd.so")
+
+IE_DIALECT = {"py": 0, "rs": 1}
+KIND_STR, KIND_INT, KIND_LIST, KIND_FLOAT, KIND_BOOL, KIND_NULL, KIND_DICT = range(7)
+(OK_STR, OK_VALUE, E_INTERP, E_ASSERT_BRACES, E_ASSERT_TYPE, E_UNHASHABLE, E_RS_PANIC, NEEDS_HOST,
+ DIVERGED, E_OVERFLOW) = range(10)
+STATUS_NAMES = ["OK_STR", "OK_VALUE", "E_INTERP", "E_ASSERT_BRACES", "E_ASSERT_TYPE",
+                "E_UNHASHABLE", "E_RS_PANIC", "NEEDS_HOST", "DIVERGED", "E_OVERFLOW"]
+VID_NONE, VID_HHMM, VID_HHMMSS = 0xFFFFFFFF, 0xFFFFFFFE, 0xFFFFFFFD
+TABLE_HAS_INSERTS_DIR = 1
+
+# every symbol include/ie_amd.h declares (tests check the .so exports exactly these)
+EXPORTS = [
+    "ie_abi_version", "ie_last_error", "ie_device_count",
+    "ie_table_build", "ie_table_free", "ie_table_entries", "ie_table_dialect",
+    "ie_exec_create", "ie_exec_destroy", "ie_exec_sync", "ie_exec_set_timing", "ie_exec_timing",
+    "ie_exec_set_scratch",
+    "ie_interpolate_device", "ie_interpolate_batch", "ie_interpolate",
+    "ie_unescape_device", "ie_escape_device", "ie_unescape_batch", "ie_escape_batch",
+    "ie_batch_free", "ie_simple_insertkey",
+    "ie_synth_create", "ie_synth_free", "ie_synth_kv", "ie_synth_strings_host",
+    "ie_synth_strings_device",
+]
+
+
+class KV(ctypes.Structure):
+    _fields_ = [("key", ctypes.c_char_p), ("key_len", ctypes.c_uint64),
+                ("text", ctypes.c_char_p), ("text_len", ctypes.c_uint64),
+                ("kind", ctypes.c_int32), ("reserved", ctypes.c_uint32)]
+
+
+class Clock(ctypes.Structure):
+    _fields_ = [("hour", ctypes.c_int32), ("minute", ctypes.c_int32), ("second", ctypes.c_int32)]
+
+
+class DevOut(ctypes.Structure):
+    _fields_ = [("bytes", ctypes.c_void_p), ("bytes_cap", ctypes.c_uint64),
+                ("offsets", ctypes.c_void_p), ("status", ctypes.c_void_p),
+                ("value_id", ctypes.c_void_p), ("total", ctypes.c_void_p)]
+
+
+class BatchRes(ctypes.Structure):
+    _fields_ = [("bytes", ctypes.POINTER(ctypes.c_uint8)), ("bytes_len", ctypes.c_uint64),
+                ("offsets", ctypes.POINTER(ctypes.c_uint64)), ("status", ctypes.POINTER(ctypes.c_uint8)),
+                ("value_id", ctypes.POINTER(ctypes.c_uint32)), ("n", ctypes.c_uint64)]
+
+
+class Timing(ctypes.Structure):
+    _fields_ = [("resolve_ms", ctypes.c_float), ("complex_ms", ctypes.c_float),
+                ("total_ms", ctypes.c_float), ("n_complex", ctypes.c_uint64)]
+
+
+_lib = None
+
+
+def lib():
+    """Load libie_amd.so (raises if it was not built: there is no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libie_amd.so is not built (%s); run `python -c \"import __graft_entry__ as g; "
+                          "g.build()\"`" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u64, i32, u32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int32, ctypes.c_uint32
+    pvp = ctypes.POINTER(ctypes.c_void_p)
+    sig = {
+        "ie_abi_version": (i32, []),
+        "ie_last_error": (ctypes.c_char_p, []),
+        "ie_device_count": (i32, []),
+        "ie_table_build": (ctypes.c_int, [vp, u64, i32, ctypes.POINTER(Clock), u32, i32, pvp]),
+        "ie_table_free": (None, [vp]),
+        "ie_table_entries": (u64, [vp]),
+        "ie_table_dialect": (i32, [vp]),
+        "ie_exec_create": (ctypes.c_int, [i32, vp, pvp]),
+        "ie_exec_destroy": (None, [vp]),
+        "ie_exec_sync": (ctypes.c_int, [vp]),
+        "ie_exec_set_timing": (ctypes.c_int, [vp, i32]),
+        "ie_exec_timing": (ctypes.c_int, [vp, ctypes.POINTER(Timing)]),
+        "ie_exec_set_scratch": (ctypes.c_int, [vp, u64]),
+        "ie_interpolate_device": (ctypes.c_int, [vp, vp, vp, vp, u64, ctypes.POINTER(DevOut)]),
+        "ie_interpolate_batch": (ctypes.c_int, [vp, vp, vp, vp, u64, ctypes.POINTER(ctypes.POINTER(BatchRes))]),
+        "ie_interpolate": (ctypes.c_int, [vp, vp, ctypes.c_char_p, u64, ctypes.POINTER(ctypes.POINTER(BatchRes))]),
+        "ie_unescape_device": (ctypes.c_int, [vp, vp, vp, u64, ctypes.POINTER(DevOut)]),
+        "ie_escape_device": (ctypes.c_int, [vp, vp, vp, u64, ctypes.POINTER(DevOut)]),
+        "ie_unescape_batch": (ctypes.c_int, [vp, vp, vp, u64, ctypes.POINTER(ctypes.POINTER(BatchRes))]),
+        "ie_escape_batch": (ctypes.c_int, [vp, vp, vp, u64, ctypes.POINTER(ctypes.POINTER(BatchRes))]),
+        "ie_batch_free": (None, [ctypes.POINTER(BatchRes)]),
+        "ie_simple_insertkey": (ctypes.c_int, [ctypes.c_char_p, u64, i32, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
+        "ie_synth_create": (ctypes.c_int, [i32, u64, pvp]),
+        "ie_synth_free": (None, [vp]),
+        "ie_synth_kv": (u64, [vp, ctypes.POINTER(ctypes.POINTER(KV))]),
+        "ie_synth_strings_host": (ctypes.c_int, [vp, u64, u64, vp, u64, vp, ctypes.POINTER(u64)]),
+        "ie_synth_strings_device": (ctypes.c_int, [vp, vp, u64, u64, vp, u64, vp, ctypes.POINTER(u64)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().ie_last_error()
+        raise RuntimeError("%s failed (%d): %s" % (what, rc, msg.decode("utf-8", "replace") if msg else ""))
+
+
+def enc(s):
+    return s.encode("utf-8", "surrogatepass")
+
+
+def dec(b):
+    return b.decode("utf-8", "surrogatepass")
+
+
+class Exec:
+    """An ie_exec: device, HIP stream, workspace. `stream` is a raw hipStream_t (int) or None."""
+
+    def __init__(self, device=0, stream=None):
+        h = ctypes.c_void_p()
+        check(lib().ie_exec_create(device, stream, ctypes.byref(h)), "ie_exec_create")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().ie_exec_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def sync(self):
+        check(lib().ie_exec_sync(self.h), "ie_exec_sync")
+
+    def set_timing(self, on):
+        check(lib().ie_exec_set_timing(self.h, 1 if on else 0), "ie_exec_set_timing")
+
+    def timing(self):
+        t = Timing()
+        check(lib().ie_exec_timing(self.h, ctypes.byref(t)), "ie_exec_timing")
+        return t
+
+
+def batch_to_python(res_ptr):
+    """Copy an ie_batch into Python: (list[bytes], list[int status], list[int vid])."""
+    r = res_ptr.contents
+    n = r.n
+    import numpy as np
+    offs = np.ctypeslib.as_array(r.offsets, shape=(n + 1,)).copy() if n else np.zeros(1, np.uint64)
+    st = np.ctypeslib.as_array(r.status, shape=(n,)).copy() if n else np.zeros(0, np.uint8)
+    vid = np.ctypeslib.as_array(r.value_id, shape=(n,)).copy() if n else np.zeros(0, np.uint32)
+    blob = ctypes.string_at(r.bytes, r.bytes_len) if r.bytes_len else b""
+    lib().ie_batch_free(res_ptr)
+    outs = [blob[int(offs[i]):int(offs[i + 1])] for i in range(n)]
+    return outs, st.tolist(), vid.tolist()
+
+
+def pack(strings):
+    """list[str|bytes] -> (bytes blob, uint64 offsets array)"""
+    import numpy as np
+    bs = [enc(s) if isinstance(s, str) else bytes(s) for s in strings]
+    offs = np.zeros(len(bs) + 1, dtype=np.uint64)
+    if bs:
+        offs[1:] = np.cumsum([len(b) for b in bs], dtype=np.uint64)
+    return b"".join(bs), offs

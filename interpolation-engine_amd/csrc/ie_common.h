@@ -1,0 +1,208 @@
+// ie_common.h — types shared by the host table builder and the gfx950 kernels.
+//
+// Device data layout of one inserts table (built once per get_interpdata snapshot, read-only):
+//   slots[cap]      uint32  entry index + 1 (0 = empty), open addressing, linear probing,
+//                           cap = next_pow2(2 * entries), so probe chains stay short
+//   entries[n]      DevEntry (32 B): 64-bit key hash, key/text spans in the arena, flags, value id
+//   arena[...]      key bytes and splice-text bytes of every entry
+// The hash is a polynomial hash over the key bytes (mod 2^64) so that a key assembled from
+// template pieces and spliced values can be hashed piecewise; slot = fmix64(hash, len) & mask.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define IE_HD __host__ __device__ __forceinline__
+#else
+#define IE_HD inline
+#endif
+
+namespace ie {
+
+constexpr uint64_t kHashP = 0x100000001B3ull;
+
+IE_HD uint64_t hash_step(uint64_t h, uint8_t b) { return h * kHashP + (uint64_t)b + 1ull; }
+
+IE_HD uint64_t fmix64(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return k;
+}
+
+IE_HD uint32_t slot_of(uint64_t h, uint32_t len, uint32_t mask) {
+  return (uint32_t)fmix64(h ^ ((uint64_t)len << 40)) & mask;
+}
+
+// DevEntry.flags
+enum : uint32_t {
+  EF_KIND_MASK = 7u,
+  EF_SPLICE_OK = 1u << 3,      // the dialect's splice type rule passes (py:530 / interp.rs:71-80)
+  EF_INERT = 1u << 4,          // splice text cannot alter brace/escape/placeholder structure
+  EF_KEY_STR = 1u << 5,        // raw value usable as a lookup key (py: str only; rs: value_to_string)
+  EF_KEY_UNHASHABLE = 1u << 6, // py: list/dict raw value as a dict key raises TypeError
+};
+
+// DevTable.flags
+enum : uint32_t { TF_HAS_DIR = 1u };
+
+struct DevEntry {
+  uint64_t hash;
+  uint32_t key_off, key_len;
+  uint32_t text_off, text_len;
+  uint32_t vid;
+  uint32_t flags;
+};
+static_assert(sizeof(DevEntry) == 32, "DevEntry must stay one 32-byte record");
+
+struct DevTable {
+  const uint32_t* slots;
+  const DevEntry* entries;
+  const uint8_t* arena;
+  uint32_t mask;
+  uint32_t n_entries;
+  uint32_t dialect;
+  uint32_t flags;
+  uint64_t maxtext;
+};
+
+// internal status: routed to the literal (complex) kernel
+constexpr uint8_t kStatusPending = 0xFE;
+
+// ------------------------------------------------------------------------------------------
+// Synthetic workloads: counter-based splitmix64, identical on host and device.
+// ------------------------------------------------------------------------------------------
+IE_HD uint64_t splitmix(uint64_t& s) {
+  s += 0x9E3779B97F4A7C15ull;
+  uint64_t z = s;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+struct SynthParams {
+  int32_t config;     // 2, 3 or 4
+  uint64_t seed;
+  uint32_t n_keys;    // config 2: k0..k{n_keys-1}
+  uint32_t n_q;       // config 3/4: q-0..q-{n_q-1}
+  uint32_t n_i;       // config 3/4: i0..i{n_i-1}
+  uint32_t n_chain;   // config 4: a-/b-/c- chain keys
+};
+
+// filler alphabet: ASCII [a-z0-9 .,:;-] plus 5% multibyte code points (é, €, 😀);
+// never '{', '}', '\\' or U+3020.
+IE_HD uint32_t synth_filler(uint64_t& st, uint8_t* out, uint32_t nbytes) {
+  const char* ascii = "abcdefghijklmnopqrstuvwxyz0123456789 .,:;-";
+  uint32_t w = 0;
+  while (w < nbytes) {
+    uint64_t r = splitmix(st);
+    uint32_t left = nbytes - w;
+    if ((r % 100) < 5 && left >= 2) {
+      uint32_t pick = (uint32_t)((r >> 8) % 3);
+      if (pick == 2 && left >= 4) {
+        if (out) { out[w] = 0xF0; out[w + 1] = 0x9F; out[w + 2] = 0x98; out[w + 3] = 0x80; }
+        w += 4;
+        continue;
+      }
+      if (pick >= 1 && left >= 3) {
+        if (out) { out[w] = 0xE2; out[w + 1] = 0x82; out[w + 2] = 0xAC; }
+        w += 3;
+        continue;
+      }
+      if (out) { out[w] = 0xC3; out[w + 1] = 0xA9; }
+      w += 2;
+      continue;
+    }
+    if (out) out[w] = (uint8_t)ascii[(r >> 16) % 42];
+    w += 1;
+  }
+  return w;
+}
+
+IE_HD uint32_t put_dec(uint8_t* out, uint32_t v) {
+  uint8_t tmp[12];
+  uint32_t n = 0;
+  do {
+    tmp[n++] = (uint8_t)('0' + v % 10);
+    v /= 10;
+  } while (v);
+  for (uint32_t k = 0; k < n; k++)
+    if (out) out[k] = tmp[n - 1 - k];
+  return n;
+}
+
+IE_HD uint64_t synth_state(const SynthParams& P, uint64_t i) {
+  uint64_t s = P.seed ^ ((uint64_t)P.config << 56);
+  s += (i + 1) * 0xD1B54A32D192ED03ull;
+  splitmix(s);
+  return s;
+}
+
+// Byte length of synthetic string i (the first draw of its stream).
+IE_HD uint32_t synth_len(const SynthParams& P, uint64_t i) {
+  uint64_t st = synth_state(P, i);
+  return 48u + (uint32_t)(splitmix(st) % 33u);
+}
+
+// Writes string i (exactly synth_len bytes) to out.
+IE_HD uint32_t synth_string(const SynthParams& P, uint64_t i, uint8_t* out) {
+  uint64_t st = synth_state(P, i);
+  const uint32_t L = 48u + (uint32_t)(splitmix(st) % 33u);
+  // references
+  uint8_t ref[4][40];
+  uint32_t rlen[4];
+  uint32_t R;
+  if (P.config == 2) {
+    R = 1 + (uint32_t)(splitmix(st) % 3);
+    for (uint32_t r = 0; r < R; r++) {
+      uint32_t j = (uint32_t)(splitmix(st) % P.n_keys);
+      uint32_t w = 0;
+      ref[r][w++] = '{';
+      ref[r][w++] = 'k';
+      w += put_dec(ref[r] + w, j);
+      ref[r][w++] = '}';
+      rlen[r] = w;
+    }
+  } else {
+    R = 1 + (uint32_t)(splitmix(st) % 2);
+    for (uint32_t r = 0; r < R; r++) {
+      uint32_t m = (uint32_t)(splitmix(st) % P.n_i);
+      uint32_t w = 0;
+      ref[r][w++] = '{';
+      ref[r][w++] = 'q';
+      ref[r][w++] = '-';
+      ref[r][w++] = '{';
+      ref[r][w++] = 'i';
+      w += put_dec(ref[r] + w, m);
+      ref[r][w++] = '}';
+      ref[r][w++] = '}';
+      rlen[r] = w;
+    }
+  }
+  uint32_t refbytes = 0;
+  for (uint32_t r = 0; r < R; r++) refbytes += rlen[r];
+  uint32_t F = L > refbytes + 1 ? L - refbytes : 1;  // L >= 48 > refbytes always
+  // split F filler bytes into R+1 gaps, gap 0 >= 1 (no whole-string simple refs)
+  uint32_t gap[5];
+  uint32_t rest = F - 1;
+  for (uint32_t g = 0; g < R; g++) {
+    uint32_t take = rest ? (uint32_t)(splitmix(st) % (rest + 1)) : 0;
+    gap[g] = take;
+    rest -= take;
+  }
+  gap[R] = rest;
+  gap[0] += 1;
+  uint32_t w = 0;
+  for (uint32_t g = 0; g <= R; g++) {
+    w += synth_filler(st, out ? out + w : nullptr, gap[g]);
+    if (g < R) {
+      for (uint32_t k = 0; k < rlen[g]; k++)
+        if (out) out[w + k] = ref[g][k];
+      w += rlen[g];
+    }
+  }
+  return w;  // == L
+}
+
+}  // namespace ie

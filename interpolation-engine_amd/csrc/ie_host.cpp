@@ -1,0 +1,691 @@
+// ie_host.cpp — host side of libie_amd.so: the C ABI of include/ie_amd.h.
+//
+//   table build    get_interpdata (py:430-467 / interp.rs:91-137) frozen into a device hash table:
+//                  dict semantics (last duplicate wins), '' never an entry, 'HH:MM' / 'HH:MM:SS'
+//                  injected from one clock per build, per-entry splice/inert/key flags.
+//   exec           one HIP stream + a grow-only device workspace; no allocation inside the
+//                  device entry points once the workspace fits (graph-capturable).
+//   batch calls    ie_interpolate_device (async, device pointers) and the synchronous host
+//                  convenience ie_interpolate_batch (H2D, kernels, D2H, capacity/overflow retry).
+// There is no CPU execution path for the resolver: every string is resolved by the kernels in
+// ie_kernels.hip; when no device is present the entry points fail with IE_ERR_NO_DEVICE.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <string_view>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/ie_amd.h"
+#include "ie_common.h"
+#include "ie_kernels.h"
+
+using namespace ie;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define IE_HIP(call)                                                                   \
+  do {                                                                                 \
+    hipError_t e_ = (call);                                                            \
+    if (e_ != hipSuccess)                                                              \
+      return fail(IE_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_));     \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  uint64_t bytes = 0;
+  hipError_t ensure(uint64_t need) {
+    if (need <= bytes && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    uint64_t n = std::max<uint64_t>(need, 256);
+    hipError_t e = hipMalloc(&p, n);
+    if (e == hipSuccess) bytes = n;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+};
+
+bool have_device() {
+  int n = 0;
+  return hipGetDeviceCount(&n) == hipSuccess && n > 0;
+}
+
+}  // namespace
+
+struct ie_table {
+  int32_t device = 0;
+  int32_t dialect = 0;
+  uint32_t flags = 0;
+  uint64_t n_entries = 0;
+  DevTable dev{};
+  DevBuf slots, entries, arena;
+  ~ie_table() {
+    slots.release();
+    entries.release();
+    arena.release();
+  }
+};
+
+struct ie_exec {
+  int32_t device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  bool timing = false;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  bool ev_recorded = false;
+  uint32_t lit_cap_max = 0;
+  uint64_t pool_request = 256ull << 20;
+  // workspace
+  DevBuf out_len, tile_sum, tile_base, counters, cx_list, cx_status, res_off, pool;
+  // host-API staging
+  DevBuf in_bytes, in_off, o_bytes, o_off, o_status, o_vid, o_total;
+  // synth scratch
+  DevBuf s_lens, s_part;
+  ~ie_exec() {
+    for (DevBuf* b : {&out_len, &tile_sum, &tile_base, &counters, &cx_list, &cx_status, &res_off,
+                      &pool, &in_bytes, &in_off, &o_bytes, &o_off, &o_status, &o_vid, &o_total,
+                      &s_lens, &s_part})
+      b->release();
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
+    if (own_stream && stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+struct ie_synth {
+  SynthParams P{};
+  std::vector<std::string> keys, texts;
+  std::vector<ie_kv> kv;
+};
+
+namespace {
+
+// ---- splice-text analysis for the fast path (see DESIGN.md "inert values") ----
+uint32_t text_flags(const std::string_view t) {
+  bool inert = true;
+  const size_t n = t.size();
+  for (size_t i = 0; i < n && inert; i++) {
+    const uint8_t c = (uint8_t)t[i];
+    if ((c == '{' || c == '}') && (i == 0 || t[i - 1] != '\\')) inert = false;  // re-resolves
+    if (c == 0xE3 && i + 2 < n && (uint8_t)t[i + 1] == 0x80 && (uint8_t)t[i + 2] == 0xA0)
+      inert = false;  // U+3020 collides with the placeholders
+    if (c == '\\' && i + 1 < n && t[i + 1] == '}') {
+      if (i == 0) inert = false;                                   // '.' + '\}' across the seam
+      else if (t[i - 1] == '.' || t[i - 1] == '}') inert = false;  // '.\}' restores as '\{.'
+    }
+  }
+  if (n && t[n - 1] == '\\') inert = false;  // escapes a following brace (trailing backslash)
+  return inert ? EF_INERT : 0u;
+}
+
+uint32_t kind_flags(int32_t kind, int32_t dialect) {
+  uint32_t f = (uint32_t)kind & EF_KIND_MASK;
+  bool splice;
+  if (dialect == IE_DIALECT_PY)  // py:530
+    splice = kind == IE_KIND_STR || kind == IE_KIND_INT || kind == IE_KIND_LIST;
+  else  // interp.rs:71-80
+    splice = kind == IE_KIND_STR || kind == IE_KIND_INT || kind == IE_KIND_FLOAT || kind == IE_KIND_LIST;
+  if (splice) f |= EF_SPLICE_OK;
+  if (dialect == IE_DIALECT_PY) {
+    if (kind == IE_KIND_STR) f |= EF_KEY_STR;
+    if (kind == IE_KIND_LIST || kind == IE_KIND_DICT) f |= EF_KEY_UNHASHABLE;
+  } else {
+    f |= EF_KEY_STR;  // value_to_string (interp.rs:48, 51)
+  }
+  return f;
+}
+
+uint64_t poly_hash(const std::string_view k) {
+  uint64_t h = 0;
+  for (unsigned char c : k) h = hash_step(h, c);
+  return h;
+}
+
+int set_device(int32_t dev) {
+  if (!have_device()) return fail(IE_ERR_NO_DEVICE, "no HIP device visible (libie_amd has no CPU path)");
+  IE_HIP(hipSetDevice(dev));
+  return IE_SUCCESS;
+}
+
+// workspace for a batch of n strings
+int ensure_work(ie_exec* x, uint64_t n) {
+  const uint64_t tiles = (n + kBlock - 1) / kBlock + 1;
+  IE_HIP(x->out_len.ensure((n + 1) * sizeof(uint32_t)));
+  IE_HIP(x->tile_sum.ensure(tiles * sizeof(uint64_t)));
+  IE_HIP(x->tile_base.ensure(tiles * sizeof(uint64_t)));
+  IE_HIP(x->counters.ensure(64));
+  IE_HIP(x->cx_list.ensure((n + 1) * sizeof(uint32_t)));
+  IE_HIP(x->cx_status.ensure(n + 1));
+  IE_HIP(x->res_off.ensure((n + 1) * sizeof(uint64_t)));
+  IE_HIP(x->pool.ensure(x->pool_request));
+  return IE_SUCCESS;
+}
+
+Work make_work(ie_exec* x) {
+  Work W{};
+  W.out_len = (uint32_t*)x->out_len.p;
+  W.tile_sum = (uint64_t*)x->tile_sum.p;
+  W.tile_base = (uint64_t*)x->tile_base.p;
+  W.cx_count = (uint32_t*)x->counters.p;
+  W.pool_used = (uint64_t*)((char*)x->counters.p + 8);
+  W.cx_list = (uint32_t*)x->cx_list.p;
+  W.cx_status = (uint8_t*)x->cx_status.p;
+  W.res_off = (uint64_t*)x->res_off.p;
+  W.pool = (uint8_t*)x->pool.p;
+  W.pool_bytes = x->pool.bytes;
+  W.lit_cap_max = x->lit_cap_max;
+  return W;
+}
+
+int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, const uint64_t* d_off,
+               uint64_t n, const ie_dev_out* out) {
+  if (!x || !d_off || !out || !out->offsets || !out->status || !out->total || (op == kOpInterp && !t))
+    return fail(IE_ERR_INVALID, "null argument");
+  if (n && !d_bytes) return fail(IE_ERR_INVALID, "null input bytes");
+  if (n && (!out->value_id && op == kOpInterp)) return fail(IE_ERR_INVALID, "null value_id");
+  if (op == kOpInterp && t->device != x->device)
+    return fail(IE_ERR_INVALID, "table and exec live on different devices");
+  int rc = set_device(x->device);
+  if (rc) return rc;
+  if (n > 0xFFFFFFF0ull) return fail(IE_ERR_INVALID, "batch larger than 2^32 strings");
+  rc = ensure_work(x, n);
+  if (rc) return rc;
+  Batch B{d_bytes, d_off, n, out->offsets, out->status, out->value_id};
+  Work W = make_work(x);
+  DevTable T = op == kOpInterp ? t->dev : DevTable{};
+  hipStream_t st = x->stream;
+  if (x->timing) IE_HIP(hipEventRecord(x->ev[0], st));
+  IE_HIP(hipMemsetAsync(x->counters.p, 0, 64, st));
+  if (n == 0) {
+    IE_HIP(hipMemsetAsync(out->offsets, 0, sizeof(uint64_t), st));
+    IE_HIP(hipMemsetAsync(out->total, 0, sizeof(uint64_t), st));
+    if (x->timing) {
+      IE_HIP(hipEventRecord(x->ev[1], st));
+      IE_HIP(hipEventRecord(x->ev[2], st));
+      IE_HIP(hipEventRecord(x->ev[3], st));
+      x->ev_recorded = true;
+    }
+    return IE_SUCCESS;
+  }
+  IE_HIP(launch_measure(op, B, W, T, st));
+  if (x->timing) IE_HIP(hipEventRecord(x->ev[1], st));
+  if (op == kOpInterp) IE_HIP(launch_literal(B, W, T, st));
+  if (x->timing) IE_HIP(hipEventRecord(x->ev[2], st));
+  IE_HIP(launch_scan_tiles(B, W, out->total, st));
+  IE_HIP(launch_emit(op, B, W, T, out->bytes, out->bytes ? out->bytes_cap : 0, out->total, st));
+  if (x->timing) {
+    IE_HIP(hipEventRecord(x->ev[3], st));
+    x->ev_recorded = true;
+  }
+  return IE_SUCCESS;
+}
+
+// synchronous host batch: H2D, run, D2H; grows the output buffer and re-runs overflowed
+// literal-path strings with the full working space until every status is final.
+int run_host(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, const uint64_t* offsets,
+             uint64_t n, ie_batch** outp) {
+  if (!x || !outp || (n && (!bytes || !offsets))) return fail(IE_ERR_INVALID, "null argument");
+  int rc = set_device(x->device);
+  if (rc) return rc;
+  const uint64_t base = n ? offsets[0] : 0;
+  const uint64_t in_bytes = n ? offsets[n] - base : 0;
+  std::vector<uint64_t> off(n + 1);
+  for (uint64_t i = 0; i <= n; i++) off[i] = n ? offsets[i] - base : 0;
+  IE_HIP(x->in_bytes.ensure(in_bytes + 16));
+  IE_HIP(x->in_off.ensure((n + 1) * 8));
+  IE_HIP(x->o_off.ensure((n + 1) * 8));
+  IE_HIP(x->o_status.ensure(n + 1));
+  IE_HIP(x->o_vid.ensure((n + 1) * 4));
+  IE_HIP(x->o_total.ensure(8));
+  if (in_bytes) IE_HIP(hipMemcpyAsync(x->in_bytes.p, bytes + base, in_bytes, hipMemcpyHostToDevice, x->stream));
+  IE_HIP(hipMemcpyAsync(x->in_off.p, off.data(), (n + 1) * 8, hipMemcpyHostToDevice, x->stream));
+  uint64_t cap = std::max<uint64_t>(2 * in_bytes + 4096, x->o_bytes.bytes);
+  IE_HIP(x->o_bytes.ensure(cap));
+  cap = x->o_bytes.bytes;
+  ie_dev_out o{(uint8_t*)x->o_bytes.p, cap, (uint64_t*)x->o_off.p, (uint8_t*)x->o_status.p,
+               (uint32_t*)x->o_vid.p, (uint64_t*)x->o_total.p};
+  rc = run_device(x, op, t, (const uint8_t*)x->in_bytes.p, (const uint64_t*)x->in_off.p, n, &o);
+  if (rc) return rc;
+  uint64_t total = 0;
+  IE_HIP(hipMemcpyAsync(&total, o.total, 8, hipMemcpyDeviceToHost, x->stream));
+  IE_HIP(hipStreamSynchronize(x->stream));
+  if (total > cap) {  // grow and re-run
+    IE_HIP(x->o_bytes.ensure(total + 4096));
+    o.bytes = (uint8_t*)x->o_bytes.p;
+    o.bytes_cap = x->o_bytes.bytes;
+    rc = run_device(x, op, t, (const uint8_t*)x->in_bytes.p, (const uint64_t*)x->in_off.p, n, &o);
+    if (rc) return rc;
+    IE_HIP(hipMemcpyAsync(&total, o.total, 8, hipMemcpyDeviceToHost, x->stream));
+    IE_HIP(hipStreamSynchronize(x->stream));
+    if (total > o.bytes_cap) return fail(IE_ERR_CAPACITY, "output grew between runs");
+  }
+  ie_batch* b = new ie_batch{};
+  b->n = n;
+  b->bytes_len = total;
+  b->bytes = new uint8_t[total + 1];
+  b->offsets = new uint64_t[n + 1];
+  b->status = new uint8_t[n + 1];
+  b->value_id = new uint32_t[n + 1];
+  if (total) IE_HIP(hipMemcpyAsync(b->bytes, o.bytes, total, hipMemcpyDeviceToHost, x->stream));
+  IE_HIP(hipMemcpyAsync(b->offsets, o.offsets, (n + 1) * 8, hipMemcpyDeviceToHost, x->stream));
+  if (n) IE_HIP(hipMemcpyAsync(b->status, o.status, n, hipMemcpyDeviceToHost, x->stream));
+  if (n) IE_HIP(hipMemcpyAsync(b->value_id, o.value_id, n * 4, hipMemcpyDeviceToHost, x->stream));
+  IE_HIP(hipStreamSynchronize(x->stream));
+  for (uint64_t i = 0; i < n; i++)
+    if (b->status[i] != IE_OK_VALUE) b->value_id[i] = IE_VID_NONE;
+
+  // literal-path strings that ran out of scratch: re-run them alone with the full working space
+  if (op == kOpInterp) {
+    std::vector<uint64_t> redo;
+    for (uint64_t i = 0; i < n; i++)
+      if (b->status[i] == IE_E_OVERFLOW) redo.push_back(i);
+    if (!redo.empty() && !x->lit_cap_max) {
+      std::vector<uint8_t> rb;
+      std::vector<uint64_t> ro(1, 0);
+      uint64_t need = 0;
+      for (uint64_t i : redo) {
+        const uint64_t len = offsets[i + 1] - offsets[i];
+        rb.insert(rb.end(), bytes + offsets[i], bytes + offsets[i + 1]);
+        ro.push_back(rb.size());
+        need += 4 * (IE_SIZE_CAP(len, t->dev.maxtext) + 4 * t->dev.maxtext + 80);
+      }
+      const uint64_t saved_pool = x->pool_request;
+      x->lit_cap_max = 1;
+      x->pool_request = std::max<uint64_t>(need + (1 << 20), saved_pool);
+      ie_batch* sub = nullptr;
+      rc = run_host(x, op, t, rb.data(), ro.data(), redo.size(), &sub);
+      x->lit_cap_max = 0;
+      x->pool_request = saved_pool;
+      if (rc) {
+        ie_batch_free(b);
+        return rc;
+      }
+      // splice the re-run results back in
+      std::vector<uint8_t> nb;
+      std::vector<uint64_t> noff(n + 1, 0);
+      nb.reserve(total + sub->bytes_len);
+      size_t r = 0;
+      for (uint64_t i = 0; i < n; i++) {
+        noff[i] = nb.size();
+        if (r < redo.size() && redo[r] == i) {
+          b->status[i] = sub->status[r];
+          b->value_id[i] = sub->value_id[r];
+          nb.insert(nb.end(), sub->bytes + sub->offsets[r], sub->bytes + sub->offsets[r + 1]);
+          r++;
+        } else {
+          nb.insert(nb.end(), b->bytes + b->offsets[i], b->bytes + b->offsets[i + 1]);
+        }
+      }
+      noff[n] = nb.size();
+      ie_batch_free(sub);
+      delete[] b->bytes;
+      b->bytes = new uint8_t[nb.size() + 1];
+      if (!nb.empty()) memcpy(b->bytes, nb.data(), nb.size());
+      b->bytes_len = nb.size();
+      memcpy(b->offsets, noff.data(), (n + 1) * 8);
+    }
+  }
+  *outp = b;
+  return IE_SUCCESS;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t ie_abi_version(void) { return IE_ABI_VERSION; }
+const char* ie_last_error(void) { return g_err.c_str(); }
+int32_t ie_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int ie_table_build(const ie_kv* kv, uint64_t n, int32_t dialect, const ie_clock* now,
+                   uint32_t flags, int32_t device, ie_table** out) {
+  if (!out || (n && !kv)) return fail(IE_ERR_INVALID, "null argument");
+  if (dialect != IE_DIALECT_PY && dialect != IE_DIALECT_RS) return fail(IE_ERR_INVALID, "bad dialect");
+  int rc = set_device(device);
+  if (rc) return rc;
+  // dict semantics: the last duplicate wins; '' is never looked up (py:446 / interp.rs:105)
+  std::unordered_map<std::string_view, uint64_t> last;
+  last.reserve(n * 2 + 4);
+  std::vector<uint64_t> order;
+  for (uint64_t i = 0; i < n; i++) {
+    std::string_view k(kv[i].key ? kv[i].key : "", kv[i].key_len);
+    if (k.empty()) continue;
+    auto it = last.find(k);
+    if (it == last.end()) {
+      last.emplace(k, i);
+      order.push_back(i);
+    } else {
+      it->second = i;
+    }
+  }
+  char hhmm[16], hhmmss[16];
+  const int h = now ? now->hour : 0, mi = now ? now->minute : 0, se = now ? now->second : 0;
+  snprintf(hhmm, sizeof hhmm, "%02d:%02d", h, mi);
+  snprintf(hhmmss, sizeof hhmmss, "%02d:%02d:%02d", h, mi, se);
+
+  std::vector<DevEntry> ents;
+  std::vector<uint8_t> arena;
+  ents.reserve(order.size() + 2);
+  uint64_t maxtext = 8;
+  auto add = [&](std::string_view k, std::string_view t, int32_t kind, uint32_t vid) {
+    DevEntry e{};
+    e.hash = poly_hash(k);
+    e.key_off = (uint32_t)arena.size();
+    e.key_len = (uint32_t)k.size();
+    arena.insert(arena.end(), k.begin(), k.end());
+    e.text_off = (uint32_t)arena.size();
+    e.text_len = (uint32_t)t.size();
+    arena.insert(arena.end(), t.begin(), t.end());
+    e.vid = vid;
+    e.flags = kind_flags(kind, dialect) | text_flags(t);
+    maxtext = std::max<uint64_t>(maxtext, t.size());
+    ents.push_back(e);
+  };
+  for (uint64_t i : order) {
+    std::string_view k(kv[i].key, kv[i].key_len);
+    uint64_t j = last[k];
+    if (k == "HH:MM" || k == "HH:MM:SS") continue;  // py:433-436: the clock always wins
+    if (kv[j].kind < 0 || kv[j].kind > IE_KIND_DICT) return fail(IE_ERR_INVALID, "bad kind");
+    add(k, std::string_view(kv[j].text ? kv[j].text : "", kv[j].text_len), kv[j].kind, (uint32_t)j);
+  }
+  add("HH:MM", hhmm, IE_KIND_STR, IE_VID_CLOCK_HHMM);
+  add("HH:MM:SS", hhmmss, IE_KIND_STR, IE_VID_CLOCK_HHMMSS);
+  if (arena.size() >= 0xFFFFFFF0ull) return fail(IE_ERR_INVALID, "table arena above 4 GiB");
+
+  uint64_t cap = 16;
+  while (cap < 2 * ents.size()) cap *= 2;
+  std::vector<uint32_t> slots(cap, 0);
+  for (size_t e = 0; e < ents.size(); e++) {
+    uint32_t s = slot_of(ents[e].hash, ents[e].key_len, (uint32_t)(cap - 1));
+    while (slots[s]) s = (s + 1) & (uint32_t)(cap - 1);
+    slots[s] = (uint32_t)(e + 1);
+  }
+  ie_table* t = new ie_table();
+  t->device = device;
+  t->dialect = dialect;
+  t->flags = flags;
+  t->n_entries = ents.size();
+  auto up = [&](DevBuf& b, const void* src, uint64_t bytes) -> hipError_t {
+    hipError_t e = b.ensure(bytes + 16);
+    if (e != hipSuccess) return e;
+    return bytes ? hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice) : hipSuccess;
+  };
+  hipError_t e1 = up(t->slots, slots.data(), slots.size() * 4);
+  hipError_t e2 = e1 == hipSuccess ? up(t->entries, ents.data(), ents.size() * sizeof(DevEntry)) : e1;
+  hipError_t e3 = e2 == hipSuccess ? up(t->arena, arena.data(), arena.size()) : e2;
+  if (e3 != hipSuccess) {
+    delete t;
+    return fail(IE_ERR_HIP, std::string("table upload: ") + hipGetErrorString(e3));
+  }
+  t->dev.slots = (const uint32_t*)t->slots.p;
+  t->dev.entries = (const DevEntry*)t->entries.p;
+  t->dev.arena = (const uint8_t*)t->arena.p;
+  t->dev.mask = (uint32_t)(cap - 1);
+  t->dev.n_entries = (uint32_t)ents.size();
+  t->dev.dialect = (uint32_t)dialect;
+  t->dev.flags = (flags & IE_TABLE_HAS_INSERTS_DIR) ? TF_HAS_DIR : 0u;
+  t->dev.maxtext = maxtext;
+  *out = t;
+  return IE_SUCCESS;
+}
+
+void ie_table_free(ie_table* t) {
+  if (t) {
+    (void)hipSetDevice(t->device);
+    delete t;
+  }
+}
+uint64_t ie_table_entries(const ie_table* t) { return t ? t->n_entries : 0; }
+int32_t ie_table_dialect(const ie_table* t) { return t ? t->dialect : -1; }
+
+int ie_exec_create(int32_t device, void* hip_stream, ie_exec** out) {
+  if (!out) return fail(IE_ERR_INVALID, "null argument");
+  int rc = set_device(device);
+  if (rc) return rc;
+  ie_exec* x = new ie_exec();
+  x->device = device;
+  if (hip_stream) {
+    x->stream = (hipStream_t)hip_stream;
+  } else {
+    hipError_t e = hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      delete x;
+      return fail(IE_ERR_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+    }
+    x->own_stream = true;
+  }
+  for (auto& e : x->ev) {
+    hipError_t r = hipEventCreate(&e);
+    if (r != hipSuccess) {
+      delete x;
+      return fail(IE_ERR_HIP, std::string("hipEventCreate: ") + hipGetErrorString(r));
+    }
+  }
+  *out = x;
+  return IE_SUCCESS;
+}
+
+void ie_exec_destroy(ie_exec* x) {
+  if (x) {
+    (void)hipSetDevice(x->device);
+    if (x->stream) (void)hipStreamSynchronize(x->stream);
+    delete x;
+  }
+}
+
+int ie_exec_sync(ie_exec* x) {
+  if (!x) return fail(IE_ERR_INVALID, "null exec");
+  IE_HIP(hipStreamSynchronize(x->stream));
+  return IE_SUCCESS;
+}
+
+int ie_exec_set_timing(ie_exec* x, int32_t enabled) {
+  if (!x) return fail(IE_ERR_INVALID, "null exec");
+  x->timing = enabled != 0;
+  x->ev_recorded = false;
+  return IE_SUCCESS;
+}
+
+int ie_exec_timing(ie_exec* x, ie_timing* out) {
+  if (!x || !out) return fail(IE_ERR_INVALID, "null argument");
+  memset(out, 0, sizeof *out);
+  if (!x->ev_recorded) return fail(IE_ERR_INVALID, "no timed call recorded");
+  IE_HIP(hipStreamSynchronize(x->stream));
+  float a = 0, b = 0, c = 0;
+  IE_HIP(hipEventElapsedTime(&a, x->ev[0], x->ev[1]));
+  IE_HIP(hipEventElapsedTime(&b, x->ev[1], x->ev[2]));
+  IE_HIP(hipEventElapsedTime(&c, x->ev[0], x->ev[3]));
+  out->resolve_ms = c - b;  // measure + scan + emit
+  out->complex_ms = b;
+  out->total_ms = c;
+  uint32_t cnt = 0;
+  if (x->counters.p) IE_HIP(hipMemcpy(&cnt, x->counters.p, 4, hipMemcpyDeviceToHost));
+  out->n_complex = cnt;
+  (void)a;
+  return IE_SUCCESS;
+}
+
+int ie_exec_set_scratch(ie_exec* x, uint64_t bytes) {
+  if (!x) return fail(IE_ERR_INVALID, "null exec");
+  x->pool_request = std::max<uint64_t>(bytes, 1 << 20);
+  return IE_SUCCESS;
+}
+
+int ie_interpolate_device(ie_exec* x, const ie_table* t, const uint8_t* d_bytes,
+                          const uint64_t* d_offsets, uint64_t n, const ie_dev_out* out) {
+  return run_device(x, kOpInterp, t, d_bytes, d_offsets, n, out);
+}
+
+int ie_interpolate_batch(ie_exec* x, const ie_table* t, const uint8_t* bytes,
+                         const uint64_t* offsets, uint64_t n, ie_batch** out) {
+  if (!t) return fail(IE_ERR_INVALID, "null table");
+  return run_host(x, kOpInterp, t, bytes, offsets, n, out);
+}
+
+int ie_interpolate(ie_exec* x, const ie_table* t, const char* s, uint64_t len, ie_batch** out) {
+  uint64_t off[2] = {0, len};
+  return ie_interpolate_batch(x, t, (const uint8_t*)s, off, 1, out);
+}
+
+int ie_unescape_device(ie_exec* x, const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t n,
+                       const ie_dev_out* out) {
+  return run_device(x, kOpUnescape, nullptr, d_bytes, d_offsets, n, out);
+}
+int ie_escape_device(ie_exec* x, const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t n,
+                     const ie_dev_out* out) {
+  return run_device(x, kOpEscape, nullptr, d_bytes, d_offsets, n, out);
+}
+int ie_unescape_batch(ie_exec* x, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                      ie_batch** out) {
+  return run_host(x, kOpUnescape, nullptr, bytes, offsets, n, out);
+}
+int ie_escape_batch(ie_exec* x, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                    ie_batch** out) {
+  return run_host(x, kOpEscape, nullptr, bytes, offsets, n, out);
+}
+
+void ie_batch_free(ie_batch* b) {
+  if (!b) return;
+  delete[] b->bytes;
+  delete[] b->offsets;
+  delete[] b->status;
+  delete[] b->value_id;
+  delete b;
+}
+
+int ie_simple_insertkey(const char* s, uint64_t len, int32_t dialect, uint64_t* key_off,
+                        uint64_t* key_len) {
+  // py:477-495 / interp.rs:11-29 on the caller's string (callers pass protected text when they
+  // mirror interpolate_inserts; recursive_interpolate passes the raw string, py:1463)
+  if (key_off) *key_off = 0;
+  if (key_len) *key_len = 0;
+  if (!s && len) return 0;
+  const uint8_t* p = (const uint8_t*)s;
+  if (dialect == IE_DIALECT_RS) {
+    if (len < 2 || p[0] != '{' || p[len - 1] != '}') return 0;
+  } else if (len < 3 || p[0] != '{' || p[len - 1] != '}') {
+    return 0;
+  }
+  int64_t depth = 0;
+  for (uint64_t k = 0; k < len; k++) {
+    if (p[k] == '}') depth--;
+    if ((depth == 0) != (k == 0 || k == len - 1)) return 0;
+    if (p[k] == '{') depth++;
+  }
+  if (key_off) *key_off = 1;
+  if (key_len) *key_len = len - 2;
+  return 1;
+}
+
+// ---- synthetic workloads ----
+int ie_synth_create(int32_t config, uint64_t seed, ie_synth** out) {
+  if (!out) return fail(IE_ERR_INVALID, "null argument");
+  if (config != 2 && config != 3) return fail(IE_ERR_INVALID, "synthetic config must be 2 or 3");
+  ie_synth* s = new ie_synth();
+  s->P.config = config;
+  s->P.seed = seed ? seed : (0x1E5EED00ull + (uint64_t)config);
+  s->P.n_keys = 1000;
+  s->P.n_q = 99000;
+  s->P.n_i = 1000;
+  uint64_t st = s->P.seed ^ 0xA5A5A5A5DEADBEEFull;
+  auto filler_value = [&]() {
+    uint32_t len = 4 + (uint32_t)(splitmix(st) % 21);
+    std::string v(len, '\0');
+    synth_filler(st, (uint8_t*)&v[0], len);
+    return v;
+  };
+  if (config == 2) {
+    for (uint32_t j = 0; j < s->P.n_keys; j++) {
+      s->keys.push_back("k" + std::to_string(j));
+      s->texts.push_back(filler_value());
+    }
+  } else {
+    for (uint32_t j = 0; j < s->P.n_q; j++) {
+      s->keys.push_back("q-" + std::to_string(j));
+      s->texts.push_back(filler_value());
+    }
+    for (uint32_t j = 0; j < s->P.n_i; j++) {
+      s->keys.push_back("i" + std::to_string(j));
+      s->texts.push_back(std::to_string(splitmix(st) % s->P.n_q));  // int value, str(int) splice
+    }
+  }
+  s->kv.resize(s->keys.size());
+  for (size_t j = 0; j < s->keys.size(); j++) {
+    const bool is_int = config == 3 && j >= s->P.n_q;
+    s->kv[j] = ie_kv{s->keys[j].data(), s->keys[j].size(), s->texts[j].data(), s->texts[j].size(),
+                     is_int ? IE_KIND_INT : IE_KIND_STR, 0};
+  }
+  *out = s;
+  return IE_SUCCESS;
+}
+
+void ie_synth_free(ie_synth* s) { delete s; }
+
+uint64_t ie_synth_kv(const ie_synth* s, const ie_kv** kv) {
+  if (!s) return 0;
+  if (kv) *kv = s->kv.data();
+  return s->kv.size();
+}
+
+int ie_synth_strings_host(const ie_synth* s, uint64_t first, uint64_t n, uint8_t* bytes,
+                          uint64_t bytes_cap, uint64_t* offsets, uint64_t* total) {
+  if (!s || !offsets) return fail(IE_ERR_INVALID, "null argument");
+  uint64_t w = 0;
+  for (uint64_t k = 0; k < n; k++) {
+    offsets[k] = w;
+    w += synth_len(s->P, first + k);
+  }
+  offsets[n] = w;
+  if (total) *total = w;
+  if (bytes) {
+    if (w > bytes_cap) return fail(IE_ERR_CAPACITY, "synthetic bytes exceed capacity");
+    for (uint64_t k = 0; k < n; k++) synth_string(s->P, first + k, bytes + offsets[k]);
+  }
+  return IE_SUCCESS;
+}
+
+int ie_synth_strings_device(ie_exec* x, const ie_synth* s, uint64_t first, uint64_t n,
+                            uint8_t* d_bytes, uint64_t bytes_cap, uint64_t* d_offsets,
+                            uint64_t* total) {
+  if (!x || !s || !d_offsets) return fail(IE_ERR_INVALID, "null argument");
+  int rc = set_device(x->device);
+  if (rc) return rc;
+  IE_HIP(x->s_lens.ensure((n + 1) * 8));
+  IE_HIP(x->s_part.ensure(((n / (kBlock * 16)) + 2) * 8 + 64));
+  uint64_t* d_total = (uint64_t*)((char*)x->s_part.p + x->s_part.bytes - 64);
+  IE_HIP(launch_synth(s->P, first, n, (uint64_t*)x->s_lens.p, (uint64_t*)x->s_part.p, d_offsets,
+                      d_total, nullptr, x->stream));
+  uint64_t tot = 0;
+  IE_HIP(hipMemcpyAsync(&tot, d_total, 8, hipMemcpyDeviceToHost, x->stream));
+  IE_HIP(hipStreamSynchronize(x->stream));
+  if (total) *total = tot;
+  if (d_bytes) {
+    if (tot > bytes_cap) return fail(IE_ERR_CAPACITY, "synthetic bytes exceed capacity");
+    IE_HIP(launch_synth(s->P, first, n, nullptr, nullptr, d_offsets, nullptr, d_bytes, x->stream));
+    IE_HIP(hipStreamSynchronize(x->stream));
+  }
+  return IE_SUCCESS;
+}
+
+}  // extern "C"

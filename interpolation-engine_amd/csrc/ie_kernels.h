@@ -1,0 +1,50 @@
+// ie_kernels.h — launch interface between the host library (ie_host.cpp) and the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ie_common.h"
+
+namespace ie {
+
+constexpr int kBlock = 256;          // lanes per workgroup = strings per tile
+constexpr int kMaxDepth = 6;         // fast-path nesting limit (deeper: literal path)
+constexpr int kKeyCap = 48;          // fast-path key bytes per lane (longer keys: literal path)
+constexpr int kTileBytes = 24576;    // LDS input stage; larger tiles read global memory directly
+constexpr int kStageBytes = 24576;   // LDS output stage; larger tiles store directly
+
+enum { kOpInterp = 0, kOpUnescape = 1, kOpEscape = 2 };
+
+struct Batch {
+  const uint8_t* bytes;     // input payload
+  const uint64_t* in_off;   // n + 1 input offsets
+  uint64_t n;
+  uint64_t* out_off;        // n + 1 output offsets
+  uint8_t* status;          // n
+  uint32_t* value_id;       // n
+};
+
+struct Work {
+  uint32_t* out_len;    // n   output length per string
+  uint64_t* tile_sum;   // tiles
+  uint64_t* tile_base;  // tiles
+  uint32_t* cx_count;   // 1   strings queued for the literal kernel
+  uint32_t* cx_list;    // n
+  uint8_t* cx_status;   // n   final status of queued strings
+  uint64_t* res_off;    // n   pool offset of a queued string's result
+  uint8_t* pool;        // literal-kernel scratch
+  uint64_t* pool_used;  // 1
+  uint64_t pool_bytes;
+  uint32_t lit_cap_max; // 1: give every queued string the full IE_SIZE_CAP working space
+};
+
+hipError_t launch_measure(int op, const Batch& B, const Work& W, const DevTable& T, hipStream_t st);
+hipError_t launch_literal(const Batch& B, const Work& W, const DevTable& T, hipStream_t st);
+hipError_t launch_scan_tiles(const Batch& B, const Work& W, uint64_t* total, hipStream_t st);
+hipError_t launch_emit(int op, const Batch& B, const Work& W, const DevTable& T, uint8_t* out,
+                       uint64_t cap, const uint64_t* total, hipStream_t st);
+hipError_t launch_synth(const SynthParams& P, uint64_t first, uint64_t n, uint64_t* d_lens,
+                        uint64_t* d_part, uint64_t* d_offsets, uint64_t* d_total, uint8_t* d_bytes,
+                        hipStream_t st);
+
+}  // namespace ie

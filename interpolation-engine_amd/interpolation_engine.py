@@ -1,0 +1,374 @@
+"""Drop-in mirror of the reference's interpolation surface, resolved by the HIP kernels.
+
+Same names, argument meaning and error behaviour as src/interpolation_engine/interpolation_engine.py:
+  InterpolationException           py:426-428
+  get_interpdata(inserts, key)     py:430-467
+  get_simple_insertkey(content)    py:477-495
+  interpolate_inserts(inserts, s)  py:497-541   -> one string through libie_amd (a batch of one)
+  recursive_unescape / _escape     py:1436-1460 -> every string leaf in ONE device batch
+  recursive_interpolate(inserts,x) py:1462-1494 -> every string leaf in ONE device batch
+plus the batch entry the GPU is for:
+  interpolate_batch(inserts, strings) -> list of results (str / typed value / exception instance)
+
+Errors map from the per-string device status: E_INTERP -> InterpolationException,
+E_ASSERT_* -> AssertionError, E_UNHASHABLE -> TypeError (py:450 `in` on an unhashable key).
+The reference loops forever on self-referential inserts; here such strings stop at the
+IE_ITER_CAP / IE_SIZE_CAP caps (include/ie_amd.h) and raise RecursionError.
+
+`get_interpdata` and `get_simple_insertkey` are the two scalar helpers the reference's callers
+use for control flow (recursive_interpolate's for/serial branch, validate_program); they are
+host glue with the reference's exact semantics. Every string interpolation, escape and
+unescape runs on the device; without libie_amd.so or a GPU the calls raise.
+"""
+import copy
+import ctypes
+import datetime as _dt
+import json
+
+from . import _native as N
+
+insert_start = "{"
+insert_stop = "}"
+escape = "\\"
+inserts_dir = None  # py:44 — a set inserts directory makes missing keys NEEDS_HOST (not supported)
+
+
+class InterpolationException(Exception):
+    # Caught in goto_map to trigger the 'NULL' key (py:426-428).
+    pass
+
+
+# ------------------------------------------------------------------------------------------
+# value rendering (the splice text of py:531 / interp.rs:71-80, value_to_string interp.rs:314)
+# ------------------------------------------------------------------------------------------
+_KIND = {str: N.KIND_STR, int: N.KIND_INT, list: N.KIND_LIST, float: N.KIND_FLOAT,
+         bool: N.KIND_BOOL, type(None): N.KIND_NULL, dict: N.KIND_DICT}
+
+
+def _rs_float(f):
+    s = repr(float(f))
+    if "e" in s:
+        m, e = s.split("e")
+        s = "%se%d" % (m, int(e))
+    return s
+
+
+def _rs_value_to_string(v):
+    if isinstance(v, str):
+        return v
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    if isinstance(v, int):
+        return str(v)
+    if isinstance(v, float):
+        return _rs_float(v)
+    if isinstance(v, list):
+        return "".join(_rs_value_to_string(x) for x in v)
+    return json.dumps(v, separators=(",", ":"), sort_keys=True, ensure_ascii=False)
+
+
+def render(v, dialect="py"):
+    kind = _KIND.get(type(v))
+    if kind is None:
+        raise TypeError("insert values must be JSON types, got %r" % type(v))
+    return kind, (str(v) if dialect == "py" else _rs_value_to_string(v))
+
+
+# ------------------------------------------------------------------------------------------
+# device context
+# ------------------------------------------------------------------------------------------
+_execs = {}
+
+
+def get_exec(device=0):
+    x = _execs.get(device)
+    if x is None:
+        x = _execs[device] = N.Exec(device)
+    return x
+
+
+class InsertsTable:
+    """An immutable device snapshot of an inserts dict (get_interpdata's view of it)."""
+
+    def __init__(self, inserts, dialect="py", clock=None, device=0, has_inserts_dir=False):
+        if clock is None:
+            now = _dt.datetime.now()
+            clock = (now.hour, now.minute, now.second)
+        self.clock = tuple(clock)
+        self.dialect = dialect
+        self.device = device
+        self.keys = list(inserts.keys())
+        self.values = list(inserts.values())
+        n = len(self.keys)
+        arr = (N.KV * max(1, n))()
+        keep = []
+        for i, k in enumerate(self.keys):
+            if not isinstance(k, str):
+                raise TypeError("insert keys must be str")
+            kind, text = render(self.values[i], dialect)
+            kb, tb = N.enc(k), N.enc(text)
+            keep += [kb, tb]
+            arr[i] = N.KV(kb, len(kb), tb, len(tb), kind, 0)
+        h = ctypes.c_void_p()
+        clk = N.Clock(*self.clock)
+        N.check(N.lib().ie_table_build(ctypes.cast(arr, ctypes.c_void_p), n, N.IE_DIALECT[dialect],
+                                       ctypes.byref(clk), N.TABLE_HAS_INSERTS_DIR if has_inserts_dir else 0,
+                                       device, ctypes.byref(h)), "ie_table_build")
+        self.h = h
+        self._snapshot = (dict(inserts), {k: text for k, text in
+                                          ((k, render(v, dialect)[1]) for k, v in inserts.items()
+                                           if isinstance(v, (list, dict)))})
+
+    def close(self):
+        if getattr(self, "h", None):
+            N.lib().ie_table_free(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def matches(self, inserts, clock):
+        snap, mutable = self._snapshot
+        if clock != self.clock or len(inserts) != len(snap):
+            return False
+        for k, v in inserts.items():
+            if k not in snap or snap[k] is not v:
+                return False
+        for k, text in mutable.items():  # lists/dicts may have been mutated in place
+            if render(inserts[k], self.dialect)[1] != text:
+                return False
+        return True
+
+    def value(self, vid):
+        if vid == N.VID_HHMM:
+            return "%02d:%02d" % self.clock[:2]
+        if vid == N.VID_HHMMSS:
+            return "%02d:%02d:%02d" % self.clock
+        return self.values[vid]
+
+    # --------------------------------------------------------------------------------------
+    def run(self, strings):
+        """Resolve a list of str on the device -> list of (status, payload)."""
+        blob, offs = N.pack(strings)
+        x = get_exec(self.device)
+        res = ctypes.POINTER(N.BatchRes)()
+        bp = ctypes.c_char_p(blob)
+        N.check(N.lib().ie_interpolate_batch(x.h, self.h, ctypes.cast(bp, ctypes.c_void_p),
+                                             offs.ctypes.data, len(strings), ctypes.byref(res)),
+                "ie_interpolate_batch")
+        outs, sts, vids = N.batch_to_python(res)
+        return [(st, N.dec(o) if st == N.OK_STR else (vids[i] if st == N.OK_VALUE else None))
+                for i, (o, st) in enumerate(zip(outs, sts))]
+
+    def results(self, strings):
+        """Like interpolate_inserts on each string; failures come back as exception instances."""
+        out = []
+        for s, (st, payload) in zip(strings, self.run(strings)):
+            out.append(self._result(s, st, payload))
+        return out
+
+    def _result(self, s, st, payload):
+        if st == N.OK_STR:
+            return payload
+        if st == N.OK_VALUE:
+            return self.value(payload)
+        return _exception(s, st, self.keys)
+
+
+def _exception(s, st, keys):
+    if st == N.E_INTERP:
+        return InterpolationException(
+            "Could not resolve an interpolation in %r. Available interpolation data keys are %r." % (s, keys))
+    if st == N.E_ASSERT_BRACES:
+        return AssertionError("Error: The following content has an uneven number of '{' and '}':\n\n\"\"\"%s\n\"\"\"" % s)
+    if st == N.E_ASSERT_TYPE:
+        return AssertionError("Error: trying to interpolate a variable of a type other than str, int or list into %r." % s)
+    if st == N.E_UNHASHABLE:
+        return TypeError("unhashable type used as an interpolation key in %r" % s)
+    if st == N.E_RS_PANIC:
+        return RuntimeError("rust dialect: unwrap() on a '}{' leftover in %r" % s)
+    if st == N.DIVERGED:
+        return RecursionError("interpolation of %r does not terminate (self-referential inserts)" % s)
+    if st == N.NEEDS_HOST:
+        return NotImplementedError("key lookup needs the inserts directory (not supported on the device path)")
+    return RuntimeError("device status %s for %r" % (N.STATUS_NAMES[st] if st < len(N.STATUS_NAMES) else st, s))
+
+
+_cache = {}
+
+
+def table_for(inserts, dialect="py", device=0):
+    """The device table for this dict, rebuilt only when the dict or the clock changed."""
+    now = _dt.datetime.now()
+    clock = (now.hour, now.minute, now.second)
+    key = (id(inserts), dialect, device)
+    t = _cache.get(key)
+    if t is None or not t.matches(inserts, clock):
+        t = InsertsTable(inserts, dialect=dialect, clock=clock, device=device,
+                         has_inserts_dir=bool(inserts_dir))
+        _cache[key] = t
+    return t
+
+
+# ------------------------------------------------------------------------------------------
+# the reference surface
+# ------------------------------------------------------------------------------------------
+def get_interpdata(inserts, insertkey):
+    """py:430-467 (host glue for callers' control flow; the device path has it in-kernel)."""
+    if insertkey == "HH:MM":
+        return _dt.datetime.now().strftime("%H:%M")
+    if insertkey == "HH:MM:SS":
+        return _dt.datetime.now().strftime("%H:%M:%S")
+    if isinstance(insertkey, str) and insertkey.startswith("ARG") and insertkey[3:].isdigit():
+        if insertkey not in inserts:
+            raise InterpolationException(
+                "Argument interpolation key '%s' is used, but the user passed less than %s program arguments."
+                % (insertkey, insertkey[3:]))
+        return inserts[insertkey]
+    if insertkey == "":
+        raise InterpolationException("Tried to interpolate empty string ''.")
+    if insertkey in inserts:
+        return inserts[insertkey]
+    raise InterpolationException("Could not find variable '%s' in interpdata. Available interpolation data keys are %r."
+                                 % (insertkey, list(inserts.keys())))
+
+
+def get_simple_insertkey(content):
+    """py:477-495: the key of a whole-string '{...}', '' / None otherwise (same falsy values)."""
+    if type(content) != str:
+        return None
+    if len(content) <= 2:  # the reference's loop, for the tiny cases ('' vs None)
+        depth = 0
+        for i, c in enumerate(content):
+            if c == insert_stop:
+                depth -= 1
+            if (depth == 0) != (i == 0 or i == len(content) - 1):
+                return None
+            if c == insert_start:
+                depth += 1
+        return content[1:-1]
+    b = N.enc(content)
+    o, l = ctypes.c_uint64(), ctypes.c_uint64()
+    if N.lib().ie_simple_insertkey(b, len(b), 0, ctypes.byref(o), ctypes.byref(l)):
+        return content[1:-1]
+    return None
+
+
+def interpolate_batch(inserts, contents, dialect="py", device=0):
+    """Resolve many strings against one inserts snapshot; failures are returned, not raised."""
+    return table_for(inserts, dialect, device).results(list(contents))
+
+
+def interpolate_inserts(inserts, content):
+    """py:497-541 — the drop-in. Raises exactly where the reference raises."""
+    r = table_for(inserts).results([content])[0]
+    if isinstance(r, BaseException):
+        raise r
+    return r
+
+
+def _escape_strings(strings, unescape):
+    if not strings:
+        return []
+    blob, offs = N.pack(strings)
+    x = get_exec(0)
+    res = ctypes.POINTER(N.BatchRes)()
+    bp = ctypes.c_char_p(blob)
+    fn = N.lib().ie_unescape_batch if unescape else N.lib().ie_escape_batch
+    N.check(fn(x.h, ctypes.cast(bp, ctypes.c_void_p), offs.ctypes.data, len(strings), ctypes.byref(res)),
+            "ie_(un)escape_batch")
+    outs, _, _ = N.batch_to_python(res)
+    return [N.dec(o) for o in outs]
+
+
+def _map_strings(x, fn_batch):
+    """Apply a batched str->str map to every str leaf (list items, dict keys and values)."""
+    leaves = []
+
+    def collect(v):
+        if type(v) == str:
+            leaves.append(v)
+        elif type(v) == list:
+            for xx in v:
+                collect(xx)
+        elif type(v) == dict:
+            for k, vv in v.items():
+                collect(k)
+                collect(vv)
+
+    collect(x)
+    done = iter(fn_batch(leaves))
+
+    def rebuild(v):
+        if type(v) == str:
+            return next(done)
+        if type(v) == list:
+            return [rebuild(xx) for xx in v]
+        if type(v) == dict:
+            return {rebuild(k): rebuild(vv) for k, vv in v.items()}
+        return v
+
+    return rebuild(x)
+
+
+def recursive_unescape(x):
+    """py:1436-1447"""
+    return _map_strings(x, lambda ss: _escape_strings(ss, True))
+
+
+def recursive_escape(x):
+    """py:1449-1460"""
+    return _map_strings(x, lambda ss: _escape_strings(ss, False))
+
+
+_LOOP_CMDS = ("for", "serial", "parallel_wait", "parallel_race")
+
+
+def recursive_interpolate(inserts, x, _depth=0):
+    """py:1462-1494 with every string leaf of `x` resolved in one device batch."""
+    if _depth > 900:
+        raise RecursionError("maximum recursion depth exceeded in recursive_interpolate")
+    tbl = table_for(inserts)
+    leaves = []
+
+    def collect(v):
+        if type(v) == str:
+            leaves.append(v)
+        elif type(v) == list:
+            for xx in v:
+                collect(xx)
+        elif type(v) == dict:
+            if v.get("cmd") in ("goto_map", "replace_map") or v.get("cmd") in _LOOP_CMDS:
+                return
+            for k, vv in v.items():
+                collect(k)
+                collect(vv)
+
+    collect(x)
+    res = iter(tbl.results(leaves) if leaves else [])
+
+    def rebuild(v):
+        if type(v) == str:
+            r = next(res)
+            if isinstance(r, BaseException):
+                raise r
+            if get_simple_insertkey(v):  # py:1463-1464: re-interpolate the typed result
+                return recursive_interpolate(inserts, r, _depth + 1)
+            return r
+        if type(v) == list:
+            return [rebuild(xx) for xx in v]
+        if type(v) == dict:
+            cmd = v.get("cmd")
+            if cmd in ("goto_map", "replace_map"):  # py:1471-1477
+                return v
+            if cmd in _LOOP_CMDS:  # py:1479-1489
+                v = copy.deepcopy(v)
+                if (k := get_simple_insertkey(v["tasks"])):
+                    v["tasks"] = get_interpdata(inserts, k)
+                for i in range(len(v["tasks"])):
+                    if (k := get_simple_insertkey(v["tasks"][i])):
+                        v["tasks"][i] = get_interpdata(inserts, k)
+                return v
+            return {rebuild(k): rebuild(vv) for k, vv in v.items()}
+        return v
+
+    return rebuild(x)

@@ -304,6 +304,44 @@ def main():
             f.write(json.dumps({"s": s, "key": ie.get_simple_insertkey(s)}, ensure_ascii=False) + "\n")
         f.write(json.dumps({"s": 5, "key": ie.get_simple_insertkey(5)}) + "\n")
 
+    # recursive_interpolate over task-shaped structures (py:1462-1494)
+    rtable = {"name": "tom", "i": 3, "question-3": "Why?", "persona_name": "Ann", "t1": {"cmd": "print", "text": "{name}"},
+              "lst": ["{name}", "x{i}", 5], "a": "{b}", "b": "B", "tasks_ref": [{"cmd": "print", "text": "hi"}],
+              "n": 7, "d": {"k": "{name}"}, "esc": "\\{raw\\}"}
+    structs = [
+        {"cmd": "print", "text": "My name is {name}."},
+        {"cmd": "user_input", "prompt": "{question-{i}}", "output_name": "{persona_name}/answer-{i}"},
+        {"cmd": "serial", "tasks": ["{t1}", {"cmd": "print", "text": "{undefined_later}"}]},
+        {"cmd": "for", "tasks": "{tasks_ref}", "x": "{name}"},
+        {"cmd": "goto_map", "value": "{missing}", "map": {"a": 1}},
+        {"cmd": "replace_map", "item": "{missing}"},
+        {"cmd": "set", "item": "{lst}", "output_name": "out-{i}"},
+        {"cmd": "set", "item": "{a}", "output_name": "o"},
+        {"cmd": "set", "item": "{d}", "output_name": "o"},
+        {"cmd": "set", "item": ["{name}", ["{i}", "{n}x"], {"{name}": "{i}"}], "output_name": "o"},
+        {"cmd": "print", "text": "{esc} and \\{name\\}"},
+        {"cmd": "print", "text": "{missing}"},
+        {"cmd": "print", "text": "a{b"},
+        ["{name}", "{i}", 3, None, True, 1.5],
+        "{lst}",
+        "{i}",
+        5,
+    ]
+    with open(os.path.join(HERE, "recursive_py.jsonl"), "w", encoding="utf-8") as f:
+        f.write(json.dumps({"table": rtable}, ensure_ascii=False) + "\n")
+        for x in structs:
+            try:
+                r = ie.recursive_interpolate(rtable, x)
+                rec = {"x": x, "st": "OK", "out": r}
+            except ie.InterpolationException:
+                rec = {"x": x, "st": "E_INTERP"}
+            except AssertionError:
+                rec = {"x": x, "st": "ASSERT"}
+            f.write(json.dumps(rec, ensure_ascii=False) + "\n")
+        for x in structs:
+            f.write(json.dumps({"esc_in": x, "esc": ie.recursive_escape(x), "unesc": ie.recursive_unescape(x)},
+                               ensure_ascii=False) + "\n")
+
     from collections import Counter
     print("interp rows:", len(rows), Counter(r["st"] for r in rows))
 

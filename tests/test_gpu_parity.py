@@ -1,0 +1,375 @@
+"""Parity of the HIP path (through the C ABI of libie_amd.so) with the reference.
+
+Checkers: the reference's own golden vectors (tests/golden/, generated from the reference Python
+module) and the C oracle (oracle/ie_oracle.c, itself pinned by those vectors in
+test_oracle_golden.py). Bar: byte-identical strings, identical status class, identical typed
+value (same insert) — bit-exact, this is byte/index work.
+"""
+import ctypes
+import random
+
+import numpy as np
+import pytest
+
+import __graft_entry__ as G
+from oracle import oracle as O
+from tests.conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+G.build()
+PKG = G.load_package()
+N = PKG._native
+CLOCK = (12, 34, 56)
+VID_SPECIAL = {"@HH:MM": N.VID_HHMM, "@HH:MM:SS": N.VID_HHMMSS}
+
+
+def run_product(table_dict, strings, dialect="py", has_dir=False):
+    t = PKG.InsertsTable(table_dict, dialect=dialect, clock=CLOCK, has_inserts_dir=has_dir)
+    return t.run(strings), t
+
+
+def compare_with_oracle(table_dict, strings, dialect="py", has_dir=False):
+    got, t = run_product(table_dict, strings, dialect, has_dir)
+    ref = O.Oracle(table_dict, dialect, clock=CLOCK, has_dir=has_dir)
+    bad = []
+    for s, (st, payload) in zip(strings, got):
+        rst, rout, rvid = ref.interpolate(s)
+        name = N.STATUS_NAMES[st]
+        ok = name == rst
+        if ok and rst == "OK_STR":
+            ok = payload == rout
+        if ok and rst == "OK_VALUE":
+            ok = payload == rvid
+        if not ok:
+            bad.append((s, name, payload, rst, rout, rvid))
+    return bad
+
+
+# ------------------------------------------------------------------------------------------
+# golden vectors from the reference itself
+# ------------------------------------------------------------------------------------------
+def test_reference_golden_vectors(golden_tables, golden_interp):
+    by_table = {}
+    for row in golden_interp:
+        by_table.setdefault(row["t"], []).append(row)
+    bad = []
+    for ti, rows in by_table.items():
+        got, t = run_product(golden_tables[ti], [r["s"] for r in rows])
+        for row, (st, payload) in zip(rows, got):
+            name = N.STATUS_NAMES[st]
+            ok = name == row["st"]
+            if ok and name == "OK_STR":
+                ok = payload == row["out"]
+            if ok and name == "OK_VALUE":
+                want = {VID_SPECIAL.get(k, t.keys.index(k) if k in t.keys else -1) for k in row["vkeys"]}
+                ok = payload in want
+            if not ok:
+                bad.append((ti, row, name, payload))
+    assert not bad, "%d mismatches; first %r" % (len(bad), bad[:4])
+
+
+def test_rust_dialect_matches_restated_oracle(golden_tables, golden_interp):
+    """Rust dialect (parity unpinned: the crate cannot be built here) vs the oracle's restatement."""
+    by_table = {}
+    for row in golden_interp:
+        by_table.setdefault(row["t"], []).append(row["s"])
+    for ti, strings in by_table.items():
+        bad = compare_with_oracle(golden_tables[ti], strings, "rs")
+        assert not bad, bad[:4]
+
+
+def test_inserts_dir_statuses(golden_tables, golden_interp):
+    strings = [r["s"] for r in golden_interp if r["t"] == 0]
+    bad = compare_with_oracle(golden_tables[0], strings, "py", has_dir=True)
+    assert not bad, bad[:4]
+
+
+# ------------------------------------------------------------------------------------------
+# randomized differential tests against the oracle
+# ------------------------------------------------------------------------------------------
+def _rand_table(rng, n, brace_values):
+    t = {}
+    for j in range(n):
+        k = "k%d" % j
+        r = rng.random()
+        if r < 0.6:
+            v = "".join(rng.choice("abcxyz é€😀-.") for _ in range(rng.randint(0, 12)))
+            if brace_values and rng.random() < 0.3:
+                v += "{k%d}" % rng.randrange(n)
+            if rng.random() < 0.05:
+                v += "\\"
+            if rng.random() < 0.05:
+                v = "\\}" + v
+        elif r < 0.8:
+            v = rng.randint(-10**6, 10**6)
+        elif r < 0.9:
+            v = ["a", rng.randint(0, 9)]
+        else:
+            v = rng.choice([1.25, True, None, {"z": 1}])
+        t[k] = v
+    t["q-"] = "Q"
+    return t
+
+
+def _rand_string(rng, n_keys, long=False):
+    parts = []
+    for _ in range(rng.randint(0, 40 if long else 8)):
+        r = rng.random()
+        if r < 0.35:
+            parts.append("".join(rng.choice("abc .,é😀\n") for _ in range(rng.randint(1, 30 if long else 6))))
+        elif r < 0.7:
+            parts.append("{k%d}" % rng.randrange(n_keys + 3))
+        elif r < 0.8:
+            parts.append("{q-{k%d}}" % rng.randrange(n_keys))
+        elif r < 0.85:
+            parts.append("{" * 7 + "k1" + "}" * 7)
+        elif r < 0.9:
+            parts.append(rng.choice(["\\{", "\\}", "\\{lit\\}", "\\", ".\\}", "〠", "}", "{"]))
+        else:
+            parts.append("{k%d-" % rng.randrange(n_keys) + "x" * rng.randint(0, 60) + "}")
+    s = "".join(parts)
+    if rng.random() < 0.1:
+        s = "{" + s + "}"
+    return s
+
+
+@pytest.mark.parametrize("seed,brace_values,dialect", [(1, False, "py"), (2, True, "py"), (3, False, "rs"),
+                                                       (4, True, "rs")])
+def test_random_vs_oracle(seed, brace_values, dialect):
+    rng = random.Random(seed)
+    table = _rand_table(rng, 60, brace_values)
+    strings = [_rand_string(rng, 60) for _ in range(3000)]
+    bad = compare_with_oracle(table, strings, dialect)
+    assert not bad, bad[:4]
+
+
+def test_long_strings_and_oversized_tiles():
+    """Tiles above the LDS stage (long strings) take the global-memory path."""
+    rng = random.Random(7)
+    table = _rand_table(rng, 40, False)
+    strings = [_rand_string(rng, 40, long=True) for _ in range(700)]
+    strings += ["x" * 5000 + "{k1}" + "y" * 3000, "{k2}" * 2000, "a" * 70000]
+    bad = compare_with_oracle(table, strings)
+    assert not bad, [b[:2] for b in bad[:4]]
+
+
+@pytest.mark.parametrize("n", [0, 1, 255, 256, 257, 511, 1000])
+def test_batch_sizes(n):
+    rng = random.Random(n)
+    table = _rand_table(rng, 30, False)
+    strings = [_rand_string(rng, 30) for _ in range(n)]
+    bad = compare_with_oracle(table, strings)
+    assert not bad, bad[:4]
+
+
+def test_runaway_inserts_diverge_like_the_oracle():
+    table = {"a": "{a}", "g": "{g}{g}", "s": "x{s}", "ok": "fine"}
+    strings = ["x{a}", "x{g}", "{s}", "y{s}", "x{ok}", "{a}"]
+    bad = compare_with_oracle(table, strings)
+    assert not bad, bad
+
+
+def test_large_growth_retries_scratch():
+    """A value that expands far beyond the default literal scratch: the host API retries."""
+    table = {"big": "{w}" * 50, "w": "word-" * 40 + "{x}", "x": "X" * 100}
+    strings = ["a{big}b", "{big}", "c{w}d"]
+    bad = compare_with_oracle(table, strings)
+    assert not bad, [b[:2] for b in bad]
+
+
+# ------------------------------------------------------------------------------------------
+# the synthetic benchmark configs
+# ------------------------------------------------------------------------------------------
+def _synth(config):
+    h = ctypes.c_void_p()
+    N.check(N.lib().ie_synth_create(config, 0, ctypes.byref(h)), "ie_synth_create")
+    kvp = ctypes.POINTER(N.KV)()
+    nkv = N.lib().ie_synth_kv(h, ctypes.byref(kvp))
+    return h, kvp, nkv
+
+
+def _table_from_kv(kvp, nkv, clock=CLOCK):
+    t = ctypes.c_void_p()
+    clk = N.Clock(*clock)
+    N.check(N.lib().ie_table_build(ctypes.cast(kvp, ctypes.c_void_p), nkv, 0, ctypes.byref(clk), 0, 0,
+                                   ctypes.byref(t)), "ie_table_build")
+    return t
+
+
+def _host_strings(h, first, n):
+    offs = np.zeros(n + 1, np.uint64)
+    total = ctypes.c_uint64()
+    N.check(N.lib().ie_synth_strings_host(h, first, n, None, 0, offs.ctypes.data, ctypes.byref(total)), "len")
+    buf = np.zeros(int(total.value) + 1, np.uint8)
+    N.check(N.lib().ie_synth_strings_host(h, first, n, buf.ctypes.data, buf.size, offs.ctypes.data,
+                                          ctypes.byref(total)), "fill")
+    return buf, offs
+
+
+@pytest.mark.parametrize("config", [2, 3])
+def test_device_synth_equals_host_synth(config):
+    import torch
+    h, kvp, nkv = _synth(config)
+    x = N.Exec(0)
+    n = 100_000
+    buf, offs = _host_strings(h, 12345, n)
+    d_off = torch.zeros(n + 1, dtype=torch.uint64, device="cuda")
+    total = ctypes.c_uint64()
+    N.check(N.lib().ie_synth_strings_device(x.h, h, 12345, n, None, 0, d_off.data_ptr(), ctypes.byref(total)), "d")
+    d_bytes = torch.zeros(int(total.value) + 16, dtype=torch.uint8, device="cuda")
+    N.check(N.lib().ie_synth_strings_device(x.h, h, 12345, n, d_bytes.data_ptr(), d_bytes.numel(),
+                                            d_off.data_ptr(), ctypes.byref(total)), "d")
+    assert np.array_equal(d_off.cpu().numpy(), offs)
+    assert np.array_equal(d_bytes.cpu().numpy()[:int(total.value)], buf[:int(total.value)])
+
+
+def _device_run(x, table, d_bytes, d_off, n, cap=None):
+    import torch
+    out_bytes = torch.empty(cap if cap is not None else int(d_bytes.numel() * 2 + 4096), dtype=torch.uint8, device="cuda")
+    out_off = torch.empty(n + 1, dtype=torch.uint64, device="cuda")
+    status = torch.empty(n, dtype=torch.uint8, device="cuda")
+    vid = torch.empty(n, dtype=torch.int32, device="cuda")
+    total = torch.zeros(1, dtype=torch.uint64, device="cuda")
+    o = N.DevOut(out_bytes.data_ptr(), out_bytes.numel(), out_off.data_ptr(), status.data_ptr(),
+                 vid.data_ptr(), total.data_ptr())
+    N.check(N.lib().ie_interpolate_device(x.h, table, d_bytes.data_ptr(), d_off.data_ptr(), n, ctypes.byref(o)),
+            "ie_interpolate_device")
+    x.sync()
+    return out_bytes, out_off, status, vid, int(total.item())
+
+
+@pytest.mark.parametrize("config", [2, 3])
+def test_synthetic_config_vs_oracle(config):
+    import torch
+    h, kvp, nkv = _synth(config)
+    table = _table_from_kv(kvp, nkv)
+    x = N.Exec(0)
+    n = 200_000
+    buf, offs = _host_strings(h, 0, n)
+    d_bytes = torch.from_numpy(buf).cuda()
+    d_off = torch.from_numpy(offs).cuda()
+    ob, oo, st, vid, total = _device_run(x, table, d_bytes, d_off, n)
+    ref = O.Oracle.from_kv(ctypes.cast(kvp, ctypes.c_void_p), nkv, "py", clock=CLOCK)
+    rst = np.zeros(n, np.uint8)
+    rlen = np.zeros(n, np.uint64)
+    rhash = np.zeros(n, np.uint64)
+    ref.run_batch(buf, offs, n, 8, rst, rlen, rhash, None)
+    st = st.cpu().numpy()
+    oo = oo.cpu().numpy()
+    ob = ob.cpu().numpy()[:total].tobytes()
+    assert np.array_equal(st, rst)
+    assert np.array_equal(np.diff(oo.astype(np.int64)), rlen.astype(np.int64))
+    hashes = np.array([O.fnv1a(ob[int(oo[i]):int(oo[i + 1])]) for i in range(n)], dtype=np.uint64)
+    assert np.array_equal(hashes, rhash)
+    N.lib().ie_table_free(table)
+
+
+def test_full_size_config3_properties():
+    """Config 3 at its BASELINE size (10M strings): size-independent properties + a sampled
+    oracle check. Properties: every status OK_STR, offsets monotone with the right total, no
+    brace left in any output, idempotence (re-interpolating the outputs is the identity)."""
+    import torch
+    h, kvp, nkv = _synth(3)
+    table = _table_from_kv(kvp, nkv)
+    x = N.Exec(0)
+    n = 10_000_000
+    d_off = torch.zeros(n + 1, dtype=torch.uint64, device="cuda")
+    total = ctypes.c_uint64()
+    N.check(N.lib().ie_synth_strings_device(x.h, h, 0, n, None, 0, d_off.data_ptr(), ctypes.byref(total)), "d")
+    d_bytes = torch.zeros(int(total.value) + 16, dtype=torch.uint8, device="cuda")
+    N.check(N.lib().ie_synth_strings_device(x.h, h, 0, n, d_bytes.data_ptr(), d_bytes.numel(),
+                                            d_off.data_ptr(), ctypes.byref(total)), "d")
+    ob, oo, st, vid, tot = _device_run(x, table, d_bytes, d_off, n)
+    assert int((st != 0).sum().item()) == 0
+    lens = oo[1:].to(torch.int64) - oo[:-1].to(torch.int64)
+    assert int((lens < 0).sum().item()) == 0 and int(oo[-1].item()) == tot
+    assert int((ob[:tot] == ord("{")).sum().item()) == 0 and int((ob[:tot] == ord("}")).sum().item()) == 0
+    # idempotence: the outputs are brace-free, so resolving them again changes nothing
+    ob2, oo2, st2, _, tot2 = _device_run(x, table, ob, oo, n)
+    assert tot2 == tot and torch.equal(oo2, oo) and torch.equal(ob2[:tot], ob[:tot])
+    # sampled oracle check across the whole index range
+    rng = np.random.default_rng(0)
+    idx = np.sort(rng.choice(n, 5000, replace=False))
+    ref = O.Oracle.from_kv(ctypes.cast(kvp, ctypes.c_void_p), nkv, "py", clock=CLOCK)
+    hb, ho = _host_strings(h, 0, 1)  # warm
+    oo_h = oo.cpu().numpy()
+    for i in idx[:5000:10]:
+        b, o = _host_strings(h, int(i), 1)
+        rs, rout, _ = ref.interpolate(b[:int(o[1])].tobytes())
+        assert rs == "OK_STR"
+        got = ob[int(oo_h[i]):int(oo_h[i + 1])].cpu().numpy().tobytes().decode("utf-8")
+        assert got == rout
+    N.lib().ie_table_free(table)
+
+
+def test_device_api_capacity_contract():
+    """bytes_cap too small: offsets/status are valid, *total reports the need, bytes untouched."""
+    import torch
+    table_d = {"a": "A" * 50}
+    t = PKG.InsertsTable(table_d, clock=CLOCK)
+    x = N.Exec(0)
+    strings = ["x{a}y"] * 600
+    blob, offs = N.pack(strings)
+    d_bytes = torch.tensor(list(blob), dtype=torch.uint8, device="cuda")
+    d_off = torch.from_numpy(offs).cuda()
+    ob, oo, st, vid, total = _device_run(x, t.h, d_bytes, d_off, len(strings), cap=100)
+    assert total == 52 * 600
+    assert int(oo[-1].item()) == total and int((st != 0).sum().item()) == 0
+    ob, oo, st, vid, total = _device_run(x, t.h, d_bytes, d_off, len(strings), cap=total)
+    assert ob.cpu().numpy().tobytes() == ("x" + "A" * 50 + "y").encode() * 600
+
+
+# ------------------------------------------------------------------------------------------
+# escape / unescape (py:1436-1460)
+# ------------------------------------------------------------------------------------------
+def test_escape_unescape_golden():
+    rows = load_golden("escape_py.jsonl")
+    ss = [r["s"] for r in rows]
+    assert PKG.recursive_escape(ss) == [r["esc"] for r in rows]
+    assert PKG.recursive_unescape(ss) == [r["unesc"] for r in rows]
+
+
+def test_escape_roundtrip_property():
+    rng = random.Random(11)
+    ss = ["".join(rng.choice(["{", "}", "\\", "a", "é", "\\{", "."]) for _ in range(rng.randint(0, 300)))
+          for _ in range(5000)]
+    assert PKG.recursive_unescape(PKG.recursive_escape(ss)) == ss
+
+
+# ------------------------------------------------------------------------------------------
+# the mirror of the reference module surface
+# ------------------------------------------------------------------------------------------
+def test_mirror_surface_raises_like_the_reference():
+    ins = {"name": "tom", "i": 3, "question-3": "Why?", "L": ["x", "y"], "f": 1.5, "d": {"k": 1}}
+    assert PKG.interpolate_inserts(ins, "My name is {name}.") == "My name is tom."
+    assert PKG.interpolate_inserts(ins, "{question-{i}}") == "Why?"
+    assert PKG.interpolate_inserts(ins, "{L}") is ins["L"]
+    with pytest.raises(PKG.InterpolationException):
+        PKG.interpolate_inserts(ins, "x{nope}")
+    with pytest.raises(AssertionError):
+        PKG.interpolate_inserts(ins, "x{f}")
+    with pytest.raises(AssertionError):
+        PKG.interpolate_inserts(ins, "a{b")
+    with pytest.raises(TypeError):
+        PKG.interpolate_inserts(ins, "{{L}}")
+    ins["name"] = "ann"  # the cached device table notices the change
+    assert PKG.interpolate_inserts(ins, "{name}") == "ann"
+    ins["L"].append("z")
+    assert PKG.interpolate_inserts(ins, "x{L}") == "x['x', 'y', 'z']"
+
+
+def test_recursive_interpolate_golden():
+    rows = load_golden("recursive_py.jsonl")
+    table = rows[0]["table"]
+    for row in rows[1:]:
+        if "x" in row:
+            if row["st"] == "OK":
+                assert PKG.recursive_interpolate(table, row["x"]) == row["out"], row
+            else:
+                exc = PKG.InterpolationException if row["st"] == "E_INTERP" else AssertionError
+                with pytest.raises(exc):
+                    PKG.recursive_interpolate(table, row["x"])
+        else:
+            assert PKG.recursive_escape(row["esc_in"]) == row["esc"]
+            assert PKG.recursive_unescape(row["esc_in"]) == row["unesc"]
