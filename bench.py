@@ -48,85 +48,84 @@ def parse():
 
 def main():
     args = parse()
-    import torch
-    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        # control plane only (barrier + max-over-ranks timing): the string shards are independent
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
 
     import __graft_entry__ as G
     G.build()
     pkg = G.load_package()
     N = pkg._native
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.cuda.current_device()
-    stream = torch.cuda.current_stream()
+    L = N.lib()
+    dev = local
 
     cfg = args.config
     n = args.n or DEFAULT_N[cfg]
     first = rank * n  # this rank's shard of the global string index space
 
-    L = N.lib()
     synth = ctypes.c_void_p()
     N.check(L.ie_synth_create(cfg, 0, ctypes.byref(synth)), "ie_synth_create")
     kvp = ctypes.POINTER(N.KV)()
     nkv = L.ie_synth_kv(synth, ctypes.byref(kvp))
-    x = N.Exec(dev, stream.cuda_stream)
+    x = N.Exec(dev)
     table = ctypes.c_void_p()
     clk = N.Clock(*CLOCK)
     N.check(L.ie_table_build(ctypes.cast(kvp, ctypes.c_void_p), nkv, 0, ctypes.byref(clk), 0, dev,
                              ctypes.byref(table)), "ie_table_build")
 
     # inputs generated straight into HBM (counter-based splitmix64: rank r owns strings [r*n, (r+1)*n))
-    d_off = torch.zeros(n + 1, dtype=torch.uint64, device="cuda")
+    d_off = N.DeviceBuffer(x, (n + 1) * 8)
     tot = ctypes.c_uint64()
-    N.check(L.ie_synth_strings_device(x.h, synth, first, n, None, 0, d_off.data_ptr(), ctypes.byref(tot)), "synth")
+    N.check(L.ie_synth_strings_device(x.h, synth, first, n, None, 0, d_off.ptr, ctypes.byref(tot)), "synth")
     in_bytes = int(tot.value)
-    d_in = torch.empty(in_bytes + 16, dtype=torch.uint8, device="cuda")
-    N.check(L.ie_synth_strings_device(x.h, synth, first, n, d_in.data_ptr(), d_in.numel(), d_off.data_ptr(),
-                                      ctypes.byref(tot)), "synth")
+    d_in = N.DeviceBuffer(x, in_bytes + 16)
+    N.check(L.ie_synth_strings_device(x.h, synth, first, n, d_in.ptr, d_in.nbytes, d_off.ptr, ctypes.byref(tot)),
+            "synth")
     out_cap = 2 * in_bytes + (1 << 20)
-    d_out = torch.empty(out_cap, dtype=torch.uint8, device="cuda")
-    d_ooff = torch.empty(n + 1, dtype=torch.uint64, device="cuda")
-    d_st = torch.empty(n, dtype=torch.uint8, device="cuda")
-    d_vid = torch.empty(n, dtype=torch.int32, device="cuda")
-    d_tot = torch.zeros(1, dtype=torch.uint64, device="cuda")
-    o = N.DevOut(d_out.data_ptr(), out_cap, d_ooff.data_ptr(), d_st.data_ptr(), d_vid.data_ptr(), d_tot.data_ptr())
+    d_out = N.DeviceBuffer(x, out_cap)
+    d_ooff = N.DeviceBuffer(x, (n + 1) * 8)
+    d_st = N.DeviceBuffer(x, n + 1)
+    d_vid = N.DeviceBuffer(x, 4 * n + 4)
+    d_tot = N.DeviceBuffer(x, 8)
+    o = N.DevOut(d_out.ptr, out_cap, d_ooff.ptr, d_st.ptr, d_vid.ptr, d_tot.ptr)
 
     def step():
-        N.check(L.ie_interpolate_device(x.h, table, d_in.data_ptr(), d_off.data_ptr(), n, ctypes.byref(o)),
+        N.check(L.ie_interpolate_device(x.h, table, d_in.ptr, d_off.ptr, n, ctypes.byref(o)),
                 "ie_interpolate_device")
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    out_bytes = int(d_tot.item())
+    x.sync()
+    out_bytes = int(d_tot.to_numpy(np.uint64, 1)[0])
     assert out_bytes <= out_cap
-    n_bad = int((d_st != 0).sum().item())
+    n_bad = int(np.count_nonzero(d_st.to_numpy(np.uint8, n)))
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
+    if dist:
         dist.barrier()
-    torch.cuda.synchronize()
+    x.sync()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        ev[k][0].record(stream)
+    for k in range(args.steps):  # HIP events on the exec's stream, around every launch
+        x.mark(2 * k)
         step()
-        ev[k][1].record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
+        x.mark(2 * k + 1)
+    x.sync()
+    if dist:
         dist.barrier()
     wall = time.perf_counter() - t0
-    step_ms = [a.elapsed_time(b) for a, b in ev]
-    t = torch.tensor([wall], dtype=torch.float64, device="cuda")
-    if world > 1:
+    step_ms = [x.elapsed(2 * k, 2 * k + 1) for k in range(args.steps)]
+    wall_max = wall
+    if dist:
+        import torch
+        t = torch.tensor([wall], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall_max = float(t.item())
+        wall_max = float(t.item())
 
-    # one timed call with the library's own HIP events (same stream) for the kernel split
+    # one timed call with the library's own HIP events for the kernel split
     x.set_timing(True)
     step()
     tm = x.timing()
@@ -141,7 +140,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(args, L, N, synth, kvp, nkv, x, table, d_in, d_off, d_ooff, d_out, d_st)
+        cpu = cpu_baseline(args, L, N, synth, kvp, nkv, d_ooff, d_out, d_st)
 
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -182,12 +181,11 @@ def main():
         print(json.dumps(line), flush=True)
     L.ie_table_free(table)
     L.ie_synth_free(synth)
-    x.close()
-    if world > 1:
+    if dist:
         dist.destroy_process_group()
 
 
-def cpu_baseline(args, L, N, synth, kvp, nkv, x, table, d_in, d_off, d_ooff, d_out, d_st):
+def cpu_baseline(args, L, N, synth, kvp, nkv, d_ooff, d_out, d_st):
     """The oracle (a literal C restatement of interpolate_inserts) on a bounded sample of the same
     workload, timed on this host; the sample's GPU results are checked against it."""
     from oracle import oracle as O
@@ -214,9 +212,9 @@ def cpu_baseline(args, L, N, synth, kvp, nkv, x, table, d_in, d_off, d_ooff, d_o
     wall = ref.run_batch(buf, offs, m, threads, st, ln, hs, None)
     sample_bytes = int(offs[m])
     # parity of the GPU's first m results with the oracle on the same strings
-    gst = d_st[:m].cpu().numpy()
-    goff = d_ooff[:m + 1].cpu().numpy()
-    gout = d_out[:int(goff[m])].cpu().numpy().tobytes()
+    gst = d_st.to_numpy(np.uint8, m)
+    goff = d_ooff.to_numpy(np.uint64, m + 1)
+    gout = d_out.to_numpy(np.uint8, int(goff[m])).tobytes()
     same = bool(np.array_equal(gst, st)) and bool(np.array_equal(np.diff(goff.astype(np.int64)), ln.astype(np.int64)))
     if same:
         k = min(m, 20000)

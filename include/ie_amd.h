@@ -162,6 +162,17 @@ int ie_exec_set_timing(ie_exec* x, int32_t enabled);
 int ie_exec_timing(ie_exec* x, ie_timing* out); /* syncs */
 int ie_exec_set_scratch(ie_exec* x, uint64_t bytes); /* literal-kernel scratch pool size */
 
+/* ---- device memory and stream markers for callers without their own HIP bindings (the Rust
+ * shim, ctypes). Copies are ordered on the exec's stream; *_sync variants wait for it. ---- */
+int ie_dev_alloc(int32_t device, uint64_t bytes, void** out);
+void ie_dev_free(void* p);
+int ie_copy_h2d(ie_exec* x, void* dst, const void* src, uint64_t bytes);  /* synchronous */
+int ie_copy_d2h(ie_exec* x, void* dst, const void* src, uint64_t bytes);  /* synchronous */
+int ie_memset_d(ie_exec* x, void* dst, int32_t value, uint64_t bytes);     /* asynchronous */
+/* HIP events recorded on the exec's stream: slot in [0, 1024). */
+int ie_exec_mark(ie_exec* x, uint32_t slot);
+int ie_exec_elapsed(ie_exec* x, uint32_t from_slot, uint32_t to_slot, float* ms); /* syncs */
+
 /* ---- interpolate_inserts over a packed batch (py:497-541 / interp.rs:31-89) ----
  * Input: UTF-8 bytes, offsets[n+1] (string i = bytes[offsets[i] .. offsets[i+1])).
  * _device: all pointers device-resident, asynchronous on the exec's stream.

@@ -25,6 +25,8 @@ EXPORTS = [
     "ie_table_build", "ie_table_free", "ie_table_entries", "ie_table_dialect",
     "ie_exec_create", "ie_exec_destroy", "ie_exec_sync", "ie_exec_set_timing", "ie_exec_timing",
     "ie_exec_set_scratch",
+    "ie_dev_alloc", "ie_dev_free", "ie_copy_h2d", "ie_copy_d2h", "ie_memset_d", "ie_exec_mark",
+    "ie_exec_elapsed",
     "ie_interpolate_device", "ie_interpolate_batch", "ie_interpolate",
     "ie_unescape_device", "ie_escape_device", "ie_unescape_batch", "ie_escape_batch",
     "ie_batch_free", "ie_simple_insertkey",
@@ -88,6 +90,13 @@ def lib():
         "ie_exec_set_timing": (ctypes.c_int, [vp, i32]),
         "ie_exec_timing": (ctypes.c_int, [vp, ctypes.POINTER(Timing)]),
         "ie_exec_set_scratch": (ctypes.c_int, [vp, u64]),
+        "ie_dev_alloc": (ctypes.c_int, [i32, u64, pvp]),
+        "ie_dev_free": (None, [vp]),
+        "ie_copy_h2d": (ctypes.c_int, [vp, vp, vp, u64]),
+        "ie_copy_d2h": (ctypes.c_int, [vp, vp, vp, u64]),
+        "ie_memset_d": (ctypes.c_int, [vp, vp, i32, u64]),
+        "ie_exec_mark": (ctypes.c_int, [vp, u32]),
+        "ie_exec_elapsed": (ctypes.c_int, [vp, u32, u32, ctypes.POINTER(ctypes.c_float)]),
         "ie_interpolate_device": (ctypes.c_int, [vp, vp, vp, vp, u64, ctypes.POINTER(DevOut)]),
         "ie_interpolate_batch": (ctypes.c_int, [vp, vp, vp, vp, u64, ctypes.POINTER(ctypes.POINTER(BatchRes))]),
         "ie_interpolate": (ctypes.c_int, [vp, vp, ctypes.c_char_p, u64, ctypes.POINTER(ctypes.POINTER(BatchRes))]),
@@ -151,6 +160,55 @@ class Exec:
         t = Timing()
         check(lib().ie_exec_timing(self.h, ctypes.byref(t)), "ie_exec_timing")
         return t
+
+    def mark(self, slot):
+        check(lib().ie_exec_mark(self.h, slot), "ie_exec_mark")
+
+    def elapsed(self, a, b):
+        ms = ctypes.c_float()
+        check(lib().ie_exec_elapsed(self.h, a, b, ctypes.byref(ms)), "ie_exec_elapsed")
+        return ms.value
+
+
+class DeviceBuffer:
+    """A device allocation owned by libie_amd (hipMalloc), with numpy copies in and out."""
+
+    def __init__(self, x, nbytes, device=None):
+        self.x = x
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p()
+        check(lib().ie_dev_alloc(x.device if device is None else device, max(self.nbytes, 16), ctypes.byref(p)),
+              "ie_dev_alloc")
+        self.p = p
+
+    @property
+    def ptr(self):
+        return self.p.value
+
+    @classmethod
+    def from_numpy(cls, x, arr):
+        import numpy as np
+        arr = np.ascontiguousarray(arr)
+        b = cls(x, arr.nbytes)
+        check(lib().ie_copy_h2d(x.h, b.p, arr.ctypes.data, arr.nbytes), "ie_copy_h2d")
+        return b
+
+    def to_numpy(self, dtype, count, offset_bytes=0):
+        import numpy as np
+        out = np.empty(count, dtype=dtype)
+        if out.nbytes:
+            check(lib().ie_copy_d2h(self.x.h, out.ctypes.data, self.ptr + offset_bytes, out.nbytes), "ie_copy_d2h")
+        return out
+
+    def zero(self):
+        check(lib().ie_memset_d(self.x.h, self.p, 0, self.nbytes), "ie_memset_d")
+
+    def free(self):
+        if getattr(self, "p", None) and self.p.value:
+            lib().ie_dev_free(self.p)
+            self.p = ctypes.c_void_p()
+
+    __del__ = free
 
 
 def batch_to_python(res_ptr):

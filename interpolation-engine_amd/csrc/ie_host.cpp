@@ -89,6 +89,7 @@ struct ie_exec {
   bool own_stream = false;
   bool timing = false;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  std::vector<hipEvent_t> marks;  // ie_exec_mark slots
   bool ev_recorded = false;
   uint32_t lit_cap_max = 0;
   uint64_t pool_request = 256ull << 20;
@@ -104,6 +105,8 @@ struct ie_exec {
                       &s_lens, &s_part})
       b->release();
     for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
+    for (auto& e : marks)
       if (e) (void)hipEventDestroy(e);
     if (own_stream && stream) (void)hipStreamDestroy(stream);
   }
@@ -529,6 +532,56 @@ int ie_exec_timing(ie_exec* x, ie_timing* out) {
 int ie_exec_set_scratch(ie_exec* x, uint64_t bytes) {
   if (!x) return fail(IE_ERR_INVALID, "null exec");
   x->pool_request = std::max<uint64_t>(bytes, 1 << 20);
+  return IE_SUCCESS;
+}
+
+int ie_dev_alloc(int32_t device, uint64_t bytes, void** out) {
+  if (!out) return fail(IE_ERR_INVALID, "null argument");
+  int rc = set_device(device);
+  if (rc) return rc;
+  IE_HIP(hipMalloc(out, bytes ? bytes : 16));
+  return IE_SUCCESS;
+}
+
+void ie_dev_free(void* p) {
+  if (p) (void)hipFree(p);
+}
+
+int ie_copy_h2d(ie_exec* x, void* dst, const void* src, uint64_t bytes) {
+  if (!x || (bytes && (!dst || !src))) return fail(IE_ERR_INVALID, "null argument");
+  if (!bytes) return IE_SUCCESS;
+  IE_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, x->stream));
+  IE_HIP(hipStreamSynchronize(x->stream));
+  return IE_SUCCESS;
+}
+
+int ie_copy_d2h(ie_exec* x, void* dst, const void* src, uint64_t bytes) {
+  if (!x || (bytes && (!dst || !src))) return fail(IE_ERR_INVALID, "null argument");
+  if (!bytes) return IE_SUCCESS;
+  IE_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, x->stream));
+  IE_HIP(hipStreamSynchronize(x->stream));
+  return IE_SUCCESS;
+}
+
+int ie_memset_d(ie_exec* x, void* dst, int32_t value, uint64_t bytes) {
+  if (!x || (bytes && !dst)) return fail(IE_ERR_INVALID, "null argument");
+  if (bytes) IE_HIP(hipMemsetAsync(dst, value, bytes, x->stream));
+  return IE_SUCCESS;
+}
+
+int ie_exec_mark(ie_exec* x, uint32_t slot) {
+  if (!x || slot >= 1024) return fail(IE_ERR_INVALID, "bad exec or slot");
+  if (x->marks.size() <= slot) x->marks.resize(slot + 1, nullptr);
+  if (!x->marks[slot]) IE_HIP(hipEventCreate(&x->marks[slot]));
+  IE_HIP(hipEventRecord(x->marks[slot], x->stream));
+  return IE_SUCCESS;
+}
+
+int ie_exec_elapsed(ie_exec* x, uint32_t a, uint32_t b, float* ms) {
+  if (!x || !ms || a >= x->marks.size() || b >= x->marks.size() || !x->marks[a] || !x->marks[b])
+    return fail(IE_ERR_INVALID, "bad exec or unrecorded slot");
+  IE_HIP(hipEventSynchronize(x->marks[b]));
+  IE_HIP(hipEventElapsedTime(ms, x->marks[a], x->marks[b]));
   return IE_SUCCESS;
 }
 
