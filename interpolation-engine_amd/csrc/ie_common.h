@@ -1,12 +1,12 @@
 // ie_common.h — types shared by the host table builder and the gfx950 kernels.
 //
 // Device data layout of one inserts table (built once per get_interpdata snapshot, read-only):
-//   slots[cap]      uint32  entry index + 1 (0 = empty), open addressing, linear probing,
-//                           cap = next_pow2(2 * entries), so probe chains stay short
-//   entries[n]      DevEntry (32 B): 64-bit key hash, key/text spans in the arena, flags, value id
-//   arena[...]      key bytes and splice-text bytes of every entry
-// The hash is a polynomial hash over the key bytes (mod 2^64) so that a key assembled from
-// template pieces and spliced values can be hashed piecewise; slot = fmix64(hash, len) & mask.
+//   buckets[cap]    Bucket (128 B = one L2 line): 64-bit key hash, lengths, flags, value id, arena
+//                   offsets, and inline copies of the key (<= 32 B) and splice text (<= 64 B), so
+//                   one probe is one line; open addressing with linear probing, cap =
+//                   next_pow2(2 * entries) keeps probe chains short (load factor <= 0.5)
+//   arena[...]      every key and splice text (texts 4-byte aligned, for dword copies)
+// The hash is a polynomial hash over the key bytes (mod 2^64); slot = fmix64(hash, len) & mask.
 #pragma once
 #include <stdint.h>
 
@@ -35,7 +35,7 @@ IE_HD uint32_t slot_of(uint64_t h, uint32_t len, uint32_t mask) {
   return (uint32_t)fmix64(h ^ ((uint64_t)len << 40)) & mask;
 }
 
-// DevEntry.flags
+// Bucket.flags
 enum : uint32_t {
   EF_KIND_MASK = 7u,
   EF_SPLICE_OK = 1u << 3,      // the dialect's splice type rule passes (py:530 / interp.rs:71-80)
@@ -47,18 +47,22 @@ enum : uint32_t {
 // DevTable.flags
 enum : uint32_t { TF_HAS_DIR = 1u };
 
-struct DevEntry {
+constexpr uint32_t EF_OCCUPIED = 1u << 7;  // Bucket.flags: the bucket holds an entry
+constexpr uint32_t kInlineKey = 32;         // bytes of key kept inline in a bucket
+constexpr uint32_t kInlineText = 64;        // bytes of splice text kept inline in a bucket
+
+struct Bucket {
   uint64_t hash;
-  uint32_t key_off, key_len;
-  uint32_t text_off, text_len;
-  uint32_t vid;
-  uint32_t flags;
+  uint32_t key_len, text_len;
+  uint32_t vid, flags;
+  uint32_t key_off, text_off;   // arena offsets (always valid)
+  uint8_t key[kInlineKey];      // zero padded
+  uint8_t text[kInlineText];    // zero padded
 };
-static_assert(sizeof(DevEntry) == 32, "DevEntry must stay one 32-byte record");
+static_assert(sizeof(Bucket) == 128, "Bucket must stay one 128-byte line");
 
 struct DevTable {
-  const uint32_t* slots;
-  const DevEntry* entries;
+  const Bucket* buckets;
   const uint8_t* arena;
   uint32_t mask;
   uint32_t n_entries;

@@ -1,0 +1,135 @@
+// ie_device.h — device-side building blocks shared by the kernels: wave primitives, the
+// get_interpdata lookup (py:430-467 / interp.rs:91-137) against the bucketed device table.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ie_amd.h"
+#include "ie_common.h"
+
+namespace ie {
+
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
+  const uint32_t lane = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t t = __shfl_up(v, d, 64);
+    if (lane >= (uint32_t)d) v += t;
+  }
+  return v;
+}
+
+__device__ __forceinline__ uint64_t w_sum(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
+__device__ __forceinline__ int64_t w_max(int64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const int64_t o = __shfl_xor(v, d, 64);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
+// ------------------------------------------------------------------------------------------
+// lookups
+// ------------------------------------------------------------------------------------------
+struct Hit {
+  uint32_t text_len, text_off, vid, flags;
+};
+
+__device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, uint32_t n) {
+  bool eq = true;
+  for (uint32_t j = 0; j < n; j++) eq &= a[j] == b[j];
+  return eq;
+}
+
+__device__ __forceinline__ Hit hit_of(uint4 q0, uint4 q1) {
+  return Hit{q0.w, q1.w, q1.x, q1.y};
+}
+
+// Probe for a key whose bytes are at `key` (any address space). Returns the bucket or -1.
+__device__ int32_t find_bytes(const DevTable& T, const uint8_t* key, uint32_t klen, Hit& h) {
+  uint64_t hash = 0;
+  for (uint32_t j = 0; j < klen; j++) hash = hash_step(hash, key[j]);
+  uint32_t s = slot_of(hash, klen, T.mask);
+  for (uint32_t probe = 0; probe <= T.mask; probe++) {
+    const uint4* bp = (const uint4*)(T.buckets + s);
+    const uint4 q0 = bp[0], q1 = bp[1];
+    if (!(q1.y & EF_OCCUPIED)) return -1;
+    if ((((uint64_t)q0.y << 32) | q0.x) == hash && q0.z == klen &&
+        bytes_eq(T.arena + q1.z, key, klen)) {
+      h = hit_of(q0, q1);
+      return (int32_t)s;
+    }
+    s = (s + 1) & T.mask;
+  }
+  return -1;
+}
+
+// Probe for a key held in LDS at a 4-byte aligned address, klen <= kInlineKey: the whole probe
+// is one 64-byte burst (header + inline key) compared dword-wise in registers.
+__device__ __forceinline__ int32_t find_small(const DevTable& T, const uint32_t* key32, uint32_t klen,
+                                              Hit& h) {
+  uint32_t kw[8];
+  uint64_t hash = 0;
+#pragma unroll
+  for (int d = 0; d < 8; d++) {
+    kw[d] = (4u * d < klen) ? key32[d] : 0u;
+#pragma unroll
+    for (int b = 0; b < 4; b++)
+      if (4u * d + b < klen) hash = hash_step(hash, (uint8_t)(kw[d] >> (8 * b)));
+  }
+#pragma unroll
+  for (int d = 0; d < 8; d++) {  // zero the bytes past the key: buckets are zero padded
+    const int32_t rem = (int32_t)klen - 4 * d;
+    if (rem < 4) kw[d] &= rem <= 0 ? 0u : ((1u << (8 * rem)) - 1u);
+  }
+  uint32_t s = slot_of(hash, klen, T.mask);
+  for (uint32_t probe = 0; probe <= T.mask; probe++) {
+    const uint4* bp = (const uint4*)(T.buckets + s);
+    const uint4 q0 = bp[0], q1 = bp[1], q2 = bp[2], q3 = bp[3];
+    if (!(q1.y & EF_OCCUPIED)) return -1;
+    const bool eq = ((((uint64_t)q0.y << 32) | q0.x) == hash) & (q0.z == klen) &
+                    (q2.x == kw[0]) & (q2.y == kw[1]) & (q2.z == kw[2]) & (q2.w == kw[3]) &
+                    (q3.x == kw[4]) & (q3.y == kw[5]) & (q3.z == kw[6]) & (q3.w == kw[7]);
+    if (eq) {
+      h = hit_of(q0, q1);
+      return (int32_t)s;
+    }
+    s = (s + 1) & T.mask;
+  }
+  return -1;
+}
+
+// status of a key that is not in the table (py:437-467 / interp.rs:105-136)
+__device__ uint8_t missing_status(const DevTable& T, const uint8_t* k, uint32_t n) {
+  if (n == 0) return IE_E_INTERP;
+  if (!(T.flags & TF_HAS_DIR)) return IE_E_INTERP;
+  bool is_arg = n >= 3 && k[0] == 'A' && k[1] == 'R' && k[2] == 'G';
+  if (T.dialect == IE_DIALECT_PY && n == 3) is_arg = false;  // ''.isdigit() is False
+  for (uint32_t j = 3; is_arg && j < n; j++) is_arg = k[j] >= '0' && k[j] <= '9';
+  return is_arg ? (uint8_t)IE_E_INTERP : (uint8_t)IE_NEEDS_HOST;
+}
+
+// lookup with the RAW value of bucket `prev` as the key (nested whole-string form,
+// py:511-512: the object itself; interp.rs:47-48: value_to_string of it)
+__device__ int32_t find_raw(const DevTable& T, const Hit& prev, uint8_t& st, Hit& h) {
+  if (!(prev.flags & EF_KEY_STR)) {
+    st = (prev.flags & EF_KEY_UNHASHABLE) ? (uint8_t)IE_E_UNHASHABLE
+         : (T.flags & TF_HAS_DIR)         ? (uint8_t)IE_NEEDS_HOST
+                                          : (uint8_t)IE_E_INTERP;
+    return -1;
+  }
+  const uint8_t* k = T.arena + prev.text_off;
+  const int32_t b = find_bytes(T, k, prev.text_len, h);
+  if (b < 0) st = missing_status(T, k, prev.text_len);
+  return b;
+}
+
+}  // namespace ie

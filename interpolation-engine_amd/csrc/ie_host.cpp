@@ -75,10 +75,9 @@ struct ie_table {
   uint32_t flags = 0;
   uint64_t n_entries = 0;
   DevTable dev{};
-  DevBuf slots, entries, arena;
+  DevBuf buckets, arena;
   ~ie_table() {
-    slots.release();
-    entries.release();
+    buckets.release();
     arena.release();
   }
 };
@@ -88,21 +87,20 @@ struct ie_exec {
   hipStream_t stream = nullptr;
   bool own_stream = false;
   bool timing = false;
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
   std::vector<hipEvent_t> marks;  // ie_exec_mark slots
   bool ev_recorded = false;
   uint32_t lit_cap_max = 0;
   uint64_t pool_request = 256ull << 20;
   // workspace
-  DevBuf out_len, tile_sum, tile_base, counters, cx_list, cx_status, res_off, pool;
+  DevBuf counters, tile_state, pool, out_len, tile_sum, tile_base;
   // host-API staging
   DevBuf in_bytes, in_off, o_bytes, o_off, o_status, o_vid, o_total;
   // synth scratch
   DevBuf s_lens, s_part;
   ~ie_exec() {
-    for (DevBuf* b : {&out_len, &tile_sum, &tile_base, &counters, &cx_list, &cx_status, &res_off,
-                      &pool, &in_bytes, &in_off, &o_bytes, &o_off, &o_status, &o_vid, &o_total,
-                      &s_lens, &s_part})
+    for (DevBuf* b : {&counters, &tile_state, &pool, &out_len, &tile_sum, &tile_base, &in_bytes,
+                      &in_off, &o_bytes, &o_off, &o_status, &o_vid, &o_total, &s_lens, &s_part})
       b->release();
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
@@ -167,33 +165,35 @@ int set_device(int32_t dev) {
   return IE_SUCCESS;
 }
 
-// workspace for a batch of n strings
-int ensure_work(ie_exec* x, uint64_t n) {
+// workspace for a batch of n strings. counters: [0] tile ticket, [1] look-back error,
+// [2..3] pool bytes used (u64); zeroed with the tile states on every call.
+int ensure_work(ie_exec* x, int op, uint64_t n) {
   const uint64_t tiles = (n + kBlock - 1) / kBlock + 1;
-  IE_HIP(x->out_len.ensure((n + 1) * sizeof(uint32_t)));
-  IE_HIP(x->tile_sum.ensure(tiles * sizeof(uint64_t)));
-  IE_HIP(x->tile_base.ensure(tiles * sizeof(uint64_t)));
   IE_HIP(x->counters.ensure(64));
-  IE_HIP(x->cx_list.ensure((n + 1) * sizeof(uint32_t)));
-  IE_HIP(x->cx_status.ensure(n + 1));
-  IE_HIP(x->res_off.ensure((n + 1) * sizeof(uint64_t)));
-  IE_HIP(x->pool.ensure(x->pool_request));
+  if (op == kOpInterp) {
+    IE_HIP(x->tile_state.ensure(tiles * sizeof(uint64_t)));
+    IE_HIP(x->pool.ensure(x->pool_request));
+  } else {
+    IE_HIP(x->out_len.ensure((n + 1) * sizeof(uint32_t)));
+    IE_HIP(x->tile_sum.ensure(tiles * sizeof(uint64_t)));
+    IE_HIP(x->tile_base.ensure(tiles * sizeof(uint64_t)));
+  }
   return IE_SUCCESS;
 }
 
-Work make_work(ie_exec* x) {
+Work make_work(ie_exec* x, uint64_t* total) {
   Work W{};
-  W.out_len = (uint32_t*)x->out_len.p;
-  W.tile_sum = (uint64_t*)x->tile_sum.p;
-  W.tile_base = (uint64_t*)x->tile_base.p;
-  W.cx_count = (uint32_t*)x->counters.p;
-  W.pool_used = (uint64_t*)((char*)x->counters.p + 8);
-  W.cx_list = (uint32_t*)x->cx_list.p;
-  W.cx_status = (uint8_t*)x->cx_status.p;
-  W.res_off = (uint64_t*)x->res_off.p;
+  W.total = total;
+  W.tile_ticket = (uint32_t*)x->counters.p;
+  W.err = (uint32_t*)x->counters.p + 1;
+  W.pool_used = (uint64_t*)x->counters.p + 1;
+  W.tile_state = (uint64_t*)x->tile_state.p;
   W.pool = (uint8_t*)x->pool.p;
   W.pool_bytes = x->pool.bytes;
   W.lit_cap_max = x->lit_cap_max;
+  W.out_len = (uint32_t*)x->out_len.p;
+  W.tile_sum = (uint64_t*)x->tile_sum.p;
+  W.tile_base = (uint64_t*)x->tile_base.p;
   return W;
 }
 
@@ -208,35 +208,39 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
   int rc = set_device(x->device);
   if (rc) return rc;
   if (n > 0xFFFFFFF0ull) return fail(IE_ERR_INVALID, "batch larger than 2^32 strings");
-  rc = ensure_work(x, n);
+  rc = ensure_work(x, op, n);
   if (rc) return rc;
   Batch B{d_bytes, d_off, n, out->offsets, out->status, out->value_id};
-  Work W = make_work(x);
-  DevTable T = op == kOpInterp ? t->dev : DevTable{};
+  Work W = make_work(x, out->total);
   hipStream_t st = x->stream;
+  const uint64_t cap = out->bytes ? out->bytes_cap : 0;
   if (x->timing) IE_HIP(hipEventRecord(x->ev[0], st));
   IE_HIP(hipMemsetAsync(x->counters.p, 0, 64, st));
   if (n == 0) {
     IE_HIP(hipMemsetAsync(out->offsets, 0, sizeof(uint64_t), st));
     IE_HIP(hipMemsetAsync(out->total, 0, sizeof(uint64_t), st));
-    if (x->timing) {
-      IE_HIP(hipEventRecord(x->ev[1], st));
-      IE_HIP(hipEventRecord(x->ev[2], st));
-      IE_HIP(hipEventRecord(x->ev[3], st));
-      x->ev_recorded = true;
-    }
-    return IE_SUCCESS;
+  } else if (op == kOpInterp) {
+    const uint64_t tiles = (n + kBlock - 1) / kBlock;
+    IE_HIP(hipMemsetAsync(x->tile_state.p, 0, tiles * sizeof(uint64_t), st));
+    if (x->timing) IE_HIP(hipEventRecord(x->ev[1], st));
+    IE_HIP(launch_resolve(B, W, t->dev, out->bytes, cap, st));
+  } else {
+    if (x->timing) IE_HIP(hipEventRecord(x->ev[1], st));
+    IE_HIP(launch_escape(op, B, W, out->bytes, cap, st));
   }
-  IE_HIP(launch_measure(op, B, W, T, st));
-  if (x->timing) IE_HIP(hipEventRecord(x->ev[1], st));
-  if (op == kOpInterp) IE_HIP(launch_literal(B, W, T, st));
-  if (x->timing) IE_HIP(hipEventRecord(x->ev[2], st));
-  IE_HIP(launch_scan_tiles(B, W, out->total, st));
-  IE_HIP(launch_emit(op, B, W, T, out->bytes, out->bytes ? out->bytes_cap : 0, out->total, st));
   if (x->timing) {
-    IE_HIP(hipEventRecord(x->ev[3], st));
+    if (n == 0) IE_HIP(hipEventRecord(x->ev[1], st));
+    IE_HIP(hipEventRecord(x->ev[2], st));
     x->ev_recorded = true;
   }
+  return IE_SUCCESS;
+}
+
+// look-back timeout flag of the last call (after a sync)
+int check_device_error(ie_exec* x) {
+  uint32_t err = 0;
+  if (x->counters.p) IE_HIP(hipMemcpy(&err, (uint32_t*)x->counters.p + 1, 4, hipMemcpyDeviceToHost));
+  if (err) return fail(IE_ERR_TIMEOUT, "look-back spin timed out (a predecessor tile never published)");
   return IE_SUCCESS;
 }
 
@@ -269,6 +273,7 @@ int run_host(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, const 
   uint64_t total = 0;
   IE_HIP(hipMemcpyAsync(&total, o.total, 8, hipMemcpyDeviceToHost, x->stream));
   IE_HIP(hipStreamSynchronize(x->stream));
+  if ((rc = check_device_error(x))) return rc;
   if (total > cap) {  // grow and re-run
     IE_HIP(x->o_bytes.ensure(total + 4096));
     o.bytes = (uint8_t*)x->o_bytes.p;
@@ -277,6 +282,7 @@ int run_host(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, const 
     if (rc) return rc;
     IE_HIP(hipMemcpyAsync(&total, o.total, 8, hipMemcpyDeviceToHost, x->stream));
     IE_HIP(hipStreamSynchronize(x->stream));
+    if ((rc = check_device_error(x))) return rc;
     if (total > o.bytes_cap) return fail(IE_ERR_CAPACITY, "output grew between runs");
   }
   ie_batch* b = new ie_batch{};
@@ -387,43 +393,53 @@ int ie_table_build(const ie_kv* kv, uint64_t n, int32_t dialect, const ie_clock*
   snprintf(hhmm, sizeof hhmm, "%02d:%02d", h, mi);
   snprintf(hhmmss, sizeof hhmmss, "%02d:%02d:%02d", h, mi, se);
 
-  std::vector<DevEntry> ents;
-  std::vector<uint8_t> arena;
-  ents.reserve(order.size() + 2);
-  uint64_t maxtext = 8;
-  auto add = [&](std::string_view k, std::string_view t, int32_t kind, uint32_t vid) {
-    DevEntry e{};
-    e.hash = poly_hash(k);
-    e.key_off = (uint32_t)arena.size();
-    e.key_len = (uint32_t)k.size();
-    arena.insert(arena.end(), k.begin(), k.end());
-    e.text_off = (uint32_t)arena.size();
-    e.text_len = (uint32_t)t.size();
-    arena.insert(arena.end(), t.begin(), t.end());
-    e.vid = vid;
-    e.flags = kind_flags(kind, dialect) | text_flags(t);
-    maxtext = std::max<uint64_t>(maxtext, t.size());
-    ents.push_back(e);
+  struct Ent {
+    std::string_view key, text;
+    uint32_t flags, vid;
   };
+  std::vector<Ent> ents;
+  ents.reserve(order.size() + 2);
   for (uint64_t i : order) {
     std::string_view k(kv[i].key, kv[i].key_len);
-    uint64_t j = last[k];
+    const uint64_t j = last[k];
     if (k == "HH:MM" || k == "HH:MM:SS") continue;  // py:433-436: the clock always wins
     if (kv[j].kind < 0 || kv[j].kind > IE_KIND_DICT) return fail(IE_ERR_INVALID, "bad kind");
-    add(k, std::string_view(kv[j].text ? kv[j].text : "", kv[j].text_len), kv[j].kind, (uint32_t)j);
+    std::string_view t(kv[j].text ? kv[j].text : "", kv[j].text_len);
+    ents.push_back(Ent{k, t, kind_flags(kv[j].kind, dialect) | text_flags(t), (uint32_t)j});
   }
-  add("HH:MM", hhmm, IE_KIND_STR, IE_VID_CLOCK_HHMM);
-  add("HH:MM:SS", hhmmss, IE_KIND_STR, IE_VID_CLOCK_HHMMSS);
-  if (arena.size() >= 0xFFFFFFF0ull) return fail(IE_ERR_INVALID, "table arena above 4 GiB");
+  ents.push_back(Ent{"HH:MM", hhmm, kind_flags(IE_KIND_STR, dialect) | text_flags(hhmm), IE_VID_CLOCK_HHMM});
+  ents.push_back(Ent{"HH:MM:SS", hhmmss, kind_flags(IE_KIND_STR, dialect) | text_flags(hhmmss), IE_VID_CLOCK_HHMMSS});
 
   uint64_t cap = 16;
   while (cap < 2 * ents.size()) cap *= 2;
-  std::vector<uint32_t> slots(cap, 0);
-  for (size_t e = 0; e < ents.size(); e++) {
-    uint32_t s = slot_of(ents[e].hash, ents[e].key_len, (uint32_t)(cap - 1));
-    while (slots[s]) s = (s + 1) & (uint32_t)(cap - 1);
-    slots[s] = (uint32_t)(e + 1);
+  if (cap > (1ull << 31)) return fail(IE_ERR_INVALID, "table too large");
+  std::vector<Bucket> buckets(cap);
+  memset(buckets.data(), 0, cap * sizeof(Bucket));
+  std::vector<uint8_t> arena;
+  uint64_t maxtext = 8;
+  for (const Ent& e : ents) {
+    while (arena.size() & 3) arena.push_back(0);  // texts 4-byte aligned (dword copies)
+    const uint64_t toff = arena.size();
+    arena.insert(arena.end(), e.text.begin(), e.text.end());
+    const uint64_t koff = arena.size();
+    arena.insert(arena.end(), e.key.begin(), e.key.end());
+    if (arena.size() >= 0xFFFFFFF0ull) return fail(IE_ERR_INVALID, "table arena above 4 GiB");
+    maxtext = std::max<uint64_t>(maxtext, e.text.size());
+    Bucket b{};
+    b.hash = poly_hash(e.key);
+    b.key_len = (uint32_t)e.key.size();
+    b.text_len = (uint32_t)e.text.size();
+    b.vid = e.vid;
+    b.flags = e.flags | EF_OCCUPIED;
+    b.key_off = (uint32_t)koff;
+    b.text_off = (uint32_t)toff;
+    if (e.key.size() <= kInlineKey) memcpy(b.key, e.key.data(), e.key.size());
+    if (e.text.size() <= kInlineText) memcpy(b.text, e.text.data(), e.text.size());
+    uint32_t sl = slot_of(b.hash, b.key_len, (uint32_t)(cap - 1));
+    while (buckets[sl].flags & EF_OCCUPIED) sl = (sl + 1) & (uint32_t)(cap - 1);
+    buckets[sl] = b;
   }
+  for (int pad = 0; pad < 16; pad++) arena.push_back(0);  // dword reads past the last text
   ie_table* t = new ie_table();
   t->device = device;
   t->dialect = dialect;
@@ -434,15 +450,13 @@ int ie_table_build(const ie_kv* kv, uint64_t n, int32_t dialect, const ie_clock*
     if (e != hipSuccess) return e;
     return bytes ? hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice) : hipSuccess;
   };
-  hipError_t e1 = up(t->slots, slots.data(), slots.size() * 4);
-  hipError_t e2 = e1 == hipSuccess ? up(t->entries, ents.data(), ents.size() * sizeof(DevEntry)) : e1;
-  hipError_t e3 = e2 == hipSuccess ? up(t->arena, arena.data(), arena.size()) : e2;
-  if (e3 != hipSuccess) {
+  hipError_t e1 = up(t->buckets, buckets.data(), buckets.size() * sizeof(Bucket));
+  hipError_t e2 = e1 == hipSuccess ? up(t->arena, arena.data(), arena.size()) : e1;
+  if (e2 != hipSuccess) {
     delete t;
-    return fail(IE_ERR_HIP, std::string("table upload: ") + hipGetErrorString(e3));
+    return fail(IE_ERR_HIP, std::string("table upload: ") + hipGetErrorString(e2));
   }
-  t->dev.slots = (const uint32_t*)t->slots.p;
-  t->dev.entries = (const DevEntry*)t->entries.p;
+  t->dev.buckets = (const Bucket*)t->buckets.p;
   t->dev.arena = (const uint8_t*)t->arena.p;
   t->dev.mask = (uint32_t)(cap - 1);
   t->dev.n_entries = (uint32_t)ents.size();
@@ -500,7 +514,7 @@ void ie_exec_destroy(ie_exec* x) {
 int ie_exec_sync(ie_exec* x) {
   if (!x) return fail(IE_ERR_INVALID, "null exec");
   IE_HIP(hipStreamSynchronize(x->stream));
-  return IE_SUCCESS;
+  return check_device_error(x);
 }
 
 int ie_exec_set_timing(ie_exec* x, int32_t enabled) {
@@ -515,18 +529,14 @@ int ie_exec_timing(ie_exec* x, ie_timing* out) {
   memset(out, 0, sizeof *out);
   if (!x->ev_recorded) return fail(IE_ERR_INVALID, "no timed call recorded");
   IE_HIP(hipStreamSynchronize(x->stream));
-  float a = 0, b = 0, c = 0;
-  IE_HIP(hipEventElapsedTime(&a, x->ev[0], x->ev[1]));
-  IE_HIP(hipEventElapsedTime(&b, x->ev[1], x->ev[2]));
-  IE_HIP(hipEventElapsedTime(&c, x->ev[0], x->ev[3]));
-  out->resolve_ms = c - b;  // measure + scan + emit
-  out->complex_ms = b;
-  out->total_ms = c;
-  uint32_t cnt = 0;
-  if (x->counters.p) IE_HIP(hipMemcpy(&cnt, x->counters.p, 4, hipMemcpyDeviceToHost));
-  out->n_complex = cnt;
-  (void)a;
-  return IE_SUCCESS;
+  float setup = 0, kern = 0;
+  IE_HIP(hipEventElapsedTime(&setup, x->ev[0], x->ev[1]));
+  IE_HIP(hipEventElapsedTime(&kern, x->ev[1], x->ev[2]));
+  out->resolve_ms = kern;   // the resolve (or escape) kernels
+  out->complex_ms = 0.0f;   // literal strings are resolved inside k_resolve
+  out->total_ms = setup + kern;
+  out->n_complex = 0;
+  return check_device_error(x);
 }
 
 int ie_exec_set_scratch(ie_exec* x, uint64_t bytes) {

@@ -10,8 +10,9 @@ namespace ie {
 constexpr int kBlock = 256;          // lanes per workgroup = strings per tile
 constexpr int kMaxDepth = 6;         // fast-path nesting limit (deeper: literal path)
 constexpr int kKeyCap = 48;          // fast-path key bytes per lane (longer keys: literal path)
-constexpr int kTileBytes = 24576;    // LDS input stage; larger tiles read global memory directly
-constexpr int kStageBytes = 24576;   // LDS output stage; larger tiles store directly
+constexpr int kMaxSeg = 7;           // depth-0 output segments recorded per string
+constexpr int kTileBytes = 18432;    // LDS input stage; larger tiles read global memory directly
+constexpr int kStageBytes = 20480;   // LDS output stage; larger tiles store directly
 
 enum { kOpInterp = 0, kOpUnescape = 1, kOpEscape = 2 };
 
@@ -25,24 +26,25 @@ struct Batch {
 };
 
 struct Work {
-  uint32_t* out_len;    // n   output length per string
-  uint64_t* tile_sum;   // tiles
-  uint64_t* tile_base;  // tiles
-  uint32_t* cx_count;   // 1   strings queued for the literal kernel
-  uint32_t* cx_list;    // n
-  uint8_t* cx_status;   // n   final status of queued strings
-  uint64_t* res_off;    // n   pool offset of a queued string's result
-  uint8_t* pool;        // literal-kernel scratch
-  uint64_t* pool_used;  // 1
+  uint64_t* total;       // 1   caller's total word
+  // single-pass resolve
+  uint32_t* tile_ticket; // 1   dynamic tile ids (zeroed per call)
+  uint64_t* tile_state;  // tiles: look-back words (zeroed per call)
+  uint32_t* err;         // 1   look-back timeout flag
+  uint8_t* pool;         // literal-path scratch
+  uint64_t* pool_used;   // 1
   uint64_t pool_bytes;
-  uint32_t lit_cap_max; // 1: give every queued string the full IE_SIZE_CAP working space
+  uint32_t lit_cap_max;  // 1: literal strings get the full IE_SIZE_CAP working space
+  // escape pipeline
+  uint32_t* out_len;     // n
+  uint64_t* tile_sum;    // tiles
+  uint64_t* tile_base;   // tiles
 };
 
-hipError_t launch_measure(int op, const Batch& B, const Work& W, const DevTable& T, hipStream_t st);
-hipError_t launch_literal(const Batch& B, const Work& W, const DevTable& T, hipStream_t st);
-hipError_t launch_scan_tiles(const Batch& B, const Work& W, uint64_t* total, hipStream_t st);
-hipError_t launch_emit(int op, const Batch& B, const Work& W, const DevTable& T, uint8_t* out,
-                       uint64_t cap, const uint64_t* total, hipStream_t st);
+hipError_t launch_resolve(const Batch& B, const Work& W, const DevTable& T, uint8_t* out,
+                          uint64_t cap, hipStream_t st);
+hipError_t launch_escape(int op, const Batch& B, const Work& W, uint8_t* out, uint64_t cap,
+                         hipStream_t st);
 hipError_t launch_synth(const SynthParams& P, uint64_t first, uint64_t n, uint64_t* d_lens,
                         uint64_t* d_part, uint64_t* d_offsets, uint64_t* d_total, uint8_t* d_bytes,
                         hipStream_t st);
