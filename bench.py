@@ -172,10 +172,10 @@ def main():
             "strings_per_s": round(strings_per_s, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "resolve pipeline (k_measure + k_literal + k_scan_tiles + k_emit)",
+                         "kernel": "k_resolve (single pass: stage, evaluate, look-back, emit)",
                          "launch_ms": round(gpu_ms, 4), "alg_bytes_per_launch": alg_bytes,
-                         "split_ms": {"measure+scan+emit": round(tm.resolve_ms, 4),
-                                      "literal": round(tm.complex_ms, 4), "n_literal": int(tm.n_complex)}},
+                         "telemetry": {"kernel_ms": round(tm.resolve_ms, 4), "literal_strings": int(tm.n_complex),
+                                       "direct_tiles": int(tm.n_direct), "lookback_polls": int(tm.n_polls)}},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -135,10 +135,12 @@ typedef struct ie_batch {
 
 /* Kernel timing of the last device call on an exec (HIP events on the exec's stream). */
 typedef struct ie_timing {
-  float resolve_ms;  /* the dominant resolve/escape kernel(s) */
-  float complex_ms;  /* literal (complex-string) kernel, 0 if none ran */
-  float total_ms;    /* first to last kernel of the call */
-  uint64_t n_complex;/* strings routed to the literal kernel (valid after ie_exec_sync) */
+  float resolve_ms;      /* the resolve (or escape) kernel(s) of the last call */
+  float complex_ms;      /* reserved: literal strings are resolved inside the resolve kernel */
+  float total_ms;        /* setup memsets + kernels of the last call */
+  uint64_t n_complex;    /* strings routed to the literal (wave-cooperative) path */
+  uint64_t n_direct;     /* tiles that bypassed the LDS stages (long strings / many segments) */
+  uint64_t n_polls;      /* look-back poll rounds that found a predecessor not yet published */
 } ie_timing;
 
 /* ---- library ---- */

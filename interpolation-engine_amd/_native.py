@@ -59,7 +59,8 @@ class BatchRes(ctypes.Structure):
 
 class Timing(ctypes.Structure):
     _fields_ = [("resolve_ms", ctypes.c_float), ("complex_ms", ctypes.c_float),
-                ("total_ms", ctypes.c_float), ("n_complex", ctypes.c_uint64)]
+                ("total_ms", ctypes.c_float), ("n_complex", ctypes.c_uint64), ("n_direct", ctypes.c_uint64),
+                ("n_polls", ctypes.c_uint64)]
 
 
 _lib = None

@@ -11,6 +11,26 @@ namespace ie {
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
+// explicit address spaces: loads through these compile to global_* / ds_* instead of flat_*
+template <class T>
+__device__ __forceinline__ T gld(const T* p) {
+  return *(const __attribute__((address_space(1))) T*)p;
+}
+template <class T>
+__device__ __forceinline__ void gst(T* p, T v) {
+  *(__attribute__((address_space(1))) T*)p = v;
+}
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 gld4(const uint4* p) {
+  const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)(const void*)p;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void gst4(uint4* p, uint4 v) {
+  u32x4 w;
+  w.x = v.x; w.y = v.y; w.z = v.z; w.w = v.w;
+  *(__attribute__((address_space(1))) u32x4*)(void*)p = w;
+}
+
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
   const uint32_t lane = lane_id();
 #pragma unroll
@@ -43,9 +63,10 @@ struct Hit {
   uint32_t text_len, text_off, vid, flags;
 };
 
+// a: table arena (global), b: any address space
 __device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, uint32_t n) {
   bool eq = true;
-  for (uint32_t j = 0; j < n; j++) eq &= a[j] == b[j];
+  for (uint32_t j = 0; j < n; j++) eq &= gld(a + j) == b[j];
   return eq;
 }
 
@@ -60,7 +81,7 @@ __device__ int32_t find_bytes(const DevTable& T, const uint8_t* key, uint32_t kl
   uint32_t s = slot_of(hash, klen, T.mask);
   for (uint32_t probe = 0; probe <= T.mask; probe++) {
     const uint4* bp = (const uint4*)(T.buckets + s);
-    const uint4 q0 = bp[0], q1 = bp[1];
+    const uint4 q0 = gld4(bp), q1 = gld4(bp + 1);
     if (!(q1.y & EF_OCCUPIED)) return -1;
     if ((((uint64_t)q0.y << 32) | q0.x) == hash && q0.z == klen &&
         bytes_eq(T.arena + q1.z, key, klen)) {
@@ -93,7 +114,7 @@ __device__ __forceinline__ int32_t find_small(const DevTable& T, const uint32_t*
   uint32_t s = slot_of(hash, klen, T.mask);
   for (uint32_t probe = 0; probe <= T.mask; probe++) {
     const uint4* bp = (const uint4*)(T.buckets + s);
-    const uint4 q0 = bp[0], q1 = bp[1], q2 = bp[2], q3 = bp[3];
+    const uint4 q0 = gld4(bp), q1 = gld4(bp + 1), q2 = gld4(bp + 2), q3 = gld4(bp + 3);
     if (!(q1.y & EF_OCCUPIED)) return -1;
     const bool eq = ((((uint64_t)q0.y << 32) | q0.x) == hash) & (q0.z == klen) &
                     (q2.x == kw[0]) & (q2.y == kw[1]) & (q2.z == kw[2]) & (q2.w == kw[3]) &

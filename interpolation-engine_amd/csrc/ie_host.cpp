@@ -165,8 +165,8 @@ int set_device(int32_t dev) {
   return IE_SUCCESS;
 }
 
-// workspace for a batch of n strings. counters: [0] tile ticket, [1] look-back error,
-// [2..3] pool bytes used (u64); zeroed with the tile states on every call.
+// workspace for a batch of n strings. counters (u32 words): [0] tile ticket, [1] look-back error,
+// [2..3] pool bytes used (u64), [4..6] telemetry; zeroed with the tile states on every call.
 int ensure_work(ie_exec* x, int op, uint64_t n) {
   const uint64_t tiles = (n + kBlock - 1) / kBlock + 1;
   IE_HIP(x->counters.ensure(64));
@@ -186,6 +186,7 @@ Work make_work(ie_exec* x, uint64_t* total) {
   W.total = total;
   W.tile_ticket = (uint32_t*)x->counters.p;
   W.err = (uint32_t*)x->counters.p + 1;
+  W.stats = (uint32_t*)x->counters.p + 4;
   W.pool_used = (uint64_t*)x->counters.p + 1;
   W.tile_state = (uint64_t*)x->tile_state.p;
   W.pool = (uint8_t*)x->pool.p;
@@ -535,7 +536,11 @@ int ie_exec_timing(ie_exec* x, ie_timing* out) {
   out->resolve_ms = kern;   // the resolve (or escape) kernels
   out->complex_ms = 0.0f;   // literal strings are resolved inside k_resolve
   out->total_ms = setup + kern;
-  out->n_complex = 0;
+  uint32_t st[3] = {0, 0, 0};
+  if (x->counters.p) IE_HIP(hipMemcpy(st, (uint32_t*)x->counters.p + 4, 12, hipMemcpyDeviceToHost));
+  out->n_complex = st[0];
+  out->n_direct = st[1];
+  out->n_polls = st[2];
   return check_device_error(x);
 }
 

@@ -5,7 +5,7 @@
 // ticket (so every tile a workgroup waits on is already running) and chained with a decoupled
 // look-back over 8-byte {flag, value} words published by agent-scope atomics. Per tile:
 //   1. stage the tile's input bytes in LDS (16-byte loads);
-//   2. every lane evaluates its string (eval_string): a skip-ahead scan that only visits the
+//   2. every lane evaluates its string (eval_rounds): a skip-ahead scan that only visits the
 //      special bytes at depth 0 ('{', '}', '\', and >= 0x7B for U+3020), builds keys of open
 //      pairs in a lane-private LDS buffer, probes the bucketed table, and records the depth-0
 //      output as <= kMaxSeg segments (template runs and splice texts) — no bytes move yet;
@@ -34,6 +34,25 @@ __device__ __forceinline__ uint64_t seg_make(uint32_t kind, uint32_t len, uint32
   return ((uint64_t)kind << 62) | ((uint64_t)len << 32) | (uint64_t)src;
 }
 
+// LDS-typed views: reads through them compile to ds_* (not flat_*) instructions
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
+
+// the string being evaluated: in the tile's LDS stage (STAGED) or in global memory
+template <bool STAGED>
+struct Src {
+  const uint8_t* p;
+  __device__ __forceinline__ uint8_t operator[](uint32_t i) const {
+    if (STAGED) return ((const lds_u8*)p)[i];
+    return gld(p + i);
+  }
+  __device__ __forceinline__ uint32_t word_at(uintptr_t aligned_addr) const {
+    if (STAGED) return *(const lds_u32*)(const lds_u8*)(const uint8_t*)aligned_addr;
+    return gld((const uint32_t*)aligned_addr);
+  }
+};
+
 // bytes the skip-ahead scan must look at: '\\' and everything >= 0x7B ('{', '}', U+3020's 0xE3,
 // other non-ASCII, '|', '~'). The lowest flagged byte is always a true candidate.
 __device__ __forceinline__ uint32_t special_mask(uint32_t w) {
@@ -44,12 +63,12 @@ __device__ __forceinline__ uint32_t special_mask(uint32_t w) {
 
 // first index j in [i, n) whose byte is a candidate, else n. Reads aligned dwords (an aligned
 // dword never crosses a page, so bytes around the string are safe to read and ignored).
-__device__ __forceinline__ uint32_t next_special(const uint8_t* s, uint32_t i, uint32_t n) {
+template <bool STAGED>
+__device__ __forceinline__ uint32_t next_special(const Src<STAGED>& s, uint32_t i, uint32_t n) {
   while (i < n) {
-    const uintptr_t a = (uintptr_t)(s + i);
+    const uintptr_t a = (uintptr_t)(s.p + i);
     const uint32_t sh = (uint32_t)(a & 3);
-    const uint32_t w = *(const uint32_t*)(a - sh);
-    const uint32_t m = special_mask(w) & (0xFFFFFFFFu << (8 * sh));
+    const uint32_t m = special_mask(s.word_at(a - sh)) & (0xFFFFFFFFu << (8 * sh));
     if (m) {
       const uint32_t j = i + ((uint32_t)__builtin_ctz(m) >> 3) - sh;
       return j < n ? j : n;
@@ -59,13 +78,30 @@ __device__ __forceinline__ uint32_t next_special(const uint8_t* s, uint32_t i, u
   return n;
 }
 
-// copy len bytes src -> dst (either address space): byte head until dst is 4-aligned, dword
-// body with v_alignbyte over the source's aligned dwords, byte tail.
+// copy len bytes src -> dst: byte head until dst is 4-aligned, dword body with v_alignbyte over
+// the source's aligned dwords, byte tail. SRC_LDS / DST_LDS select ds_* vs global access.
+template <bool DST_LDS, bool SRC_LDS>
 __device__ __forceinline__ void copy_bytes(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
                                            uint32_t len) {
+  auto rd8 = [&](uint32_t k) -> uint8_t {
+    if (SRC_LDS) return ((const lds_u8*)src)[k];
+    return gld(src + k);
+  };
+  auto rd32 = [&](const uint32_t* p, uint32_t q) -> uint32_t {
+    if (SRC_LDS) return ((const lds_u32*)(const lds_u8*)(const uint8_t*)p)[q];
+    return gld(p + q);
+  };
+  auto wr8 = [&](uint32_t k, uint8_t v) {
+    if (DST_LDS) ((lds_u8*)dst)[k] = v;
+    else gst(dst + k, v);
+  };
+  auto wr32 = [&](uint32_t* p, uint32_t q, uint32_t v) {
+    if (DST_LDS) ((lds_u32*)(lds_u8*)(uint8_t*)p)[q] = v;
+    else gst(p + q, v);
+  };
   uint32_t k = 0;
   while (k < len && (((uintptr_t)(dst + k)) & 3)) {
-    dst[k] = src[k];
+    wr8(k, rd8(k));
     k++;
   }
   if (k + 4 <= len) {
@@ -75,33 +111,39 @@ __device__ __forceinline__ void copy_bytes(uint8_t* __restrict__ dst, const uint
     uint32_t* d32 = (uint32_t*)(dst + k);
     const uint32_t nw = (len - k) >> 2;
     if (sh == 0) {
-      for (uint32_t q = 0; q < nw; q++) d32[q] = s32[q];
+      for (uint32_t q = 0; q < nw; q++) wr32(d32, q, rd32(s32, q));
     } else {
-      uint32_t w0 = s32[0];
+      uint32_t w0 = rd32(s32, 0);
       for (uint32_t q = 0; q < nw; q++) {
-        const uint32_t w1 = s32[q + 1];
-        d32[q] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+        const uint32_t w1 = rd32(s32, q + 1);
+        wr32(d32, q, __builtin_amdgcn_alignbyte(w1, w0, sh));
         w0 = w1;
       }
     }
     k += nw << 2;
   }
-  for (; k < len; k++) dst[k] = src[k];
+  for (; k < len; k++) wr8(k, rd8(k));
 }
 
 struct LaneLds {
-  uint8_t* kbuf;    // kKeyCap bytes, 4-aligned
-  uint32_t* stack;  // [kMaxDepth] stride kBlock: (key start << 24) | opening offset
-  uint64_t* seg;    // [kMaxSeg] stride kBlock
+  lds_u8* kbuf;     // kKeyCap bytes, 4-aligned
+  lds_u32* stack;   // [kMaxDepth] stride kBlock: (enclosing key length << 24) | opening offset
+  lds_u64* seg;     // [kMaxSeg] stride kBlock
 };
 
-// Evaluate one string. RECORD mode (WRITE = false) stores depth-0 output segments in L.seg and
-// returns their count in nseg (may exceed kMaxSeg: then only the count is valid). WRITE mode
-// copies every segment's bytes to dst as it is produced (only for strings known to be OK_STR).
-template <bool WRITE>
-__device__ uint8_t eval_string(const DevTable& T, const uint8_t* __restrict__ s, uint32_t n,
+// Evaluate one string in ROUNDS: every lane scans (LDS only) up to its next closing brace, then
+// all lanes that reached one probe the table in the same instructions, so a wave pays one memory
+// latency per lookup round instead of one per special byte of any of its lanes.
+// RECORD mode (WRITE = false) stores depth-0 output segments in L.seg and returns their count in
+// nseg (may exceed kMaxSeg: then only the count is valid). WRITE mode copies every segment's
+// bytes to dst as it is produced (only for strings already known to be OK_STR).
+// `active` lanes take part; the call is wave-uniform (all lanes must call it).
+template <bool STAGED, bool WRITE>
+__device__ uint8_t eval_rounds(const DevTable& T, const Src<STAGED> s, uint32_t n, bool active,
                                const LaneLds& L, uint8_t* __restrict__ dst, uint32_t& out_len,
                                uint32_t& vid, uint32_t& nseg) {
+  constexpr uint8_t kRunning = 0xFF;
+  uint8_t status = active ? kRunning : (uint8_t)IE_OK_STR;
   uint32_t depth = 0, klen = 0, olen = 0, ns = 0;
   uint32_t nopen = 0, nclose = 0;
   bool negclose = false;
@@ -111,11 +153,16 @@ __device__ uint8_t eval_string(const DevTable& T, const uint8_t* __restrict__ s,
   bool wrapped = false;  // a whole-string pair resolved (typed result so far in wrap_h)
   Hit wrap_h{0, 0, IE_VID_NONE, 0};
   uint32_t run_start = 0;
+  uint32_t i = 0;
+  // the close waiting for its lookup
+  uint32_t c_open = 0, c_ks = 0, c_kl = 0;
+  bool c_wrapping = false;
 
   auto emit = [&](uint32_t kind, uint32_t len, uint32_t src) {
     if (!len) return;
     if (WRITE) {
-      copy_bytes(dst + olen, kind == kSegTemplate ? s + src : T.arena + src, len);
+      if (kind == kSegTemplate) copy_bytes<false, STAGED>(dst + olen, s.p + src, len);
+      else copy_bytes<false, false>(dst + olen, T.arena + src, len);
     } else if (ns < (uint32_t)kMaxSeg) {
       L.seg[ns * kBlock] = seg_make(kind, len, src);
     }
@@ -127,127 +174,158 @@ __device__ uint8_t eval_string(const DevTable& T, const uint8_t* __restrict__ s,
     L.kbuf[klen++] = c;
     return true;
   };
+  // end of string: the reference's checks in order (py:516-519, 522, 540)
+  auto finish = [&]() -> uint8_t {
+    if (nopen == 0) {
+      emit(kSegTemplate, n - run_start, run_start);
+      return IE_OK_STR;
+    }
+    if (nopen != nclose) return IE_E_ASSERT_BRACES;
+    if (negclose) return kStatusPending;  // balanced but '}{': py break / rs panic
+    if (err_off >= 0) return err_cls;
+    if (wrapped) {
+      vid = wrap_h.vid;
+      return IE_OK_VALUE;
+    }
+    emit(kSegTemplate, n - run_start, run_start);
+    return IE_OK_STR;
+  };
 
-  uint32_t i = 0;
-  while (i < n) {
-    if (depth == 0) {
-      i = next_special(s, i, n);
-      if (i >= n) break;
-    } else {
-      const uint32_t j = next_special(s, i, n);
-      if (klen + (j - i) > (uint32_t)kKeyCap) return kStatusPending;  // long key: literal path
-      for (; i < j; i++) L.kbuf[klen++] = s[i];
-      if (i >= n) break;
-    }
-    const uint8_t c = s[i];
-    if (c == '\\') {
-      const uint8_t nx = i + 1 < n ? s[i + 1] : 0;
-      if (nx == '{' || nx == '}') {  // an escape pair (py:505-508): plain text
-        // '.\}' and '}\}' can restore as '\{...' (py:537-540 replace order): literal path
-        if (nx == '}' && i > 0 && (s[i - 1] == '.' || s[i - 1] == '}')) return kStatusPending;
-        if (depth && !(kput(c) && kput(nx))) return kStatusPending;
-        i += 2;
-        continue;
+  for (;;) {
+    // ---- scan phase: LDS only, up to this lane's next closing brace ----
+    bool need = false;
+    while (status == kRunning) {
+      if (depth == 0) {
+        i = next_special(s, i, n);
+      } else {
+        const uint32_t j = next_special(s, i, n);
+        if (klen + (j - i) > (uint32_t)kKeyCap) {  // long key: literal path
+          status = kStatusPending;
+          break;
+        }
+        for (; i < j; i++) L.kbuf[klen++] = s[i];
       }
-      if (depth && !kput(c)) return kStatusPending;
-      i++;
-      continue;
-    }
-    if (c == '{') {
-      nopen++;
-      if (depth >= (uint32_t)kMaxDepth || i >= (1u << 24)) return kStatusPending;
-      if (depth == 0) emit(kSegTemplate, i - run_start, run_start);
-      const uint32_t ks = (klen + 3) & ~3u;  // keys start dword-aligned
-      if (ks > (uint32_t)kKeyCap) return kStatusPending;
-      L.stack[depth * kBlock] = (ks << 24) | i;
-      klen = ks;
-      poison &= ~(1u << depth);
-      depth++;
-      i++;
-      continue;
-    }
-    if (c == '}') {
-      nclose++;
-      if (depth == 0) {  // unmatched '}': text, unless the count check fails (py:517-519)
-        negclose = true;
+      if (i >= n) {
+        status = finish();
+        break;
+      }
+      const uint8_t c = s[i];
+      if (c == '\\') {
+        const uint8_t nx = i + 1 < n ? s[i + 1] : 0;
+        if (nx == '{' || nx == '}') {  // an escape pair (py:505-508): plain text
+          // '.\}' and '}\}' can restore as '\{...' (py:537-540 replace order): literal path
+          if ((nx == '}' && i > 0 && (s[i - 1] == '.' || s[i - 1] == '}')) ||
+              (depth && !(kput(c) && kput(nx)))) {
+            status = kStatusPending;
+            break;
+          }
+          i += 2;
+          continue;
+        }
+        if (depth && !kput(c)) {
+          status = kStatusPending;
+          break;
+        }
         i++;
         continue;
       }
-      depth--;
-      const uint32_t st = L.stack[depth * kBlock];
-      const uint32_t open = st & 0xFFFFFFu, ks = st >> 24;
-      const uint32_t kl = klen - ks;
-      klen = ks;
-      if ((poison >> depth) & 1u) {  // an inner pair failed first: this one is never evaluated
-        if (depth) poison |= 1u << (depth - 1);
+      if (c == '{') {
+        nopen++;
+        const uint32_t ks = (klen + 3) & ~3u;  // keys start dword-aligned (pad bytes are not key)
+        if (depth >= (uint32_t)kMaxDepth || i >= (1u << 24) || ks > (uint32_t)kKeyCap) {
+          status = kStatusPending;
+          break;
+        }
+        if (depth == 0) emit(kSegTemplate, i - run_start, run_start);
+        L.stack[depth * kBlock] = (klen << 24) | i;  // the enclosing key resumes at klen
+        klen = ks;
+        poison &= ~(1u << depth);
+        depth++;
         i++;
         continue;
       }
-      // a whole-string pair at this nesting level (get_simple_insertkey truthy, py:510-514)
-      const bool wrapping = (open == depth) && (i == n - 1 - depth) && (i - open >= 2);
+      if (c == '}') {
+        nclose++;
+        if (depth == 0) {  // unmatched '}': text, unless the count check fails (py:517-519)
+          negclose = true;
+          i++;
+          continue;
+        }
+        depth--;
+        const uint32_t st = L.stack[depth * kBlock];
+        const uint32_t open = st & 0xFFFFFFu, resume = st >> 24, ks = (resume + 3) & ~3u;
+        c_kl = klen - ks;
+        c_ks = ks;
+        c_open = open;
+        klen = resume;
+        if ((poison >> depth) & 1u) {  // an inner pair failed first: never evaluated
+          if (depth) poison |= 1u << (depth - 1);
+          i++;
+          continue;
+        }
+        // a whole-string pair at this level (get_simple_insertkey truthy, py:510-514)
+        c_wrapping = (open == depth) && (i == n - 1 - depth) && (i - open >= 2);
+        need = true;
+        break;
+      }
+      if (c == 0xE3 && i + 2 < n && s[i + 1] == 0x80 && s[i + 2] == 0xA0) {
+        status = kStatusPending;  // a literal U+3020 collides with the placeholders (py:502-503)
+        break;
+      }
+      if (depth && !kput(c)) {  // other flagged bytes are plain text
+        status = kStatusPending;
+        break;
+      }
+      i++;
+    }
+    if (!__any(need)) break;  // every lane is finished (or pending)
+    // ---- lookup phase: all lanes with a pending close probe together ----
+    if (need) {
       uint8_t est = 0;
       Hit h;
       int32_t b;
-      if (wrapping && wrapped) {
+      if (c_wrapping && wrapped) {
         b = find_raw(T, wrap_h, est, h);  // the key is the inner level's raw value
       } else {
-        b = kl <= kInlineKey ? find_small(T, (const uint32_t*)(L.kbuf + ks), kl, h)
-                             : find_bytes(T, L.kbuf + ks, kl, h);
-        if (b < 0) est = missing_status(T, L.kbuf + ks, kl);
+        b = c_kl <= kInlineKey ? find_small(T, (const uint32_t*)(uint8_t*)(L.kbuf + c_ks), c_kl, h)
+                               : find_bytes(T, (const uint8_t*)(L.kbuf + c_ks), c_kl, h);
+        if (b < 0) est = missing_status(T, (const uint8_t*)(L.kbuf + c_ks), c_kl);
       }
-      if (b >= 0 && !wrapping) {
+      if (b >= 0 && !c_wrapping) {
         if (!(h.flags & EF_SPLICE_OK)) {  // py:530 / interp.rs:76-79
           b = -1;
           est = IE_E_ASSERT_TYPE;
         } else if (!(h.flags & EF_INERT)) {
-          return kStatusPending;  // re-resolution / escape hazard
-        } else if (depth) {       // splice into the enclosing key
-          if (klen + h.text_len > (uint32_t)kKeyCap) return kStatusPending;
-          const uint8_t* t = h.text_len <= kInlineText ? T.buckets[b].text : T.arena + h.text_off;
-          copy_bytes(L.kbuf + klen, t, h.text_len);
-          klen += h.text_len;
+          status = kStatusPending;  // re-resolution / escape hazard
+        } else if (depth) {         // splice into the enclosing key
+          if (klen + h.text_len > (uint32_t)kKeyCap) {
+            status = kStatusPending;
+          } else {
+            const uint8_t* t = h.text_len <= kInlineText ? T.buckets[b].text : T.arena + h.text_off;
+            copy_bytes<true, false>((uint8_t*)(L.kbuf + klen), t, h.text_len);
+            klen += h.text_len;
+          }
         } else {
           emit(kSegValue, h.text_len, h.text_off);
           run_start = i + 1;
         }
       }
       if (b < 0) {
-        if ((int64_t)open > err_off) {
-          err_off = open;
+        if ((int64_t)c_open > err_off) {
+          err_off = c_open;
           err_cls = est;
         }
         if (depth) poison |= 1u << (depth - 1);
-      } else if (wrapping) {
+      } else if (c_wrapping) {
         wrapped = true;
         wrap_h = h;
       }
       i++;
-      continue;
     }
-    if (c == 0xE3 && i + 2 < n && s[i + 1] == 0x80 && s[i + 2] == 0xA0)
-      return kStatusPending;  // a literal U+3020 collides with the placeholders (py:502-503)
-    if (depth && !kput(c)) return kStatusPending;  // other flagged bytes are plain text
-    i++;
   }
   nseg = ns;
-  out_len = 0;
-  if (nopen == 0) {  // no loop at all (py:516): the text as is
-    emit(kSegTemplate, n - run_start, run_start);
-    nseg = ns;
-    out_len = olen;
-    return IE_OK_STR;
-  }
-  if (nopen != nclose) return IE_E_ASSERT_BRACES;  // py:517-519
-  if (negclose) return kStatusPending;             // balanced but '}{': py break / rs panic
-  if (err_off >= 0) return err_cls;
-  if (wrapped) {
-    vid = wrap_h.vid;
-    return IE_OK_VALUE;
-  }
-  emit(kSegTemplate, n - run_start, run_start);
-  nseg = ns;
-  out_len = olen;
-  return IE_OK_STR;
+  out_len = status == IE_OK_STR ? olen : 0;
+  return status;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -259,7 +337,8 @@ __device__ __forceinline__ void publish(uint64_t* state, uint32_t tile, uint64_t
   __hip_atomic_store(state + tile, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ uint64_t look_back(uint64_t* state, uint32_t tile, uint64_t agg, uint32_t* err) {
+__device__ uint64_t look_back(uint64_t* state, uint32_t tile, uint64_t agg, uint32_t* err,
+                              uint32_t* polls) {
   const uint32_t lane = lane_id();
   if (tile == 0) {
     if (lane == 0) publish(state, 0, kFlagIncl | agg);
@@ -279,6 +358,7 @@ __device__ uint64_t look_back(uint64_t* state, uint32_t tile, uint64_t agg, uint
     const uint32_t first = incl_m ? (uint32_t)__builtin_ctzll(incl_m) : 64u;
     const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);
     if (wait_m & need) {
+      if (lane == 0) atomicAdd(polls, 1u);
       __builtin_amdgcn_s_sleep(1);
       // bounded spin: 60 s of s_memrealtime (100 MHz); a missing predecessor is a bug
       if (__builtin_amdgcn_s_memrealtime() - t0 > 6000000000ull) {
@@ -322,27 +402,26 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
                                                     uint64_t cap) {
   __shared__ __attribute__((aligned(16))) uint8_t s_in[kTileBytes + 32];
   __shared__ __attribute__((aligned(16))) uint8_t s_u[kUnionLds];  // eval: keys+stacks; emit: stage
-  __shared__ uint64_t s_seg[kMaxSeg * kBlock];
+  __shared__ __attribute__((aligned(16))) uint64_t s_seg[kMaxSeg * kBlock];
   __shared__ uint32_t s_olen[kBlock];
   __shared__ uint32_t s_vid[kBlock];
   __shared__ uint8_t s_st[kBlock];
   __shared__ uint8_t s_nseg[kBlock];
   __shared__ uint16_t s_pend[kBlock];
-  __shared__ uint32_t s_misc[4];  // tile, pending count, direct-emit flag
+  __shared__ uint32_t s_misc[4];  // tile, pending count
   __shared__ uint64_t s_red[kBlock / 64 + 1];
 
   const uint32_t tid = threadIdx.x, wave = tid >> 6;
   if (tid == 0) {
     s_misc[0] = atomicAdd(W.tile_ticket, 1u);
     s_misc[1] = 0;
-    s_misc[2] = 0;
   }
   __syncthreads();
   const uint32_t tile = s_misc[0];
   const uint64_t first = (uint64_t)tile * kBlock;
   const uint64_t last = min(first + (uint64_t)kBlock, B.n);
   const uint64_t i = first + tid;
-  const uint64_t lo = B.in_off[first], hi = B.in_off[last];
+  const uint64_t lo = gld(B.in_off + first), hi = gld(B.in_off + last);
   const bool staged = (hi - lo) <= (uint64_t)kTileBytes;
   const uintptr_t plo = (uintptr_t)(B.bytes + lo);
   const uint32_t shift = (uint32_t)(plo & 15);
@@ -350,24 +429,35 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
     const uint4* src = (const uint4*)(plo - shift);
     uint4* dst = (uint4*)s_in;
     const uint32_t nv = (uint32_t)((shift + (hi - lo) + 15) >> 4);
-    for (uint32_t j = tid; j < nv; j += kBlock) dst[j] = src[j];
+    for (uint32_t j = tid; j < nv; j += kBlock) dst[j] = gld4(src + j);
   }
   __syncthreads();
 
   // ---- 2. evaluate (fast path) ----
   uint64_t so = 0, sn = 0;
+  const LaneLds L{(lds_u8*)(s_u + tid * kKeyCap), (lds_u32*)(lds_u8*)(s_u + kBlock * kKeyCap) + tid,
+                  (lds_u64*)s_seg + tid};
   const uint8_t* s = nullptr;
-  LaneLds L{s_u + tid * kKeyCap, (uint32_t*)(s_u + kBlock * kKeyCap) + tid, s_seg + tid};
   {
     uint8_t st = IE_OK_STR;
     uint32_t olen = 0, vid = IE_VID_NONE, ns = 0;
+    bool active = false;
     if (i < B.n) {
-      so = B.in_off[i];
-      sn = B.in_off[i + 1] - so;
+      so = gld(B.in_off + i);
+      sn = gld(B.in_off + i + 1) - so;
       s = staged ? s_in + shift + (so - lo) : B.bytes + so;
-      st = sn >= 0xFFFF0000ull ? kStatusPending : eval_string<false>(T, s, (uint32_t)sn, L, nullptr, olen, vid, ns);
+      active = sn < 0xFFFF0000ull;
+      if (!active) st = kStatusPending;
+    }
+    // one wave-uniform call (the rounds vote across the wave); idle lanes ride along
+    const uint8_t r = staged ? eval_rounds<true, false>(T, Src<true>{s}, (uint32_t)sn, active, L, nullptr,
+                                                        olen, vid, ns)
+                             : eval_rounds<false, false>(T, Src<false>{s}, (uint32_t)sn, active, L, nullptr,
+                                                         olen, vid, ns);
+    if (active) st = r;
+    if (i < B.n) {
+      if (st == IE_OK_STR && ns > (uint32_t)kMaxSeg) st = kStatusPending;  // too many segments
       if (st == kStatusPending) s_pend[atomicAdd(&s_misc[1], 1u)] = (uint16_t)tid;
-      if (st == IE_OK_STR && ns > (uint32_t)kMaxSeg) atomicOr(&s_misc[2], 1u);
     }
     s_st[tid] = st;
     s_olen[tid] = st == IE_OK_STR ? olen : 0u;
@@ -378,10 +468,11 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
 
   // ---- 3. literal path for the pending strings, one wave each ----
   const uint32_t npend = s_misc[1];
+  if (tid == 0 && npend) atomicAdd(W.stats, npend);
   for (uint32_t k = wave; k < npend; k += kBlock / 64) {
     const uint32_t j = s_pend[k];
     const uint64_t gi = first + j;
-    const uint64_t po = B.in_off[gi], pn = B.in_off[gi + 1] - po;
+    const uint64_t po = gld(B.in_off + gi), pn = gld(B.in_off + gi + 1) - po;
     uint64_t rcap = W.lit_cap_max ? IE_SIZE_CAP(pn, T.maxtext) + 4 * T.maxtext + 64
                                   : 4 * pn + 4 * T.maxtext + 256;
     rcap = (rcap + 15) & ~15ull;
@@ -407,15 +498,15 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
   uint64_t tile_total;
   const uint64_t local = block_scan(olen, s_red, &tile_total);
   if (wave == 0) {
-    const uint64_t b = look_back(W.tile_state, tile, tile_total, W.err);
+    const uint64_t b = look_back(W.tile_state, tile, tile_total, W.err, W.stats + 2);
     if (tid == 0) s_red[kBlock / 64] = b;
   }
   __syncthreads();
   const uint64_t base = s_red[kBlock / 64];
   if (i < B.n) {
-    B.out_off[i] = base + local;
-    B.status[i] = st;
-    if (st == IE_OK_VALUE) B.value_id[i] = s_vid[tid];
+    gst(B.out_off + i, base + local);
+    gst(B.status + i, st);
+    if (st == IE_OK_VALUE) gst(B.value_id + i, s_vid[tid]);
   }
   if (last == B.n && tid == 0) {
     B.out_off[B.n] = base + tile_total;
@@ -426,26 +517,22 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
   // ---- 5. bytes ----
   uint8_t* g = out + base;
   const uint32_t oshift = (uint32_t)(((uintptr_t)g) & 15);
-  const bool direct = s_misc[2] != 0 || !staged || tile_total + oshift > (uint64_t)kStageBytes;
+  const bool direct = !staged || tile_total + oshift > (uint64_t)kStageBytes;
   const uint32_t ns = s_nseg[tid];
-  if (direct) {  // rare: lanes store their own bytes straight to HBM
+  if (direct) {  // rare (long strings): lanes store their own bytes straight to HBM
+    if (tid == 0) atomicAdd(W.stats + 1, 1u);
     if (i < B.n && st == IE_OK_STR && olen) {
       uint8_t* d = g + local;
-      if (ns > (uint32_t)kMaxSeg) {
-        uint32_t o2 = 0, v2 = 0, n2 = 0;
-        eval_string<true>(T, s, (uint32_t)sn, L, d, o2, v2, n2);
-      } else {
-        uint32_t w = 0;
-        for (uint32_t k = 0; k < ns; k++) {
-          const uint64_t sg = s_seg[k * kBlock + tid];
-          const uint32_t kind = (uint32_t)(sg >> 62), len = (uint32_t)(sg >> 32) & 0x3FFFFFFFu,
-                         src = (uint32_t)sg;
-          const uint8_t* p = kind == kSegTemplate ? s + src
-                             : kind == kSegValue  ? T.arena + src
-                                                  : W.pool + ((uint64_t)src << 4);
-          for (uint32_t q = 0; q < len; q++) d[w + q] = p[q];
-          w += len;
-        }
+      uint32_t w = 0;
+      for (uint32_t k = 0; k < ns; k++) {
+        const uint64_t sg = ((const lds_u64*)s_seg)[k * kBlock + tid];
+        const uint32_t kind = (uint32_t)(sg >> 62), len = (uint32_t)(sg >> 32) & 0x3FFFFFFFu,
+                       src = (uint32_t)sg;
+        const uint8_t* p = kind == kSegTemplate ? s + src
+                           : kind == kSegValue  ? T.arena + src
+                                                : W.pool + ((uint64_t)src << 4);
+        for (uint32_t q = 0; q < len; q++) gst(d + w + q, p[q]);
+        w += len;
       }
     }
     return;
@@ -455,15 +542,15 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
     uint8_t* d = s_u + oshift + local;
     uint32_t w = 0;
     for (uint32_t k = 0; k < ns; k++) {
-      const uint64_t sg = s_seg[k * kBlock + tid];
+      const uint64_t sg = ((const lds_u64*)s_seg)[k * kBlock + tid];
       const uint32_t kind = (uint32_t)(sg >> 62), len = (uint32_t)(sg >> 32) & 0x3FFFFFFFu,
                      src = (uint32_t)sg;
       if (kind == kSegTemplate)
-        copy_bytes(d + w, s + src, len);
+        copy_bytes<true, true>(d + w, s + src, len);
       else if (kind == kSegValue)
-        copy_bytes(d + w, T.arena + src, len);
+        copy_bytes<true, false>(d + w, T.arena + src, len);
       else
-        copy_bytes(d + w, W.pool + ((uint64_t)src << 4), len);
+        copy_bytes<true, false>(d + w, W.pool + ((uint64_t)src << 4), len);
       w += len;
     }
   }
@@ -472,18 +559,18 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
   const uintptr_t pg = (uintptr_t)g, pe = pg + tile_total;
   const uintptr_t a_up = (pg + 15) & ~(uintptr_t)15, b_down = pe & ~(uintptr_t)15;
   if (a_up >= b_down) {
-    for (uint32_t k = tid; k < tile_total; k += kBlock) g[k] = s_u[oshift + k];
+    for (uint32_t k = tid; k < tile_total; k += kBlock) gst(g + k, s_u[oshift + k]);
   } else {
     const uint32_t head = (uint32_t)(a_up - pg), tail = (uint32_t)(pe - b_down);
-    if (tid < head) g[tid] = s_u[oshift + tid];
+    if (tid < head) gst(g + tid, s_u[oshift + tid]);
     if (tid < tail) {
       const uint32_t k = (uint32_t)(b_down - pg) + tid;
-      g[k] = s_u[oshift + k];
+      gst(g + k, s_u[oshift + k]);
     }
     const uint32_t nv = (uint32_t)((b_down - a_up) >> 4);
     const uint4* src = (const uint4*)(s_u + oshift + head);
     uint4* dstv = (uint4*)a_up;
-    for (uint32_t j = tid; j < nv; j += kBlock) dstv[j] = src[j];
+    for (uint32_t j = tid; j < nv; j += kBlock) gst4(dstv + j, src[j]);
   }
 }
 
