@@ -6,7 +6,8 @@
 //                   one probe is one line; open addressing with linear probing, cap =
 //                   next_pow2(2 * entries) keeps probe chains short (load factor <= 0.5)
 //   arena[...]      every key and splice text (texts 4-byte aligned, for dword copies)
-// The hash is a polynomial hash over the key bytes (mod 2^64); slot = fmix64(hash, len) & mask.
+// The key hash mixes the key's little-endian 4-byte words (zero padded) seeded with its length;
+// slot = fmix64(hash) & mask.
 #pragma once
 #include <stdint.h>
 
@@ -18,9 +19,22 @@
 
 namespace ie {
 
-constexpr uint64_t kHashP = 0x100000001B3ull;
+IE_HD uint64_t hash_word(uint64_t h, uint32_t w) {
+  h = (h ^ (uint64_t)w) * 0x9E3779B97F4A7C15ull;
+  return h ^ (h >> 32);
+}
 
-IE_HD uint64_t hash_step(uint64_t h, uint8_t b) { return h * kHashP + (uint64_t)b + 1ull; }
+// hash of n key bytes (any address space via the byte reader)
+template <class ByteAt>
+IE_HD uint64_t hash_key(uint32_t n, ByteAt at) {
+  uint64_t h = 0xA0761D6478BD642Full ^ (uint64_t)n;
+  for (uint32_t j = 0; j < n; j += 4) {
+    uint32_t w = 0;
+    for (uint32_t b = 0; b < 4 && j + b < n; b++) w |= (uint32_t)at(j + b) << (8 * b);
+    h = hash_word(h, w);
+  }
+  return h;
+}
 
 IE_HD uint64_t fmix64(uint64_t k) {
   k ^= k >> 33;
@@ -31,9 +45,7 @@ IE_HD uint64_t fmix64(uint64_t k) {
   return k;
 }
 
-IE_HD uint32_t slot_of(uint64_t h, uint32_t len, uint32_t mask) {
-  return (uint32_t)fmix64(h ^ ((uint64_t)len << 40)) & mask;
-}
+IE_HD uint32_t slot_of(uint64_t h, uint32_t mask) { return (uint32_t)fmix64(h) & mask; }
 
 // Bucket.flags
 enum : uint32_t {

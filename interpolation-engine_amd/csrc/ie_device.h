@@ -76,9 +76,8 @@ __device__ __forceinline__ Hit hit_of(uint4 q0, uint4 q1) {
 
 // Probe for a key whose bytes are at `key` (any address space). Returns the bucket or -1.
 __device__ int32_t find_bytes(const DevTable& T, const uint8_t* key, uint32_t klen, Hit& h) {
-  uint64_t hash = 0;
-  for (uint32_t j = 0; j < klen; j++) hash = hash_step(hash, key[j]);
-  uint32_t s = slot_of(hash, klen, T.mask);
+  const uint64_t hash = hash_key(klen, [&](uint32_t j) { return key[j]; });
+  uint32_t s = slot_of(hash, T.mask);
   for (uint32_t probe = 0; probe <= T.mask; probe++) {
     const uint4* bp = (const uint4*)(T.buckets + s);
     const uint4 q0 = gld4(bp), q1 = gld4(bp + 1);
@@ -93,25 +92,26 @@ __device__ int32_t find_bytes(const DevTable& T, const uint8_t* key, uint32_t kl
   return -1;
 }
 
-// Probe for a key held in LDS at a 4-byte aligned address, klen <= kInlineKey: the whole probe
-// is one 64-byte burst (header + inline key) compared dword-wise in registers.
-__device__ __forceinline__ int32_t find_small(const DevTable& T, const uint32_t* key32, uint32_t klen,
-                                              Hit& h) {
+// Probe for a key held in LDS at a 4-byte aligned address, klen <= kInlineKey: the key is read
+// as dwords, hashed word-wise, and each probe is one 64-byte burst (header + inline key) compared
+// dword-wise in registers.
+__device__ __forceinline__ int32_t find_small(const DevTable& T, const __attribute__((address_space(3))) uint32_t* key32,
+                                              uint32_t klen, Hit& h) {
+  const uint32_t nw = (klen + 3) >> 2;
+  uint64_t hash = 0xA0761D6478BD642Full ^ (uint64_t)klen;
   uint32_t kw[8];
-  uint64_t hash = 0;
 #pragma unroll
   for (int d = 0; d < 8; d++) {
-    kw[d] = (4u * d < klen) ? key32[d] : 0u;
-#pragma unroll
-    for (int b = 0; b < 4; b++)
-      if (4u * d + b < klen) hash = hash_step(hash, (uint8_t)(kw[d] >> (8 * b)));
-  }
-#pragma unroll
-  for (int d = 0; d < 8; d++) {  // zero the bytes past the key: buckets are zero padded
     const int32_t rem = (int32_t)klen - 4 * d;
-    if (rem < 4) kw[d] &= rem <= 0 ? 0u : ((1u << (8 * rem)) - 1u);
+    kw[d] = 0;
+    if (rem > 0) {
+      const uint32_t w = key32[d];
+      kw[d] = rem >= 4 ? w : (w & ((1u << (8 * rem)) - 1u));  // buckets are zero padded
+      hash = hash_word(hash, kw[d]);
+    }
   }
-  uint32_t s = slot_of(hash, klen, T.mask);
+  (void)nw;
+  uint32_t s = slot_of(hash, T.mask);
   for (uint32_t probe = 0; probe <= T.mask; probe++) {
     const uint4* bp = (const uint4*)(T.buckets + s);
     const uint4 q0 = gld4(bp), q1 = gld4(bp + 1), q2 = gld4(bp + 2), q3 = gld4(bp + 3);

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -98,9 +99,11 @@ struct ie_exec {
   DevBuf in_bytes, in_off, o_bytes, o_off, o_status, o_vid, o_total;
   // synth scratch
   DevBuf s_lens, s_part;
+  DevBuf stamps;        // diagnostic phase stamps (env IE_DEBUG_STAMPS=<file>)
+  uint64_t stamp_tiles = 0;
   ~ie_exec() {
     for (DevBuf* b : {&counters, &tile_state, &pool, &out_len, &tile_sum, &tile_base, &in_bytes,
-                      &in_off, &o_bytes, &o_off, &o_status, &o_vid, &o_total, &s_lens, &s_part})
+                      &in_off, &o_bytes, &o_off, &o_status, &o_vid, &o_total, &s_lens, &s_part, &stamps})
       b->release();
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
@@ -153,10 +156,8 @@ uint32_t kind_flags(int32_t kind, int32_t dialect) {
   return f;
 }
 
-uint64_t poly_hash(const std::string_view k) {
-  uint64_t h = 0;
-  for (unsigned char c : k) h = hash_step(h, c);
-  return h;
+uint64_t key_hash(const std::string_view k) {
+  return hash_key((uint32_t)k.size(), [&](uint32_t j) { return (uint8_t)k[j]; });
 }
 
 int set_device(int32_t dev) {
@@ -187,6 +188,7 @@ Work make_work(ie_exec* x, uint64_t* total) {
   W.tile_ticket = (uint32_t*)x->counters.p;
   W.err = (uint32_t*)x->counters.p + 1;
   W.stats = (uint32_t*)x->counters.p + 4;
+  W.stamps = x->stamp_tiles ? (uint64_t*)x->stamps.p : nullptr;
   W.pool_used = (uint64_t*)x->counters.p + 1;
   W.tile_state = (uint64_t*)x->tile_state.p;
   W.pool = (uint8_t*)x->pool.p;
@@ -211,6 +213,12 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
   if (n > 0xFFFFFFF0ull) return fail(IE_ERR_INVALID, "batch larger than 2^32 strings");
   rc = ensure_work(x, op, n);
   if (rc) return rc;
+  x->stamp_tiles = 0;
+  if (op == kOpInterp && getenv("IE_DEBUG_STAMPS")) {  // diagnostic build hook, see DESIGN.md
+    const uint64_t tiles = (n + kBlock - 1) / kBlock;
+    IE_HIP(x->stamps.ensure(tiles * 64));
+    x->stamp_tiles = tiles;
+  }
   Batch B{d_bytes, d_off, n, out->offsets, out->status, out->value_id};
   Work W = make_work(x, out->total);
   hipStream_t st = x->stream;
@@ -427,7 +435,7 @@ int ie_table_build(const ie_kv* kv, uint64_t n, int32_t dialect, const ie_clock*
     if (arena.size() >= 0xFFFFFFF0ull) return fail(IE_ERR_INVALID, "table arena above 4 GiB");
     maxtext = std::max<uint64_t>(maxtext, e.text.size());
     Bucket b{};
-    b.hash = poly_hash(e.key);
+    b.hash = key_hash(e.key);
     b.key_len = (uint32_t)e.key.size();
     b.text_len = (uint32_t)e.text.size();
     b.vid = e.vid;
@@ -436,7 +444,7 @@ int ie_table_build(const ie_kv* kv, uint64_t n, int32_t dialect, const ie_clock*
     b.text_off = (uint32_t)toff;
     if (e.key.size() <= kInlineKey) memcpy(b.key, e.key.data(), e.key.size());
     if (e.text.size() <= kInlineText) memcpy(b.text, e.text.data(), e.text.size());
-    uint32_t sl = slot_of(b.hash, b.key_len, (uint32_t)(cap - 1));
+    uint32_t sl = slot_of(b.hash, (uint32_t)(cap - 1));
     while (buckets[sl].flags & EF_OCCUPIED) sl = (sl + 1) & (uint32_t)(cap - 1);
     buckets[sl] = b;
   }
@@ -527,6 +535,15 @@ int ie_exec_set_timing(ie_exec* x, int32_t enabled) {
 
 int ie_exec_timing(ie_exec* x, ie_timing* out) {
   if (!x || !out) return fail(IE_ERR_INVALID, "null argument");
+  if (x->stamp_tiles && getenv("IE_DEBUG_STAMPS")) {  // dump the last call's phase stamps
+    IE_HIP(hipStreamSynchronize(x->stream));
+    std::vector<uint64_t> h(x->stamp_tiles * 8);
+    IE_HIP(hipMemcpy(h.data(), x->stamps.p, h.size() * 8, hipMemcpyDeviceToHost));
+    if (FILE* f = fopen(getenv("IE_DEBUG_STAMPS"), "wb")) {
+      fwrite(h.data(), 8, h.size(), f);
+      fclose(f);
+    }
+  }
   memset(out, 0, sizeof *out);
   if (!x->ev_recorded) return fail(IE_ERR_INVALID, "no timed call recorded");
   IE_HIP(hipStreamSynchronize(x->stream));

@@ -32,6 +32,7 @@ struct Work {
   uint64_t* tile_state;  // tiles: look-back words (zeroed per call)
   uint32_t* err;         // 1   look-back timeout flag
   uint32_t* stats;       // 3   telemetry: literal strings, direct tiles, look-back polls
+  uint64_t* stamps;      // diagnostic (IE_DEBUG_STAMPS): 8 words per tile, or null
   uint8_t* pool;         // literal-path scratch
   uint64_t* pool_used;   // 1
   uint64_t pool_bytes;

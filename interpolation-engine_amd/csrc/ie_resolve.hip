@@ -287,7 +287,7 @@ __device__ uint8_t eval_rounds(const DevTable& T, const Src<STAGED> s, uint32_t 
       if (c_wrapping && wrapped) {
         b = find_raw(T, wrap_h, est, h);  // the key is the inner level's raw value
       } else {
-        b = c_kl <= kInlineKey ? find_small(T, (const uint32_t*)(uint8_t*)(L.kbuf + c_ks), c_kl, h)
+        b = c_kl <= kInlineKey ? find_small(T, (const lds_u32*)(L.kbuf + c_ks), c_kl, h)
                                : find_bytes(T, (const uint8_t*)(L.kbuf + c_ks), c_kl, h);
         if (b < 0) est = missing_status(T, (const uint8_t*)(L.kbuf + c_ks), c_kl);
       }
@@ -321,6 +321,221 @@ __device__ uint8_t eval_rounds(const DevTable& T, const Src<STAGED> s, uint32_t 
         wrap_h = h;
       }
       i++;
+    }
+  }
+  nseg = ns;
+  out_len = status == IE_OK_STR ? olen : 0;
+  return status;
+}
+
+// ------------------------------------------------------------------------------------------
+// Cooperative classification of a staged tile: one 16-bit mask per 16-byte LDS chunk, bit k set
+// when byte k is '{', '}', '\' or 0xE3 (U+3020's lead byte): the only bytes that can change the
+// reference's result. Exact per-byte test: no carries cross bytes.
+// ------------------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {  // 0x80 in every zero byte of x
+  return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+}
+__device__ __forceinline__ uint32_t event_nibble(uint32_t w) {
+  const uint32_t z = zero_bytes(w ^ 0x7B7B7B7Bu) | zero_bytes(w ^ 0x7D7D7D7Du) |
+                     zero_bytes(w ^ 0x5C5C5C5Cu) | zero_bytes(w ^ 0xE3E3E3E3u);
+  return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+}
+
+// Event-driven evaluation of a staged string: the same rounds and the same semantics as
+// eval_rounds, but the lane visits only its event bytes (from the chunk masks) and copies key
+// text between events with dword copies. s = the string in LDS at stage position p0.
+__device__ uint8_t eval_events(const DevTable& T, const lds_u8* s, uint32_t p0, uint32_t n,
+                               const lds_u16* cm, bool active, const LaneLds& L, uint32_t& out_len,
+                               uint32_t& vid, uint32_t& nseg) {
+  constexpr uint8_t kRunning = 0xFF;
+  uint8_t status = active ? kRunning : (uint8_t)IE_OK_STR;
+  uint32_t depth = 0, klen = 0, olen = 0, ns = 0;
+  uint32_t nopen = 0, nclose = 0;
+  bool negclose = false;
+  uint32_t poison = 0;
+  int64_t err_off = -1;
+  uint8_t err_cls = 0;
+  bool wrapped = false;
+  Hit wrap_h{0, 0, IE_VID_NONE, 0};
+  uint32_t run_start = 0;
+  uint32_t c_open = 0, c_ks = 0, c_kl = 0, c_pos = 0;
+  bool c_wrapping = false;
+  // event cursor over the chunk masks
+  const uint32_t end = p0 + n;
+  uint32_t ch = p0 >> 4, m = 0, skip_below = 0, last = 0;
+  bool m_loaded = false;
+
+  auto next_event = [&]() -> uint32_t {  // string-relative position of the next event, or n
+    for (;;) {
+      if (!m_loaded) {
+        const uint32_t cb = ch << 4;
+        if (cb >= end) return n;
+        m = cm[ch];
+        if (cb < p0) m &= 0xFFFFu << (p0 - cb);
+        if (cb + 16 > end) m &= (1u << (end - cb)) - 1u;
+        m_loaded = true;
+      }
+      if (m) {
+        const uint32_t e = (ch << 4) + (uint32_t)__builtin_ctz(m) - p0;
+        m &= m - 1;
+        if (e < skip_below) continue;
+        return e;
+      }
+      ch++;
+      m_loaded = false;
+    }
+  };
+  auto emit = [&](uint32_t kind, uint32_t len, uint32_t src) {
+    if (!len) return;
+    if (ns < (uint32_t)kMaxSeg) L.seg[ns * kBlock] = seg_make(kind, len, src);
+    ns++;
+    olen += len;
+  };
+  auto kput = [&](uint8_t c) -> bool {
+    if (klen >= (uint32_t)kKeyCap) return false;
+    L.kbuf[klen++] = c;
+    return true;
+  };
+  auto finish = [&]() -> uint8_t {
+    if (nopen == 0) {
+      emit(kSegTemplate, n - run_start, run_start);
+      return IE_OK_STR;
+    }
+    if (nopen != nclose) return IE_E_ASSERT_BRACES;  // py:517-519
+    if (negclose) return kStatusPending;             // balanced but '}{'
+    if (err_off >= 0) return err_cls;
+    if (wrapped) {
+      vid = wrap_h.vid;
+      return IE_OK_VALUE;
+    }
+    emit(kSegTemplate, n - run_start, run_start);
+    return IE_OK_STR;
+  };
+
+  for (;;) {
+    bool need = false;
+    while (status == kRunning) {
+      const uint32_t e = next_event();
+      if (depth) {  // the template bytes since the last event are key text
+        const uint32_t len = e - last;
+        if (klen + len > (uint32_t)kKeyCap) {
+          status = kStatusPending;
+          break;
+        }
+        copy_bytes<true, true>((uint8_t*)(L.kbuf + klen), (const uint8_t*)(s + last), len);
+        klen += len;
+      }
+      if (e >= n) {
+        status = finish();
+        break;
+      }
+      const uint8_t c = s[e];
+      last = e + 1;
+      if (c == '\\') {
+        const uint8_t nx = e + 1 < n ? s[e + 1] : 0;
+        if (nx == '{' || nx == '}') {  // escape pair (py:505-508)
+          if ((nx == '}' && e > 0 && (s[e - 1] == '.' || s[e - 1] == '}')) ||
+              (depth && !(kput(c) && kput(nx)))) {
+            status = kStatusPending;
+            break;
+          }
+          skip_below = e + 2;
+          last = e + 2;
+          continue;
+        }
+        if (depth && !kput(c)) {
+          status = kStatusPending;
+          break;
+        }
+        continue;
+      }
+      if (c == 0xE3) {
+        if ((e + 2 < n && s[e + 1] == 0x80 && s[e + 2] == 0xA0) || (depth && !kput(c))) {
+          status = kStatusPending;  // U+3020 collides with the placeholders (py:502-503)
+          break;
+        }
+        continue;
+      }
+      if (c == '{') {
+        nopen++;
+        const uint32_t ks = (klen + 3) & ~3u;
+        if (depth >= (uint32_t)kMaxDepth || ks > (uint32_t)kKeyCap) {
+          status = kStatusPending;
+          break;
+        }
+        if (depth == 0) emit(kSegTemplate, e - run_start, run_start);
+        L.stack[depth * kBlock] = (klen << 24) | e;
+        klen = ks;
+        poison &= ~(1u << depth);
+        depth++;
+        continue;
+      }
+      // '}'
+      nclose++;
+      if (depth == 0) {
+        negclose = true;
+        continue;
+      }
+      depth--;
+      const uint32_t st = L.stack[depth * kBlock];
+      const uint32_t open = st & 0xFFFFFFu, resume = st >> 24, ks = (resume + 3) & ~3u;
+      c_kl = klen - ks;
+      c_ks = ks;
+      c_open = open;
+      c_pos = e;
+      klen = resume;
+      if ((poison >> depth) & 1u) {
+        if (depth) poison |= 1u << (depth - 1);
+        continue;
+      }
+      c_wrapping = (open == depth) && (e == n - 1 - depth) && (e - open >= 2);
+      need = true;
+      break;
+    }
+    if (!__any(need)) break;
+    if (need) {
+      uint8_t est = 0;
+      Hit h;
+      int32_t b;
+      if (c_wrapping && wrapped) {
+        b = find_raw(T, wrap_h, est, h);
+      } else {
+        b = c_kl <= kInlineKey ? find_small(T, (const lds_u32*)(L.kbuf + c_ks), c_kl, h)
+                               : find_bytes(T, (const uint8_t*)(L.kbuf + c_ks), c_kl, h);
+        if (b < 0) est = missing_status(T, (const uint8_t*)(L.kbuf + c_ks), c_kl);
+      }
+      if (b >= 0 && !c_wrapping) {
+        if (!(h.flags & EF_SPLICE_OK)) {
+          b = -1;
+          est = IE_E_ASSERT_TYPE;
+        } else if (!(h.flags & EF_INERT)) {
+          status = kStatusPending;
+        } else if (depth) {
+          if (klen + h.text_len > (uint32_t)kKeyCap) {
+            status = kStatusPending;
+          } else {
+            const uint8_t* t = h.text_len <= kInlineText ? T.buckets[b].text : T.arena + h.text_off;
+            copy_bytes<true, false>((uint8_t*)(L.kbuf + klen), t, h.text_len);
+            klen += h.text_len;
+          }
+        } else {
+          emit(kSegValue, h.text_len, h.text_off);
+          run_start = c_pos + 1;
+        }
+      }
+      if (b < 0) {
+        if ((int64_t)c_open > err_off) {
+          err_off = c_open;
+          err_cls = est;
+        }
+        if (depth) poison |= 1u << (depth - 1);
+      } else if (c_wrapping) {
+        wrapped = true;
+        wrap_h = h;
+      }
     }
   }
   nseg = ns;
@@ -410,14 +625,30 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
   __shared__ uint16_t s_pend[kBlock];
   __shared__ uint32_t s_misc[4];  // tile, pending count
   __shared__ uint64_t s_red[kBlock / 64 + 1];
+  __shared__ uint16_t s_cm[(kTileBytes + 32) / 16];  // event masks of the staged chunks
 
   const uint32_t tid = threadIdx.x, wave = tid >> 6;
+  uint64_t t_start = 0;
   if (tid == 0) {
+    if (W.stamps) t_start = __builtin_amdgcn_s_memrealtime();
     s_misc[0] = atomicAdd(W.tile_ticket, 1u);
     s_misc[1] = 0;
   }
   __syncthreads();
   const uint32_t tile = s_misc[0];
+  // diagnostic phase stamps (100 MHz s_memrealtime), one row of 8 words per tile
+  uint64_t* const stamp_row = W.stamps ? W.stamps + (uint64_t)tile * 8 : nullptr;
+#define IE_STAMP(k)                                                                  \
+  do {                                                                               \
+    if (stamp_row && tid == 0) stamp_row[k] = __builtin_amdgcn_s_memrealtime();      \
+  } while (0)
+  if (stamp_row && tid == 0) {
+    stamp_row[0] = t_start;
+    uint32_t hw = 0, xcc = 0;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    stamp_row[7] = ((uint64_t)xcc << 32) | hw;
+  }
   const uint64_t first = (uint64_t)tile * kBlock;
   const uint64_t last = min(first + (uint64_t)kBlock, B.n);
   const uint64_t i = first + tid;
@@ -430,8 +661,15 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
     uint4* dst = (uint4*)s_in;
     const uint32_t nv = (uint32_t)((shift + (hi - lo) + 15) >> 4);
     for (uint32_t j = tid; j < nv; j += kBlock) dst[j] = gld4(src + j);
+    __syncthreads();
+    for (uint32_t c = tid; c < nv; c += kBlock) {  // classify: one event mask per chunk
+      const lds_u32* w = (const lds_u32*)(lds_u8*)s_in + 4 * c;
+      ((lds_u16*)s_cm)[c] = (uint16_t)(event_nibble(w[0]) | (event_nibble(w[1]) << 4) |
+                                       (event_nibble(w[2]) << 8) | (event_nibble(w[3]) << 12));
+    }
   }
   __syncthreads();
+  IE_STAMP(1);
 
   // ---- 2. evaluate (fast path) ----
   uint64_t so = 0, sn = 0;
@@ -450,8 +688,9 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
       if (!active) st = kStatusPending;
     }
     // one wave-uniform call (the rounds vote across the wave); idle lanes ride along
-    const uint8_t r = staged ? eval_rounds<true, false>(T, Src<true>{s}, (uint32_t)sn, active, L, nullptr,
-                                                        olen, vid, ns)
+    const uint32_t p0 = shift + (uint32_t)(so - lo);
+    const uint8_t r = staged ? eval_events(T, (const lds_u8*)s_in + p0, p0, (uint32_t)sn, (const lds_u16*)s_cm,
+                                           active, L, olen, vid, ns)
                              : eval_rounds<false, false>(T, Src<false>{s}, (uint32_t)sn, active, L, nullptr,
                                                          olen, vid, ns);
     if (active) st = r;
@@ -465,6 +704,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
     s_nseg[tid] = (uint8_t)(ns > 255u ? 255u : ns);
   }
   __syncthreads();
+  IE_STAMP(2);
 
   // ---- 3. literal path for the pending strings, one wave each ----
   const uint32_t npend = s_misc[1];
@@ -491,6 +731,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
     }
   }
   __syncthreads();
+  IE_STAMP(3);
 
   // ---- 4. offsets: workgroup scan + decoupled look-back ----
   const uint8_t st = s_st[tid];
@@ -502,6 +743,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
     if (tid == 0) s_red[kBlock / 64] = b;
   }
   __syncthreads();
+  IE_STAMP(4);
   const uint64_t base = s_red[kBlock / 64];
   if (i < B.n) {
     gst(B.out_off + i, base + local);
@@ -535,6 +777,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
         w += len;
       }
     }
+    IE_STAMP(5);
     return;
   }
   __syncthreads();  // the union region switches from keys/stacks to the output stage
@@ -572,6 +815,8 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
     uint4* dstv = (uint4*)a_up;
     for (uint32_t j = tid; j < nv; j += kBlock) gst4(dstv + j, src[j]);
   }
+  IE_STAMP(5);
+#undef IE_STAMP
 }
 
 hipError_t launch_resolve(const Batch& B, const Work& W, const DevTable& T, uint8_t* out, uint64_t cap,
