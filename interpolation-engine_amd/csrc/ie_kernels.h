@@ -9,10 +9,10 @@ namespace ie {
 
 constexpr int kBlock = 256;          // lanes per workgroup = strings per tile
 constexpr int kMaxDepth = 6;         // fast-path nesting limit (deeper: literal path)
-constexpr int kKeyCap = 48;          // fast-path key bytes per lane (longer keys: literal path)
+constexpr int kKeyCap = 40;          // fast-path key bytes per lane (longer keys: literal path)
 constexpr int kMaxSeg = 7;           // depth-0 output segments recorded per string
-constexpr int kTileBytes = 18432;    // LDS input stage; larger tiles read global memory directly
-constexpr int kStageBytes = 20480;   // LDS output stage; larger tiles store directly
+constexpr int kTileBytes = 17920;    // LDS input stage; larger tiles read global memory directly
+constexpr int kStageBytes = 10240;   // LDS output stage per half tile; larger halves store directly
 
 enum { kOpInterp = 0, kOpUnescape = 1, kOpEscape = 2 };
 

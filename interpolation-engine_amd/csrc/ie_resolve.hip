@@ -618,13 +618,12 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
   __shared__ __attribute__((aligned(16))) uint8_t s_in[kTileBytes + 32];
   __shared__ __attribute__((aligned(16))) uint8_t s_u[kUnionLds];  // eval: keys+stacks; emit: stage
   __shared__ __attribute__((aligned(16))) uint64_t s_seg[kMaxSeg * kBlock];
-  __shared__ uint32_t s_olen[kBlock];
-  __shared__ uint32_t s_vid[kBlock];
+  __shared__ uint32_t s_olen[kBlock];  // output length; the value id for IE_OK_VALUE strings
   __shared__ uint8_t s_st[kBlock];
   __shared__ uint8_t s_nseg[kBlock];
   __shared__ uint16_t s_pend[kBlock];
   __shared__ uint32_t s_misc[4];  // tile, pending count
-  __shared__ uint64_t s_red[kBlock / 64 + 1];
+  __shared__ uint64_t s_red[kBlock / 64 + 2];
   __shared__ uint16_t s_cm[(kTileBytes + 32) / 16];  // event masks of the staged chunks
 
   const uint32_t tid = threadIdx.x, wave = tid >> 6;
@@ -699,8 +698,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
       if (st == kStatusPending) s_pend[atomicAdd(&s_misc[1], 1u)] = (uint16_t)tid;
     }
     s_st[tid] = st;
-    s_olen[tid] = st == IE_OK_STR ? olen : 0u;
-    s_vid[tid] = vid;
+    s_olen[tid] = st == IE_OK_STR ? olen : (st == IE_OK_VALUE ? vid : 0u);
     s_nseg[tid] = (uint8_t)(ns > 255u ? 255u : ns);
   }
   __syncthreads();
@@ -724,8 +722,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
       r = w_literal(T, B.bytes + po, pn, W.pool + pbase, rcap, pbase, W.lit_cap_max != 0);
     if (lane_id() == 0) {
       s_st[j] = r.status;
-      s_olen[j] = r.status == IE_OK_STR ? (uint32_t)r.res_len : 0u;
-      s_vid[j] = r.vid;
+      s_olen[j] = r.status == IE_OK_STR ? (uint32_t)r.res_len : (r.status == IE_OK_VALUE ? r.vid : 0u);
       s_seg[j] = seg_make(kSegPool, (uint32_t)r.res_len, (uint32_t)(r.res_off >> 4));
       s_nseg[j] = 1;
     }
@@ -735,9 +732,10 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
 
   // ---- 4. offsets: workgroup scan + decoupled look-back ----
   const uint8_t st = s_st[tid];
-  const uint32_t olen = s_olen[tid];
+  const uint32_t olen = st == IE_OK_STR ? s_olen[tid] : 0u;
   uint64_t tile_total;
   const uint64_t local = block_scan(olen, s_red, &tile_total);
+  if (tid == 128) s_red[kBlock / 64 + 1] = local;  // output offset where the second half starts
   if (wave == 0) {
     const uint64_t b = look_back(W.tile_state, tile, tile_total, W.err, W.stats + 2);
     if (tid == 0) s_red[kBlock / 64] = b;
@@ -748,72 +746,80 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
   if (i < B.n) {
     gst(B.out_off + i, base + local);
     gst(B.status + i, st);
-    if (st == IE_OK_VALUE) gst(B.value_id + i, s_vid[tid]);
+    if (st == IE_OK_VALUE) gst(B.value_id + i, s_olen[tid]);
   }
   if (last == B.n && tid == 0) {
     B.out_off[B.n] = base + tile_total;
     *W.total = base + tile_total;
   }
   if (base + tile_total > cap) return;  // caller's buffer too small: offsets only
+  __syncthreads();  // s_red[kBlock / 64 + 1] (the half boundary) is visible
 
-  // ---- 5. bytes ----
-  uint8_t* g = out + base;
-  const uint32_t oshift = (uint32_t)(((uintptr_t)g) & 15);
-  const bool direct = !staged || tile_total + oshift > (uint64_t)kStageBytes;
-  const uint32_t ns = s_nseg[tid];
-  if (direct) {  // rare (long strings): lanes store their own bytes straight to HBM
-    if (tid == 0) atomicAdd(W.stats + 1, 1u);
-    if (i < B.n && st == IE_OK_STR && olen) {
-      uint8_t* d = g + local;
+  // ---- 5. bytes: each half tile (128 strings) through the LDS stage, then 16-byte stores ----
+  const uint32_t half = tid >> 7;
+  for (uint32_t hsel = 0; hsel < 2; hsel++) {
+    // the half's output range [h_lo, h_hi) relative to the tile
+    const uint64_t h_lo = hsel == 0 ? 0 : s_red[kBlock / 64 + 1];
+    const uint64_t h_hi = hsel == 0 ? s_red[kBlock / 64 + 1] : tile_total;
+    uint8_t* g = out + base + h_lo;
+    const uint64_t h_len = h_hi - h_lo;
+    const uint32_t oshift = (uint32_t)(((uintptr_t)g) & 15);
+    const bool direct = !staged || h_len + oshift > (uint64_t)kStageBytes;
+    const bool mine = half == hsel && i < B.n && st == IE_OK_STR && olen;
+    const uint32_t ns = s_nseg[tid];
+    if (direct) {  // rare (long strings): lanes store their own bytes straight to HBM
+      if (tid == 0) atomicAdd(W.stats + 1, 1u);
+      if (mine) {
+        uint8_t* d = g + (local - h_lo);
+        uint32_t w = 0;
+        for (uint32_t k = 0; k < ns; k++) {
+          const uint64_t sg = ((const lds_u64*)s_seg)[k * kBlock + tid];
+          const uint32_t kind = (uint32_t)(sg >> 62), len = (uint32_t)(sg >> 32) & 0x3FFFFFFFu,
+                         src = (uint32_t)sg;
+          const uint8_t* p = kind == kSegTemplate ? s + src
+                             : kind == kSegValue  ? T.arena + src
+                                                  : W.pool + ((uint64_t)src << 4);
+          for (uint32_t q = 0; q < len; q++) gst(d + w + q, p[q]);
+          w += len;
+        }
+      }
+      continue;
+    }
+    __syncthreads();  // the union region becomes the output stage (keys/stacks are dead)
+    if (mine) {
+      uint8_t* d = s_u + oshift + (local - h_lo);
       uint32_t w = 0;
       for (uint32_t k = 0; k < ns; k++) {
         const uint64_t sg = ((const lds_u64*)s_seg)[k * kBlock + tid];
         const uint32_t kind = (uint32_t)(sg >> 62), len = (uint32_t)(sg >> 32) & 0x3FFFFFFFu,
                        src = (uint32_t)sg;
-        const uint8_t* p = kind == kSegTemplate ? s + src
-                           : kind == kSegValue  ? T.arena + src
-                                                : W.pool + ((uint64_t)src << 4);
-        for (uint32_t q = 0; q < len; q++) gst(d + w + q, p[q]);
+        if (kind == kSegTemplate)
+          copy_bytes<true, true>(d + w, s + src, len);
+        else if (kind == kSegValue)
+          copy_bytes<true, false>(d + w, T.arena + src, len);
+        else
+          copy_bytes<true, false>(d + w, W.pool + ((uint64_t)src << 4), len);
         w += len;
       }
     }
-    IE_STAMP(5);
-    return;
-  }
-  __syncthreads();  // the union region switches from keys/stacks to the output stage
-  if (i < B.n && st == IE_OK_STR && olen) {
-    uint8_t* d = s_u + oshift + local;
-    uint32_t w = 0;
-    for (uint32_t k = 0; k < ns; k++) {
-      const uint64_t sg = ((const lds_u64*)s_seg)[k * kBlock + tid];
-      const uint32_t kind = (uint32_t)(sg >> 62), len = (uint32_t)(sg >> 32) & 0x3FFFFFFFu,
-                     src = (uint32_t)sg;
-      if (kind == kSegTemplate)
-        copy_bytes<true, true>(d + w, s + src, len);
-      else if (kind == kSegValue)
-        copy_bytes<true, false>(d + w, T.arena + src, len);
-      else
-        copy_bytes<true, false>(d + w, W.pool + ((uint64_t)src << 4), len);
-      w += len;
+    __syncthreads();
+    // stream the stage out: LDS position oshift + k holds output byte h_lo + k
+    const uintptr_t pg = (uintptr_t)g, pe = pg + h_len;
+    const uintptr_t a_up = (pg + 15) & ~(uintptr_t)15, b_down = pe & ~(uintptr_t)15;
+    if (a_up >= b_down) {
+      for (uint32_t k = tid; k < h_len; k += kBlock) gst(g + k, s_u[oshift + k]);
+    } else {
+      const uint32_t head = (uint32_t)(a_up - pg), tail = (uint32_t)(pe - b_down);
+      if (tid < head) gst(g + tid, s_u[oshift + tid]);
+      if (tid < tail) {
+        const uint32_t k = (uint32_t)(b_down - pg) + tid;
+        gst(g + k, s_u[oshift + k]);
+      }
+      const uint32_t nv = (uint32_t)((b_down - a_up) >> 4);
+      const uint4* src = (const uint4*)(s_u + oshift + head);
+      uint4* dstv = (uint4*)a_up;
+      for (uint32_t j = tid; j < nv; j += kBlock) gst4(dstv + j, src[j]);
     }
-  }
-  __syncthreads();
-  // stream the stage out: LDS position oshift + k holds output byte base + k
-  const uintptr_t pg = (uintptr_t)g, pe = pg + tile_total;
-  const uintptr_t a_up = (pg + 15) & ~(uintptr_t)15, b_down = pe & ~(uintptr_t)15;
-  if (a_up >= b_down) {
-    for (uint32_t k = tid; k < tile_total; k += kBlock) gst(g + k, s_u[oshift + k]);
-  } else {
-    const uint32_t head = (uint32_t)(a_up - pg), tail = (uint32_t)(pe - b_down);
-    if (tid < head) gst(g + tid, s_u[oshift + tid]);
-    if (tid < tail) {
-      const uint32_t k = (uint32_t)(b_down - pg) + tid;
-      gst(g + k, s_u[oshift + k]);
-    }
-    const uint32_t nv = (uint32_t)((b_down - a_up) >> 4);
-    const uint4* src = (const uint4*)(s_u + oshift + head);
-    uint4* dstv = (uint4*)a_up;
-    for (uint32_t j = tid; j < nv; j += kBlock) gst4(dstv + j, src[j]);
   }
   IE_STAMP(5);
 #undef IE_STAMP
