@@ -755,12 +755,14 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
   if (base + tile_total > cap) return;  // caller's buffer too small: offsets only
   __syncthreads();  // s_red[kBlock / 64 + 1] (the half boundary) is visible
 
-  // ---- 5. bytes: each half tile (128 strings) through the LDS stage, then 16-byte stores ----
-  const uint32_t half = tid >> 7;
-  for (uint32_t hsel = 0; hsel < 2; hsel++) {
-    // the half's output range [h_lo, h_hi) relative to the tile
-    const uint64_t h_lo = hsel == 0 ? 0 : s_red[kBlock / 64 + 1];
-    const uint64_t h_hi = hsel == 0 ? s_red[kBlock / 64 + 1] : tile_total;
+  // ---- 5. bytes: the tile (or, if it does not fit, each half) through the LDS output stage,
+  //      then 16-byte stores ----
+  const uint32_t whole = tile_total + 15 <= (uint64_t)kStageBytes;
+  const uint32_t half = whole ? 0u : tid >> 7;
+  for (uint32_t hsel = 0; hsel < (whole ? 1u : 2u); hsel++) {
+    // the part's output range [h_lo, h_hi) relative to the tile
+    const uint64_t h_lo = whole || hsel == 0 ? 0 : s_red[kBlock / 64 + 1];
+    const uint64_t h_hi = whole ? tile_total : (hsel == 0 ? s_red[kBlock / 64 + 1] : tile_total);
     uint8_t* g = out + base + h_lo;
     const uint64_t h_len = h_hi - h_lo;
     const uint32_t oshift = (uint32_t)(((uintptr_t)g) & 15);
