@@ -33,6 +33,21 @@ WORKLOADS = {
 DEFAULT_N = {2: 1_000_000, 3: 10_000_000}
 
 
+def shard_first(rank, n_per_rank):
+    """First global string index of a rank's shard (weak scaling: every rank owns n strings)."""
+    return rank * n_per_rank
+
+
+def max_over_ranks(x, dist):
+    """Max of a float over all ranks (the step time the driver compares against its clock)."""
+    if dist is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -66,7 +81,7 @@ def main():
 
     cfg = args.config
     n = args.n or DEFAULT_N[cfg]
-    first = rank * n  # this rank's shard of the global string index space
+    first = shard_first(rank, n)  # this rank's shard of the global string index space
 
     synth = ctypes.c_void_p()
     N.check(L.ie_synth_create(cfg, 0, ctypes.byref(synth)), "ie_synth_create")
@@ -118,12 +133,7 @@ def main():
         dist.barrier()
     wall = time.perf_counter() - t0
     step_ms = [x.elapsed(2 * k, 2 * k + 1) for k in range(args.steps)]
-    wall_max = wall
-    if dist:
-        import torch
-        t = torch.tensor([wall], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall_max = float(t.item())
+    wall_max = max_over_ranks(wall, dist)
 
     # one timed call with the library's own HIP events for the kernel split
     x.set_timing(True)
