@@ -189,6 +189,8 @@ Work make_work(ie_exec* x, uint64_t* total) {
   W.err = (uint32_t*)x->counters.p + 1;
   W.stats = (uint32_t*)x->counters.p + 4;
   W.stamps = x->stamp_tiles ? (uint64_t*)x->stamps.p : nullptr;
+  W.debug_noeval = getenv("IE_DEBUG_NOEVAL") ? 1u : 0u;  // diagnostic hooks, see DESIGN.md
+  W.fast_mode = getenv("IE_FAST") ? (uint32_t)atoi(getenv("IE_FAST")) : 0u;
   W.pool_used = (uint64_t*)x->counters.p + 1;
   W.tile_state = (uint64_t*)x->tile_state.p;
   W.pool = (uint8_t*)x->pool.p;

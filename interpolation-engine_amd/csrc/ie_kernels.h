@@ -33,6 +33,8 @@ struct Work {
   uint32_t* err;         // 1   look-back timeout flag
   uint32_t* stats;       // 3   telemetry: literal strings, direct tiles, look-back polls
   uint64_t* stamps;      // diagnostic (IE_DEBUG_STAMPS): 8 words per tile, or null
+  uint32_t debug_noeval; // diagnostic (IE_DEBUG_NOEVAL): copy strings verbatim (pipeline floor)
+  uint32_t fast_mode;    // level evaluator: 0 off, 1 on; diagnostics 2 = parse only, 3 = no probes
   uint8_t* pool;         // literal-path scratch
   uint64_t* pool_used;   // 1
   uint64_t pool_bytes;

@@ -28,7 +28,9 @@
 
 namespace ie {
 
-enum : uint32_t { kSegTemplate = 0, kSegValue = 1, kSegPool = 2 };
+// segment sources: template bytes (string offset), arena text (offset), literal-path pool
+// (16-byte units), a bucket's inline text (bucket index; splice texts <= kInlineText)
+enum : uint32_t { kSegTemplate = 0, kSegValue = 1, kSegPool = 2, kSegBucket = 3 };
 
 __device__ __forceinline__ uint64_t seg_make(uint32_t kind, uint32_t len, uint32_t src) {
   return ((uint64_t)kind << 62) | ((uint64_t)len << 32) | (uint64_t)src;
@@ -123,6 +125,36 @@ __device__ __forceinline__ void copy_bytes(uint8_t* __restrict__ dst, const uint
     k += nw << 2;
   }
   for (; k < len; k++) wr8(k, rd8(k));
+}
+
+// a bucket's inline text (16-byte aligned, len <= kInlineText) -> LDS at any byte offset: the
+// four 16-byte loads go out together (one memory latency), dwords are re-aligned with alignbyte
+__device__ __forceinline__ void put_bucket_text(lds_u8* dst, const Bucket* b, uint32_t len) {
+  const uint4* tp = (const uint4*)b->text;
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  const uint4 t0 = gld4(tp), t1 = len > 16 ? gld4(tp + 1) : z, t2 = len > 32 ? gld4(tp + 2) : z,
+              t3 = len > 48 ? gld4(tp + 3) : z;
+  const uint32_t tw[17] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w,
+                           t2.x, t2.y, t2.z, t2.w, t3.x, t3.y, t3.z, t3.w, 0u};
+  const uint32_t a = (uint32_t)(uintptr_t)dst & 3u;
+  const uint32_t head = min(len, (4u - a) & 3u);
+#pragma unroll
+  for (uint32_t k = 0; k < 3; k++)
+    if (k < head) dst[k] = (uint8_t)(tw[0] >> (8 * k));
+  // dword q of the aligned body = text bytes head + 4q .. head + 4q + 3
+  lds_u32* d32 = (lds_u32*)(dst + head);
+  const uint32_t rest = len - head, nq = rest >> 2, tail = rest & 3u;
+  uint32_t x = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < 16; q++) {
+    const uint32_t v = __builtin_amdgcn_alignbyte(tw[q + 1], tw[q], head);
+    if (q < nq) d32[q] = v;
+    if (q == nq) x = v;
+  }
+  lds_u8* t = dst + head + 4 * nq;
+#pragma unroll
+  for (uint32_t k = 0; k < 3; k++)
+    if (k < tail) t[k] = (uint8_t)(x >> (8 * k));
 }
 
 struct LaneLds {
@@ -338,17 +370,26 @@ typedef __attribute__((address_space(3))) uint16_t lds_u16;
 __device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {  // 0x80 in every zero byte of x
   return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
 }
-__device__ __forceinline__ uint32_t event_nibble(uint32_t w) {
-  const uint32_t z = zero_bytes(w ^ 0x7B7B7B7Bu) | zero_bytes(w ^ 0x7D7D7D7Du) |
-                     zero_bytes(w ^ 0x5C5C5C5Cu) | zero_bytes(w ^ 0xE3E3E3E3u);
+__device__ __forceinline__ uint32_t nibble_of(uint32_t z) {  // bit k: byte k of z has its top bit
   return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+}
+// chunk mask: bits 0-15 '{' / '}', bits 16-31 '\' / 0xE3 ("odd" bytes) of the 16-byte chunk
+__device__ __forceinline__ uint32_t chunk_mask(const lds_u32* w) {
+  uint32_t br = 0, odd = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t x = w[k];
+    br |= nibble_of(zero_bytes(x ^ 0x7B7B7B7Bu) | zero_bytes(x ^ 0x7D7D7D7Du)) << (4 * k);
+    odd |= nibble_of(zero_bytes(x ^ 0x5C5C5C5Cu) | zero_bytes(x ^ 0xE3E3E3E3u)) << (4 * k);
+  }
+  return br | (odd << 16);
 }
 
 // Event-driven evaluation of a staged string: the same rounds and the same semantics as
 // eval_rounds, but the lane visits only its event bytes (from the chunk masks) and copies key
 // text between events with dword copies. s = the string in LDS at stage position p0.
 __device__ uint8_t eval_events(const DevTable& T, const lds_u8* s, uint32_t p0, uint32_t n,
-                               const lds_u16* cm, bool active, const LaneLds& L, uint32_t& out_len,
+                               const lds_u32* cm, bool active, const LaneLds& L, uint32_t& out_len,
                                uint32_t& vid, uint32_t& nseg) {
   constexpr uint8_t kRunning = 0xFF;
   uint8_t status = active ? kRunning : (uint8_t)IE_OK_STR;
@@ -374,6 +415,7 @@ __device__ uint8_t eval_events(const DevTable& T, const lds_u8* s, uint32_t p0, 
         const uint32_t cb = ch << 4;
         if (cb >= end) return n;
         m = cm[ch];
+        m = (m | (m >> 16)) & 0xFFFFu;
         if (cb < p0) m &= 0xFFFFu << (p0 - cb);
         if (cb + 16 > end) m &= (1u << (end - cb)) - 1u;
         m_loaded = true;
@@ -522,7 +564,8 @@ __device__ uint8_t eval_events(const DevTable& T, const lds_u8* s, uint32_t p0, 
             klen += h.text_len;
           }
         } else {
-          emit(kSegValue, h.text_len, h.text_off);
+          if (h.text_len <= kInlineText) emit(kSegBucket, h.text_len, (uint32_t)b);
+          else emit(kSegValue, h.text_len, h.text_off);
           run_start = c_pos + 1;
         }
       }
@@ -541,6 +584,273 @@ __device__ uint8_t eval_events(const DevTable& T, const lds_u8* s, uint32_t p0, 
   nseg = ns;
   out_len = status == IE_OK_STR ? olen : 0;
   return status;
+}
+
+// ------------------------------------------------------------------------------------------
+// Level evaluator for CLEAN strings (the common case): only '{' / '}' events, properly nested to
+// depth <= kFastDepth, <= kFastPairs pairs, <= 3 top-level pairs, no whole-string pair, every
+// lookup a hit on an inert splice-able value with keys <= kInlineKey bytes. For such strings every
+// order of evaluation gives the reference's result (the values never create braces), so pairs are
+// resolved by HEIGHT: round h looks up every pair whose children are all resolved, up to two
+// probes in flight per lane. A lane whose string breaks any condition returns false with nothing
+// committed, and the caller re-evaluates it with eval_events (exact reference semantics).
+// ------------------------------------------------------------------------------------------
+constexpr int kFastDepth = 4;
+constexpr int kFastPairs = 6;
+constexpr int kFastVb = 32;  // bytes of resolved inner values per lane
+
+struct FastLds {
+  lds_u8* kbuf;   // lane-private key buffer (kKeyCap bytes, 4-aligned)
+  lds_u64* pair;  // [kFastPairs] stride kBlock: pair records
+  lds_u8* vbuf;   // lane-private kFastVb bytes: texts of resolved inner pairs
+};
+
+// pair record: open:16 | close:16 | depth:4 | height:4 | vb_off:8 | vlen:8 | top ordinal:8
+__device__ __forceinline__ uint32_t pr_open(uint64_t r) { return (uint32_t)r & 0xFFFFu; }
+__device__ __forceinline__ uint32_t pr_close(uint64_t r) { return (uint32_t)(r >> 16) & 0xFFFFu; }
+__device__ __forceinline__ uint32_t pr_depth(uint64_t r) { return (uint32_t)(r >> 32) & 0xFu; }
+__device__ __forceinline__ uint32_t pr_height(uint64_t r) { return (uint32_t)(r >> 36) & 0xFu; }
+__device__ __forceinline__ uint32_t pr_vboff(uint64_t r) { return (uint32_t)(r >> 40) & 0xFFu; }
+__device__ __forceinline__ uint32_t pr_vlen(uint64_t r) { return (uint32_t)(r >> 48) & 0xFFu; }
+__device__ __forceinline__ uint32_t pr_top(uint64_t r) { return (uint32_t)(r >> 56); }
+
+struct FastKey {
+  uint32_t w[8];  // key bytes, zero padded like the buckets' inline keys
+  uint32_t len;
+  uint64_t hash;
+};
+
+// key of pair `idx`: its template bytes with the direct children replaced by their texts
+__device__ __forceinline__ bool fast_key(const lds_u8* s, const FastLds& F, uint32_t idx, FastKey& K) {
+  const uint64_t rec = F.pair[idx * kBlock];
+  const uint32_t open = pr_open(rec), close = pr_close(rec), d = pr_depth(rec);
+  uint32_t w = 0, pos = open + 1;
+  if (pr_height(rec) > 1) {
+    for (uint32_t j = 0; j < idx; j++) {  // postorder: descendants precede the pair
+      const uint64_t c = F.pair[j * kBlock];
+      if (pr_depth(c) != d + 1 || pr_open(c) < open) continue;
+      const uint32_t t = pr_open(c) - pos, v = pr_vlen(c);
+      if (w + t + v > (uint32_t)kInlineKey) return false;
+      copy_bytes<true, true>((uint8_t*)(F.kbuf + w), (const uint8_t*)(s + pos), t);
+      copy_bytes<true, true>((uint8_t*)(F.kbuf + w + t), (const uint8_t*)(F.vbuf + pr_vboff(c)), v);
+      w += t + v;
+      pos = pr_close(c) + 1;
+    }
+  }
+  const uint32_t t = close - pos;
+  if (w + t > (uint32_t)kInlineKey) return false;
+  copy_bytes<true, true>((uint8_t*)(F.kbuf + w), (const uint8_t*)(s + pos), t);
+  w += t;
+  K.len = w;
+  uint64_t hash = 0xA0761D6478BD642Full ^ (uint64_t)w;
+  const lds_u32* k32 = (const lds_u32*)F.kbuf;
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    const int32_t rem = (int32_t)w - 4 * q;
+    uint32_t x = 0;
+    if (rem > 0) {
+      x = k32[q];
+      if (rem < 4) x &= (1u << (8 * rem)) - 1u;
+      hash = hash_word(hash, x);
+    }
+    K.w[q] = x;
+  }
+  K.hash = hash;
+  return true;
+}
+
+struct FastProbe {
+  uint4 q0, q1, q2, q3, q4, q5;
+};
+
+__device__ __forceinline__ void fast_load(const DevTable& T, uint32_t slot, bool text, FastProbe& P) {
+  const uint4* bp = (const uint4*)(T.buckets + slot);
+  P.q0 = gld4(bp);
+  P.q1 = gld4(bp + 1);
+  P.q2 = gld4(bp + 2);
+  P.q3 = gld4(bp + 3);
+  if (text) {  // inline text bytes 0..31 (an inner value must fit a key, so never longer)
+    P.q4 = gld4(bp + 4);
+    P.q5 = gld4(bp + 5);
+  }
+}
+
+// 0: hit, 1: probe the next slot, 2: miss
+__device__ __forceinline__ uint32_t fast_match(const FastProbe& P, const FastKey& K) {
+  if (!(P.q1.y & EF_OCCUPIED)) return 2;
+  const bool eq = ((((uint64_t)P.q0.y << 32) | P.q0.x) == K.hash) & (P.q0.z == K.len) &
+                  (P.q2.x == K.w[0]) & (P.q2.y == K.w[1]) & (P.q2.z == K.w[2]) & (P.q2.w == K.w[3]) &
+                  (P.q3.x == K.w[4]) & (P.q3.y == K.w[5]) & (P.q3.z == K.w[6]) & (P.q3.w == K.w[7]);
+  return eq ? 0u : 1u;
+}
+
+// commit a hit for pair idx; false when the value is not fast-path material
+__device__ __forceinline__ bool fast_commit(const FastLds& F, const LaneLds& L, uint32_t idx, uint32_t slot,
+                                            const FastProbe& P, uint32_t& vb_used, uint32_t& vsum) {
+  const uint32_t flags = P.q1.y, tlen = P.q0.w;
+  if (!(flags & EF_SPLICE_OK) || !(flags & EF_INERT)) return false;
+  uint64_t rec = F.pair[idx * kBlock];
+  if (pr_depth(rec) == 0) {
+    L.seg[(2 * pr_top(rec) + 1) * kBlock] =
+        tlen <= kInlineText ? seg_make(kSegBucket, tlen, slot) : seg_make(kSegValue, tlen, P.q1.w);
+    vsum += tlen;
+    return true;
+  }
+  if (tlen > (uint32_t)kInlineKey || vb_used + tlen > (uint32_t)kFastVb) return false;
+  const uint32_t tw[8] = {P.q4.x, P.q4.y, P.q4.z, P.q4.w, P.q5.x, P.q5.y, P.q5.z, P.q5.w};
+  lds_u32* v32 = (lds_u32*)(F.vbuf + vb_used);
+#pragma unroll
+  for (int q = 0; q < 8; q++)
+    if (4 * q < (int)tlen) v32[q] = tw[q];
+  rec = (rec & ~(0xFFFFull << 40)) | ((uint64_t)vb_used << 40) | ((uint64_t)tlen << 48);
+  F.pair[idx * kBlock] = rec;
+  vb_used += (tlen + 3) & ~3u;
+  return true;
+}
+
+// Wave-uniform call. s = the string in LDS at stage position p0; cm = chunk masks.
+// On success: depth-0 segments in L.seg (2 * top pairs + 1 of them), nseg, out_len.
+__device__ bool eval_fast(const DevTable& T, const lds_u8* s, uint32_t p0, uint32_t n,
+                          const lds_u32* cm, bool active, uint32_t mode, const FastLds& F, const LaneLds& L,
+                          uint32_t& out_len, uint32_t& nseg) {
+  bool ok = active && n < 0xFFFFu;
+  uint32_t np = 0, H = 0, depth = 0, ntop = 0, run = 0, tmpl = 0;
+  uint32_t st0 = 0, st1 = 0, st2 = 0, st3 = 0;  // open offset | max child height << 16, per level
+  // ---- parse: pair records in close order (LDS only) ----
+  if (ok) {
+    const uint32_t end = p0 + n;
+    for (uint32_t cb = p0 & ~15u; ok && cb < end; cb += 16) {
+      uint32_t keep = 0xFFFFu;
+      if (cb < p0) keep &= 0xFFFFu << (p0 - cb);
+      if (cb + 16 > end) keep &= (1u << (end - cb)) - 1u;
+      const uint32_t cmw = cm[cb >> 4];
+      if ((cmw >> 16) & keep) {  // '\' or 0xE3: escapes / U+3020 need the exact evaluator
+        ok = false;
+        break;
+      }
+      uint32_t m = cmw & keep;
+      while (m) {
+        const uint32_t e = cb + (uint32_t)__builtin_ctz(m) - p0;
+        m &= m - 1;
+        if (s[e] == '{') {
+          if (depth == (uint32_t)kFastDepth) {
+            ok = false;
+            break;
+          }
+          st0 = depth == 0 ? e : st0;
+          st1 = depth == 1 ? e : st1;
+          st2 = depth == 2 ? e : st2;
+          st3 = depth == 3 ? e : st3;
+          depth++;
+          continue;
+        }
+        if (depth == 0 || np == (uint32_t)kFastPairs) {  // '}{' or too many pairs
+          ok = false;
+          break;
+        }
+        depth--;
+        const uint32_t st = depth == 0 ? st0 : depth == 1 ? st1 : depth == 2 ? st2 : st3;
+        const uint32_t open = st & 0xFFFFu, h = (st >> 16) + 1;
+        if (open == depth && e == n - 1 - depth) {  // whole-string pair: typed-result rules
+          ok = false;
+          break;
+        }
+        uint64_t rec = (uint64_t)open | ((uint64_t)e << 16) | ((uint64_t)depth << 32) | ((uint64_t)h << 36);
+        if (depth == 0) {
+          if (2 * ntop + 3 > (uint32_t)kMaxSeg) {
+            ok = false;
+            break;
+          }
+          rec |= (uint64_t)ntop << 56;
+          L.seg[2 * ntop * kBlock] = seg_make(kSegTemplate, open - run, run);
+          tmpl += open - run;
+          run = e + 1;
+          ntop++;
+        } else {  // the parent's height is at least h + 1
+          const uint32_t hp = h << 16;
+          const uint32_t pd = depth - 1;
+          st0 = pd == 0 && (st0 >> 16) < h ? (st0 & 0xFFFFu) | hp : st0;
+          st1 = pd == 1 && (st1 >> 16) < h ? (st1 & 0xFFFFu) | hp : st1;
+          st2 = pd == 2 && (st2 >> 16) < h ? (st2 & 0xFFFFu) | hp : st2;
+        }
+        F.pair[np * kBlock] = rec;
+        np++;
+        H = h > H ? h : H;
+      }
+    }
+    if (depth) ok = false;  // unbalanced: the exact evaluator reports it
+  }
+  // ---- rounds by height: every probe of a round in flight together ----
+  uint32_t vb_used = 0, vsum = 0;
+  if (mode == 2) {  // diagnostic: parse only (output = template)
+    if (ok) nseg = 1, out_len = n, L.seg[0] = seg_make(kSegTemplate, n, 0);
+    return ok;
+  }
+  const uint32_t Hw = (uint32_t)w_max(ok ? (int64_t)H : 0);
+  for (uint32_t h = 1; h <= Hw; h++) {
+    uint32_t hm = 0;
+    if (ok)
+      for (uint32_t j = 0; j < np; j++)
+        if (pr_height(F.pair[j * kBlock]) == h) hm |= 1u << j;
+    while (__any(hm != 0)) {
+      const uint32_t a = hm ? (uint32_t)__builtin_ctz(hm) : 0u;
+      bool pa = hm != 0;
+      hm &= hm - 1;
+      const uint32_t b = hm ? (uint32_t)__builtin_ctz(hm) : 0u;
+      bool pb = hm != 0;
+      hm &= hm - 1;
+      FastKey ka, kb;
+      if (pa && !fast_key(s, F, a, ka)) ok = false;
+      if (pb && ok && !fast_key(s, F, b, kb)) ok = false;
+      if (!ok || mode == 3) pa = pb = false, hm = ok ? hm : 0;  // mode 3: keys only
+      const bool ta = pa && pr_depth(F.pair[a * kBlock]) != 0;
+      const bool tb = pb && pr_depth(F.pair[b * kBlock]) != 0;
+      uint32_t sa = pa ? slot_of(ka.hash, T.mask) : 0u, sb = pb ? slot_of(kb.hash, T.mask) : 0u;
+      uint32_t guard = 0;
+      while (__any(pa || pb)) {
+        FastProbe A, B;
+        if (pa) fast_load(T, sa, ta, A);
+        if (pb) fast_load(T, sb, tb, B);
+        if (pa) {
+          const uint32_t r = fast_match(A, ka);
+          if (r == 0) {
+            pa = false;
+            if (!fast_commit(F, L, a, sa, A, vb_used, vsum)) ok = false;
+          } else if (r == 2) {
+            pa = false;
+            ok = false;  // a miss: the exact evaluator decides the error
+          } else {
+            sa = (sa + 1) & T.mask;
+          }
+        }
+        if (pb) {
+          const uint32_t r = fast_match(B, kb);
+          if (r == 0) {
+            pb = false;
+            if (!fast_commit(F, L, b, sb, B, vb_used, vsum)) ok = false;
+          } else if (r == 2) {
+            pb = false;
+            ok = false;
+          } else {
+            sb = (sb + 1) & T.mask;
+          }
+        }
+        if (++guard > T.mask) pa = pb = false, ok = false;  // full table: cannot happen (load <= 1/2)
+      }
+      if (!ok) hm = 0;
+    }
+  }
+  if (ok && mode == 3) {
+    nseg = 1, out_len = n, L.seg[0] = seg_make(kSegTemplate, n, 0);
+    return ok;
+  }
+  if (ok) {
+    L.seg[2 * ntop * kBlock] = seg_make(kSegTemplate, n - run, run);
+    tmpl += n - run;
+    nseg = 2 * ntop + 1;
+    out_len = tmpl + vsum;
+  }
+  return ok;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -563,16 +873,35 @@ __device__ uint64_t look_back(uint64_t* state, uint32_t tile, uint64_t agg, uint
   uint64_t excl = 0;
   int64_t pos = (int64_t)tile - 1;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  // each poll reads a window of 4 x 64 predecessors (one memory round trip): sub-window q holds
+  // distances 64q .. 64q+63 from pos, lane l at distance 64q + l
   for (;;) {
-    const int64_t idx = pos - (int64_t)lane;
-    const uint64_t w = idx >= 0 ? __hip_atomic_load(state + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                : kFlagIncl;
-    const uint64_t flag = w >> 62;
-    const uint64_t incl_m = __ballot(flag == 2);
-    const uint64_t wait_m = __ballot(flag == 0);
-    const uint32_t first = incl_m ? (uint32_t)__builtin_ctzll(incl_m) : 64u;
-    const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);
-    if (wait_m & need) {
+    uint64_t w[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int64_t idx = pos - 64 * q - (int64_t)lane;
+      w[q] = idx >= 0 ? __hip_atomic_load(state + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFlagIncl;
+    }
+    bool done = false, wait = false;
+    uint64_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      if (done || wait) continue;  // uniform across the wave
+      const uint64_t flag = w[q] >> 62;
+      const uint64_t incl_m = __ballot(flag == 2);
+      const uint64_t wait_m = __ballot(flag == 0);
+      const uint32_t first = incl_m ? (uint32_t)__builtin_ctzll(incl_m) : 64u;
+      const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);
+      if (wait_m & need) {
+        wait = true;
+        continue;
+      }
+      sum += w_sum(lane <= first ? (w[q] & kValMask) : 0ull);
+      if (first < 64) done = true;
+    }
+    if (wait) {
+      // consume what was complete before the gap: windows before it are final
+      // (re-read from the same pos next time, so nothing is double counted)
       if (lane == 0) atomicAdd(polls, 1u);
       __builtin_amdgcn_s_sleep(1);
       // bounded spin: 60 s of s_memrealtime (100 MHz); a missing predecessor is a bug
@@ -582,9 +911,9 @@ __device__ uint64_t look_back(uint64_t* state, uint32_t tile, uint64_t agg, uint
       }
       continue;
     }
-    excl += w_sum(lane <= first ? (w & kValMask) : 0ull);
-    if (first < 64) break;
-    pos -= 64;
+    excl += sum;
+    if (done) break;
+    pos -= 256;
   }
   if (lane == 0) publish(state, tile, kFlagIncl | (excl + agg));
   return excl;
@@ -610,7 +939,13 @@ __device__ uint64_t block_scan(uint64_t v, uint64_t* lds_w, uint64_t* total) {
   return base + inc - v;
 }
 
-constexpr uint32_t kEvalLds = kBlock * kKeyCap + kMaxDepth * kBlock * 4;
+// eval region: key buffers | eval_events' stacks | pair records | inner values. Every lane owns
+// one column of each; nothing may alias across columns of different width (waves run the fast
+// and the exact evaluator at different times).
+constexpr uint32_t kKbufLds = kBlock * kKeyCap;
+constexpr uint32_t kStackLds = kMaxDepth * kBlock * 4;
+constexpr uint32_t kPairLds = kFastPairs * kBlock * 8;
+constexpr uint32_t kEvalLds = kKbufLds + kStackLds + kPairLds + kBlock * kFastVb;
 constexpr uint32_t kUnionLds = (kEvalLds > (uint32_t)kStageBytes + 32 ? kEvalLds : (uint32_t)kStageBytes + 32);
 
 __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T, uint8_t* out,
@@ -624,7 +959,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
   __shared__ uint16_t s_pend[kBlock];
   __shared__ uint32_t s_misc[4];  // tile, pending count
   __shared__ uint64_t s_red[kBlock / 64 + 2];
-  __shared__ uint16_t s_cm[(kTileBytes + 32) / 16];  // event masks of the staged chunks
+  __shared__ uint32_t s_cm[(kTileBytes + 32) / 16];  // event masks of the staged chunks
 
   const uint32_t tid = threadIdx.x, wave = tid >> 6;
   uint64_t t_start = 0;
@@ -662,9 +997,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
     for (uint32_t j = tid; j < nv; j += kBlock) dst[j] = gld4(src + j);
     __syncthreads();
     for (uint32_t c = tid; c < nv; c += kBlock) {  // classify: one event mask per chunk
-      const lds_u32* w = (const lds_u32*)(lds_u8*)s_in + 4 * c;
-      ((lds_u16*)s_cm)[c] = (uint16_t)(event_nibble(w[0]) | (event_nibble(w[1]) << 4) |
-                                       (event_nibble(w[2]) << 8) | (event_nibble(w[3]) << 12));
+      ((lds_u32*)s_cm)[c] = chunk_mask((const lds_u32*)(lds_u8*)s_in + 4 * c);
     }
   }
   __syncthreads();
@@ -672,7 +1005,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
 
   // ---- 2. evaluate (fast path) ----
   uint64_t so = 0, sn = 0;
-  const LaneLds L{(lds_u8*)(s_u + tid * kKeyCap), (lds_u32*)(lds_u8*)(s_u + kBlock * kKeyCap) + tid,
+  const LaneLds L{(lds_u8*)(s_u + tid * kKeyCap), (lds_u32*)(lds_u8*)(s_u + kKbufLds) + tid,
                   (lds_u64*)s_seg + tid};
   const uint8_t* s = nullptr;
   {
@@ -686,12 +1019,29 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
       active = sn < 0xFFFF0000ull;
       if (!active) st = kStatusPending;
     }
-    // one wave-uniform call (the rounds vote across the wave); idle lanes ride along
+    // wave-uniform calls (the rounds vote across the wave); idle lanes ride along. Clean strings
+    // take the level evaluator; the rest (and its failures) the exact event evaluator.
     const uint32_t p0 = shift + (uint32_t)(so - lo);
-    const uint8_t r = staged ? eval_events(T, (const lds_u8*)s_in + p0, p0, (uint32_t)sn, (const lds_u16*)s_cm,
-                                           active, L, olen, vid, ns)
-                             : eval_rounds<false, false>(T, Src<false>{s}, (uint32_t)sn, active, L, nullptr,
-                                                         olen, vid, ns);
+    uint8_t r = IE_OK_STR;
+    if (W.debug_noeval) {
+      ns = 1;
+      olen = (uint32_t)sn;
+      L.seg[0] = seg_make(kSegTemplate, (uint32_t)sn, 0);
+    } else if (staged) {
+      const FastLds F{(lds_u8*)(s_u + tid * kKeyCap), (lds_u64*)(lds_u8*)(s_u + kKbufLds + kStackLds) + tid,
+                      (lds_u8*)(s_u + kKbufLds + kStackLds + kPairLds + tid * kFastVb)};
+      const bool fast = eval_fast(T, (const lds_u8*)s_in + p0, p0, (uint32_t)sn, (const lds_u32*)s_cm,
+                                  active && W.fast_mode, W.fast_mode, F, L, olen, ns);
+      const bool slow = active && !fast;
+      if (__any(slow)) {
+        uint32_t o2 = 0, n2 = 0;
+        const uint8_t r2 = eval_events(T, (const lds_u8*)s_in + p0, p0, (uint32_t)sn, (const lds_u32*)s_cm,
+                                       slow, L, o2, vid, n2);
+        if (slow) r = r2, olen = o2, ns = n2;
+      }
+    } else {
+      r = eval_rounds<false, false>(T, Src<false>{s}, (uint32_t)sn, active, L, nullptr, olen, vid, ns);
+    }
     if (active) st = r;
     if (i < B.n) {
       if (st == IE_OK_STR && ns > (uint32_t)kMaxSeg) st = kStatusPending;  // too many segments
@@ -780,6 +1130,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
                          src = (uint32_t)sg;
           const uint8_t* p = kind == kSegTemplate ? s + src
                              : kind == kSegValue  ? T.arena + src
+                             : kind == kSegBucket ? T.buckets[src].text
                                                   : W.pool + ((uint64_t)src << 4);
           for (uint32_t q = 0; q < len; q++) gst(d + w + q, p[q]);
           w += len;
@@ -797,6 +1148,8 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
                        src = (uint32_t)sg;
         if (kind == kSegTemplate)
           copy_bytes<true, true>(d + w, s + src, len);
+        else if (kind == kSegBucket)
+          put_bucket_text((lds_u8*)(d + w), T.buckets + src, len);
         else if (kind == kSegValue)
           copy_bytes<true, false>(d + w, T.arena + src, len);
         else
