@@ -185,7 +185,8 @@ def main():
                          "kernel": "k_resolve (single pass: stage, evaluate, look-back, emit)",
                          "launch_ms": round(gpu_ms, 4), "alg_bytes_per_launch": alg_bytes,
                          "telemetry": {"kernel_ms": round(tm.resolve_ms, 4), "literal_strings": int(tm.n_complex),
-                                       "direct_tiles": int(tm.n_direct), "lookback_polls": int(tm.n_polls)}},
+                                       "direct_tiles": int(tm.n_direct), "lookback_polls": int(tm.n_polls),
+                                       "exact_strings": int(tm.n_exact)}},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -141,6 +141,7 @@ typedef struct ie_timing {
   uint64_t n_complex;    /* strings routed to the literal (wave-cooperative) path */
   uint64_t n_direct;     /* tiles that bypassed the LDS stages (long strings / many segments) */
   uint64_t n_polls;      /* look-back poll rounds that found a predecessor not yet published */
+  uint64_t n_exact;      /* strings the level evaluator handed to the exact event evaluator */
 } ie_timing;
 
 /* ---- library ---- */
@@ -163,6 +164,10 @@ int ie_exec_sync(ie_exec* x);
 int ie_exec_set_timing(ie_exec* x, int32_t enabled);
 int ie_exec_timing(ie_exec* x, ie_timing* out); /* syncs */
 int ie_exec_set_scratch(ie_exec* x, uint64_t bytes); /* literal-kernel scratch pool size */
+
+/* Diagnostic (no reference counterpart): one key through the device lookups next to the host's
+ * view of the same table; out[12] as documented in ie_host.cpp. */
+int ie_debug_probe(const ie_table* t, const char* key, uint64_t len, uint64_t* out);
 
 /* ---- device memory and stream markers for callers without their own HIP bindings (the Rust
  * shim, ctypes). Copies are ordered on the exec's stream; *_sync variants wait for it. ---- */

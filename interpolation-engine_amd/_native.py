@@ -31,7 +31,7 @@ EXPORTS = [
     "ie_unescape_device", "ie_escape_device", "ie_unescape_batch", "ie_escape_batch",
     "ie_batch_free", "ie_simple_insertkey",
     "ie_synth_create", "ie_synth_free", "ie_synth_kv", "ie_synth_strings_host",
-    "ie_synth_strings_device",
+    "ie_synth_strings_device", "ie_debug_probe",
 ]
 
 
@@ -60,7 +60,7 @@ class BatchRes(ctypes.Structure):
 class Timing(ctypes.Structure):
     _fields_ = [("resolve_ms", ctypes.c_float), ("complex_ms", ctypes.c_float),
                 ("total_ms", ctypes.c_float), ("n_complex", ctypes.c_uint64), ("n_direct", ctypes.c_uint64),
-                ("n_polls", ctypes.c_uint64)]
+                ("n_polls", ctypes.c_uint64), ("n_exact", ctypes.c_uint64)]
 
 
 _lib = None

@@ -3,11 +3,11 @@
 // Device data layout of one inserts table (built once per get_interpdata snapshot, read-only):
 //   buckets[cap]    Bucket (128 B = one L2 line): 64-bit key hash, lengths, flags, value id, arena
 //                   offsets, and inline copies of the key (<= 32 B) and splice text (<= 64 B), so
-//                   one probe is one line; open addressing with linear probing, cap =
-//                   next_pow2(2 * entries) keeps probe chains short (load factor <= 0.5)
+//                   one probe is one line; two-choice cuckoo placement (slots_of), cap =
+//                   next_pow2(4 * entries) (load factor <= 0.25): a lookup reads two buckets
 //   arena[...]      every key and splice text (texts 4-byte aligned, for dword copies)
 // The key hash mixes the key's little-endian 4-byte words (zero padded) seeded with its length;
-// slot = fmix64(hash) & mask.
+// slots = two bit fields of fmix64(hash).
 #pragma once
 #include <stdint.h>
 
@@ -45,7 +45,16 @@ IE_HD uint64_t fmix64(uint64_t k) {
   return k;
 }
 
-IE_HD uint32_t slot_of(uint64_t h, uint32_t mask) { return (uint32_t)fmix64(h) & mask; }
+// Two-choice cuckoo placement: a key lives in slot s1 or s2 (two bit fields of one mixed hash;
+// s2 = s1 ^ 1 when they collide), so every lookup is ONE round trip that reads both buckets.
+struct SlotPair {
+  uint32_t s1, s2;
+};
+IE_HD SlotPair slots_of(uint64_t h, uint32_t mask) {
+  const uint64_t f = fmix64(h);
+  const uint32_t a = (uint32_t)f & mask, b = (uint32_t)(f >> 32) & mask;
+  return SlotPair{a, b == a ? a ^ 1u : b};
+}
 
 // Bucket.flags
 enum : uint32_t {

@@ -74,30 +74,29 @@ __device__ __forceinline__ Hit hit_of(uint4 q0, uint4 q1) {
   return Hit{q0.w, q1.w, q1.x, q1.y};
 }
 
-// Probe for a key whose bytes are at `key` (any address space). Returns the bucket or -1.
+// Lookup of a key whose bytes are at `key` (any address space): both cuckoo slots. Returns the
+// bucket or -1.
+// (Written without a loop: an unrolled two-iteration loop with an early return compiled to code
+// that returned the second slot's index without writing `h`.)
 __device__ int32_t find_bytes(const DevTable& T, const uint8_t* key, uint32_t klen, Hit& h) {
   const uint64_t hash = hash_key(klen, [&](uint32_t j) { return key[j]; });
-  uint32_t s = slot_of(hash, T.mask);
-  for (uint32_t probe = 0; probe <= T.mask; probe++) {
-    const uint4* bp = (const uint4*)(T.buckets + s);
-    const uint4 q0 = gld4(bp), q1 = gld4(bp + 1);
-    if (!(q1.y & EF_OCCUPIED)) return -1;
-    if ((((uint64_t)q0.y << 32) | q0.x) == hash && q0.z == klen &&
-        bytes_eq(T.arena + q1.z, key, klen)) {
-      h = hit_of(q0, q1);
-      return (int32_t)s;
-    }
-    s = (s + 1) & T.mask;
-  }
-  return -1;
+  const SlotPair sp = slots_of(hash, T.mask);
+  const uint4* b1 = (const uint4*)(T.buckets + sp.s1);
+  const uint4* b2 = (const uint4*)(T.buckets + sp.s2);
+  const uint4 a0 = gld4(b1), a1 = gld4(b1 + 1), c0 = gld4(b2), c1 = gld4(b2 + 1);
+  const bool ma = ((a1.y & EF_OCCUPIED) != 0) & ((((uint64_t)a0.y << 32) | a0.x) == hash) & (a0.z == klen);
+  const bool mc = ((c1.y & EF_OCCUPIED) != 0) & ((((uint64_t)c0.y << 32) | c0.x) == hash) & (c0.z == klen);
+  const bool ha = ma && bytes_eq(T.arena + a1.z, key, klen);
+  const bool hc = !ha && mc && bytes_eq(T.arena + c1.z, key, klen);
+  h = ha ? hit_of(a0, a1) : hit_of(c0, c1);
+  return ha ? (int32_t)sp.s1 : hc ? (int32_t)sp.s2 : -1;
 }
 
-// Probe for a key held in LDS at a 4-byte aligned address, klen <= kInlineKey: the key is read
-// as dwords, hashed word-wise, and each probe is one 64-byte burst (header + inline key) compared
-// dword-wise in registers.
+// Lookup of a key held in LDS at a 4-byte aligned address, klen <= kInlineKey: the key is read
+// as dwords and hashed word-wise; both slots' 64-byte bursts (header + inline key) go out
+// together and are compared dword-wise in registers.
 __device__ __forceinline__ int32_t find_small(const DevTable& T, const __attribute__((address_space(3))) uint32_t* key32,
                                               uint32_t klen, Hit& h) {
-  const uint32_t nw = (klen + 3) >> 2;
   uint64_t hash = 0xA0761D6478BD642Full ^ (uint64_t)klen;
   uint32_t kw[8];
 #pragma unroll
@@ -110,20 +109,23 @@ __device__ __forceinline__ int32_t find_small(const DevTable& T, const __attribu
       hash = hash_word(hash, kw[d]);
     }
   }
-  (void)nw;
-  uint32_t s = slot_of(hash, T.mask);
-  for (uint32_t probe = 0; probe <= T.mask; probe++) {
-    const uint4* bp = (const uint4*)(T.buckets + s);
-    const uint4 q0 = gld4(bp), q1 = gld4(bp + 1), q2 = gld4(bp + 2), q3 = gld4(bp + 3);
-    if (!(q1.y & EF_OCCUPIED)) return -1;
-    const bool eq = ((((uint64_t)q0.y << 32) | q0.x) == hash) & (q0.z == klen) &
-                    (q2.x == kw[0]) & (q2.y == kw[1]) & (q2.z == kw[2]) & (q2.w == kw[3]) &
-                    (q3.x == kw[4]) & (q3.y == kw[5]) & (q3.z == kw[6]) & (q3.w == kw[7]);
-    if (eq) {
-      h = hit_of(q0, q1);
-      return (int32_t)s;
-    }
-    s = (s + 1) & T.mask;
+  const SlotPair sp = slots_of(hash, T.mask);
+  const uint4* b1 = (const uint4*)(T.buckets + sp.s1);
+  const uint4* b2 = (const uint4*)(T.buckets + sp.s2);
+  const uint4 a0 = gld4(b1), a1 = gld4(b1 + 1), a2 = gld4(b1 + 2), a3 = gld4(b1 + 3);
+  const uint4 c0 = gld4(b2), c1 = gld4(b2 + 1), c2 = gld4(b2 + 2), c3 = gld4(b2 + 3);
+  auto eq = [&](uint4 q0, uint4 q1, uint4 q2, uint4 q3) {
+    return ((q1.y & EF_OCCUPIED) != 0) & ((((uint64_t)q0.y << 32) | q0.x) == hash) & (q0.z == klen) &
+           (q2.x == kw[0]) & (q2.y == kw[1]) & (q2.z == kw[2]) & (q2.w == kw[3]) &
+           (q3.x == kw[4]) & (q3.y == kw[5]) & (q3.z == kw[6]) & (q3.w == kw[7]);
+  };
+  if (eq(a0, a1, a2, a3)) {
+    h = hit_of(a0, a1);
+    return (int32_t)sp.s1;
+  }
+  if (eq(c0, c1, c2, c3)) {
+    h = hit_of(c0, c1);
+    return (int32_t)sp.s2;
   }
   return -1;
 }

@@ -190,7 +190,7 @@ Work make_work(ie_exec* x, uint64_t* total) {
   W.stats = (uint32_t*)x->counters.p + 4;
   W.stamps = x->stamp_tiles ? (uint64_t*)x->stamps.p : nullptr;
   W.debug_noeval = getenv("IE_DEBUG_NOEVAL") ? 1u : 0u;  // diagnostic hooks, see DESIGN.md
-  W.fast_mode = getenv("IE_FAST") ? (uint32_t)atoi(getenv("IE_FAST")) : 0u;
+  W.fast_mode = getenv("IE_FAST") ? (uint32_t)atoi(getenv("IE_FAST")) : 1u;  // 0: exact evaluator only
   W.pool_used = (uint64_t*)x->counters.p + 1;
   W.tile_state = (uint64_t*)x->tile_state.p;
   W.pool = (uint8_t*)x->pool.p;
@@ -421,12 +421,9 @@ int ie_table_build(const ie_kv* kv, uint64_t n, int32_t dialect, const ie_clock*
   ents.push_back(Ent{"HH:MM", hhmm, kind_flags(IE_KIND_STR, dialect) | text_flags(hhmm), IE_VID_CLOCK_HHMM});
   ents.push_back(Ent{"HH:MM:SS", hhmmss, kind_flags(IE_KIND_STR, dialect) | text_flags(hhmmss), IE_VID_CLOCK_HHMMSS});
 
-  uint64_t cap = 16;
-  while (cap < 2 * ents.size()) cap *= 2;
-  if (cap > (1ull << 31)) return fail(IE_ERR_INVALID, "table too large");
-  std::vector<Bucket> buckets(cap);
-  memset(buckets.data(), 0, cap * sizeof(Bucket));
   std::vector<uint8_t> arena;
+  std::vector<Bucket> items;
+  items.reserve(ents.size());
   uint64_t maxtext = 8;
   for (const Ent& e : ents) {
     while (arena.size() & 3) arena.push_back(0);  // texts 4-byte aligned (dword copies)
@@ -446,9 +443,36 @@ int ie_table_build(const ie_kv* kv, uint64_t n, int32_t dialect, const ie_clock*
     b.text_off = (uint32_t)toff;
     if (e.key.size() <= kInlineKey) memcpy(b.key, e.key.data(), e.key.size());
     if (e.text.size() <= kInlineText) memcpy(b.text, e.text.data(), e.text.size());
-    uint32_t sl = slot_of(b.hash, (uint32_t)(cap - 1));
-    while (buckets[sl].flags & EF_OCCUPIED) sl = (sl + 1) & (uint32_t)(cap - 1);
-    buckets[sl] = b;
+    items.push_back(b);
+  }
+  // cuckoo placement: random walk of evictions; a failed walk doubles the capacity
+  uint64_t cap = 16;
+  while (cap < 4 * items.size()) cap *= 2;
+  std::vector<Bucket> buckets;
+  uint64_t rng = 0x243F6A8885A308D3ull;
+  for (;;) {
+    if (cap > (1ull << 31)) return fail(IE_ERR_INVALID, "table too large");
+    buckets.assign(cap, Bucket{});
+    const uint32_t mask = (uint32_t)(cap - 1);
+    bool placed_all = true;
+    for (const Bucket& it : items) {
+      Bucket cur = it;
+      SlotPair sp = slots_of(cur.hash, mask);
+      uint32_t pos = sp.s1;
+      bool placed = false;
+      for (int kick = 0; kick < 1000 && !placed; kick++) {
+        sp = slots_of(cur.hash, mask);
+        if (!(buckets[sp.s1].flags & EF_OCCUPIED)) { buckets[sp.s1] = cur; placed = true; break; }
+        if (!(buckets[sp.s2].flags & EF_OCCUPIED)) { buckets[sp.s2] = cur; placed = true; break; }
+        // evict from the slot we did not come from (random first move)
+        rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17;
+        pos = kick == 0 ? ((rng & 1) ? sp.s1 : sp.s2) : (pos == sp.s1 ? sp.s2 : sp.s1);
+        std::swap(cur, buckets[pos]);
+      }
+      if (!placed) { placed_all = false; break; }
+    }
+    if (placed_all) break;
+    cap *= 2;
   }
   for (int pad = 0; pad < 16; pad++) arena.push_back(0);  // dword reads past the last text
   ie_table* t = new ie_table();
@@ -555,12 +579,43 @@ int ie_exec_timing(ie_exec* x, ie_timing* out) {
   out->resolve_ms = kern;   // the resolve (or escape) kernels
   out->complex_ms = 0.0f;   // literal strings are resolved inside k_resolve
   out->total_ms = setup + kern;
-  uint32_t st[3] = {0, 0, 0};
-  if (x->counters.p) IE_HIP(hipMemcpy(st, (uint32_t*)x->counters.p + 4, 12, hipMemcpyDeviceToHost));
+  uint32_t st[4] = {0, 0, 0, 0};
+  if (x->counters.p) IE_HIP(hipMemcpy(st, (uint32_t*)x->counters.p + 4, 16, hipMemcpyDeviceToHost));
   out->n_complex = st[0];
   out->n_direct = st[1];
   out->n_polls = st[2];
+  out->n_exact = st[3];
   return check_device_error(x);
+}
+
+// diagnostic (not part of the reference surface): device vs host view of one key's lookup.
+// out[0..6] device: hash lo/hi, s1, s2, find_bytes, find_small, mask; out[7..10] host: hash
+// lo/hi, s1, s2 and out[11] the host's bucket index holding the key (or -1)
+int ie_debug_probe(const ie_table* t, const char* key, uint64_t len, uint64_t* out) {
+  if (!t || !out || (len && !key) || len > 4096) return fail(IE_ERR_INVALID, "bad argument");
+  int rc = set_device(t->device);
+  if (rc) return rc;
+  DevBuf dk, dout;
+  IE_HIP(dk.ensure(len + 16));
+  IE_HIP(dout.ensure(16 * 8));
+  if (len) IE_HIP(hipMemcpy(dk.p, key, len, hipMemcpyHostToDevice));
+  IE_HIP(launch_debug_probe(t->dev, (const uint8_t*)dk.p, (uint32_t)len, (uint64_t*)dout.p, 0));
+  IE_HIP(hipDeviceSynchronize());
+  IE_HIP(hipMemcpy(out, dout.p, 16 * 8, hipMemcpyDeviceToHost));
+  const uint64_t w12 = out[12], w13 = out[13], w14 = out[14], w15 = out[15];
+  const uint64_t h = key_hash(std::string_view(key ? key : "", len));
+  const SlotPair sp = slots_of(h, t->dev.mask);
+  out[7] = h & 0xFFFFFFFFull;
+  out[8] = h >> 32;
+  out[9] = sp.s1;
+  out[10] = sp.s2;
+  out[11] = (uint64_t)-1;
+  std::vector<Bucket> hb((uint64_t)t->dev.mask + 1);
+  IE_HIP(hipMemcpy(hb.data(), t->dev.buckets, hb.size() * sizeof(Bucket), hipMemcpyDeviceToHost));
+  for (uint64_t i = 0; i < hb.size(); i++)
+    if ((hb[i].flags & EF_OCCUPIED) && hb[i].hash == h && hb[i].key_len == len) out[11] = i;
+  out[12] = w12, out[13] = w13, out[14] = w14, out[15] = w15;
+  return IE_SUCCESS;
 }
 
 int ie_exec_set_scratch(ie_exec* x, uint64_t bytes) {

@@ -31,10 +31,10 @@ struct Work {
   uint32_t* tile_ticket; // 1   dynamic tile ids (zeroed per call)
   uint64_t* tile_state;  // tiles: look-back words (zeroed per call)
   uint32_t* err;         // 1   look-back timeout flag
-  uint32_t* stats;       // 3   telemetry: literal strings, direct tiles, look-back polls
+  uint32_t* stats;       // 4   telemetry: literal strings, direct tiles, look-back polls, exact-path strings
   uint64_t* stamps;      // diagnostic (IE_DEBUG_STAMPS): 8 words per tile, or null
   uint32_t debug_noeval; // diagnostic (IE_DEBUG_NOEVAL): copy strings verbatim (pipeline floor)
-  uint32_t fast_mode;    // level evaluator: 0 off, 1 on; diagnostics 2 = parse only, 3 = no probes
+  uint32_t fast_mode;    // level evaluator: 1 on (default), 0 off; diagnostics 2 = parse only, 3 = no probes
   uint8_t* pool;         // literal-path scratch
   uint64_t* pool_used;   // 1
   uint64_t pool_bytes;
@@ -49,6 +49,8 @@ hipError_t launch_resolve(const Batch& B, const Work& W, const DevTable& T, uint
                           uint64_t cap, hipStream_t st);
 hipError_t launch_escape(int op, const Batch& B, const Work& W, uint8_t* out, uint64_t cap,
                          hipStream_t st);
+hipError_t launch_debug_probe(const DevTable& T, const uint8_t* key, uint32_t klen, uint64_t* out,
+                              hipStream_t st);
 hipError_t launch_synth(const SynthParams& P, uint64_t first, uint64_t n, uint64_t* d_lens,
                         uint64_t* d_part, uint64_t* d_offsets, uint64_t* d_total, uint8_t* d_bytes,
                         hipStream_t st);

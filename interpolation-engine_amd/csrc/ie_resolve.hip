@@ -127,34 +127,62 @@ __device__ __forceinline__ void copy_bytes(uint8_t* __restrict__ dst, const uint
   for (; k < len; k++) wr8(k, rd8(k));
 }
 
+// Branch-free LDS writers: a lane that has nothing to write for some step stores to its own
+// sink dword instead (an address select, no exec-mask branch); trip counts are wave-uniform.
+__device__ __forceinline__ void st8(lds_u8* p, bool on, lds_u8* sink, uint8_t v) { *(on ? p : sink) = v; }
+__device__ __forceinline__ void st32(lds_u32* p, bool on, lds_u8* sink, uint32_t v) {
+  *(on ? p : (lds_u32*)sink) = v;
+}
+
 // a bucket's inline text (16-byte aligned, len <= kInlineText) -> LDS at any byte offset: the
 // four 16-byte loads go out together (one memory latency), dwords are re-aligned with alignbyte
-__device__ __forceinline__ void put_bucket_text(lds_u8* dst, const Bucket* b, uint32_t len) {
+__device__ __forceinline__ void put_bucket_text(lds_u8* dst, const Bucket* b, uint32_t len, lds_u8* sink) {
   const uint4* tp = (const uint4*)b->text;
-  const uint4 z = make_uint4(0, 0, 0, 0);
-  const uint4 t0 = gld4(tp), t1 = len > 16 ? gld4(tp + 1) : z, t2 = len > 32 ? gld4(tp + 2) : z,
-              t3 = len > 48 ? gld4(tp + 3) : z;
+  const uint4 t0 = gld4(tp), t1 = gld4(tp + 1), t2 = gld4(tp + 2), t3 = gld4(tp + 3);  // one line
   const uint32_t tw[17] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w,
                            t2.x, t2.y, t2.z, t2.w, t3.x, t3.y, t3.z, t3.w, 0u};
   const uint32_t a = (uint32_t)(uintptr_t)dst & 3u;
   const uint32_t head = min(len, (4u - a) & 3u);
 #pragma unroll
-  for (uint32_t k = 0; k < 3; k++)
-    if (k < head) dst[k] = (uint8_t)(tw[0] >> (8 * k));
+  for (uint32_t k = 0; k < 3; k++) st8(dst + k, k < head, sink, (uint8_t)(tw[0] >> (8 * k)));
   // dword q of the aligned body = text bytes head + 4q .. head + 4q + 3
   lds_u32* d32 = (lds_u32*)(dst + head);
   const uint32_t rest = len - head, nq = rest >> 2, tail = rest & 3u;
   uint32_t x = 0;
 #pragma unroll
   for (uint32_t q = 0; q < 16; q++) {
+    if (!__any(q <= nq)) break;  // wave-uniform exit
     const uint32_t v = __builtin_amdgcn_alignbyte(tw[q + 1], tw[q], head);
-    if (q < nq) d32[q] = v;
-    if (q == nq) x = v;
+    st32(d32 + q, q < nq, sink, v);
+    x = q == nq ? v : x;
   }
   lds_u8* t = dst + head + 4 * nq;
 #pragma unroll
-  for (uint32_t k = 0; k < 3; k++)
-    if (k < tail) t[k] = (uint8_t)(x >> (8 * k));
+  for (uint32_t k = 0; k < 3; k++) st8(t + k, k < tail, sink, (uint8_t)(x >> (8 * k)));
+}
+
+// len bytes LDS -> LDS, any alignments: dst-aligned dword body built with alignbyte from the
+// source's aligned dwords (reads may touch up to 3 bytes around the source; the tile is padded)
+__device__ __forceinline__ void lds_copy(lds_u8* dst, const lds_u8* src, uint32_t len, lds_u8* sink) {
+  const uint32_t a = (uint32_t)(uintptr_t)dst & 3u;
+  const uint32_t head = min(len, (4u - a) & 3u);
+#pragma unroll
+  for (uint32_t k = 0; k < 3; k++) st8(dst + k, k < head, sink, src[k]);
+  const uint32_t s2 = (uint32_t)(uintptr_t)(src + head);
+  const uint32_t sh = s2 & 3u;
+  const lds_u32* sw = (const lds_u32*)(lds_u8*)(uintptr_t)(s2 - sh);
+  lds_u32* d32 = (lds_u32*)(dst + head);
+  const uint32_t rest = len - head, nq = rest >> 2, tail = rest & 3u;
+  uint32_t prev = sw[0];
+  for (uint32_t q = 0; __any(q < nq); q++) {  // wave-uniform trip count
+    const uint32_t nx = sw[q + 1];
+    st32(d32 + q, q < nq, sink, __builtin_amdgcn_alignbyte(nx, prev, sh));
+    prev = nx;
+  }
+  const lds_u8* ts = src + head + 4 * nq;
+  lds_u8* td = dst + head + 4 * nq;
+#pragma unroll
+  for (uint32_t k = 0; k < 3; k++) st8(td + k, k < tail, sink, ts[k]);
 }
 
 struct LaneLds {
@@ -620,68 +648,89 @@ struct FastKey {
   uint64_t hash;
 };
 
-// key of pair `idx`: its template bytes with the direct children replaced by their texts
-__device__ __forceinline__ bool fast_key(const lds_u8* s, const FastLds& F, uint32_t idx, FastKey& K) {
-  const uint64_t rec = F.pair[idx * kBlock];
-  const uint32_t open = pr_open(rec), close = pr_close(rec), d = pr_depth(rec);
-  uint32_t w = 0, pos = open + 1;
-  if (pr_height(rec) > 1) {
-    for (uint32_t j = 0; j < idx; j++) {  // postorder: descendants precede the pair
-      const uint64_t c = F.pair[j * kBlock];
-      if (pr_depth(c) != d + 1 || pr_open(c) < open) continue;
-      const uint32_t t = pr_open(c) - pos, v = pr_vlen(c);
-      if (w + t + v > (uint32_t)kInlineKey) return false;
-      copy_bytes<true, true>((uint8_t*)(F.kbuf + w), (const uint8_t*)(s + pos), t);
-      copy_bytes<true, true>((uint8_t*)(F.kbuf + w + t), (const uint8_t*)(F.vbuf + pr_vboff(c)), v);
-      w += t + v;
-      pos = pr_close(c) + 1;
+// key of pair `idx` (string s in LDS): a leaf pair's key is its template bytes, read as dwords
+// straight from the staged tile; a chain pair's key is template + its one child's text (vbuf) +
+// template, assembled bytewise in the lane's key buffer. Wave-uniform call (early exits vote).
+__device__ __forceinline__ bool fast_key(const lds_u8* s, const FastLds& F, uint32_t idx, bool on,
+                                         FastKey& K) {
+  const uint64_t rec = on ? F.pair[idx * kBlock] : 0ull;
+  const uint32_t open = pr_open(rec), close = pr_close(rec);
+  const bool leaf = pr_height(rec) <= 1;
+  uint32_t len = 0, la = 0, lv = 0, vb = 0, b0 = 0;
+  if (on) {
+    if (leaf) {
+      len = close - open - 1;
+    } else {
+      const uint64_t c = F.pair[(idx - 1) * kBlock];  // postorder: the only child closes just before
+      la = pr_open(c) - open - 1;
+      lv = pr_vlen(c);
+      vb = pr_vboff(c);
+      b0 = pr_close(c) + 1;
+      len = la + lv + (close - b0);
     }
   }
-  const uint32_t t = close - pos;
-  if (w + t > (uint32_t)kInlineKey) return false;
-  copy_bytes<true, true>((uint8_t*)(F.kbuf + w), (const uint8_t*)(s + pos), t);
-  w += t;
-  K.len = w;
-  uint64_t hash = 0xA0761D6478BD642Full ^ (uint64_t)w;
-  const lds_u32* k32 = (const lds_u32*)F.kbuf;
+  const bool fits = len <= (uint32_t)kInlineKey;
+  if (!fits) len = 0;
+  const lds_u8* src = s + open + 1;
+  if (on && fits && !leaf) {  // assemble: A | child text | B
+    for (uint32_t k = 0; k < len; k++) {
+      const uint8_t c = k < la ? src[k] : k < la + lv ? F.vbuf[vb + k - la] : s[b0 + (k - la - lv)];
+      F.kbuf[k] = c;
+    }
+  }
+  // dwords of the key: from the tile (leaf, any alignment) or the key buffer (chain, aligned)
+  const uint32_t addr = (uint32_t)(uintptr_t)src;
+  const uint32_t sh = addr & 3u;
+  const lds_u32* lw = (const lds_u32*)(lds_u8*)(uintptr_t)(addr - sh);
+  const lds_u32* kw = (const lds_u32*)F.kbuf;
+  uint64_t hash = 0xA0761D6478BD642Full ^ (uint64_t)len;
+  uint32_t prev = leaf && on && fits ? lw[0] : 0u;
 #pragma unroll
   for (int q = 0; q < 8; q++) {
-    const int32_t rem = (int32_t)w - 4 * q;
-    uint32_t x = 0;
+    K.w[q] = 0;
+    if (!__any(4 * q < (int)len)) continue;  // wave-uniform: no lane has this word
+    const int32_t rem = (int32_t)len - 4 * q;
     if (rem > 0) {
-      x = k32[q];
+      uint32_t x;
+      if (leaf) {
+        const uint32_t nx = lw[q + 1];
+        x = __builtin_amdgcn_alignbyte(nx, prev, sh);
+        prev = nx;
+      } else {
+        x = kw[q];
+      }
       if (rem < 4) x &= (1u << (8 * rem)) - 1u;
+      K.w[q] = x;
       hash = hash_word(hash, x);
     }
-    K.w[q] = x;
   }
+  K.len = len;
   K.hash = hash;
-  return true;
+  return fits;
 }
 
 struct FastProbe {
   uint4 q0, q1, q2, q3, q4, q5;
 };
 
-__device__ __forceinline__ void fast_load(const DevTable& T, uint32_t slot, bool text, FastProbe& P) {
+// one probe = the bucket's first 96 bytes (header, inline key, inline text 0..31): unconditional,
+// so the loop carries no partially-defined registers (idle lanes read slot 0)
+__device__ __forceinline__ void fast_load(const DevTable& T, uint32_t slot, FastProbe& P) {
   const uint4* bp = (const uint4*)(T.buckets + slot);
   P.q0 = gld4(bp);
   P.q1 = gld4(bp + 1);
   P.q2 = gld4(bp + 2);
   P.q3 = gld4(bp + 3);
-  if (text) {  // inline text bytes 0..31 (an inner value must fit a key, so never longer)
-    P.q4 = gld4(bp + 4);
-    P.q5 = gld4(bp + 5);
-  }
+  P.q4 = gld4(bp + 4);
+  P.q5 = gld4(bp + 5);
 }
 
-// 0: hit, 1: probe the next slot, 2: miss
-__device__ __forceinline__ uint32_t fast_match(const FastProbe& P, const FastKey& K) {
-  if (!(P.q1.y & EF_OCCUPIED)) return 2;
-  const bool eq = ((((uint64_t)P.q0.y << 32) | P.q0.x) == K.hash) & (P.q0.z == K.len) &
-                  (P.q2.x == K.w[0]) & (P.q2.y == K.w[1]) & (P.q2.z == K.w[2]) & (P.q2.w == K.w[3]) &
-                  (P.q3.x == K.w[4]) & (P.q3.y == K.w[5]) & (P.q3.z == K.w[6]) & (P.q3.w == K.w[7]);
-  return eq ? 0u : 1u;
+// does the bucket hold key K (branch-free)
+__device__ __forceinline__ bool fast_match(const FastProbe& P, const FastKey& K) {
+  return ((P.q1.y & EF_OCCUPIED) != 0) & ((((uint64_t)P.q0.y << 32) | P.q0.x) == K.hash) &
+         (P.q0.z == K.len) & (P.q2.x == K.w[0]) & (P.q2.y == K.w[1]) & (P.q2.z == K.w[2]) &
+         (P.q2.w == K.w[3]) & (P.q3.x == K.w[4]) & (P.q3.y == K.w[5]) & (P.q3.z == K.w[6]) &
+         (P.q3.w == K.w[7]);
 }
 
 // commit a hit for pair idx; false when the value is not fast-path material
@@ -700,87 +749,115 @@ __device__ __forceinline__ bool fast_commit(const FastLds& F, const LaneLds& L, 
   const uint32_t tw[8] = {P.q4.x, P.q4.y, P.q4.z, P.q4.w, P.q5.x, P.q5.y, P.q5.z, P.q5.w};
   lds_u32* v32 = (lds_u32*)(F.vbuf + vb_used);
 #pragma unroll
-  for (int q = 0; q < 8; q++)
+  for (int q = 0; q < 8; q++) {
+    if (!__any(4 * q < (int)tlen)) break;  // wave-uniform exit
     if (4 * q < (int)tlen) v32[q] = tw[q];
+  }
   rec = (rec & ~(0xFFFFull << 40)) | ((uint64_t)vb_used << 40) | ((uint64_t)tlen << 48);
   F.pair[idx * kBlock] = rec;
   vb_used += (tlen + 3) & ~3u;
   return true;
 }
 
-// Wave-uniform call. s = the string in LDS at stage position p0; cm = chunk masks.
-// On success: depth-0 segments in L.seg (2 * top pairs + 1 of them), nseg, out_len.
-__device__ bool eval_fast(const DevTable& T, const lds_u8* s, uint32_t p0, uint32_t n,
-                          const lds_u32* cm, bool active, uint32_t mode, const FastLds& F, const LaneLds& L,
-                          uint32_t& out_len, uint32_t& nseg) {
-  bool ok = active && n < 0xFFFFu;
-  uint32_t np = 0, H = 0, depth = 0, ntop = 0, run = 0, tmpl = 0;
-  uint32_t st0 = 0, st1 = 0, st2 = 0, st3 = 0;  // open offset | max child height << 16, per level
-  // ---- parse: pair records in close order (LDS only) ----
-  if (ok) {
-    const uint32_t end = p0 + n;
-    for (uint32_t cb = p0 & ~15u; ok && cb < end; cb += 16) {
-      uint32_t keep = 0xFFFFu;
-      if (cb < p0) keep &= 0xFFFFu << (p0 - cb);
-      if (cb + 16 > end) keep &= (1u << (end - cb)) - 1u;
-      const uint32_t cmw = cm[cb >> 4];
-      if ((cmw >> 16) & keep) {  // '\' or 0xE3: escapes / U+3020 need the exact evaluator
+constexpr uint32_t kLeanMax = 112;  // strings the 128-bit event window covers
+
+// Wave-uniform call. tile = the staged tile; the string starts at stage position p0; cm = chunk
+// masks. On success: depth-0 segments in L.seg (2 * top pairs + 1 of them), nseg, out_len.
+// Shape rules on top of the clean-string rules above: n <= kLeanMax, every pair has at most one
+// child (chains such as {q-{i}}), so a chain pair's key is template + child text + template.
+__device__ bool eval_fast(const DevTable& T, const lds_u8* tile, uint32_t p0, uint32_t n,
+                          const lds_u32* cm, bool active, uint32_t mode, const FastLds& F,
+                          const LaneLds& L, uint32_t& out_len, uint32_t& nseg) {
+  bool ok = active && n <= kLeanMax;
+  const lds_u8* s = tile + p0;
+  // ---- 1. the string's brace events as a 128-bit window (straight-line) ----
+  uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+  {
+    const uint32_t c0 = ok ? p0 >> 4 : 0u, o = p0 & 15u;
+    uint32_t Wb[5], Wd[5];
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+      const uint32_t x = cm[c0 + 2 * j], y = j < 4 ? cm[c0 + 2 * j + 1] : 0u;
+      Wb[j] = (x & 0xFFFFu) | (y << 16);
+      Wd[j] = (x >> 16) | (y & 0xFFFF0000u);
+    }
+    uint32_t odd = 0;
+    uint32_t* wp[4] = {&w0, &w1, &w2, &w3};
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int32_t r = (int32_t)n - 32 * j;
+      const uint32_t keep = r >= 32 ? 0xFFFFFFFFu : r > 0 ? (1u << r) - 1u : 0u;
+      *wp[j] = __builtin_amdgcn_alignbit(Wb[j + 1], Wb[j], o) & keep;
+      odd |= __builtin_amdgcn_alignbit(Wd[j + 1], Wd[j], o) & keep;
+    }
+    if (odd) ok = false;  // '\' or 0xE3: escapes / U+3020 need the exact evaluator
+    if (!ok) w0 = w1 = w2 = w3 = 0;
+  }
+  // ---- 2. pairs: one wave-uniform pass over the events, predicated push / pop ----
+  const uint32_t E = __builtin_popcount(w0) + __builtin_popcount(w1) + __builtin_popcount(w2) +
+                     __builtin_popcount(w3);
+  const uint32_t Ew = (uint32_t)w_max((int64_t)E);
+  uint32_t depth = 0, np = 0, H = 0, ntop = 0, run = 0, tmpl = 0;
+  uint32_t hm1 = 0, hm2 = 0, hm3 = 0, hm4 = 0;
+  uint32_t st0 = 0, st1 = 0, st2 = 0, st3 = 0;  // open | height << 16 | children << 20
+  for (uint32_t k = 0; k < Ew; k++) {
+    const bool z0 = w0 == 0, z1 = w1 == 0, z2 = w2 == 0;
+    const uint32_t e = !z0 ? (uint32_t)__builtin_ctz(w0 | 0x80000000u * z0)
+                     : !z1 ? 32u + (uint32_t)__builtin_ctz(w1 | 0x80000000u * z1)
+                     : !z2 ? 64u + (uint32_t)__builtin_ctz(w2 | 0x80000000u * z2)
+                           : 96u + (uint32_t)__builtin_ctz(w3 | 0x80000000u);
+    if (!z0) w0 &= w0 - 1;
+    else if (!z1) w1 &= w1 - 1;
+    else if (!z2) w2 &= w2 - 1;
+    else w3 &= w3 - 1;
+    const bool valid = ok && k < E;
+    const uint8_t c = valid ? s[e] : (uint8_t)0;
+    if (valid && c == '{') {
+      if (depth == (uint32_t)kFastDepth) ok = false;
+      st0 = depth == 0 ? e : st0;
+      st1 = depth == 1 ? e : st1;
+      st2 = depth == 2 ? e : st2;
+      st3 = depth == 3 ? e : st3;
+      depth++;
+    } else if (valid) {  // '}'
+      const uint32_t d1 = depth - 1;
+      const uint32_t sv = d1 == 0 ? st0 : d1 == 1 ? st1 : d1 == 2 ? st2 : st3;
+      const uint32_t open = sv & 0xFFFFu, h = ((sv >> 16) & 0xFu) + 1, nch = sv >> 20;
+      // '}{', too many pairs, two children, a whole-string pair (typed-result rules), > 3 top pairs
+      if (depth == 0 || np == (uint32_t)kFastPairs || nch > 1 || (open == d1 && e == n - 1 - d1) ||
+          (d1 == 0 && ntop == 3))
         ok = false;
-        break;
-      }
-      uint32_t m = cmw & keep;
-      while (m) {
-        const uint32_t e = cb + (uint32_t)__builtin_ctz(m) - p0;
-        m &= m - 1;
-        if (s[e] == '{') {
-          if (depth == (uint32_t)kFastDepth) {
-            ok = false;
-            break;
-          }
-          st0 = depth == 0 ? e : st0;
-          st1 = depth == 1 ? e : st1;
-          st2 = depth == 2 ? e : st2;
-          st3 = depth == 3 ? e : st3;
-          depth++;
-          continue;
-        }
-        if (depth == 0 || np == (uint32_t)kFastPairs) {  // '}{' or too many pairs
-          ok = false;
-          break;
-        }
-        depth--;
-        const uint32_t st = depth == 0 ? st0 : depth == 1 ? st1 : depth == 2 ? st2 : st3;
-        const uint32_t open = st & 0xFFFFu, h = (st >> 16) + 1;
-        if (open == depth && e == n - 1 - depth) {  // whole-string pair: typed-result rules
-          ok = false;
-          break;
-        }
-        uint64_t rec = (uint64_t)open | ((uint64_t)e << 16) | ((uint64_t)depth << 32) | ((uint64_t)h << 36);
-        if (depth == 0) {
-          if (2 * ntop + 3 > (uint32_t)kMaxSeg) {
-            ok = false;
-            break;
-          }
+      if (ok) {
+        uint64_t rec = (uint64_t)open | ((uint64_t)e << 16) | ((uint64_t)d1 << 32) | ((uint64_t)h << 36);
+        if (d1 == 0) {
           rec |= (uint64_t)ntop << 56;
           L.seg[2 * ntop * kBlock] = seg_make(kSegTemplate, open - run, run);
           tmpl += open - run;
           run = e + 1;
           ntop++;
-        } else {  // the parent's height is at least h + 1
-          const uint32_t hp = h << 16;
-          const uint32_t pd = depth - 1;
-          st0 = pd == 0 && (st0 >> 16) < h ? (st0 & 0xFFFFu) | hp : st0;
-          st1 = pd == 1 && (st1 >> 16) < h ? (st1 & 0xFFFFu) | hp : st1;
-          st2 = pd == 2 && (st2 >> 16) < h ? (st2 & 0xFFFFu) | hp : st2;
         }
         F.pair[np * kBlock] = rec;
+        const uint32_t bit = 1u << np;
+        hm1 |= h == 1 ? bit : 0u;
+        hm2 |= h == 2 ? bit : 0u;
+        hm3 |= h == 3 ? bit : 0u;
+        hm4 |= h == 4 ? bit : 0u;
         np++;
         H = h > H ? h : H;
+        // the parent (level d1 - 1) gains a child of height h
+        auto raise = [h](uint32_t v) {
+          const uint32_t hh = ((v >> 16) & 0xFu) > h ? ((v >> 16) & 0xFu) : h;
+          return (v & 0xFFFFu) | (hh << 16) | (((v >> 20) + 1u) << 20);
+        };
+        st0 = d1 == 1 ? raise(st0) : st0;
+        st1 = d1 == 2 ? raise(st1) : st1;
+        st2 = d1 == 3 ? raise(st2) : st2;
       }
+      depth = d1;
     }
-    if (depth) ok = false;  // unbalanced: the exact evaluator reports it
   }
-  // ---- rounds by height: every probe of a round in flight together ----
+  if (depth) ok = false;  // unbalanced: the exact evaluator reports it
+  // ---- 3. rounds by height: every probe of a round in flight together ----
   uint32_t vb_used = 0, vsum = 0;
   if (mode == 2) {  // diagnostic: parse only (output = template)
     if (ok) nseg = 1, out_len = n, L.seg[0] = seg_make(kSegTemplate, n, 0);
@@ -788,10 +865,7 @@ __device__ bool eval_fast(const DevTable& T, const lds_u8* s, uint32_t p0, uint3
   }
   const uint32_t Hw = (uint32_t)w_max(ok ? (int64_t)H : 0);
   for (uint32_t h = 1; h <= Hw; h++) {
-    uint32_t hm = 0;
-    if (ok)
-      for (uint32_t j = 0; j < np; j++)
-        if (pr_height(F.pair[j * kBlock]) == h) hm |= 1u << j;
+    uint32_t hm = !ok ? 0u : h == 1 ? hm1 : h == 2 ? hm2 : h == 3 ? hm3 : hm4;
     while (__any(hm != 0)) {
       const uint32_t a = hm ? (uint32_t)__builtin_ctz(hm) : 0u;
       bool pa = hm != 0;
@@ -800,42 +874,25 @@ __device__ bool eval_fast(const DevTable& T, const lds_u8* s, uint32_t p0, uint3
       bool pb = hm != 0;
       hm &= hm - 1;
       FastKey ka, kb;
-      if (pa && !fast_key(s, F, a, ka)) ok = false;
-      if (pb && ok && !fast_key(s, F, b, kb)) ok = false;
+      if (!fast_key(s, F, a, pa, ka) && pa) ok = false;
+      if (!fast_key(s, F, b, pb, kb) && pb) ok = false;
       if (!ok || mode == 3) pa = pb = false, hm = ok ? hm : 0;  // mode 3: keys only
-      const bool ta = pa && pr_depth(F.pair[a * kBlock]) != 0;
-      const bool tb = pb && pr_depth(F.pair[b * kBlock]) != 0;
-      uint32_t sa = pa ? slot_of(ka.hash, T.mask) : 0u, sb = pb ? slot_of(kb.hash, T.mask) : 0u;
-      uint32_t guard = 0;
-      while (__any(pa || pb)) {
-        FastProbe A, B;
-        if (pa) fast_load(T, sa, ta, A);
-        if (pb) fast_load(T, sb, tb, B);
-        if (pa) {
-          const uint32_t r = fast_match(A, ka);
-          if (r == 0) {
-            pa = false;
-            if (!fast_commit(F, L, a, sa, A, vb_used, vsum)) ok = false;
-          } else if (r == 2) {
-            pa = false;
-            ok = false;  // a miss: the exact evaluator decides the error
-          } else {
-            sa = (sa + 1) & T.mask;
-          }
-        }
-        if (pb) {
-          const uint32_t r = fast_match(B, kb);
-          if (r == 0) {
-            pb = false;
-            if (!fast_commit(F, L, b, sb, B, vb_used, vsum)) ok = false;
-          } else if (r == 2) {
-            pb = false;
-            ok = false;
-          } else {
-            sb = (sb + 1) & T.mask;
-          }
-        }
-        if (++guard > T.mask) pa = pb = false, ok = false;  // full table: cannot happen (load <= 1/2)
+      // both cuckoo slots of both keys in flight together: one memory latency per sub-round
+      const SlotPair xa = slots_of(ka.hash, T.mask), xb = slots_of(kb.hash, T.mask);
+      FastProbe A1, A2, B1, B2;
+      fast_load(T, pa ? xa.s1 : 0u, A1);
+      fast_load(T, pa ? xa.s2 : 0u, A2);
+      fast_load(T, pb ? xb.s1 : 0u, B1);
+      fast_load(T, pb ? xb.s2 : 0u, B2);
+      if (pa) {
+        const bool h1 = fast_match(A1, ka), h2 = fast_match(A2, ka);
+        if (!(h1 || h2) || !fast_commit(F, L, a, h1 ? xa.s1 : xa.s2, h1 ? A1 : A2, vb_used, vsum))
+          ok = false;  // a miss: the exact evaluator decides the error
+      }
+      if (pb) {
+        const bool h1 = fast_match(B1, kb), h2 = fast_match(B2, kb);
+        if (!(h1 || h2) || !fast_commit(F, L, b, h1 ? xb.s1 : xb.s2, h1 ? B1 : B2, vb_used, vsum))
+          ok = false;
       }
       if (!ok) hm = 0;
     }
@@ -959,7 +1016,8 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
   __shared__ uint16_t s_pend[kBlock];
   __shared__ uint32_t s_misc[4];  // tile, pending count
   __shared__ uint64_t s_red[kBlock / 64 + 2];
-  __shared__ uint32_t s_cm[(kTileBytes + 32) / 16];  // event masks of the staged chunks
+  __shared__ uint32_t s_sink[kBlock];  // per-lane write sink of the branch-free LDS writers
+  __shared__ uint32_t s_cm[(kTileBytes + 32) / 16 + 10];  // event masks of the staged chunks (+ window pad)
 
   const uint32_t tid = threadIdx.x, wave = tid >> 6;
   uint64_t t_start = 0;
@@ -1030,10 +1088,12 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
     } else if (staged) {
       const FastLds F{(lds_u8*)(s_u + tid * kKeyCap), (lds_u64*)(lds_u8*)(s_u + kKbufLds + kStackLds) + tid,
                       (lds_u8*)(s_u + kKbufLds + kStackLds + kPairLds + tid * kFastVb)};
-      const bool fast = eval_fast(T, (const lds_u8*)s_in + p0, p0, (uint32_t)sn, (const lds_u32*)s_cm,
+      const bool fast = eval_fast(T, (const lds_u8*)s_in, p0, (uint32_t)sn, (const lds_u32*)s_cm,
                                   active && W.fast_mode, W.fast_mode, F, L, olen, ns);
       const bool slow = active && !fast;
-      if (__any(slow)) {
+      const uint64_t slow_m = __ballot(slow);
+      if (slow_m) {
+        if (lane_id() == 0 && W.fast_mode) atomicAdd(W.stats + 3, (uint32_t)__popcll(slow_m));
         uint32_t o2 = 0, n2 = 0;
         const uint8_t r2 = eval_events(T, (const lds_u8*)s_in + p0, p0, (uint32_t)sn, (const lds_u32*)s_cm,
                                        slow, L, o2, vid, n2);
@@ -1139,22 +1199,26 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
       continue;
     }
     __syncthreads();  // the union region becomes the output stage (keys/stacks are dead)
-    if (mine) {
-      uint8_t* d = s_u + oshift + (local - h_lo);
+    {
+      // wave-uniform loop over segment indices; lanes without that segment write nothing
+      lds_u8* const sink = (lds_u8*)(s_sink + tid);
+      lds_u8* const d = (lds_u8*)(s_u + oshift + (mine ? local - h_lo : 0));
+      const uint32_t nsl = mine ? ns : 0u;
       uint32_t w = 0;
-      for (uint32_t k = 0; k < ns; k++) {
-        const uint64_t sg = ((const lds_u64*)s_seg)[k * kBlock + tid];
+      for (uint32_t k = 0; __any(k < nsl); k++) {
+        const bool has = k < nsl;
+        const uint64_t sg = has ? ((const lds_u64*)s_seg)[k * kBlock + tid] : 0ull;
         const uint32_t kind = (uint32_t)(sg >> 62), len = (uint32_t)(sg >> 32) & 0x3FFFFFFFu,
                        src = (uint32_t)sg;
-        if (kind == kSegTemplate)
-          copy_bytes<true, true>(d + w, s + src, len);
-        else if (kind == kSegBucket)
-          put_bucket_text((lds_u8*)(d + w), T.buckets + src, len);
-        else if (kind == kSegValue)
-          copy_bytes<true, false>(d + w, T.arena + src, len);
-        else
-          copy_bytes<true, false>(d + w, W.pool + ((uint64_t)src << 4), len);
-        w += len;
+        const bool tpl = has && kind == kSegTemplate, bkt = has && kind == kSegBucket;
+        if (__any(tpl))
+          lds_copy(d + w, tpl ? (const lds_u8*)s + src : (const lds_u8*)s_in, tpl ? len : 0u, sink);
+        if (__any(bkt)) put_bucket_text(d + w, T.buckets + (bkt ? src : 0u), bkt ? len : 0u, sink);
+        if (has && kind == kSegValue)
+          copy_bytes<true, false>((uint8_t*)(d + w), T.arena + src, len);
+        else if (has && kind == kSegPool)
+          copy_bytes<true, false>((uint8_t*)(d + w), W.pool + ((uint64_t)src << 4), len);
+        w += has ? len : 0u;
       }
     }
     __syncthreads();
@@ -1178,6 +1242,44 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
   }
   IE_STAMP(5);
 #undef IE_STAMP
+}
+
+// diagnostic: one key through the device lookups. out[0..1] hash, out[2] s1, out[3] s2,
+// out[4] find_bytes, out[5] find_small (klen <= kInlineKey), out[6] mask
+__global__ void k_debug_probe(DevTable T, const uint8_t* key, uint32_t klen, uint64_t* out) {
+  __shared__ uint32_t kb[16];
+  const uint32_t lane = threadIdx.x;
+  if (lane < 16) kb[lane] = 0;
+  __syncthreads();
+  if (lane == 0)
+    for (uint32_t j = 0; j < klen && j < 64; j++) ((uint8_t*)kb)[j] = key[j];
+  __syncthreads();
+  // all 64 lanes, uniformly (as the literal path calls it)
+  Hit hw{0, 0, 0, 0};
+  const int32_t fw = find_bytes(T, key, klen, hw);
+  const uint64_t agree = __ballot(fw == __shfl(fw, 0, 64) && hw.text_off == __shfl(hw.text_off, 0, 64));
+  if (lane != 0) return;
+  const uint64_t hash = hash_key(klen, [&](uint32_t j) { return key[j]; });
+  const SlotPair sp = slots_of(hash, T.mask);
+  Hit h;
+  const int32_t fb = find_bytes(T, key, klen, h);
+  const int32_t fs = klen <= kInlineKey ? find_small(T, (const lds_u32*)(lds_u8*)(uint8_t*)kb, klen, h) : -2;
+  out[0] = hash;
+  out[1] = hash >> 32;
+  out[2] = sp.s1;
+  out[3] = sp.s2;
+  out[4] = (uint64_t)(int64_t)fb;
+  out[5] = (uint64_t)(int64_t)fs;
+  out[6] = T.mask;
+  out[12] = (uint64_t)(int64_t)fw;
+  out[13] = agree;
+  out[14] = hw.text_off;
+  out[15] = h.text_off;
+}
+
+hipError_t launch_debug_probe(const DevTable& T, const uint8_t* key, uint32_t klen, uint64_t* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_debug_probe, dim3(1), dim3(64), 0, st, T, key, klen, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_resolve(const Batch& B, const Work& W, const DevTable& T, uint8_t* out, uint64_t cap,
