@@ -8,7 +8,7 @@ import ctypes
 import os
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libie_amd.so")
+LIB_PATH = os.environ.get("IE_LIB_PATH") or os.path.join(PKG_DIR, "libie_amd.so")  # override: experiments
 
 IE_DIALECT = {"py": 0, "rs": 1}
 KIND_STR, KIND_INT, KIND_LIST, KIND_FLOAT, KIND_BOOL, KIND_NULL, KIND_DICT = range(7)

@@ -1,13 +1,14 @@
 // ie_common.h — types shared by the host table builder and the gfx950 kernels.
 //
 // Device data layout of one inserts table (built once per get_interpdata snapshot, read-only):
-//   buckets[cap]    Bucket (128 B = one L2 line): 64-bit key hash, lengths, flags, value id, arena
-//                   offsets, and inline copies of the key (<= 32 B) and splice text (<= 64 B), so
-//                   one probe is one line; two-choice cuckoo placement (slots_of), cap =
-//                   next_pow2(4 * entries) (load factor <= 0.25): a lookup reads two buckets
-//   arena[...]      every key and splice text (texts 4-byte aligned, for dword copies)
-// The key hash mixes the key's little-endian 4-byte words (zero padded) seeded with its length;
-// slots = two bit fields of fmix64(hash).
+//   pilots[nb]      uint16 per pilot group: the displacement that sends every key of the group to
+//                   its own entry (a perfect hash: each key has exactly ONE candidate entry)
+//   entries[m]      Entry (64 B): lengths, flags, arena offset, value id, and inline copies of the
+//                   key (<= 16 B) and splice text (<= 28 B), so a lookup is one 64-byte read;
+//                   m = next_pow2(1.25 * entries) (load <= 0.8)
+//   arena[...]      every splice text (4-byte aligned) followed by its key (4-byte aligned)
+// Lookup of key k: h = hash_key(k, seed); group g = ph_group(h, nb); slot = ph_slot(h, pilots[g]);
+// the key is present iff entries[slot] holds it (full byte compare: exact, never a hash test).
 #pragma once
 #include <stdint.h>
 
@@ -24,10 +25,13 @@ IE_HD uint64_t hash_word(uint64_t h, uint32_t w) {
   return h ^ (h >> 32);
 }
 
-// hash of n key bytes (any address space via the byte reader)
+IE_HD uint64_t hash_init(uint32_t n, uint64_t seed) { return seed ^ (uint64_t)n; }
+
+// hash of n key bytes (any address space via the byte reader): the key's little-endian 4-byte
+// words (zero padded) mixed into a state seeded with the table seed and the length
 template <class ByteAt>
-IE_HD uint64_t hash_key(uint32_t n, ByteAt at) {
-  uint64_t h = 0xA0761D6478BD642Full ^ (uint64_t)n;
+IE_HD uint64_t hash_key(uint32_t n, ByteAt at, uint64_t seed) {
+  uint64_t h = hash_init(n, seed);
   for (uint32_t j = 0; j < n; j += 4) {
     uint32_t w = 0;
     for (uint32_t b = 0; b < 4 && j + b < n; b++) w |= (uint32_t)at(j + b) << (8 * b);
@@ -36,56 +40,56 @@ IE_HD uint64_t hash_key(uint32_t n, ByteAt at) {
   return h;
 }
 
-IE_HD uint64_t fmix64(uint64_t k) {
-  k ^= k >> 33;
-  k *= 0xff51afd7ed558ccdull;
-  k ^= k >> 33;
-  k *= 0xc4ceb9fe1a85ec53ull;
-  k ^= k >> 33;
-  return k;
+IE_HD uint32_t fmix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x85EBCA6Bu;
+  x ^= x >> 13;
+  x *= 0xC2B2AE35u;
+  x ^= x >> 16;
+  return x;
 }
 
-// Two-choice cuckoo placement: a key lives in slot s1 or s2 (two bit fields of one mixed hash;
-// s2 = s1 ^ 1 when they collide), so every lookup is ONE round trip that reads both buckets.
-struct SlotPair {
-  uint32_t s1, s2;
-};
-IE_HD SlotPair slots_of(uint64_t h, uint32_t mask) {
-  const uint64_t f = fmix64(h);
-  const uint32_t a = (uint32_t)f & mask, b = (uint32_t)(f >> 32) & mask;
-  return SlotPair{a, b == a ? a ^ 1u : b};
+// pilot group of a key hash (multiply-shift range reduction of the high word)
+IE_HD uint32_t ph_group(uint64_t h, uint32_t nb) { return (uint32_t)(((h >> 32) * (uint64_t)nb) >> 32); }
+// entry slot of a key hash under its group's pilot
+IE_HD uint32_t ph_slot(uint64_t h, uint32_t pilot, uint32_t mask) {
+  return fmix32((uint32_t)h ^ (pilot * 0x9E3779B9u)) & mask;
 }
 
-// Bucket.flags
+// Entry.flags
 enum : uint32_t {
   EF_KIND_MASK = 7u,
   EF_SPLICE_OK = 1u << 3,      // the dialect's splice type rule passes (py:530 / interp.rs:71-80)
   EF_INERT = 1u << 4,          // splice text cannot alter brace/escape/placeholder structure
   EF_KEY_STR = 1u << 5,        // raw value usable as a lookup key (py: str only; rs: value_to_string)
   EF_KEY_UNHASHABLE = 1u << 6, // py: list/dict raw value as a dict key raises TypeError
+  EF_OCCUPIED = 1u << 7,       // the entry holds a key
 };
 
 // DevTable.flags
 enum : uint32_t { TF_HAS_DIR = 1u };
 
-constexpr uint32_t EF_OCCUPIED = 1u << 7;  // Bucket.flags: the bucket holds an entry
-constexpr uint32_t kInlineKey = 32;         // bytes of key kept inline in a bucket
-constexpr uint32_t kInlineText = 64;        // bytes of splice text kept inline in a bucket
+constexpr uint32_t kInlineKey = 16;   // bytes of key kept inline in an entry
+constexpr uint32_t kInlineText = 28;  // bytes of splice text kept inline in an entry
 
-struct Bucket {
-  uint64_t hash;
-  uint32_t key_len, text_len;
-  uint32_t vid, flags;
-  uint32_t key_off, text_off;   // arena offsets (always valid)
-  uint8_t key[kInlineKey];      // zero padded
-  uint8_t text[kInlineText];    // zero padded
+struct Entry {
+  uint32_t key_len, text_len, flags, text_off;  // 16-byte word 0
+  uint8_t key[kInlineKey];                      // word 1: zero padded
+  uint32_t vid;                                 // word 2.x
+  uint8_t text[kInlineText];                    // words 2.yzw, 3: zero padded
 };
-static_assert(sizeof(Bucket) == 128, "Bucket must stay one 128-byte line");
+static_assert(sizeof(Entry) == 64, "Entry must stay one 64-byte block");
+
+// the key's arena offset: right after the (4-aligned) splice text
+IE_HD uint32_t key_off_of(uint32_t text_off, uint32_t text_len) { return text_off + ((text_len + 3u) & ~3u); }
 
 struct DevTable {
-  const Bucket* buckets;
+  const Entry* entries;
+  const uint16_t* pilots;
   const uint8_t* arena;
-  uint32_t mask;
+  uint64_t seed;
+  uint32_t mask;  // entries - 1
+  uint32_t nb;    // pilot groups
   uint32_t n_entries;
   uint32_t dialect;
   uint32_t flags;

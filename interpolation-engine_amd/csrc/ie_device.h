@@ -1,5 +1,5 @@
 // ie_device.h — device-side building blocks shared by the kernels: wave primitives, the
-// get_interpdata lookup (py:430-467 / interp.rs:91-137) against the bucketed device table.
+// get_interpdata lookup (py:430-467 / interp.rs:91-137) against the perfect-hash device table.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -57,77 +57,66 @@ __device__ __forceinline__ int64_t w_max(int64_t v) {
 }
 
 // ------------------------------------------------------------------------------------------
-// lookups
+// lookups: perfect hash (ie_common.h) -> one candidate entry, full byte compare
 // ------------------------------------------------------------------------------------------
 struct Hit {
   uint32_t text_len, text_off, vid, flags;
 };
 
-// a: table arena (global), b: any address space
-__device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, uint32_t n) {
+__device__ __forceinline__ uint32_t ph_lookup_slot(const DevTable& T, uint64_t h) {
+  const uint32_t pilot = gld(T.pilots + ph_group(h, T.nb));
+  return ph_slot(h, pilot, T.mask);
+}
+
+// the rest of a long key (bytes 16..klen) against the arena copy; b in any address space
+__device__ __forceinline__ bool long_key_eq(const DevTable& T, uint4 q0, const uint8_t* b, uint32_t klen) {
+  const uint8_t* a = T.arena + key_off_of(q0.w, q0.y);
   bool eq = true;
-  for (uint32_t j = 0; j < n; j++) eq &= gld(a + j) == b[j];
+  for (uint32_t j = kInlineKey; j < klen; j++) eq &= gld(a + j) == b[j];
   return eq;
 }
 
-__device__ __forceinline__ Hit hit_of(uint4 q0, uint4 q1) {
-  return Hit{q0.w, q1.w, q1.x, q1.y};
+__device__ __forceinline__ bool entry_head_ok(uint4 q0, uint32_t klen) {
+  return ((q0.z & EF_OCCUPIED) != 0) & (q0.x == klen);
 }
 
-// Lookup of a key whose bytes are at `key` (any address space): both cuckoo slots. Returns the
-// bucket or -1.
-// (Written without a loop: an unrolled two-iteration loop with an early return compiled to code
-// that returned the second slot's index without writing `h`.)
+// Lookup of a key whose bytes are at `key` (generic pointer: LDS or global). Returns the entry
+// index or -1.
 __device__ int32_t find_bytes(const DevTable& T, const uint8_t* key, uint32_t klen, Hit& h) {
-  const uint64_t hash = hash_key(klen, [&](uint32_t j) { return key[j]; });
-  const SlotPair sp = slots_of(hash, T.mask);
-  const uint4* b1 = (const uint4*)(T.buckets + sp.s1);
-  const uint4* b2 = (const uint4*)(T.buckets + sp.s2);
-  const uint4 a0 = gld4(b1), a1 = gld4(b1 + 1), c0 = gld4(b2), c1 = gld4(b2 + 1);
-  const bool ma = ((a1.y & EF_OCCUPIED) != 0) & ((((uint64_t)a0.y << 32) | a0.x) == hash) & (a0.z == klen);
-  const bool mc = ((c1.y & EF_OCCUPIED) != 0) & ((((uint64_t)c0.y << 32) | c0.x) == hash) & (c0.z == klen);
-  const bool ha = ma && bytes_eq(T.arena + a1.z, key, klen);
-  const bool hc = !ha && mc && bytes_eq(T.arena + c1.z, key, klen);
-  h = ha ? hit_of(a0, a1) : hit_of(c0, c1);
-  return ha ? (int32_t)sp.s1 : hc ? (int32_t)sp.s2 : -1;
+  const uint64_t hash = hash_key(klen, [&](uint32_t j) { return key[j]; }, T.seed);
+  const uint32_t slot = ph_lookup_slot(T, hash);
+  const Entry* e = T.entries + slot;
+  const uint4 q0 = gld4((const uint4*)e), q1 = gld4((const uint4*)e + 1);
+  const uint32_t kw[4] = {q1.x, q1.y, q1.z, q1.w};
+  bool eq = entry_head_ok(q0, klen);
+  const uint32_t ni = klen < kInlineKey ? klen : kInlineKey;
+  for (uint32_t j = 0; j < ni; j++) eq &= (uint8_t)(kw[j >> 2] >> (8 * (j & 3))) == key[j];
+  if (eq && klen > kInlineKey) eq = long_key_eq(T, q0, key, klen);
+  h = Hit{q0.y, q0.w, gld(&e->vid), q0.z};
+  return eq ? (int32_t)slot : -1;
 }
 
-// Lookup of a key held in LDS at a 4-byte aligned address, klen <= kInlineKey: the key is read
-// as dwords and hashed word-wise; both slots' 64-byte bursts (header + inline key) go out
-// together and are compared dword-wise in registers.
-__device__ __forceinline__ int32_t find_small(const DevTable& T, const __attribute__((address_space(3))) uint32_t* key32,
-                                              uint32_t klen, Hit& h) {
-  uint64_t hash = 0xA0761D6478BD642Full ^ (uint64_t)klen;
-  uint32_t kw[8];
+// Lookup of a key held as dwords at a 4-byte aligned address (generic pointer),
+// klen <= kInlineKey: hashed word-wise, compared against the entry's inline key in registers.
+__device__ __forceinline__ int32_t find_small(const DevTable& T, const uint32_t* key32, uint32_t klen, Hit& h) {
+  uint64_t hash = hash_init(klen, T.seed);
+  uint32_t kw[4];
 #pragma unroll
-  for (int d = 0; d < 8; d++) {
+  for (int d = 0; d < 4; d++) {
     const int32_t rem = (int32_t)klen - 4 * d;
     kw[d] = 0;
     if (rem > 0) {
       const uint32_t w = key32[d];
-      kw[d] = rem >= 4 ? w : (w & ((1u << (8 * rem)) - 1u));  // buckets are zero padded
+      kw[d] = rem >= 4 ? w : (w & ((1u << (8 * rem)) - 1u));  // entries are zero padded
       hash = hash_word(hash, kw[d]);
     }
   }
-  const SlotPair sp = slots_of(hash, T.mask);
-  const uint4* b1 = (const uint4*)(T.buckets + sp.s1);
-  const uint4* b2 = (const uint4*)(T.buckets + sp.s2);
-  const uint4 a0 = gld4(b1), a1 = gld4(b1 + 1), a2 = gld4(b1 + 2), a3 = gld4(b1 + 3);
-  const uint4 c0 = gld4(b2), c1 = gld4(b2 + 1), c2 = gld4(b2 + 2), c3 = gld4(b2 + 3);
-  auto eq = [&](uint4 q0, uint4 q1, uint4 q2, uint4 q3) {
-    return ((q1.y & EF_OCCUPIED) != 0) & ((((uint64_t)q0.y << 32) | q0.x) == hash) & (q0.z == klen) &
-           (q2.x == kw[0]) & (q2.y == kw[1]) & (q2.z == kw[2]) & (q2.w == kw[3]) &
-           (q3.x == kw[4]) & (q3.y == kw[5]) & (q3.z == kw[6]) & (q3.w == kw[7]);
-  };
-  if (eq(a0, a1, a2, a3)) {
-    h = hit_of(a0, a1);
-    return (int32_t)sp.s1;
-  }
-  if (eq(c0, c1, c2, c3)) {
-    h = hit_of(c0, c1);
-    return (int32_t)sp.s2;
-  }
-  return -1;
+  const uint32_t slot = ph_lookup_slot(T, hash);
+  const Entry* e = T.entries + slot;
+  const uint4 q0 = gld4((const uint4*)e), q1 = gld4((const uint4*)e + 1);
+  const bool eq = entry_head_ok(q0, klen) & (q1.x == kw[0]) & (q1.y == kw[1]) & (q1.z == kw[2]) & (q1.w == kw[3]);
+  h = Hit{q0.y, q0.w, gld(&e->vid), q0.z};
+  return eq ? (int32_t)slot : -1;
 }
 
 // status of a key that is not in the table (py:437-467 / interp.rs:105-136)

@@ -76,9 +76,10 @@ struct ie_table {
   uint32_t flags = 0;
   uint64_t n_entries = 0;
   DevTable dev{};
-  DevBuf buckets, arena;
+  DevBuf entries, pilots, arena;
   ~ie_table() {
-    buckets.release();
+    entries.release();
+    pilots.release();
     arena.release();
   }
 };
@@ -156,8 +157,66 @@ uint32_t kind_flags(int32_t kind, int32_t dialect) {
   return f;
 }
 
-uint64_t key_hash(const std::string_view k) {
-  return hash_key((uint32_t)k.size(), [&](uint32_t j) { return (uint8_t)k[j]; });
+uint64_t fmix64_host(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return k;
+}
+
+uint64_t key_hash(const std::string_view k, uint64_t seed) {
+  return hash_key((uint32_t)k.size(), [&](uint32_t j) { return (uint8_t)k[j]; }, seed);
+}
+
+// Perfect-hash placement (hash-and-displace): keys are grouped by ph_group (about 4 per group);
+// groups, largest first, each get the smallest 16-bit pilot that sends all their keys to free,
+// distinct entries. Fails (false) when some group has no such pilot; the caller then grows the
+// table or changes the seed.
+bool ph_place(const std::vector<uint64_t>& hash, uint64_t m, uint32_t nb, std::vector<uint16_t>& pilots,
+              std::vector<uint32_t>& slot_of) {
+  const uint32_t mask = (uint32_t)(m - 1);
+  std::vector<uint32_t> start(nb + 1, 0), order(hash.size());
+  for (uint64_t h : hash) start[ph_group(h, nb) + 1]++;
+  for (uint32_t g = 0; g < nb; g++) start[g + 1] += start[g];
+  {
+    std::vector<uint32_t> fill(start.begin(), start.end() - 1);
+    for (uint32_t i = 0; i < (uint32_t)hash.size(); i++) order[fill[ph_group(hash[i], nb)]++] = i;
+  }
+  std::vector<uint32_t> groups(nb);
+  for (uint32_t g = 0; g < nb; g++) groups[g] = g;
+  std::stable_sort(groups.begin(), groups.end(), [&](uint32_t a, uint32_t b) {
+    return start[a + 1] - start[a] > start[b + 1] - start[b];
+  });
+  std::vector<uint8_t> taken(m, 0);
+  pilots.assign(nb, 0);
+  slot_of.assign(hash.size(), 0);
+  std::vector<uint32_t> cand;
+  for (uint32_t g : groups) {
+    const uint32_t lo = start[g], hi = start[g + 1];
+    if (lo == hi) break;  // sorted by size: the rest are empty
+    bool found = false;
+    for (uint32_t p = 0; p < 65536 && !found; p++) {
+      cand.clear();
+      bool ok = true;
+      for (uint32_t k = lo; k < hi && ok; k++) {
+        const uint32_t s = ph_slot(hash[order[k]], p, mask);
+        if (taken[s]) ok = false;
+        for (uint32_t c : cand) ok &= c != s;
+        cand.push_back(s);
+      }
+      if (!ok) continue;
+      for (uint32_t k = lo; k < hi; k++) {
+        taken[cand[k - lo]] = 1;
+        slot_of[order[k]] = cand[k - lo];
+      }
+      pilots[g] = (uint16_t)p;
+      found = true;
+    }
+    if (!found) return false;
+  }
+  return true;
 }
 
 int set_device(int32_t dev) {
@@ -422,58 +481,46 @@ int ie_table_build(const ie_kv* kv, uint64_t n, int32_t dialect, const ie_clock*
   ents.push_back(Ent{"HH:MM:SS", hhmmss, kind_flags(IE_KIND_STR, dialect) | text_flags(hhmmss), IE_VID_CLOCK_HHMMSS});
 
   std::vector<uint8_t> arena;
-  std::vector<Bucket> items;
+  std::vector<Entry> items;
   items.reserve(ents.size());
   uint64_t maxtext = 8;
   for (const Ent& e : ents) {
     while (arena.size() & 3) arena.push_back(0);  // texts 4-byte aligned (dword copies)
     const uint64_t toff = arena.size();
     arena.insert(arena.end(), e.text.begin(), e.text.end());
-    const uint64_t koff = arena.size();
+    while (arena.size() & 3) arena.push_back(0);  // the key follows at key_off_of(toff, len)
     arena.insert(arena.end(), e.key.begin(), e.key.end());
     if (arena.size() >= 0xFFFFFFF0ull) return fail(IE_ERR_INVALID, "table arena above 4 GiB");
+    if (e.key.size() >= 0xFFFFFFF0ull || e.text.size() >= 0xFFFFFFF0ull) return fail(IE_ERR_INVALID, "key or text above 4 GiB");
     maxtext = std::max<uint64_t>(maxtext, e.text.size());
-    Bucket b{};
-    b.hash = key_hash(e.key);
+    Entry b{};
     b.key_len = (uint32_t)e.key.size();
     b.text_len = (uint32_t)e.text.size();
     b.vid = e.vid;
     b.flags = e.flags | EF_OCCUPIED;
-    b.key_off = (uint32_t)koff;
     b.text_off = (uint32_t)toff;
-    if (e.key.size() <= kInlineKey) memcpy(b.key, e.key.data(), e.key.size());
-    if (e.text.size() <= kInlineText) memcpy(b.text, e.text.data(), e.text.size());
+    memcpy(b.key, e.key.data(), std::min<size_t>(e.key.size(), kInlineKey));
+    memcpy(b.text, e.text.data(), std::min<size_t>(e.text.size(), kInlineText));
     items.push_back(b);
   }
-  // cuckoo placement: random walk of evictions; a failed walk doubles the capacity
-  uint64_t cap = 16;
-  while (cap < 4 * items.size()) cap *= 2;
-  std::vector<Bucket> buckets;
-  uint64_t rng = 0x243F6A8885A308D3ull;
-  for (;;) {
-    if (cap > (1ull << 31)) return fail(IE_ERR_INVALID, "table too large");
-    buckets.assign(cap, Bucket{});
-    const uint32_t mask = (uint32_t)(cap - 1);
-    bool placed_all = true;
-    for (const Bucket& it : items) {
-      Bucket cur = it;
-      SlotPair sp = slots_of(cur.hash, mask);
-      uint32_t pos = sp.s1;
-      bool placed = false;
-      for (int kick = 0; kick < 1000 && !placed; kick++) {
-        sp = slots_of(cur.hash, mask);
-        if (!(buckets[sp.s1].flags & EF_OCCUPIED)) { buckets[sp.s1] = cur; placed = true; break; }
-        if (!(buckets[sp.s2].flags & EF_OCCUPIED)) { buckets[sp.s2] = cur; placed = true; break; }
-        // evict from the slot we did not come from (random first move)
-        rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17;
-        pos = kick == 0 ? ((rng & 1) ? sp.s1 : sp.s2) : (pos == sp.s1 ? sp.s2 : sp.s1);
-        std::swap(cur, buckets[pos]);
-      }
-      if (!placed) { placed_all = false; break; }
-    }
-    if (placed_all) break;
-    cap *= 2;
+  // perfect-hash placement: a failed search grows the table (or, twice in a row at one size,
+  // changes the seed: two keys with one 64-bit hash can never be separated)
+  uint64_t m = 16;
+  while (m < items.size() + items.size() / 4 + 1) m *= 2;
+  const uint32_t nb = (uint32_t)std::max<uint64_t>(1, (items.size() + 3) / 4);
+  uint64_t seed = 0xA0761D6478BD642Full;
+  std::vector<uint16_t> pilots;
+  std::vector<uint32_t> slot_of;
+  for (int attempt = 0;; attempt++) {
+    if (m > (1ull << 31)) return fail(IE_ERR_INVALID, "table too large");
+    std::vector<uint64_t> hs(items.size());
+    for (size_t i = 0; i < items.size(); i++) hs[i] = key_hash(ents[i].key, seed);
+    if (ph_place(hs, m, nb, pilots, slot_of)) break;
+    if (attempt & 1) m *= 2;
+    else seed = fmix64_host(seed + 0x9E3779B97F4A7C15ull);
   }
+  std::vector<Entry> entries(m);
+  for (size_t i = 0; i < items.size(); i++) entries[slot_of[i]] = items[i];
   for (int pad = 0; pad < 16; pad++) arena.push_back(0);  // dword reads past the last text
   ie_table* t = new ie_table();
   t->device = device;
@@ -485,15 +532,19 @@ int ie_table_build(const ie_kv* kv, uint64_t n, int32_t dialect, const ie_clock*
     if (e != hipSuccess) return e;
     return bytes ? hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice) : hipSuccess;
   };
-  hipError_t e1 = up(t->buckets, buckets.data(), buckets.size() * sizeof(Bucket));
-  hipError_t e2 = e1 == hipSuccess ? up(t->arena, arena.data(), arena.size()) : e1;
-  if (e2 != hipSuccess) {
+  hipError_t e1 = up(t->entries, entries.data(), entries.size() * sizeof(Entry));
+  hipError_t e2 = e1 == hipSuccess ? up(t->pilots, pilots.data(), pilots.size() * sizeof(uint16_t)) : e1;
+  hipError_t e3 = e2 == hipSuccess ? up(t->arena, arena.data(), arena.size()) : e2;
+  if (e3 != hipSuccess) {
     delete t;
-    return fail(IE_ERR_HIP, std::string("table upload: ") + hipGetErrorString(e2));
+    return fail(IE_ERR_HIP, std::string("table upload: ") + hipGetErrorString(e3));
   }
-  t->dev.buckets = (const Bucket*)t->buckets.p;
+  t->dev.entries = (const Entry*)t->entries.p;
+  t->dev.pilots = (const uint16_t*)t->pilots.p;
   t->dev.arena = (const uint8_t*)t->arena.p;
-  t->dev.mask = (uint32_t)(cap - 1);
+  t->dev.seed = seed;
+  t->dev.nb = nb;
+  t->dev.mask = (uint32_t)(m - 1);
   t->dev.n_entries = (uint32_t)ents.size();
   t->dev.dialect = (uint32_t)dialect;
   t->dev.flags = (flags & IE_TABLE_HAS_INSERTS_DIR) ? TF_HAS_DIR : 0u;
@@ -589,8 +640,9 @@ int ie_exec_timing(ie_exec* x, ie_timing* out) {
 }
 
 // diagnostic (not part of the reference surface): device vs host view of one key's lookup.
-// out[0..6] device: hash lo/hi, s1, s2, find_bytes, find_small, mask; out[7..10] host: hash
-// lo/hi, s1, s2 and out[11] the host's bucket index holding the key (or -1)
+// out[0..1] device hash lo/hi, out[2] device slot, out[3] find_bytes, out[4] find_small (klen <= 16),
+// out[5] mask, out[7..8] host hash lo/hi, out[9] host slot, out[10] the host's entry index holding
+// the key (or -1), out[12] find_bytes by all 64 lanes, out[13] lane agreement ballot
 int ie_debug_probe(const ie_table* t, const char* key, uint64_t len, uint64_t* out) {
   if (!t || !out || (len && !key) || len > 4096) return fail(IE_ERR_INVALID, "bad argument");
   int rc = set_device(t->device);
@@ -602,19 +654,19 @@ int ie_debug_probe(const ie_table* t, const char* key, uint64_t len, uint64_t* o
   IE_HIP(launch_debug_probe(t->dev, (const uint8_t*)dk.p, (uint32_t)len, (uint64_t*)dout.p, 0));
   IE_HIP(hipDeviceSynchronize());
   IE_HIP(hipMemcpy(out, dout.p, 16 * 8, hipMemcpyDeviceToHost));
-  const uint64_t w12 = out[12], w13 = out[13], w14 = out[14], w15 = out[15];
-  const uint64_t h = key_hash(std::string_view(key ? key : "", len));
-  const SlotPair sp = slots_of(h, t->dev.mask);
+  const uint64_t h = key_hash(std::string_view(key ? key : "", len), t->dev.seed);
+  std::vector<uint16_t> pil(t->dev.nb);
+  IE_HIP(hipMemcpy(pil.data(), t->dev.pilots, pil.size() * sizeof(uint16_t), hipMemcpyDeviceToHost));
   out[7] = h & 0xFFFFFFFFull;
   out[8] = h >> 32;
-  out[9] = sp.s1;
-  out[10] = sp.s2;
-  out[11] = (uint64_t)-1;
-  std::vector<Bucket> hb((uint64_t)t->dev.mask + 1);
-  IE_HIP(hipMemcpy(hb.data(), t->dev.buckets, hb.size() * sizeof(Bucket), hipMemcpyDeviceToHost));
-  for (uint64_t i = 0; i < hb.size(); i++)
-    if ((hb[i].flags & EF_OCCUPIED) && hb[i].hash == h && hb[i].key_len == len) out[11] = i;
-  out[12] = w12, out[13] = w13, out[14] = w14, out[15] = w15;
+  out[9] = ph_slot(h, pil[ph_group(h, t->dev.nb)], t->dev.mask);
+  out[10] = (uint64_t)-1;
+  std::vector<Entry> he((uint64_t)t->dev.mask + 1);
+  IE_HIP(hipMemcpy(he.data(), t->dev.entries, he.size() * sizeof(Entry), hipMemcpyDeviceToHost));
+  for (uint64_t i = 0; i < he.size(); i++)
+    if ((he[i].flags & EF_OCCUPIED) && he[i].key_len == len &&
+        memcmp(he[i].key, key, std::min<uint64_t>(len, kInlineKey)) == 0)
+      out[10] = i;
   return IE_SUCCESS;
 }
 

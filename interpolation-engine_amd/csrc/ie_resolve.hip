@@ -4,21 +4,25 @@
 // One 256-lane workgroup per tile of 256 consecutive strings; tiles are taken from an atomic
 // ticket (so every tile a workgroup waits on is already running) and chained with a decoupled
 // look-back over 8-byte {flag, value} words published by agent-scope atomics. Per tile:
-//   1. stage the tile's input bytes in LDS (16-byte loads);
-//   2. every lane evaluates its string (eval_rounds): a skip-ahead scan that only visits the
-//      special bytes at depth 0 ('{', '}', '\', and >= 0x7B for U+3020), builds keys of open
-//      pairs in a lane-private LDS buffer, probes the bucketed table, and records the depth-0
-//      output as <= kMaxSeg segments (template runs and splice texts) — no bytes move yet;
-//   3. strings the fast path cannot prove equal to the reference are resolved by the tile's
-//      waves with the literal emulator (ie_literal.h), results in the scratch pool;
-//   4. workgroup scan of output lengths, look-back for the tile's global offset;
-//   5. each lane copies its segments (dword copies) into an LDS stage aligned like the
-//      destination; the stage streams out with 16-byte stores; offsets/status/value ids.
+//   1. stage the tile's input bytes in LDS (16-byte loads) and classify every 16-byte chunk into
+//      an open-brace and a close-brace mask (plus one "odd byte" bit per chunk: '\' or 0xE3);
+//   2. every lane evaluates its string. Clean strings (no odd byte, brace pairs forming chains
+//      such as {q-{i}}, keys <= 16 B) take the chain evaluator: pairs are parsed from the masks,
+//      then resolved level by level, innermost first, all chains of all lanes of a wave in the
+//      same round (one pilot read + one 64-byte entry read per lookup). Everything else takes the
+//      exact evaluator (a literal stack evaluation, scratch in global memory), and what that
+//      cannot prove equal to the reference goes to the literal path (one wave per string);
+//   3. the result of each string is a descriptor (<= 3 top-level pairs and their values) kept
+//      in registers; workgroup scan of output lengths, look-back for the tile's global offset;
+//   4. lanes copy template runs and value texts into an LDS stage aligned like the destination;
+//      the stage streams out with 16-byte stores; offsets, status and value ids are coalesced.
 //
-// Fast-path correctness (DESIGN.md "fast path"): for properly nested strings whose
-// spliced values are inert, the reference's rightmost-innermost loop equals this left-to-right
+// Correctness of the evaluators (DESIGN.md "fast path"): for properly nested strings
+// whose spliced values are inert, the reference's rightmost-innermost loop equals a left-to-right
 // stack evaluation, and its first failure is the failing pair with the largest opening offset
-// (pairs enclosing a failed pair are never evaluated). Everything else is PENDING -> literal.
+// (pairs enclosing a failed pair are never evaluated). The chain evaluator only commits strings
+// whose every lookup hits an inert value (then any evaluation order gives the reference's bytes);
+// any miss or doubt is re-evaluated by the exact evaluator, which reproduces the error order.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -28,18 +32,33 @@
 
 namespace ie {
 
-// segment sources: template bytes (string offset), arena text (offset), literal-path pool
-// (16-byte units), a bucket's inline text (bucket index; splice texts <= kInlineText)
-enum : uint32_t { kSegTemplate = 0, kSegValue = 1, kSegPool = 2, kSegBucket = 3 };
+// value kinds of a descriptor: arena text, literal-path pool result (16-byte units), an entry's
+// inline text (entry index; texts <= kInlineText)
+enum : uint32_t { kValArena = 1, kValPool = 2, kValEntry = 3 };
+constexpr uint32_t kLenMask = (1u << 30) - 1;
 
-__device__ __forceinline__ uint64_t seg_make(uint32_t kind, uint32_t len, uint32_t src) {
-  return ((uint64_t)kind << 62) | ((uint64_t)len << 32) | (uint64_t)src;
-}
-
-// LDS-typed views: reads through them compile to ds_* (not flat_*) instructions
+// LDS-typed views: accesses through them compile to ds_* (not flat_*) instructions
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) uint64_t lds_u64;
+typedef __attribute__((address_space(3))) u32x4 lds_u128;
+
+// The result of one string: its template with up to kMaxTop top-level pairs [open, close]
+// replaced by values. Template run j is [close[j-1] + 1, open[j]) (run 0 starts at 0, the last
+// ends at n).
+constexpr int kMaxTop = 3;
+struct Desc {
+  uint32_t ntop;
+  uint32_t open[kMaxTop], close[kMaxTop];
+  uint32_t vk[kMaxTop];  // value kind << 30 | text length
+  uint32_t vs[kMaxTop];  // entry index / arena offset / pool offset >> 4
+};
+
+__device__ __forceinline__ uint32_t value_kl(uint32_t text_len, uint32_t text_off, uint32_t slot, uint32_t& src) {
+  const bool inl = text_len <= kInlineText;
+  src = inl ? slot : text_off;
+  return ((inl ? kValEntry : kValArena) << 30) | text_len;
+}
 
 // the string being evaluated: in the tile's LDS stage (STAGED) or in global memory
 template <bool STAGED>
@@ -134,31 +153,37 @@ __device__ __forceinline__ void st32(lds_u32* p, bool on, lds_u8* sink, uint32_t
   *(on ? p : (lds_u32*)sink) = v;
 }
 
-// a bucket's inline text (16-byte aligned, len <= kInlineText) -> LDS at any byte offset: the
-// four 16-byte loads go out together (one memory latency), dwords are re-aligned with alignbyte
-__device__ __forceinline__ void put_bucket_text(lds_u8* dst, const Bucket* b, uint32_t len, lds_u8* sink) {
-  const uint4* tp = (const uint4*)b->text;
-  const uint4 t0 = gld4(tp), t1 = gld4(tp + 1), t2 = gld4(tp + 2), t3 = gld4(tp + 3);  // one line
-  const uint32_t tw[17] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w,
-                           t2.x, t2.y, t2.z, t2.w, t3.x, t3.y, t3.z, t3.w, 0u};
+// len bytes held in registers (w[0..NW-1] little-endian, w[NW] = 0 pad) -> LDS at any byte
+// offset: head bytes until dst is 4-aligned, dwords re-aligned with alignbyte, tail bytes.
+// Wave-uniform call.
+template <int NW>
+__device__ __forceinline__ void put_words(lds_u8* dst, const uint32_t (&w)[NW + 1], uint32_t len, lds_u8* sink) {
   const uint32_t a = (uint32_t)(uintptr_t)dst & 3u;
   const uint32_t head = min(len, (4u - a) & 3u);
 #pragma unroll
-  for (uint32_t k = 0; k < 3; k++) st8(dst + k, k < head, sink, (uint8_t)(tw[0] >> (8 * k)));
-  // dword q of the aligned body = text bytes head + 4q .. head + 4q + 3
+  for (uint32_t k = 0; k < 3; k++) st8(dst + k, k < head, sink, (uint8_t)(w[0] >> (8 * k)));
+  // dword q of the aligned body = bytes head + 4q .. head + 4q + 3
   lds_u32* d32 = (lds_u32*)(dst + head);
   const uint32_t rest = len - head, nq = rest >> 2, tail = rest & 3u;
   uint32_t x = 0;
 #pragma unroll
-  for (uint32_t q = 0; q < 16; q++) {
+  for (uint32_t q = 0; q < (uint32_t)NW; q++) {
     if (!__any(q <= nq)) break;  // wave-uniform exit
-    const uint32_t v = __builtin_amdgcn_alignbyte(tw[q + 1], tw[q], head);
+    const uint32_t v = __builtin_amdgcn_alignbyte(w[q + 1], w[q], head);
     st32(d32 + q, q < nq, sink, v);
     x = q == nq ? v : x;
   }
   lds_u8* t = dst + head + 4 * nq;
 #pragma unroll
   for (uint32_t k = 0; k < 3; k++) st8(t + k, k < tail, sink, (uint8_t)(x >> (8 * k)));
+}
+
+// an entry's inline text (len <= kInlineText) -> LDS at any byte offset (two 16-byte loads)
+__device__ __forceinline__ void put_entry_text(lds_u8* dst, const Entry* e, uint32_t len, lds_u8* sink) {
+  const uint4* tp = (const uint4*)e + 2;
+  const uint4 t2 = gld4(tp), t3 = gld4(tp + 1);
+  const uint32_t tw[8] = {t2.y, t2.z, t2.w, t3.x, t3.y, t3.z, t3.w, 0u};
+  put_words<7>(dst, tw, len, sink);
 }
 
 // len bytes LDS -> LDS, any alignments: dst-aligned dword body built with alignbyte from the
@@ -185,26 +210,18 @@ __device__ __forceinline__ void lds_copy(lds_u8* dst, const lds_u8* src, uint32_
   for (uint32_t k = 0; k < 3; k++) st8(td + k, k < tail, sink, ts[k]);
 }
 
-struct LaneLds {
-  lds_u8* kbuf;     // kKeyCap bytes, 4-aligned
-  lds_u32* stack;   // [kMaxDepth] stride kBlock: (enclosing key length << 24) | opening offset
-  lds_u64* seg;     // [kMaxSeg] stride kBlock
-};
-
-// Evaluate one string in ROUNDS: every lane scans (LDS only) up to its next closing brace, then
-// all lanes that reached one probe the table in the same instructions, so a wave pays one memory
-// latency per lookup round instead of one per special byte of any of its lanes.
-// RECORD mode (WRITE = false) stores depth-0 output segments in L.seg and returns their count in
-// nseg (may exceed kMaxSeg: then only the count is valid). WRITE mode copies every segment's
-// bytes to dst as it is produced (only for strings already known to be OK_STR).
-// `active` lanes take part; the call is wave-uniform (all lanes must call it).
-template <bool STAGED, bool WRITE>
-__device__ uint8_t eval_rounds(const DevTable& T, const Src<STAGED> s, uint32_t n, bool active,
-                               const LaneLds& L, uint8_t* __restrict__ dst, uint32_t& out_len,
-                               uint32_t& vid, uint32_t& nseg) {
+// ------------------------------------------------------------------------------------------
+// Exact evaluator (any string; the reference semantics of SURVEY §3.3). Rounds: every lane scans
+// up to its next closing brace, then all lanes that reached one probe the table together.
+// Scratch is lane-private LDS: the key buffer (kKeyCap bytes, 4-aligned) and the stack
+// (kMaxDepth words, stride kBlock) reuse the lane's own chain-evaluator columns.
+// ------------------------------------------------------------------------------------------
+template <bool STAGED>
+__device__ uint8_t eval_exact(const DevTable& T, const Src<STAGED> s, uint32_t n, bool active, lds_u8* kbuf,
+                              lds_u32* stack, Desc& d, uint32_t& out_len, uint32_t& vid) {
   constexpr uint8_t kRunning = 0xFF;
   uint8_t status = active ? kRunning : (uint8_t)IE_OK_STR;
-  uint32_t depth = 0, klen = 0, olen = 0, ns = 0;
+  uint32_t depth = 0, klen = 0, vsum = 0, span = 0, ntop = 0;
   uint32_t nopen = 0, nclose = 0;
   bool negclose = false;
   uint32_t poison = 0;  // bit d: the pair open at level d contains a failed pair
@@ -212,34 +229,18 @@ __device__ uint8_t eval_rounds(const DevTable& T, const Src<STAGED> s, uint32_t 
   uint8_t err_cls = 0;
   bool wrapped = false;  // a whole-string pair resolved (typed result so far in wrap_h)
   Hit wrap_h{0, 0, IE_VID_NONE, 0};
-  uint32_t run_start = 0;
   uint32_t i = 0;
-  // the close waiting for its lookup
-  uint32_t c_open = 0, c_ks = 0, c_kl = 0;
+  uint32_t c_open = 0, c_ks = 0, c_kl = 0;  // the close waiting for its lookup
   bool c_wrapping = false;
 
-  auto emit = [&](uint32_t kind, uint32_t len, uint32_t src) {
-    if (!len) return;
-    if (WRITE) {
-      if (kind == kSegTemplate) copy_bytes<false, STAGED>(dst + olen, s.p + src, len);
-      else copy_bytes<false, false>(dst + olen, T.arena + src, len);
-    } else if (ns < (uint32_t)kMaxSeg) {
-      L.seg[ns * kBlock] = seg_make(kind, len, src);
-    }
-    ns++;
-    olen += len;
-  };
   auto kput = [&](uint8_t c) -> bool {
     if (klen >= (uint32_t)kKeyCap) return false;
-    L.kbuf[klen++] = c;
+    kbuf[klen++] = c;
     return true;
   };
   // end of string: the reference's checks in order (py:516-519, 522, 540)
   auto finish = [&]() -> uint8_t {
-    if (nopen == 0) {
-      emit(kSegTemplate, n - run_start, run_start);
-      return IE_OK_STR;
-    }
+    if (nopen == 0) return IE_OK_STR;
     if (nopen != nclose) return IE_E_ASSERT_BRACES;
     if (negclose) return kStatusPending;  // balanced but '}{': py break / rs panic
     if (err_off >= 0) return err_cls;
@@ -247,12 +248,11 @@ __device__ uint8_t eval_rounds(const DevTable& T, const Src<STAGED> s, uint32_t 
       vid = wrap_h.vid;
       return IE_OK_VALUE;
     }
-    emit(kSegTemplate, n - run_start, run_start);
     return IE_OK_STR;
   };
 
   for (;;) {
-    // ---- scan phase: LDS only, up to this lane's next closing brace ----
+    // ---- scan phase: up to this lane's next closing brace ----
     bool need = false;
     while (status == kRunning) {
       if (depth == 0) {
@@ -263,7 +263,7 @@ __device__ uint8_t eval_rounds(const DevTable& T, const Src<STAGED> s, uint32_t 
           status = kStatusPending;
           break;
         }
-        for (; i < j; i++) L.kbuf[klen++] = s[i];
+        for (; i < j; i++) kbuf[klen++] = s[i];
       }
       if (i >= n) {
         status = finish();
@@ -296,8 +296,7 @@ __device__ uint8_t eval_rounds(const DevTable& T, const Src<STAGED> s, uint32_t 
           status = kStatusPending;
           break;
         }
-        if (depth == 0) emit(kSegTemplate, i - run_start, run_start);
-        L.stack[depth * kBlock] = (klen << 24) | i;  // the enclosing key resumes at klen
+        stack[depth * kBlock] = (klen << 24) | i;  // the enclosing key resumes at klen
         klen = ks;
         poison &= ~(1u << depth);
         depth++;
@@ -312,7 +311,7 @@ __device__ uint8_t eval_rounds(const DevTable& T, const Src<STAGED> s, uint32_t 
           continue;
         }
         depth--;
-        const uint32_t st = L.stack[depth * kBlock];
+        const uint32_t st = stack[depth * kBlock];
         const uint32_t open = st & 0xFFFFFFu, resume = st >> 24, ks = (resume + 3) & ~3u;
         c_kl = klen - ks;
         c_ks = ks;
@@ -347,9 +346,9 @@ __device__ uint8_t eval_rounds(const DevTable& T, const Src<STAGED> s, uint32_t 
       if (c_wrapping && wrapped) {
         b = find_raw(T, wrap_h, est, h);  // the key is the inner level's raw value
       } else {
-        b = c_kl <= kInlineKey ? find_small(T, (const lds_u32*)(L.kbuf + c_ks), c_kl, h)
-                               : find_bytes(T, (const uint8_t*)(L.kbuf + c_ks), c_kl, h);
-        if (b < 0) est = missing_status(T, (const uint8_t*)(L.kbuf + c_ks), c_kl);
+        const uint8_t* kg = (const uint8_t*)(kbuf + c_ks);  // generic view of the LDS key
+        b = c_kl <= kInlineKey ? find_small(T, (const uint32_t*)kg, c_kl, h) : find_bytes(T, kg, c_kl, h);
+        if (b < 0) est = missing_status(T, kg, c_kl);
       }
       if (b >= 0 && !c_wrapping) {
         if (!(h.flags & EF_SPLICE_OK)) {  // py:530 / interp.rs:76-79
@@ -361,13 +360,27 @@ __device__ uint8_t eval_rounds(const DevTable& T, const Src<STAGED> s, uint32_t 
           if (klen + h.text_len > (uint32_t)kKeyCap) {
             status = kStatusPending;
           } else {
-            const uint8_t* t = h.text_len <= kInlineText ? T.buckets[b].text : T.arena + h.text_off;
-            copy_bytes<true, false>((uint8_t*)(L.kbuf + klen), t, h.text_len);
+            const uint8_t* t = T.arena + h.text_off;
+            for (uint32_t k = 0; k < h.text_len; k++) kbuf[klen + k] = gld(t + k);
             klen += h.text_len;
           }
+        } else if (ntop == (uint32_t)kMaxTop) {
+          status = kStatusPending;  // more top-level pairs than a descriptor holds
         } else {
-          emit(kSegValue, h.text_len, h.text_off);
-          run_start = i + 1;
+          uint32_t src;
+          const uint32_t kl = value_kl(h.text_len, h.text_off, (uint32_t)b, src);
+#pragma unroll
+          for (int q = 0; q < kMaxTop; q++) {
+            if (ntop == (uint32_t)q) {
+              d.open[q] = c_open;
+              d.close[q] = i;
+              d.vk[q] = kl;
+              d.vs[q] = src;
+            }
+          }
+          ntop++;
+          vsum += h.text_len;
+          span += i - c_open + 1;
         }
       }
       if (b < 0) {
@@ -383,530 +396,268 @@ __device__ uint8_t eval_rounds(const DevTable& T, const Src<STAGED> s, uint32_t 
       i++;
     }
   }
-  nseg = ns;
-  out_len = status == IE_OK_STR ? olen : 0;
+  if (active) d.ntop = status == IE_OK_STR ? ntop : 0u;
+  out_len = status == IE_OK_STR ? n - span + vsum : 0;
   return status;
 }
 
 // ------------------------------------------------------------------------------------------
-// Cooperative classification of a staged tile: one 16-bit mask per 16-byte LDS chunk, bit k set
-// when byte k is '{', '}', '\' or 0xE3 (U+3020's lead byte): the only bytes that can change the
-// reference's result. Exact per-byte test: no carries cross bytes.
+// Classification of a staged tile: per 16-byte chunk, bits 0-15 = '{' bytes, bits 16-31 = '}'
+// bytes (exact per-byte tests, no carries across bytes), and an "odd" flag for '\' or 0xE3.
 // ------------------------------------------------------------------------------------------
-typedef __attribute__((address_space(3))) uint16_t lds_u16;
-
-__device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {  // 0x80 in every zero byte of x
-  return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+__device__ __forceinline__ uint32_t nib(uint32_t v) {  // bit k: byte k of v has its top bit
+  return ((v & 0x80808080u) * 0x00204081u) >> 28;
 }
-__device__ __forceinline__ uint32_t nibble_of(uint32_t z) {  // bit k: byte k of z has its top bit
-  return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
-}
-// chunk mask: bits 0-15 '{' / '}', bits 16-31 '\' / 0xE3 ("odd" bytes) of the 16-byte chunk
-__device__ __forceinline__ uint32_t chunk_mask(const lds_u32* w) {
-  uint32_t br = 0, odd = 0;
+__device__ __forceinline__ uint32_t chunk_classify(const lds_u32* w, bool& odd) {
+  uint32_t op = 0, cl = 0, od = 0;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const uint32_t x = w[k];
-    br |= nibble_of(zero_bytes(x ^ 0x7B7B7B7Bu) | zero_bytes(x ^ 0x7D7D7D7Du)) << (4 * k);
-    odd |= nibble_of(zero_bytes(x ^ 0x5C5C5C5Cu) | zero_bytes(x ^ 0xE3E3E3E3u)) << (4 * k);
+    const uint32_t x7 = x & 0x7F7F7F7Fu;
+    // top bit of each byte CLEAR exactly where the byte equals the target
+    const uint32_t no = ((x7 ^ 0x7B7B7B7Bu) + 0x7F7F7F7Fu) | x;
+    const uint32_t nc = ((x7 ^ 0x7D7D7D7Du) + 0x7F7F7F7Fu) | x;
+    const uint32_t nb = ((x7 ^ 0x5C5C5C5Cu) + 0x7F7F7F7Fu) | x;
+    const uint32_t ne = ((x7 ^ 0x63636363u) + 0x7F7F7F7Fu) | ~x;
+    od |= ~(nb & ne);
+    op |= nib(~no) << (4 * k);
+    cl |= nib(~nc) << (4 * k);
   }
-  return br | (odd << 16);
-}
-
-// Event-driven evaluation of a staged string: the same rounds and the same semantics as
-// eval_rounds, but the lane visits only its event bytes (from the chunk masks) and copies key
-// text between events with dword copies. s = the string in LDS at stage position p0.
-__device__ uint8_t eval_events(const DevTable& T, const lds_u8* s, uint32_t p0, uint32_t n,
-                               const lds_u32* cm, bool active, const LaneLds& L, uint32_t& out_len,
-                               uint32_t& vid, uint32_t& nseg) {
-  constexpr uint8_t kRunning = 0xFF;
-  uint8_t status = active ? kRunning : (uint8_t)IE_OK_STR;
-  uint32_t depth = 0, klen = 0, olen = 0, ns = 0;
-  uint32_t nopen = 0, nclose = 0;
-  bool negclose = false;
-  uint32_t poison = 0;
-  int64_t err_off = -1;
-  uint8_t err_cls = 0;
-  bool wrapped = false;
-  Hit wrap_h{0, 0, IE_VID_NONE, 0};
-  uint32_t run_start = 0;
-  uint32_t c_open = 0, c_ks = 0, c_kl = 0, c_pos = 0;
-  bool c_wrapping = false;
-  // event cursor over the chunk masks
-  const uint32_t end = p0 + n;
-  uint32_t ch = p0 >> 4, m = 0, skip_below = 0, last = 0;
-  bool m_loaded = false;
-
-  auto next_event = [&]() -> uint32_t {  // string-relative position of the next event, or n
-    for (;;) {
-      if (!m_loaded) {
-        const uint32_t cb = ch << 4;
-        if (cb >= end) return n;
-        m = cm[ch];
-        m = (m | (m >> 16)) & 0xFFFFu;
-        if (cb < p0) m &= 0xFFFFu << (p0 - cb);
-        if (cb + 16 > end) m &= (1u << (end - cb)) - 1u;
-        m_loaded = true;
-      }
-      if (m) {
-        const uint32_t e = (ch << 4) + (uint32_t)__builtin_ctz(m) - p0;
-        m &= m - 1;
-        if (e < skip_below) continue;
-        return e;
-      }
-      ch++;
-      m_loaded = false;
-    }
-  };
-  auto emit = [&](uint32_t kind, uint32_t len, uint32_t src) {
-    if (!len) return;
-    if (ns < (uint32_t)kMaxSeg) L.seg[ns * kBlock] = seg_make(kind, len, src);
-    ns++;
-    olen += len;
-  };
-  auto kput = [&](uint8_t c) -> bool {
-    if (klen >= (uint32_t)kKeyCap) return false;
-    L.kbuf[klen++] = c;
-    return true;
-  };
-  auto finish = [&]() -> uint8_t {
-    if (nopen == 0) {
-      emit(kSegTemplate, n - run_start, run_start);
-      return IE_OK_STR;
-    }
-    if (nopen != nclose) return IE_E_ASSERT_BRACES;  // py:517-519
-    if (negclose) return kStatusPending;             // balanced but '}{'
-    if (err_off >= 0) return err_cls;
-    if (wrapped) {
-      vid = wrap_h.vid;
-      return IE_OK_VALUE;
-    }
-    emit(kSegTemplate, n - run_start, run_start);
-    return IE_OK_STR;
-  };
-
-  for (;;) {
-    bool need = false;
-    while (status == kRunning) {
-      const uint32_t e = next_event();
-      if (depth) {  // the template bytes since the last event are key text
-        const uint32_t len = e - last;
-        if (klen + len > (uint32_t)kKeyCap) {
-          status = kStatusPending;
-          break;
-        }
-        copy_bytes<true, true>((uint8_t*)(L.kbuf + klen), (const uint8_t*)(s + last), len);
-        klen += len;
-      }
-      if (e >= n) {
-        status = finish();
-        break;
-      }
-      const uint8_t c = s[e];
-      last = e + 1;
-      if (c == '\\') {
-        const uint8_t nx = e + 1 < n ? s[e + 1] : 0;
-        if (nx == '{' || nx == '}') {  // escape pair (py:505-508)
-          if ((nx == '}' && e > 0 && (s[e - 1] == '.' || s[e - 1] == '}')) ||
-              (depth && !(kput(c) && kput(nx)))) {
-            status = kStatusPending;
-            break;
-          }
-          skip_below = e + 2;
-          last = e + 2;
-          continue;
-        }
-        if (depth && !kput(c)) {
-          status = kStatusPending;
-          break;
-        }
-        continue;
-      }
-      if (c == 0xE3) {
-        if ((e + 2 < n && s[e + 1] == 0x80 && s[e + 2] == 0xA0) || (depth && !kput(c))) {
-          status = kStatusPending;  // U+3020 collides with the placeholders (py:502-503)
-          break;
-        }
-        continue;
-      }
-      if (c == '{') {
-        nopen++;
-        const uint32_t ks = (klen + 3) & ~3u;
-        if (depth >= (uint32_t)kMaxDepth || ks > (uint32_t)kKeyCap) {
-          status = kStatusPending;
-          break;
-        }
-        if (depth == 0) emit(kSegTemplate, e - run_start, run_start);
-        L.stack[depth * kBlock] = (klen << 24) | e;
-        klen = ks;
-        poison &= ~(1u << depth);
-        depth++;
-        continue;
-      }
-      // '}'
-      nclose++;
-      if (depth == 0) {
-        negclose = true;
-        continue;
-      }
-      depth--;
-      const uint32_t st = L.stack[depth * kBlock];
-      const uint32_t open = st & 0xFFFFFFu, resume = st >> 24, ks = (resume + 3) & ~3u;
-      c_kl = klen - ks;
-      c_ks = ks;
-      c_open = open;
-      c_pos = e;
-      klen = resume;
-      if ((poison >> depth) & 1u) {
-        if (depth) poison |= 1u << (depth - 1);
-        continue;
-      }
-      c_wrapping = (open == depth) && (e == n - 1 - depth) && (e - open >= 2);
-      need = true;
-      break;
-    }
-    if (!__any(need)) break;
-    if (need) {
-      uint8_t est = 0;
-      Hit h;
-      int32_t b;
-      if (c_wrapping && wrapped) {
-        b = find_raw(T, wrap_h, est, h);
-      } else {
-        b = c_kl <= kInlineKey ? find_small(T, (const lds_u32*)(L.kbuf + c_ks), c_kl, h)
-                               : find_bytes(T, (const uint8_t*)(L.kbuf + c_ks), c_kl, h);
-        if (b < 0) est = missing_status(T, (const uint8_t*)(L.kbuf + c_ks), c_kl);
-      }
-      if (b >= 0 && !c_wrapping) {
-        if (!(h.flags & EF_SPLICE_OK)) {
-          b = -1;
-          est = IE_E_ASSERT_TYPE;
-        } else if (!(h.flags & EF_INERT)) {
-          status = kStatusPending;
-        } else if (depth) {
-          if (klen + h.text_len > (uint32_t)kKeyCap) {
-            status = kStatusPending;
-          } else {
-            const uint8_t* t = h.text_len <= kInlineText ? T.buckets[b].text : T.arena + h.text_off;
-            copy_bytes<true, false>((uint8_t*)(L.kbuf + klen), t, h.text_len);
-            klen += h.text_len;
-          }
-        } else {
-          if (h.text_len <= kInlineText) emit(kSegBucket, h.text_len, (uint32_t)b);
-          else emit(kSegValue, h.text_len, h.text_off);
-          run_start = c_pos + 1;
-        }
-      }
-      if (b < 0) {
-        if ((int64_t)c_open > err_off) {
-          err_off = c_open;
-          err_cls = est;
-        }
-        if (depth) poison |= 1u << (depth - 1);
-      } else if (c_wrapping) {
-        wrapped = true;
-        wrap_h = h;
-      }
-    }
-  }
-  nseg = ns;
-  out_len = status == IE_OK_STR ? olen : 0;
-  return status;
+  odd = (od & 0x80808080u) != 0;
+  return op | (cl << 16);
 }
 
 // ------------------------------------------------------------------------------------------
-// Level evaluator for CLEAN strings (the common case): only '{' / '}' events, properly nested to
-// depth <= kFastDepth, <= kFastPairs pairs, <= 3 top-level pairs, no whole-string pair, every
-// lookup a hit on an inert splice-able value with keys <= kInlineKey bytes. For such strings every
-// order of evaluation gives the reference's result (the values never create braces), so pairs are
-// resolved by HEIGHT: round h looks up every pair whose children are all resolved, up to two
-// probes in flight per lane. A lane whose string breaks any condition returns false with nothing
-// committed, and the caller re-evaluates it with eval_events (exact reference semantics).
+// Chain evaluator for CLEAN strings (the common case): no '\' or 0xE3 byte, n <= kChainMax, every
+// top-level pair a chain (each pair has at most one child: {a}, {q-{i}}, {a-{b-{c-{d}}}}), at most
+// kMaxTop chains of depth <= kChainDepth, no whole-string pair, keys <= 16 bytes, every lookup a
+// hit on an inert splice-able value. Chains resolve innermost first; round r looks up level r
+// (from the bottom) of every chain of every lane at once. A lane that breaks any condition
+// returns false with nothing committed; the exact evaluator then decides its result.
 // ------------------------------------------------------------------------------------------
-constexpr int kFastDepth = 4;
-constexpr int kFastPairs = 6;
-constexpr int kFastVb = 32;  // bytes of resolved inner values per lane
+constexpr int kChainPairs = 8;
+constexpr int kChainDepth = 4;
+constexpr uint32_t kChainMax = 112;  // bytes covered by the 128-bit event window
 
-struct FastLds {
-  lds_u8* kbuf;   // lane-private key buffer (kKeyCap bytes, 4-aligned)
-  lds_u64* pair;  // [kFastPairs] stride kBlock: pair records
-  lds_u8* vbuf;   // lane-private kFastVb bytes: texts of resolved inner pairs
+struct ChainLds {
+  lds_u32* pairs;  // [kChainPairs] stride kBlock: open | close << 16 (postorder)
+  lds_u8* kbuf;    // lane-private kMaxTop x 16 B: key prefix (A | child text) of each chain
 };
 
-// pair record: open:16 | close:16 | depth:4 | height:4 | vb_off:8 | vlen:8 | top ordinal:8
-__device__ __forceinline__ uint32_t pr_open(uint64_t r) { return (uint32_t)r & 0xFFFFu; }
-__device__ __forceinline__ uint32_t pr_close(uint64_t r) { return (uint32_t)(r >> 16) & 0xFFFFu; }
-__device__ __forceinline__ uint32_t pr_depth(uint64_t r) { return (uint32_t)(r >> 32) & 0xFu; }
-__device__ __forceinline__ uint32_t pr_height(uint64_t r) { return (uint32_t)(r >> 36) & 0xFu; }
-__device__ __forceinline__ uint32_t pr_vboff(uint64_t r) { return (uint32_t)(r >> 40) & 0xFFu; }
-__device__ __forceinline__ uint32_t pr_vlen(uint64_t r) { return (uint32_t)(r >> 48) & 0xFFu; }
-__device__ __forceinline__ uint32_t pr_top(uint64_t r) { return (uint32_t)(r >> 56); }
-
-struct FastKey {
-  uint32_t w[8];  // key bytes, zero padded like the buckets' inline keys
-  uint32_t len;
-  uint64_t hash;
+struct Probe {
+  uint4 q0, q1, q2, q3;
 };
 
-// key of pair `idx` (string s in LDS): a leaf pair's key is its template bytes, read as dwords
-// straight from the staged tile; a chain pair's key is template + its one child's text (vbuf) +
-// template, assembled bytewise in the lane's key buffer. Wave-uniform call (early exits vote).
-__device__ __forceinline__ bool fast_key(const lds_u8* s, const FastLds& F, uint32_t idx, bool on,
-                                         FastKey& K) {
-  const uint64_t rec = on ? F.pair[idx * kBlock] : 0ull;
-  const uint32_t open = pr_open(rec), close = pr_close(rec);
-  const bool leaf = pr_height(rec) <= 1;
-  uint32_t len = 0, la = 0, lv = 0, vb = 0, b0 = 0;
-  if (on) {
-    if (leaf) {
-      len = close - open - 1;
-    } else {
-      const uint64_t c = F.pair[(idx - 1) * kBlock];  // postorder: the only child closes just before
-      la = pr_open(c) - open - 1;
-      lv = pr_vlen(c);
-      vb = pr_vboff(c);
-      b0 = pr_close(c) + 1;
-      len = la + lv + (close - b0);
-    }
-  }
-  const bool fits = len <= (uint32_t)kInlineKey;
-  if (!fits) len = 0;
-  const lds_u8* src = s + open + 1;
-  if (on && fits && !leaf) {  // assemble: A | child text | B
-    for (uint32_t k = 0; k < len; k++) {
-      const uint8_t c = k < la ? src[k] : k < la + lv ? F.vbuf[vb + k - la] : s[b0 + (k - la - lv)];
-      F.kbuf[k] = c;
-    }
-  }
-  // dwords of the key: from the tile (leaf, any alignment) or the key buffer (chain, aligned)
-  const uint32_t addr = (uint32_t)(uintptr_t)src;
-  const uint32_t sh = addr & 3u;
-  const lds_u32* lw = (const lds_u32*)(lds_u8*)(uintptr_t)(addr - sh);
-  const lds_u32* kw = (const lds_u32*)F.kbuf;
-  uint64_t hash = 0xA0761D6478BD642Full ^ (uint64_t)len;
-  uint32_t prev = leaf && on && fits ? lw[0] : 0u;
+__device__ __forceinline__ void probe_load(const DevTable& T, uint32_t slot, Probe& P) {
+  const uint4* e = (const uint4*)(T.entries + slot);
+  P.q0 = gld4(e);
+  P.q1 = gld4(e + 1);
+  P.q2 = gld4(e + 2);
+  P.q3 = gld4(e + 3);
+}
+
+__device__ __forceinline__ uint32_t w_max32(uint32_t v) {
 #pragma unroll
-  for (int q = 0; q < 8; q++) {
-    K.w[q] = 0;
-    if (!__any(4 * q < (int)len)) continue;  // wave-uniform: no lane has this word
-    const int32_t rem = (int32_t)len - 4 * q;
-    if (rem > 0) {
-      uint32_t x;
-      if (leaf) {
-        const uint32_t nx = lw[q + 1];
-        x = __builtin_amdgcn_alignbyte(nx, prev, sh);
-        prev = nx;
-      } else {
-        x = kw[q];
-      }
-      if (rem < 4) x &= (1u << (8 * rem)) - 1u;
-      K.w[q] = x;
-      hash = hash_word(hash, x);
-    }
-  }
-  K.len = len;
-  K.hash = hash;
-  return fits;
+  for (int d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, d, 64));
+  return v;
 }
 
-struct FastProbe {
-  uint4 q0, q1, q2, q3, q4, q5;
-};
-
-// one probe = the bucket's first 96 bytes (header, inline key, inline text 0..31): unconditional,
-// so the loop carries no partially-defined registers (idle lanes read slot 0)
-__device__ __forceinline__ void fast_load(const DevTable& T, uint32_t slot, FastProbe& P) {
-  const uint4* bp = (const uint4*)(T.buckets + slot);
-  P.q0 = gld4(bp);
-  P.q1 = gld4(bp + 1);
-  P.q2 = gld4(bp + 2);
-  P.q3 = gld4(bp + 3);
-  P.q4 = gld4(bp + 4);
-  P.q5 = gld4(bp + 5);
-}
-
-// does the bucket hold key K (branch-free)
-__device__ __forceinline__ bool fast_match(const FastProbe& P, const FastKey& K) {
-  return ((P.q1.y & EF_OCCUPIED) != 0) & ((((uint64_t)P.q0.y << 32) | P.q0.x) == K.hash) &
-         (P.q0.z == K.len) & (P.q2.x == K.w[0]) & (P.q2.y == K.w[1]) & (P.q2.z == K.w[2]) &
-         (P.q2.w == K.w[3]) & (P.q3.x == K.w[4]) & (P.q3.y == K.w[5]) & (P.q3.z == K.w[6]) &
-         (P.q3.w == K.w[7]);
-}
-
-// commit a hit for pair idx; false when the value is not fast-path material
-__device__ __forceinline__ bool fast_commit(const FastLds& F, const LaneLds& L, uint32_t idx, uint32_t slot,
-                                            const FastProbe& P, uint32_t& vb_used, uint32_t& vsum) {
-  const uint32_t flags = P.q1.y, tlen = P.q0.w;
-  if (!(flags & EF_SPLICE_OK) || !(flags & EF_INERT)) return false;
-  uint64_t rec = F.pair[idx * kBlock];
-  if (pr_depth(rec) == 0) {
-    L.seg[(2 * pr_top(rec) + 1) * kBlock] =
-        tlen <= kInlineText ? seg_make(kSegBucket, tlen, slot) : seg_make(kSegValue, tlen, P.q1.w);
-    vsum += tlen;
-    return true;
-  }
-  if (tlen > (uint32_t)kInlineKey || vb_used + tlen > (uint32_t)kFastVb) return false;
-  const uint32_t tw[8] = {P.q4.x, P.q4.y, P.q4.z, P.q4.w, P.q5.x, P.q5.y, P.q5.z, P.q5.w};
-  lds_u32* v32 = (lds_u32*)(F.vbuf + vb_used);
-#pragma unroll
-  for (int q = 0; q < 8; q++) {
-    if (!__any(4 * q < (int)tlen)) break;  // wave-uniform exit
-    if (4 * q < (int)tlen) v32[q] = tw[q];
-  }
-  rec = (rec & ~(0xFFFFull << 40)) | ((uint64_t)vb_used << 40) | ((uint64_t)tlen << 48);
-  F.pair[idx * kBlock] = rec;
-  vb_used += (tlen + 3) & ~3u;
-  return true;
-}
-
-constexpr uint32_t kLeanMax = 112;  // strings the 128-bit event window covers
-
-// Wave-uniform call. tile = the staged tile; the string starts at stage position p0; cm = chunk
-// masks. On success: depth-0 segments in L.seg (2 * top pairs + 1 of them), nseg, out_len.
-// Shape rules on top of the clean-string rules above: n <= kLeanMax, every pair has at most one
-// child (chains such as {q-{i}}), so a chain pair's key is template + child text + template.
-__device__ bool eval_fast(const DevTable& T, const lds_u8* tile, uint32_t p0, uint32_t n,
-                          const lds_u32* cm, bool active, uint32_t mode, const FastLds& F,
-                          const LaneLds& L, uint32_t& out_len, uint32_t& nseg) {
-  bool ok = active && n <= kLeanMax;
+__device__ bool eval_chains(const DevTable& T, const lds_u8* tile, uint32_t p0, uint32_t n, const lds_u32* cm,
+                            const lds_u32* oddbits, bool active, const ChainLds& CL, lds_u8* sink, Desc& d,
+                            uint32_t& out_len) {
+  bool ok = active && n <= kChainMax;
   const lds_u8* s = tile + p0;
-  // ---- 1. the string's brace events as a 128-bit window (straight-line) ----
-  uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+  // ---- 1. the string's open / close events as 128-bit windows ----
+  uint32_t O[4], C[4];
   {
     const uint32_t c0 = ok ? p0 >> 4 : 0u, o = p0 & 15u;
-    uint32_t Wb[5], Wd[5];
+    const uint32_t cl = ok && n ? (p0 + n - 1) >> 4 : c0;
+    // any odd chunk in [c0, cl] (<= 8 chunks): escapes / U+3020 need the exact evaluator
+    const uint64_t ob = ((uint64_t)oddbits[(c0 >> 5) + 1] << 32) | oddbits[c0 >> 5];
+    if ((ob >> (c0 & 31)) & ((2ull << (cl - c0)) - 1ull)) ok = false;
+    uint32_t Wo[5], Wc[5];
 #pragma unroll
     for (int j = 0; j < 5; j++) {
       const uint32_t x = cm[c0 + 2 * j], y = j < 4 ? cm[c0 + 2 * j + 1] : 0u;
-      Wb[j] = (x & 0xFFFFu) | (y << 16);
-      Wd[j] = (x >> 16) | (y & 0xFFFF0000u);
+      Wo[j] = (x & 0xFFFFu) | (y << 16);
+      Wc[j] = (x >> 16) | (y & 0xFFFF0000u);
     }
-    uint32_t odd = 0;
-    uint32_t* wp[4] = {&w0, &w1, &w2, &w3};
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       const int32_t r = (int32_t)n - 32 * j;
-      const uint32_t keep = r >= 32 ? 0xFFFFFFFFu : r > 0 ? (1u << r) - 1u : 0u;
-      *wp[j] = __builtin_amdgcn_alignbit(Wb[j + 1], Wb[j], o) & keep;
-      odd |= __builtin_amdgcn_alignbit(Wd[j + 1], Wd[j], o) & keep;
+      const uint32_t keep = !ok ? 0u : r >= 32 ? 0xFFFFFFFFu : r > 0 ? (1u << r) - 1u : 0u;
+      O[j] = __builtin_amdgcn_alignbit(Wo[j + 1], Wo[j], o) & keep;
+      C[j] = __builtin_amdgcn_alignbit(Wc[j + 1], Wc[j], o) & keep;
     }
-    if (odd) ok = false;  // '\' or 0xE3: escapes / U+3020 need the exact evaluator
-    if (!ok) w0 = w1 = w2 = w3 = 0;
   }
-  // ---- 2. pairs: one wave-uniform pass over the events, predicated push / pop ----
-  const uint32_t E = __builtin_popcount(w0) + __builtin_popcount(w1) + __builtin_popcount(w2) +
-                     __builtin_popcount(w3);
-  const uint32_t Ew = (uint32_t)w_max((int64_t)E);
-  uint32_t depth = 0, np = 0, H = 0, ntop = 0, run = 0, tmpl = 0;
-  uint32_t hm1 = 0, hm2 = 0, hm3 = 0, hm4 = 0;
-  uint32_t st0 = 0, st1 = 0, st2 = 0, st3 = 0;  // open | height << 16 | children << 20
+  // ---- 2. parse: events in order, a 4-deep stack in one 64-bit register ----
+  uint32_t e0 = O[0] | C[0], e1 = O[1] | C[1], e2 = O[2] | C[2], e3 = O[3] | C[3];
+  const uint32_t E = __builtin_popcount(e0) + __builtin_popcount(e1) + __builtin_popcount(e2) +
+                     __builtin_popcount(e3);
+  const uint32_t Ew = w_max32(ok ? E : 0u);
+  uint32_t depth = 0, np = 0, nch = 0, cstart = 0, cinfo = 0, maxd = 0;
+  uint64_t stk = 0;
+  bool prev_close = false;
   for (uint32_t k = 0; k < Ew; k++) {
-    const bool z0 = w0 == 0, z1 = w1 == 0, z2 = w2 == 0;
-    const uint32_t e = !z0 ? (uint32_t)__builtin_ctz(w0 | 0x80000000u * z0)
-                     : !z1 ? 32u + (uint32_t)__builtin_ctz(w1 | 0x80000000u * z1)
-                     : !z2 ? 64u + (uint32_t)__builtin_ctz(w2 | 0x80000000u * z2)
-                           : 96u + (uint32_t)__builtin_ctz(w3 | 0x80000000u);
-    if (!z0) w0 &= w0 - 1;
-    else if (!z1) w1 &= w1 - 1;
-    else if (!z2) w2 &= w2 - 1;
-    else w3 &= w3 - 1;
     const bool valid = ok && k < E;
-    const uint8_t c = valid ? s[e] : (uint8_t)0;
-    if (valid && c == '{') {
-      if (depth == (uint32_t)kFastDepth) ok = false;
-      st0 = depth == 0 ? e : st0;
-      st1 = depth == 1 ? e : st1;
-      st2 = depth == 2 ? e : st2;
-      st3 = depth == 3 ? e : st3;
-      depth++;
-    } else if (valid) {  // '}'
-      const uint32_t d1 = depth - 1;
-      const uint32_t sv = d1 == 0 ? st0 : d1 == 1 ? st1 : d1 == 2 ? st2 : st3;
-      const uint32_t open = sv & 0xFFFFu, h = ((sv >> 16) & 0xFu) + 1, nch = sv >> 20;
-      // '}{', too many pairs, two children, a whole-string pair (typed-result rules), > 3 top pairs
-      if (depth == 0 || np == (uint32_t)kFastPairs || nch > 1 || (open == d1 && e == n - 1 - d1) ||
-          (d1 == 0 && ntop == 3))
-        ok = false;
-      if (ok) {
-        uint64_t rec = (uint64_t)open | ((uint64_t)e << 16) | ((uint64_t)d1 << 32) | ((uint64_t)h << 36);
-        if (d1 == 0) {
-          rec |= (uint64_t)ntop << 56;
-          L.seg[2 * ntop * kBlock] = seg_make(kSegTemplate, open - run, run);
-          tmpl += open - run;
-          run = e + 1;
-          ntop++;
-        }
-        F.pair[np * kBlock] = rec;
-        const uint32_t bit = 1u << np;
-        hm1 |= h == 1 ? bit : 0u;
-        hm2 |= h == 2 ? bit : 0u;
-        hm3 |= h == 3 ? bit : 0u;
-        hm4 |= h == 4 ? bit : 0u;
+    const bool z0 = e0 == 0, z1 = e1 == 0, z2 = e2 == 0;
+    const uint32_t w = !z0 ? e0 : !z1 ? e1 : !z2 ? e2 : e3;
+    const uint32_t ow = !z0 ? O[0] : !z1 ? O[1] : !z2 ? O[2] : O[3];
+    const uint32_t bit = (uint32_t)__builtin_ctz(w | (w ? 0u : 0x80000000u));
+    const uint32_t pos = (!z0 ? 0u : !z1 ? 32u : !z2 ? 64u : 96u) + bit;
+    const uint32_t wc = w & (w - 1);
+    e0 = !z0 ? wc : e0;
+    e1 = z0 && !z1 ? wc : e1;
+    e2 = z0 && z1 && !z2 ? wc : e2;
+    e3 = z0 && z1 && z2 ? wc : e3;
+    const bool is_open = (ow >> bit) & 1u;
+    if (valid) {
+      if (is_open) {
+        // a second child (a '{' right after a '}' inside a pair) or too deep: not a chain
+        if (depth == (uint32_t)kChainDepth || (prev_close && depth > 0)) ok = false;
+        if (depth == 0) cstart = np;
+        stk = (stk << 16) | pos;
+        depth++;
+        prev_close = false;
+      } else {
+        if (depth == 0 || np == (uint32_t)kChainPairs) ok = false;  // '}{' / too many pairs
+        const uint32_t open = (uint32_t)stk & 0xFFFFu;
+        stk >>= 16;
+        depth--;
+        if (ok) CL.pairs[np * kBlock] = open | (pos << 16);
         np++;
-        H = h > H ? h : H;
-        // the parent (level d1 - 1) gains a child of height h
-        auto raise = [h](uint32_t v) {
-          const uint32_t hh = ((v >> 16) & 0xFu) > h ? ((v >> 16) & 0xFu) : h;
-          return (v & 0xFFFFu) | (hh << 16) | (((v >> 20) + 1u) << 20);
-        };
-        st0 = d1 == 1 ? raise(st0) : st0;
-        st1 = d1 == 2 ? raise(st1) : st1;
-        st2 = d1 == 3 ? raise(st2) : st2;
+        prev_close = true;
+        if (depth == 0) {
+          const uint32_t dc = np - cstart;
+          if (nch == (uint32_t)kMaxTop) ok = false;
+          cinfo |= (cstart | (dc << 3)) << (6 * nch);
+          maxd = dc > maxd ? dc : maxd;
+          nch++;
+        }
       }
-      depth = d1;
     }
   }
   if (depth) ok = false;  // unbalanced: the exact evaluator reports it
-  // ---- 3. rounds by height: every probe of a round in flight together ----
-  uint32_t vb_used = 0, vsum = 0;
-  if (mode == 2) {  // diagnostic: parse only (output = template)
-    if (ok) nseg = 1, out_len = n, L.seg[0] = seg_make(kSegTemplate, n, 0);
-    return ok;
+  if (ok && nch == 1) {   // a whole-string pair: typed result (py:510-514), exact evaluator
+    const uint32_t top = CL.pairs[(np - 1) * kBlock];
+    if ((top & 0xFFFFu) == 0 && (top >> 16) == n - 1) ok = false;
   }
-  const uint32_t Hw = (uint32_t)w_max(ok ? (int64_t)H : 0);
-  for (uint32_t h = 1; h <= Hw; h++) {
-    uint32_t hm = !ok ? 0u : h == 1 ? hm1 : h == 2 ? hm2 : h == 3 ? hm3 : hm4;
-    while (__any(hm != 0)) {
-      const uint32_t a = hm ? (uint32_t)__builtin_ctz(hm) : 0u;
-      bool pa = hm != 0;
-      hm &= hm - 1;
-      const uint32_t b = hm ? (uint32_t)__builtin_ctz(hm) : 0u;
-      bool pb = hm != 0;
-      hm &= hm - 1;
-      FastKey ka, kb;
-      if (!fast_key(s, F, a, pa, ka) && pa) ok = false;
-      if (!fast_key(s, F, b, pb, kb) && pb) ok = false;
-      if (!ok || mode == 3) pa = pb = false, hm = ok ? hm : 0;  // mode 3: keys only
-      // both cuckoo slots of both keys in flight together: one memory latency per sub-round
-      const SlotPair xa = slots_of(ka.hash, T.mask), xb = slots_of(kb.hash, T.mask);
-      FastProbe A1, A2, B1, B2;
-      fast_load(T, pa ? xa.s1 : 0u, A1);
-      fast_load(T, pa ? xa.s2 : 0u, A2);
-      fast_load(T, pb ? xb.s1 : 0u, B1);
-      fast_load(T, pb ? xb.s2 : 0u, B2);
-      if (pa) {
-        const bool h1 = fast_match(A1, ka), h2 = fast_match(A2, ka);
-        if (!(h1 || h2) || !fast_commit(F, L, a, h1 ? xa.s1 : xa.s2, h1 ? A1 : A2, vb_used, vsum))
-          ok = false;  // a miss: the exact evaluator decides the error
+  // ---- 3. rounds: level r of every chain, all lookups of a round in flight together ----
+  uint32_t kl[kMaxTop] = {0, 0, 0}, pcl[kMaxTop] = {0, 0, 0};
+  uint32_t vsum = 0, span = 0;
+  const uint32_t R = w_max32(ok ? maxd : 0u);
+  for (uint32_t r = 0; r < R; r++) {
+    bool on[kMaxTop];
+    uint32_t idx[kMaxTop], open[kMaxTop], close[kMaxTop], klen[kMaxTop], kw[kMaxTop][4], dcs[kMaxTop];
+    uint64_t h[kMaxTop];
+#pragma unroll
+    for (int c = 0; c < kMaxTop; c++) {
+      const uint32_t first = (cinfo >> (6 * c)) & 7u;
+      dcs[c] = (cinfo >> (6 * c + 3)) & 7u;
+      on[c] = ok && (uint32_t)c < nch && r < dcs[c];
+      idx[c] = first + r;
+      const uint32_t rec = on[c] ? CL.pairs[idx[c] * kBlock] : 0u;
+      open[c] = rec & 0xFFFFu;
+      close[c] = rec >> 16;
+      kw[c][0] = kw[c][1] = kw[c][2] = kw[c][3] = 0;
+      klen[c] = 0;
+      h[c] = 0;
+      if (!__any(on[c])) continue;
+      if (r == 0) {  // a leaf: the key is template bytes, read as dwords from the stage
+        const uint32_t len = on[c] ? close[c] - open[c] - 1 : 0u;
+        const uint32_t a = (uint32_t)(uintptr_t)(s + open[c] + 1);
+        const uint32_t sh = a & 3u;
+        const lds_u32* lw = (const lds_u32*)(lds_u8*)(uintptr_t)(a - sh);
+        uint32_t prev = lw[0];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          if (!__any(on[c] && 4 * q < (int)len)) break;
+          const uint32_t nx = lw[q + 1];
+          kw[c][q] = __builtin_amdgcn_alignbyte(nx, prev, sh);
+          prev = nx;
+        }
+        klen[c] = len;
+      } else {  // key = A | child text (already in kbuf) | B (template after the child)
+        lds_u8* kb = CL.kbuf + 16 * c;
+        const uint32_t lb = on[c] ? close[c] - pcl[c] - 1 : 0u;
+        const uint32_t len = kl[c] + lb;
+        const bool fit = len <= 16u;
+        if (__any(on[c] && fit && lb)) lds_copy(kb + kl[c], s + pcl[c] + 1, on[c] && fit ? lb : 0u, sink);
+        const u32x4 v = *(const lds_u128*)kb;
+        kw[c][0] = v.x, kw[c][1] = v.y, kw[c][2] = v.z, kw[c][3] = v.w;
+        klen[c] = len;
       }
-      if (pb) {
-        const bool h1 = fast_match(B1, kb), h2 = fast_match(B2, kb);
-        if (!(h1 || h2) || !fast_commit(F, L, b, h1 ? xb.s1 : xb.s2, h1 ? B1 : B2, vb_used, vsum))
-          ok = false;
+      if (on[c] && klen[c] > 16u) {  // longer keys live in the arena: exact evaluator
+        ok = false;
+        on[c] = false;
       }
-      if (!ok) hm = 0;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {  // zero the bytes past the key (entries are zero padded)
+        const int32_t rem = (int32_t)klen[c] - 4 * q;
+        kw[c][q] = rem >= 4 ? kw[c][q] : rem > 0 ? kw[c][q] & ((1u << (8 * rem)) - 1u) : 0u;
+      }
+      h[c] = hash_init(klen[c], T.seed);
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        if (!__any(on[c] && 4 * q < (int)klen[c])) break;
+        if (4 * q < (int)klen[c]) h[c] = hash_word(h[c], kw[c][q]);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < kMaxTop; c++) on[c] = on[c] && ok;
+    // pilots of every chain, then every entry: two memory latencies per round
+    uint32_t slot[kMaxTop];
+#pragma unroll
+    for (int c = 0; c < kMaxTop; c++) {
+      const uint32_t pilot = on[c] ? (uint32_t)gld(T.pilots + ph_group(h[c], T.nb)) : 0u;
+      slot[c] = on[c] ? ph_slot(h[c], pilot, T.mask) : 0u;
+    }
+    Probe P[kMaxTop];
+#pragma unroll
+    for (int c = 0; c < kMaxTop; c++) {
+      if (__any(on[c])) probe_load(T, slot[c], P[c]);
+    }
+#pragma unroll
+    for (int c = 0; c < kMaxTop; c++) {
+      if (!__any(on[c])) continue;
+      const Probe& E = P[c];
+      const bool hit = on[c] && (entry_head_ok(E.q0, klen[c]) & (E.q1.x == kw[c][0]) & (E.q1.y == kw[c][1]) &
+                                 (E.q1.z == kw[c][2]) & (E.q1.w == kw[c][3]));
+      const uint32_t flags = E.q0.z, tlen = E.q0.y;
+      const bool good = hit && (flags & EF_SPLICE_OK) && (flags & EF_INERT);
+      if (on[c] && !good) ok = false;  // a miss or a value needing care: exact evaluator
+      const bool top = r + 1 == dcs[c];
+      // inner level: the parent's key prefix = A (template between the parent's '{' and this
+      // pair's '{') | this pair's text; it must fit the 16-byte key
+      const bool inner = on[c] && good && !top;
+      const uint32_t prec = inner ? CL.pairs[(idx[c] + 1) * kBlock] : 0u;
+      const uint32_t la = inner ? open[c] - (prec & 0xFFFFu) - 1 : 0u;
+      const bool fits = la + tlen <= 16u;
+      if (inner && !fits) ok = false;
+      const bool wr = inner && fits;
+      if (__any(wr)) {
+        lds_u8* kb = CL.kbuf + 16 * c;
+        lds_copy(kb, s + (prec & 0xFFFFu) + 1, wr ? la : 0u, sink);
+        const uint32_t tw[5] = {E.q2.y, E.q2.z, E.q2.w, E.q3.x, 0u};
+        put_words<4>(kb + la, tw, wr ? tlen : 0u, sink);
+      }
+      if (wr) {
+        kl[c] = la + tlen;
+        pcl[c] = close[c];
+      }
+      if (on[c] && good && top) {
+        uint32_t src;
+        d.vk[c] = value_kl(tlen, E.q0.w, slot[c], src);
+        d.vs[c] = src;
+        d.open[c] = open[c];
+        d.close[c] = close[c];
+        vsum += tlen;
+        span += close[c] - open[c] + 1;
+      }
     }
   }
-  if (ok && mode == 3) {
-    nseg = 1, out_len = n, L.seg[0] = seg_make(kSegTemplate, n, 0);
-    return ok;
-  }
-  if (ok) {
-    L.seg[2 * ntop * kBlock] = seg_make(kSegTemplate, n - run, run);
-    tmpl += n - run;
-    nseg = 2 * ntop + 1;
-    out_len = tmpl + vsum;
-  }
+  d.ntop = ok ? nch : 0u;
+  out_len = ok ? n - span + vsum : 0u;
   return ok;
 }
 
@@ -930,37 +681,22 @@ __device__ uint64_t look_back(uint64_t* state, uint32_t tile, uint64_t agg, uint
   uint64_t excl = 0;
   int64_t pos = (int64_t)tile - 1;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  // each poll reads a window of 4 x 64 predecessors (one memory round trip): sub-window q holds
-  // distances 64q .. 64q+63 from pos, lane l at distance 64q + l
+  uint32_t nap = 1, npoll = 0;
+  // each poll reads a window of 64 predecessors (lane l at distance l from pos): one 512-byte
+  // request; a window with a gap before its first inclusive word is re-read after a backoff
   for (;;) {
-    uint64_t w[4];
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const int64_t idx = pos - 64 * q - (int64_t)lane;
-      w[q] = idx >= 0 ? __hip_atomic_load(state + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFlagIncl;
-    }
-    bool done = false, wait = false;
-    uint64_t sum = 0;
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      if (done || wait) continue;  // uniform across the wave
-      const uint64_t flag = w[q] >> 62;
-      const uint64_t incl_m = __ballot(flag == 2);
-      const uint64_t wait_m = __ballot(flag == 0);
-      const uint32_t first = incl_m ? (uint32_t)__builtin_ctzll(incl_m) : 64u;
-      const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);
-      if (wait_m & need) {
-        wait = true;
-        continue;
-      }
-      sum += w_sum(lane <= first ? (w[q] & kValMask) : 0ull);
-      if (first < 64) done = true;
-    }
-    if (wait) {
-      // consume what was complete before the gap: windows before it are final
-      // (re-read from the same pos next time, so nothing is double counted)
-      if (lane == 0) atomicAdd(polls, 1u);
-      __builtin_amdgcn_s_sleep(1);
+    const int64_t idx = pos - (int64_t)lane;
+    const uint64_t w = idx >= 0 ? __hip_atomic_load(state + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFlagIncl;
+    const uint64_t flag = w >> 62;
+    const uint64_t incl_m = __ballot(flag == 2);
+    const uint64_t wait_m = __ballot(flag == 0);
+    const uint32_t first = incl_m ? (uint32_t)__builtin_ctzll(incl_m) : 64u;
+    const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);
+    if (wait_m & need) {
+      npoll++;
+      // backoff: 64 * nap cycles, doubling up to ~1 us
+      for (uint32_t k = 0; k < nap; k++) __builtin_amdgcn_s_sleep(1);
+      nap = nap < 32 ? 2 * nap : 32;
       // bounded spin: 60 s of s_memrealtime (100 MHz); a missing predecessor is a bug
       if (__builtin_amdgcn_s_memrealtime() - t0 > 6000000000ull) {
         if (lane == 0) atomicOr(err, 1u);
@@ -968,11 +704,12 @@ __device__ uint64_t look_back(uint64_t* state, uint32_t tile, uint64_t agg, uint
       }
       continue;
     }
-    excl += sum;
-    if (done) break;
-    pos -= 256;
+    excl += w_sum(lane <= first ? (w & kValMask) : 0ull);
+    if (first < 64) break;
+    pos -= 64;
   }
   if (lane == 0) publish(state, tile, kFlagIncl | (excl + agg));
+  if (polls && lane == 0 && npoll) atomicAdd(polls, npoll);  // telemetry (diagnostic runs only)
   return excl;
 }
 
@@ -996,34 +733,38 @@ __device__ uint64_t block_scan(uint64_t v, uint64_t* lds_w, uint64_t* total) {
   return base + inc - v;
 }
 
-// eval region: key buffers | eval_events' stacks | pair records | inner values. Every lane owns
-// one column of each; nothing may alias across columns of different width (waves run the fast
-// and the exact evaluator at different times).
-constexpr uint32_t kKbufLds = kBlock * kKeyCap;
-constexpr uint32_t kStackLds = kMaxDepth * kBlock * 4;
-constexpr uint32_t kPairLds = kFastPairs * kBlock * 8;
-constexpr uint32_t kEvalLds = kKbufLds + kStackLds + kPairLds + kBlock * kFastVb;
+// union region: chain-evaluator scratch (key prefixes | pair records) during evaluation, the
+// literal path's results after it, the output stage last
+constexpr uint32_t kKbufLds = kBlock * 16 * kMaxTop;
+static_assert(16 * kMaxTop >= kKeyCap && kChainPairs >= kMaxDepth, "exact-evaluator scratch");
+constexpr uint32_t kPairLds = kBlock * 4 * kChainPairs;
+constexpr uint32_t kEvalLds = kKbufLds + kPairLds;
 constexpr uint32_t kUnionLds = (kEvalLds > (uint32_t)kStageBytes + 32 ? kEvalLds : (uint32_t)kStageBytes + 32);
+constexpr uint32_t kChunks = (kTileBytes + 32) / 16;
+constexpr uint32_t kOddWords = ((kChunks + kBlock - 1) / kBlock) * (kBlock / 32) + 2;
 
 __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T, uint8_t* out,
                                                     uint64_t cap) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_in[kTileBytes + 32];
-  __shared__ __attribute__((aligned(16))) uint8_t s_u[kUnionLds];  // eval: keys+stacks; emit: stage
-  __shared__ __attribute__((aligned(16))) uint64_t s_seg[kMaxSeg * kBlock];
+  __shared__ __attribute__((aligned(16))) uint8_t s_in[kTileBytes + 48];
+  __shared__ __attribute__((aligned(16))) uint8_t s_u[kUnionLds];
   __shared__ uint32_t s_olen[kBlock];  // output length; the value id for IE_OK_VALUE strings
   __shared__ uint8_t s_st[kBlock];
-  __shared__ uint8_t s_nseg[kBlock];
   __shared__ uint16_t s_pend[kBlock];
   __shared__ uint32_t s_misc[4];  // tile, pending count
   __shared__ uint64_t s_red[kBlock / 64 + 2];
-  __shared__ uint32_t s_sink[kBlock];  // per-lane write sink of the branch-free LDS writers
-  __shared__ uint32_t s_cm[(kTileBytes + 32) / 16 + 10];  // event masks of the staged chunks (+ window pad)
+  __shared__ uint32_t s_sink[kBlock];     // per-lane write sink of the branch-free LDS writers
+  __shared__ uint32_t s_cm[kChunks + 10];  // event masks of the staged chunks (+ window pad)
+  __shared__ uint32_t s_odd[kOddWords];    // one bit per chunk: '\' or 0xE3 inside
 
-  const uint32_t tid = threadIdx.x, wave = tid >> 6;
+  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
   uint64_t t_start = 0;
   if (tid == 0) {
     if (W.stamps) t_start = __builtin_amdgcn_s_memrealtime();
+#ifdef IE_EXP_NOTICKET
+    s_misc[0] = blockIdx.x;
+#else
     s_misc[0] = atomicAdd(W.tile_ticket, 1u);
+#endif
     s_misc[1] = 0;
   }
   __syncthreads();
@@ -1048,73 +789,86 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
   const bool staged = (hi - lo) <= (uint64_t)kTileBytes;
   const uintptr_t plo = (uintptr_t)(B.bytes + lo);
   const uint32_t shift = (uint32_t)(plo & 15);
+  uint64_t so = 0, sn = 0;
+  if (i < B.n) {
+    so = gld(B.in_off + i);
+    sn = gld(B.in_off + i + 1) - so;
+  }
   if (staged) {  // whole 16-byte chunks covering [lo, hi): an aligned chunk never crosses a page
     const uint4* src = (const uint4*)(plo - shift);
     uint4* dst = (uint4*)s_in;
     const uint32_t nv = (uint32_t)((shift + (hi - lo) + 15) >> 4);
     for (uint32_t j = tid; j < nv; j += kBlock) dst[j] = gld4(src + j);
     __syncthreads();
-    for (uint32_t c = tid; c < nv; c += kBlock) {  // classify: one event mask per chunk
-      ((lds_u32*)s_cm)[c] = chunk_mask((const lds_u32*)(lds_u8*)s_in + 4 * c);
+    for (uint32_t c0 = 0; c0 < nv; c0 += kBlock) {  // uniform trip count: ballots below
+      const uint32_t c = c0 + tid;
+      bool odd = false;
+      if (c < nv) ((lds_u32*)s_cm)[c] = chunk_classify((const lds_u32*)(lds_u8*)s_in + 4 * c, odd);
+      const uint64_t ob = __ballot(odd);
+      if (lane == 0) {  // 64 consecutive chunks = two words of the odd bit array
+        ((lds_u32*)s_odd)[(c0 + 64 * wave) >> 5] = (uint32_t)ob;
+        ((lds_u32*)s_odd)[((c0 + 64 * wave) >> 5) + 1] = (uint32_t)(ob >> 32);
+      }
     }
+    if (tid < 10) ((lds_u32*)s_cm)[nv + tid] = 0;  // the event windows read past the last chunk
   }
   __syncthreads();
   IE_STAMP(1);
 
-  // ---- 2. evaluate (fast path) ----
-  uint64_t so = 0, sn = 0;
-  const LaneLds L{(lds_u8*)(s_u + tid * kKeyCap), (lds_u32*)(lds_u8*)(s_u + kKbufLds) + tid,
-                  (lds_u64*)s_seg + tid};
+  // ---- 2. evaluate ----
+  lds_u8* const sink = (lds_u8*)(s_sink + tid);
+  Desc d;
+  d.ntop = 0;
+#pragma unroll
+  for (int q = 0; q < kMaxTop; q++) d.open[q] = d.close[q] = d.vk[q] = d.vs[q] = 0;
   const uint8_t* s = nullptr;
+  const uint32_t p0 = shift + (uint32_t)(so - lo);
+  bool pend = false;
   {
     uint8_t st = IE_OK_STR;
-    uint32_t olen = 0, vid = IE_VID_NONE, ns = 0;
+    uint32_t olen = 0, vid = IE_VID_NONE;
     bool active = false;
     if (i < B.n) {
-      so = gld(B.in_off + i);
-      sn = gld(B.in_off + i + 1) - so;
-      s = staged ? s_in + shift + (so - lo) : B.bytes + so;
+      s = staged ? s_in + p0 : B.bytes + so;
       active = sn < 0xFFFF0000ull;
       if (!active) st = kStatusPending;
     }
-    // wave-uniform calls (the rounds vote across the wave); idle lanes ride along. Clean strings
-    // take the level evaluator; the rest (and its failures) the exact event evaluator.
-    const uint32_t p0 = shift + (uint32_t)(so - lo);
     uint8_t r = IE_OK_STR;
-    if (W.debug_noeval) {
-      ns = 1;
+    bool slow = active;
+    if (W.debug_noeval) {  // diagnostic: copy verbatim (the pipeline floor)
       olen = (uint32_t)sn;
-      L.seg[0] = seg_make(kSegTemplate, (uint32_t)sn, 0);
-    } else if (staged) {
-      const FastLds F{(lds_u8*)(s_u + tid * kKeyCap), (lds_u64*)(lds_u8*)(s_u + kKbufLds + kStackLds) + tid,
-                      (lds_u8*)(s_u + kKbufLds + kStackLds + kPairLds + tid * kFastVb)};
-      const bool fast = eval_fast(T, (const lds_u8*)s_in, p0, (uint32_t)sn, (const lds_u32*)s_cm,
-                                  active && W.fast_mode, W.fast_mode, F, L, olen, ns);
-      const bool slow = active && !fast;
-      const uint64_t slow_m = __ballot(slow);
-      if (slow_m) {
-        if (lane_id() == 0 && W.fast_mode) atomicAdd(W.stats + 3, (uint32_t)__popcll(slow_m));
-        uint32_t o2 = 0, n2 = 0;
-        const uint8_t r2 = eval_events(T, (const lds_u8*)s_in + p0, p0, (uint32_t)sn, (const lds_u32*)s_cm,
-                                       slow, L, o2, vid, n2);
-        if (slow) r = r2, olen = o2, ns = n2;
-      }
-    } else {
-      r = eval_rounds<false, false>(T, Src<false>{s}, (uint32_t)sn, active, L, nullptr, olen, vid, ns);
+      slow = false;
+    } else if (staged && W.fast_mode) {
+      const ChainLds CL{(lds_u32*)(lds_u8*)(s_u + kKbufLds) + tid, (lds_u8*)(s_u + tid * 16 * kMaxTop)};
+      const bool fast = eval_chains(T, (const lds_u8*)s_in, p0, (uint32_t)sn, (const lds_u32*)s_cm,
+                                    (const lds_u32*)s_odd, active, CL, sink, d, olen);
+      slow = active && !fast;
+    }
+    // the rest: the exact evaluator (scratch: the lane's own chain-evaluator columns)
+    const uint64_t slow_m = __ballot(slow);
+    if (slow_m) {
+      if (lane == 0 && W.fast_mode) atomicAdd(W.stats + 3, (uint32_t)__popcll(slow_m));  // rare
+      lds_u8* const kb = (lds_u8*)(s_u + tid * 16 * kMaxTop);
+      lds_u32* const stk = (lds_u32*)(lds_u8*)(s_u + kKbufLds) + tid;
+      uint32_t o2 = 0;
+      uint8_t r2;
+      if (staged)
+        r2 = eval_exact<true>(T, Src<true>{s}, (uint32_t)sn, slow, kb, stk, d, o2, vid);
+      else
+        r2 = eval_exact<false>(T, Src<false>{s}, (uint32_t)sn, slow, kb, stk, d, o2, vid);
+      if (slow) r = r2, olen = o2;
     }
     if (active) st = r;
-    if (i < B.n) {
-      if (st == IE_OK_STR && ns > (uint32_t)kMaxSeg) st = kStatusPending;  // too many segments
-      if (st == kStatusPending) s_pend[atomicAdd(&s_misc[1], 1u)] = (uint16_t)tid;
-    }
+    pend = i < B.n && st == kStatusPending;
+    if (pend) s_pend[atomicAdd(&s_misc[1], 1u)] = (uint16_t)tid;
     s_st[tid] = st;
     s_olen[tid] = st == IE_OK_STR ? olen : (st == IE_OK_VALUE ? vid : 0u);
-    s_nseg[tid] = (uint8_t)(ns > 255u ? 255u : ns);
   }
   __syncthreads();
   IE_STAMP(2);
 
-  // ---- 3. literal path for the pending strings, one wave each ----
+  // ---- 3. literal path for the pending strings, one wave each; results in the union ----
+  lds_u64* const s_lit = (lds_u64*)(lds_u8*)s_u;  // [kBlock]: pool offset >> 4 | length << 32
   const uint32_t npend = s_misc[1];
   if (tid == 0 && npend) atomicAdd(W.stats, npend);
   for (uint32_t k = wave; k < npend; k += kBlock / 64) {
@@ -1125,16 +879,17 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
                                   : 4 * pn + 4 * T.maxtext + 256;
     rcap = (rcap + 15) & ~15ull;
     uint64_t pbase = 0;
-    if (lane_id() == 0) pbase = atomicAdd((unsigned long long*)W.pool_used, (unsigned long long)(4 * rcap));
+    if (lane == 0) pbase = atomicAdd((unsigned long long*)W.pool_used, (unsigned long long)(4 * rcap));
     pbase = __shfl(pbase, 0, 64);
     LitOut r{IE_E_OVERFLOW, 0, 0, IE_VID_NONE};
     if (pbase + 4 * rcap <= W.pool_bytes)
       r = w_literal(T, B.bytes + po, pn, W.pool + pbase, rcap, pbase, W.lit_cap_max != 0);
-    if (lane_id() == 0) {
+    if (r.status == IE_OK_STR && (r.res_len > kLenMask || (r.res_off >> 4) > 0xFFFFFFFFull))
+      r.status = IE_E_OVERFLOW;
+    if (lane == 0) {
       s_st[j] = r.status;
       s_olen[j] = r.status == IE_OK_STR ? (uint32_t)r.res_len : (r.status == IE_OK_VALUE ? r.vid : 0u);
-      s_seg[j] = seg_make(kSegPool, (uint32_t)r.res_len, (uint32_t)(r.res_off >> 4));
-      s_nseg[j] = 1;
+      s_lit[j] = (r.res_off >> 4) | ((uint64_t)r.res_len << 32);
     }
   }
   __syncthreads();
@@ -1143,11 +898,20 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
   // ---- 4. offsets: workgroup scan + decoupled look-back ----
   const uint8_t st = s_st[tid];
   const uint32_t olen = st == IE_OK_STR ? s_olen[tid] : 0u;
+  const uint32_t n32 = (uint32_t)sn;
+  if (pend) {  // a literal-path result: the whole output is one pool value
+    const uint64_t lr = s_lit[tid];
+    d.ntop = 1;
+    d.open[0] = 0;
+    d.close[0] = n32 - 1u;
+    d.vk[0] = (kValPool << 30) | (uint32_t)(lr >> 32);
+    d.vs[0] = (uint32_t)lr;
+  }
   uint64_t tile_total;
   const uint64_t local = block_scan(olen, s_red, &tile_total);
   if (tid == 128) s_red[kBlock / 64 + 1] = local;  // output offset where the second half starts
   if (wave == 0) {
-    const uint64_t b = look_back(W.tile_state, tile, tile_total, W.err, W.stats + 2);
+    const uint64_t b = look_back(W.tile_state, tile, tile_total, W.err, W.stamps ? W.stats + 2 : nullptr);
     if (tid == 0) s_red[kBlock / 64] = b;
   }
   __syncthreads();
@@ -1178,47 +942,57 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
     const uint32_t oshift = (uint32_t)(((uintptr_t)g) & 15);
     const bool direct = !staged || h_len + oshift > (uint64_t)kStageBytes;
     const bool mine = half == hsel && i < B.n && st == IE_OK_STR && olen;
-    const uint32_t ns = s_nseg[tid];
     if (direct) {  // rare (long strings): lanes store their own bytes straight to HBM
       if (tid == 0) atomicAdd(W.stats + 1, 1u);
       if (mine) {
-        uint8_t* d = g + (local - h_lo);
+        uint8_t* dd = g + (local - h_lo);
         uint32_t w = 0;
-        for (uint32_t k = 0; k < ns; k++) {
-          const uint64_t sg = ((const lds_u64*)s_seg)[k * kBlock + tid];
-          const uint32_t kind = (uint32_t)(sg >> 62), len = (uint32_t)(sg >> 32) & 0x3FFFFFFFu,
-                         src = (uint32_t)sg;
-          const uint8_t* p = kind == kSegTemplate ? s + src
-                             : kind == kSegValue  ? T.arena + src
-                             : kind == kSegBucket ? T.buckets[src].text
-                                                  : W.pool + ((uint64_t)src << 4);
-          for (uint32_t q = 0; q < len; q++) gst(d + w + q, p[q]);
-          w += len;
+        for (uint32_t j = 0; j <= d.ntop; j++) {
+          uint32_t t_lo = 0, t_hi = n32, vk = 0, vs = 0;
+#pragma unroll
+          for (int q = 0; q < kMaxTop; q++) {
+            if (j == (uint32_t)q + 1) t_lo = d.close[q] + 1;
+            if (j == (uint32_t)q && j < d.ntop) t_hi = d.open[q], vk = d.vk[q], vs = d.vs[q];
+          }
+          for (uint32_t q = t_lo; q < t_hi; q++)
+            gst(dd + w++, staged ? ((const lds_u8*)s)[q] : gld(s + q));
+          if (j < d.ntop) {
+            const uint32_t kind = vk >> 30, len = vk & kLenMask;
+            const uint8_t* p = kind == kValEntry ? T.entries[vs].text
+                               : kind == kValArena ? T.arena + vs
+                                                   : W.pool + ((uint64_t)vs << 4);
+            for (uint32_t q = 0; q < len; q++) gst(dd + w++, gld(p + q));
+          }
         }
       }
       continue;
     }
-    __syncthreads();  // the union region becomes the output stage (keys/stacks are dead)
+    __syncthreads();  // the union region becomes the output stage (scratch/literal results are dead)
     {
-      // wave-uniform loop over segment indices; lanes without that segment write nothing
-      lds_u8* const sink = (lds_u8*)(s_sink + tid);
-      lds_u8* const d = (lds_u8*)(s_u + oshift + (mine ? local - h_lo : 0));
-      const uint32_t nsl = mine ? ns : 0u;
+      lds_u8* const dd = (lds_u8*)(s_u + oshift + (mine ? local - h_lo : 0));
+      const lds_u8* const ls = (const lds_u8*)s;
+      const uint32_t ntop = mine ? d.ntop : 0u;
       uint32_t w = 0;
-      for (uint32_t k = 0; __any(k < nsl); k++) {
-        const bool has = k < nsl;
-        const uint64_t sg = has ? ((const lds_u64*)s_seg)[k * kBlock + tid] : 0ull;
-        const uint32_t kind = (uint32_t)(sg >> 62), len = (uint32_t)(sg >> 32) & 0x3FFFFFFFu,
-                       src = (uint32_t)sg;
-        const bool tpl = has && kind == kSegTemplate, bkt = has && kind == kSegBucket;
-        if (__any(tpl))
-          lds_copy(d + w, tpl ? (const lds_u8*)s + src : (const lds_u8*)s_in, tpl ? len : 0u, sink);
-        if (__any(bkt)) put_bucket_text(d + w, T.buckets + (bkt ? src : 0u), bkt ? len : 0u, sink);
-        if (has && kind == kSegValue)
-          copy_bytes<true, false>((uint8_t*)(d + w), T.arena + src, len);
-        else if (has && kind == kSegPool)
-          copy_bytes<true, false>((uint8_t*)(d + w), W.pool + ((uint64_t)src << 4), len);
-        w += has ? len : 0u;
+#pragma unroll
+      for (int j = 0; j <= kMaxTop; j++) {
+        // template run j
+        const bool ton = mine && (uint32_t)j <= ntop;
+        const uint32_t t_lo = j == 0 ? 0u : d.close[j - 1] + 1;
+        const uint32_t t_hi = (uint32_t)j < ntop ? d.open[j] : n32;
+        const uint32_t tl = ton ? t_hi - t_lo : 0u;
+        if (__any(tl != 0)) lds_copy(dd + w, tl ? ls + t_lo : (const lds_u8*)s_in, tl, sink);
+        w += tl;
+        if (j == kMaxTop) break;
+        // value j
+        const bool von = mine && (uint32_t)j < ntop;
+        const uint32_t kind = d.vk[j] >> 30, len = von ? d.vk[j] & kLenMask : 0u;
+        const bool ent = von && kind == kValEntry;
+        if (__any(ent)) put_entry_text(dd + w, T.entries + (ent ? d.vs[j] : 0u), ent ? len : 0u, sink);
+        if (von && kind == kValArena)
+          copy_bytes<true, false>((uint8_t*)(dd + w), T.arena + d.vs[j], len);
+        else if (von && kind == kValPool)
+          copy_bytes<true, false>((uint8_t*)(dd + w), W.pool + ((uint64_t)d.vs[j] << 4), len);
+        w += len;
       }
     }
     __syncthreads();
@@ -1244,8 +1018,9 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
 #undef IE_STAMP
 }
 
-// diagnostic: one key through the device lookups. out[0..1] hash, out[2] s1, out[3] s2,
-// out[4] find_bytes, out[5] find_small (klen <= kInlineKey), out[6] mask
+// diagnostic: one key through the device lookups. out[0..1] hash, out[2] slot, out[3] find_bytes,
+// out[4] find_small (klen <= kInlineKey), out[5] mask, out[12] find_bytes by all 64 lanes,
+// out[13] lane agreement ballot
 __global__ void k_debug_probe(DevTable T, const uint8_t* key, uint32_t klen, uint64_t* out) {
   __shared__ uint32_t kb[16];
   const uint32_t lane = threadIdx.x;
@@ -1254,27 +1029,22 @@ __global__ void k_debug_probe(DevTable T, const uint8_t* key, uint32_t klen, uin
   if (lane == 0)
     for (uint32_t j = 0; j < klen && j < 64; j++) ((uint8_t*)kb)[j] = key[j];
   __syncthreads();
-  // all 64 lanes, uniformly (as the literal path calls it)
   Hit hw{0, 0, 0, 0};
   const int32_t fw = find_bytes(T, key, klen, hw);
   const uint64_t agree = __ballot(fw == __shfl(fw, 0, 64) && hw.text_off == __shfl(hw.text_off, 0, 64));
   if (lane != 0) return;
-  const uint64_t hash = hash_key(klen, [&](uint32_t j) { return key[j]; });
-  const SlotPair sp = slots_of(hash, T.mask);
+  const uint64_t hash = hash_key(klen, [&](uint32_t j) { return key[j]; }, T.seed);
   Hit h;
   const int32_t fb = find_bytes(T, key, klen, h);
-  const int32_t fs = klen <= kInlineKey ? find_small(T, (const lds_u32*)(lds_u8*)(uint8_t*)kb, klen, h) : -2;
-  out[0] = hash;
+  const int32_t fs = klen <= kInlineKey ? find_small(T, (const uint32_t*)kb, klen, h) : -2;
+  out[0] = hash & 0xFFFFFFFFull;
   out[1] = hash >> 32;
-  out[2] = sp.s1;
-  out[3] = sp.s2;
-  out[4] = (uint64_t)(int64_t)fb;
-  out[5] = (uint64_t)(int64_t)fs;
-  out[6] = T.mask;
+  out[2] = ph_lookup_slot(T, hash);
+  out[3] = (uint64_t)(int64_t)fb;
+  out[4] = (uint64_t)(int64_t)fs;
+  out[5] = T.mask;
   out[12] = (uint64_t)(int64_t)fw;
   out[13] = agree;
-  out[14] = hw.text_off;
-  out[15] = h.text_off;
 }
 
 hipError_t launch_debug_probe(const DevTable& T, const uint8_t* key, uint32_t klen, uint64_t* out, hipStream_t st) {
