@@ -31,6 +31,23 @@ __device__ __forceinline__ void gst4(uint4* p, uint4 v) {
   *(__attribute__((address_space(1))) u32x4*)(void*)p = w;
 }
 
+// Tile staging: nv 16-byte chunks src -> dst (LDS), every load of the thread in flight before
+// the first LDS write (a plain strided loop waits for each load before issuing the next).
+template <int BLOCK, int MAXV>
+__device__ __forceinline__ void stage_chunks(uint4* dst, const uint4* src, uint32_t nv, uint32_t tid) {
+  uint4 v[MAXV];
+#pragma unroll
+  for (int k = 0; k < MAXV; k++) {
+    const uint32_t j = tid + (uint32_t)k * BLOCK;
+    if (j < nv) v[k] = gld4(src + j);
+  }
+#pragma unroll
+  for (int k = 0; k < MAXV; k++) {
+    const uint32_t j = tid + (uint32_t)k * BLOCK;
+    if (j < nv) dst[j] = v[k];
+  }
+}
+
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
   const uint32_t lane = lane_id();
 #pragma unroll

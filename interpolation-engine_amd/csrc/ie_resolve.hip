@@ -670,14 +670,16 @@ __device__ __forceinline__ void publish(uint64_t* state, uint32_t tile, uint64_t
   __hip_atomic_store(state + tile, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// the tile's aggregate (or, for tile 0, its inclusive prefix) as soon as it is known
+__device__ __forceinline__ void publish_aggregate(uint64_t* state, uint32_t tile, uint64_t agg) {
+  if (lane_id() == 0) publish(state, tile, (tile == 0 ? kFlagIncl : kFlagAgg) | agg);
+}
+
+// the exclusive prefix of `tile` from its predecessors' words; publishes the inclusive prefix
 __device__ uint64_t look_back(uint64_t* state, uint32_t tile, uint64_t agg, uint32_t* err,
                               uint32_t* polls) {
   const uint32_t lane = lane_id();
-  if (tile == 0) {
-    if (lane == 0) publish(state, 0, kFlagIncl | agg);
-    return 0;
-  }
-  if (lane == 0) publish(state, tile, kFlagAgg | agg);
+  if (tile == 0) return 0;
   uint64_t excl = 0;
   int64_t pos = (int64_t)tile - 1;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -733,13 +735,13 @@ __device__ uint64_t block_scan(uint64_t v, uint64_t* lds_w, uint64_t* total) {
   return base + inc - v;
 }
 
-// union region: chain-evaluator scratch (key prefixes | pair records) during evaluation, the
-// literal path's results after it, the output stage last
+// union region: chain-evaluator / exact-evaluator scratch during evaluation, the output stage
+// (tile-relative) after it
 constexpr uint32_t kKbufLds = kBlock * 16 * kMaxTop;
 static_assert(16 * kMaxTop >= kKeyCap && kChainPairs >= kMaxDepth, "exact-evaluator scratch");
 constexpr uint32_t kPairLds = kBlock * 4 * kChainPairs;
 constexpr uint32_t kEvalLds = kKbufLds + kPairLds;
-constexpr uint32_t kUnionLds = (kEvalLds > (uint32_t)kStageBytes + 32 ? kEvalLds : (uint32_t)kStageBytes + 32);
+constexpr uint32_t kUnionLds = (kEvalLds > (uint32_t)kStageBytes + 32 ? kEvalLds : (uint32_t)kStageBytes + 32);  // +32: the stream-out reads one block past the end
 constexpr uint32_t kChunks = (kTileBytes + 32) / 16;
 constexpr uint32_t kOddWords = ((kChunks + kBlock - 1) / kBlock) * (kBlock / 32) + 2;
 
@@ -750,6 +752,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
   __shared__ uint32_t s_olen[kBlock];  // output length; the value id for IE_OK_VALUE strings
   __shared__ uint8_t s_st[kBlock];
   __shared__ uint16_t s_pend[kBlock];
+  __shared__ uint32_t s_lit[kBlock];   // literal-path result: pool offset >> 4
   __shared__ uint32_t s_misc[4];  // tile, pending count
   __shared__ uint64_t s_red[kBlock / 64 + 2];
   __shared__ uint32_t s_sink[kBlock];     // per-lane write sink of the branch-free LDS writers
@@ -798,7 +801,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
     const uint4* src = (const uint4*)(plo - shift);
     uint4* dst = (uint4*)s_in;
     const uint32_t nv = (uint32_t)((shift + (hi - lo) + 15) >> 4);
-    for (uint32_t j = tid; j < nv; j += kBlock) dst[j] = gld4(src + j);
+    stage_chunks<kBlock, ((kTileBytes + 31) / 16 + kBlock - 1) / kBlock>(dst, src, nv, tid);
     __syncthreads();
     for (uint32_t c0 = 0; c0 < nv; c0 += kBlock) {  // uniform trip count: ballots below
       const uint32_t c = c0 + tid;
@@ -868,7 +871,6 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
   IE_STAMP(2);
 
   // ---- 3. literal path for the pending strings, one wave each; results in the union ----
-  lds_u64* const s_lit = (lds_u64*)(lds_u8*)s_u;  // [kBlock]: pool offset >> 4 | length << 32
   const uint32_t npend = s_misc[1];
   if (tid == 0 && npend) atomicAdd(W.stats, npend);
   for (uint32_t k = wave; k < npend; k += kBlock / 64) {
@@ -889,33 +891,64 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
     if (lane == 0) {
       s_st[j] = r.status;
       s_olen[j] = r.status == IE_OK_STR ? (uint32_t)r.res_len : (r.status == IE_OK_VALUE ? r.vid : 0u);
-      s_lit[j] = (r.res_off >> 4) | ((uint64_t)r.res_len << 32);
+      s_lit[j] = (uint32_t)(r.res_off >> 4);
     }
   }
   __syncthreads();
   IE_STAMP(3);
 
-  // ---- 4. offsets: workgroup scan + decoupled look-back ----
+  // ---- 4. offsets: workgroup scan; the aggregate goes out at once ----
   const uint8_t st = s_st[tid];
   const uint32_t olen = st == IE_OK_STR ? s_olen[tid] : 0u;
   const uint32_t n32 = (uint32_t)sn;
   if (pend) {  // a literal-path result: the whole output is one pool value
-    const uint64_t lr = s_lit[tid];
     d.ntop = 1;
     d.open[0] = 0;
     d.close[0] = n32 - 1u;
-    d.vk[0] = (kValPool << 30) | (uint32_t)(lr >> 32);
-    d.vs[0] = (uint32_t)lr;
+    d.vk[0] = (kValPool << 30) | olen;
+    d.vs[0] = s_lit[tid];
   }
   uint64_t tile_total;
-  const uint64_t local = block_scan(olen, s_red, &tile_total);
-  if (tid == 128) s_red[kBlock / 64 + 1] = local;  // output offset where the second half starts
+  const uint64_t local = block_scan(olen, s_red, &tile_total);  // (its barriers also retire s_lit)
+  if (wave == 0) publish_aggregate(W.tile_state, tile, tile_total);
+
+  // ---- 5. the tile's output bytes into the LDS stage (tile-relative offsets) while the
+  //      look-back is pending; tiles whose output does not fit store straight to HBM later ----
+  const bool in_stage = staged && tile_total <= (uint64_t)kStageBytes;
+  const bool mine = i < B.n && st == IE_OK_STR && olen;
+  if (in_stage) {
+    lds_u8* const dd = (lds_u8*)(s_u + (mine ? local : 0));
+    const lds_u8* const ls = (const lds_u8*)s;
+    const uint32_t ntop = mine ? d.ntop : 0u;
+    uint32_t w = 0;
+#pragma unroll
+    for (int j = 0; j <= kMaxTop; j++) {
+      // template run j
+      const bool ton = mine && (uint32_t)j <= ntop;
+      const uint32_t t_lo = j == 0 ? 0u : d.close[j - 1] + 1;
+      const uint32_t t_hi = (uint32_t)j < ntop ? d.open[j] : n32;
+      const uint32_t tl = ton ? t_hi - t_lo : 0u;
+      if (__any(tl != 0)) lds_copy(dd + w, tl ? ls + t_lo : (const lds_u8*)s_in, tl, sink);
+      w += tl;
+      if (j == kMaxTop) break;
+      // value j
+      const bool von = mine && (uint32_t)j < ntop;
+      const uint32_t kind = d.vk[j] >> 30, len = von ? d.vk[j] & kLenMask : 0u;
+      const bool ent = von && kind == kValEntry;
+      if (__any(ent)) put_entry_text(dd + w, T.entries + (ent ? d.vs[j] : 0u), ent ? len : 0u, sink);
+      if (von && kind == kValArena)
+        copy_bytes<true, false>((uint8_t*)(dd + w), T.arena + d.vs[j], len);
+      else if (von && kind == kValPool)
+        copy_bytes<true, false>((uint8_t*)(dd + w), W.pool + ((uint64_t)d.vs[j] << 4), len);
+      w += len;
+    }
+  }
+  IE_STAMP(4);
   if (wave == 0) {
     const uint64_t b = look_back(W.tile_state, tile, tile_total, W.err, W.stamps ? W.stats + 2 : nullptr);
     if (tid == 0) s_red[kBlock / 64] = b;
   }
   __syncthreads();
-  IE_STAMP(4);
   const uint64_t base = s_red[kBlock / 64];
   if (i < B.n) {
     gst(B.out_off + i, base + local);
@@ -927,91 +960,69 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
     *W.total = base + tile_total;
   }
   if (base + tile_total > cap) return;  // caller's buffer too small: offsets only
-  __syncthreads();  // s_red[kBlock / 64 + 1] (the half boundary) is visible
 
-  // ---- 5. bytes: the tile (or, if it does not fit, each half) through the LDS output stage,
-  //      then 16-byte stores ----
-  const uint32_t whole = tile_total + 15 <= (uint64_t)kStageBytes;
-  const uint32_t half = whole ? 0u : tid >> 7;
-  for (uint32_t hsel = 0; hsel < (whole ? 1u : 2u); hsel++) {
-    // the part's output range [h_lo, h_hi) relative to the tile
-    const uint64_t h_lo = whole || hsel == 0 ? 0 : s_red[kBlock / 64 + 1];
-    const uint64_t h_hi = whole ? tile_total : (hsel == 0 ? s_red[kBlock / 64 + 1] : tile_total);
-    uint8_t* g = out + base + h_lo;
-    const uint64_t h_len = h_hi - h_lo;
-    const uint32_t oshift = (uint32_t)(((uintptr_t)g) & 15);
-    const bool direct = !staged || h_len + oshift > (uint64_t)kStageBytes;
-    const bool mine = half == hsel && i < B.n && st == IE_OK_STR && olen;
-    if (direct) {  // rare (long strings): lanes store their own bytes straight to HBM
-      if (tid == 0) atomicAdd(W.stats + 1, 1u);
-      if (mine) {
-        uint8_t* dd = g + (local - h_lo);
-        uint32_t w = 0;
-        for (uint32_t j = 0; j <= d.ntop; j++) {
-          uint32_t t_lo = 0, t_hi = n32, vk = 0, vs = 0;
-#pragma unroll
-          for (int q = 0; q < kMaxTop; q++) {
-            if (j == (uint32_t)q + 1) t_lo = d.close[q] + 1;
-            if (j == (uint32_t)q && j < d.ntop) t_hi = d.open[q], vk = d.vk[q], vs = d.vs[q];
-          }
-          for (uint32_t q = t_lo; q < t_hi; q++)
-            gst(dd + w++, staged ? ((const lds_u8*)s)[q] : gld(s + q));
-          if (j < d.ntop) {
-            const uint32_t kind = vk >> 30, len = vk & kLenMask;
-            const uint8_t* p = kind == kValEntry ? T.entries[vs].text
-                               : kind == kValArena ? T.arena + vs
-                                                   : W.pool + ((uint64_t)vs << 4);
-            for (uint32_t q = 0; q < len; q++) gst(dd + w++, gld(p + q));
-          }
-        }
-      }
-      continue;
-    }
-    __syncthreads();  // the union region becomes the output stage (scratch/literal results are dead)
-    {
-      lds_u8* const dd = (lds_u8*)(s_u + oshift + (mine ? local - h_lo : 0));
-      const lds_u8* const ls = (const lds_u8*)s;
-      const uint32_t ntop = mine ? d.ntop : 0u;
-      uint32_t w = 0;
-#pragma unroll
-      for (int j = 0; j <= kMaxTop; j++) {
-        // template run j
-        const bool ton = mine && (uint32_t)j <= ntop;
-        const uint32_t t_lo = j == 0 ? 0u : d.close[j - 1] + 1;
-        const uint32_t t_hi = (uint32_t)j < ntop ? d.open[j] : n32;
-        const uint32_t tl = ton ? t_hi - t_lo : 0u;
-        if (__any(tl != 0)) lds_copy(dd + w, tl ? ls + t_lo : (const lds_u8*)s_in, tl, sink);
-        w += tl;
-        if (j == kMaxTop) break;
-        // value j
-        const bool von = mine && (uint32_t)j < ntop;
-        const uint32_t kind = d.vk[j] >> 30, len = von ? d.vk[j] & kLenMask : 0u;
-        const bool ent = von && kind == kValEntry;
-        if (__any(ent)) put_entry_text(dd + w, T.entries + (ent ? d.vs[j] : 0u), ent ? len : 0u, sink);
-        if (von && kind == kValArena)
-          copy_bytes<true, false>((uint8_t*)(dd + w), T.arena + d.vs[j], len);
-        else if (von && kind == kValPool)
-          copy_bytes<true, false>((uint8_t*)(dd + w), W.pool + ((uint64_t)d.vs[j] << 4), len);
-        w += len;
-      }
-    }
-    __syncthreads();
-    // stream the stage out: LDS position oshift + k holds output byte h_lo + k
-    const uintptr_t pg = (uintptr_t)g, pe = pg + h_len;
+  // ---- 6. stream out: 16-byte stores at 16-byte aligned addresses, each assembled from the
+  //      two stage blocks it straddles (the shift is uniform over the tile) ----
+  uint8_t* const g = out + base;
+  if (in_stage) {
+    const uintptr_t pg = (uintptr_t)g, pe = pg + tile_total;
     const uintptr_t a_up = (pg + 15) & ~(uintptr_t)15, b_down = pe & ~(uintptr_t)15;
     if (a_up >= b_down) {
-      for (uint32_t k = tid; k < h_len; k += kBlock) gst(g + k, s_u[oshift + k]);
+      for (uint32_t k = tid; k < tile_total; k += kBlock) gst(g + k, s_u[k]);
     } else {
       const uint32_t head = (uint32_t)(a_up - pg), tail = (uint32_t)(pe - b_down);
-      if (tid < head) gst(g + tid, s_u[oshift + tid]);
+      if (tid < head) gst(g + tid, s_u[tid]);
       if (tid < tail) {
         const uint32_t k = (uint32_t)(b_down - pg) + tid;
-        gst(g + k, s_u[oshift + k]);
+        gst(g + k, s_u[k]);
       }
       const uint32_t nv = (uint32_t)((b_down - a_up) >> 4);
-      const uint4* src = (const uint4*)(s_u + oshift + head);
+      const uint32_t q = head >> 2, sh = head & 3u;  // dword / byte shift of chunk c in the stage
+      constexpr int kOutV = (kStageBytes + kBlock * 16 - 1) / (kBlock * 16);
+      uint4 v[kOutV];
+#pragma unroll
+      for (int k = 0; k < kOutV; k++) {  // LDS reads first, then the stores
+        const uint32_t c = tid + (uint32_t)k * kBlock;
+        if (c < nv) {
+          const lds_u128* blk = (const lds_u128*)(lds_u8*)(s_u + 16 * c);
+          const u32x4 x = blk[0], y = blk[1];
+          const uint32_t wv[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+          uint32_t o4[4];
+#pragma unroll
+          for (int e = 0; e < 4; e++) {
+            const uint32_t lo = q == 0 ? wv[e] : q == 1 ? wv[e + 1] : q == 2 ? wv[e + 2] : wv[e + 3];
+            const uint32_t hi = q == 0 ? wv[e + 1] : q == 1 ? wv[e + 2] : q == 2 ? wv[e + 3] : wv[e + 4];
+            o4[e] = __builtin_amdgcn_alignbyte(hi, lo, sh);
+          }
+          v[k] = make_uint4(o4[0], o4[1], o4[2], o4[3]);
+        }
+      }
       uint4* dstv = (uint4*)a_up;
-      for (uint32_t j = tid; j < nv; j += kBlock) gst4(dstv + j, src[j]);
+#pragma unroll
+      for (int k = 0; k < kOutV; k++) {
+        const uint32_t c = tid + (uint32_t)k * kBlock;
+        if (c < nv) gst4(dstv + c, v[k]);
+      }
+    }
+  } else if (mine) {  // rare (long strings / large tiles): lanes store their own bytes
+    if (tid == 0) atomicAdd(W.stats + 1, 1u);
+    uint8_t* dd = g + local;
+    uint32_t w = 0;
+    for (uint32_t j = 0; j <= d.ntop; j++) {
+      uint32_t t_lo = 0, t_hi = n32, vk = 0, vs = 0;
+#pragma unroll
+      for (int q = 0; q < kMaxTop; q++) {
+        if (j == (uint32_t)q + 1) t_lo = d.close[q] + 1;
+        if (j == (uint32_t)q && j < d.ntop) t_hi = d.open[q], vk = d.vk[q], vs = d.vs[q];
+      }
+      for (uint32_t q = t_lo; q < t_hi; q++) gst(dd + w++, staged ? ((const lds_u8*)s)[q] : gld(s + q));
+      if (j < d.ntop) {
+        const uint32_t kind = vk >> 30, len = vk & kLenMask;
+        const uint8_t* p = kind == kValEntry ? T.entries[vs].text
+                           : kind == kValArena ? T.arena + vs
+                                               : W.pool + ((uint64_t)vs << 4);
+        for (uint32_t q = 0; q < len; q++) gst(dd + w++, gld(p + q));
+      }
     }
   }
   IE_STAMP(5);

@@ -12,4 +12,4 @@ run() {  # name, env...
   env "$@" timeout -s KILL 90 rocprofv3 --pmc $C --output-format csv -d gpurun_out/${TAGP}_$name -o run -- \
     python3 bench.py --steps 3 --warmup 1 --no-cpu ${BENCH_ARGS:-} > gpurun_out/${TAGP}_$name.log 2>&1
 }
-run noeval IE_DEBUG_NOEVAL=1 && run parse IE_FAST=2 && run keys IE_FAST=3 && run fast IE_FAST=1
+run noeval IE_DEBUG_NOEVAL=1 && run fast IE_FAST=1
