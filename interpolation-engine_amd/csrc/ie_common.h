@@ -20,15 +20,21 @@
 
 namespace ie {
 
+// Key hash: two 32-bit multiplicative lanes over the key's little-endian 4-byte words (zero
+// padded), seeded with the table seed and the length; the high lane picks the pilot group
+// (its top bits), the low lane the slot under the pilot (ph_slot mixes it). One multiply per
+// word and lane (the device hashes keys straight from registers).
 IE_HD uint64_t hash_word(uint64_t h, uint32_t w) {
-  h = (h ^ (uint64_t)w) * 0x9E3779B97F4A7C15ull;
-  return h ^ (h >> 32);
+  const uint32_t a = ((uint32_t)(h >> 32) ^ w) * 0x9E3779B1u;
+  const uint32_t b = ((uint32_t)h ^ w) * 0xCC9E2D51u;
+  return ((uint64_t)a << 32) | b;
 }
 
-IE_HD uint64_t hash_init(uint32_t n, uint64_t seed) { return seed ^ (uint64_t)n; }
+IE_HD uint64_t hash_init(uint32_t n, uint64_t seed) {
+  return seed ^ (((uint64_t)n << 32) | (uint64_t)(n * 0x85EBCA77u));
+}
 
-// hash of n key bytes (any address space via the byte reader): the key's little-endian 4-byte
-// words (zero padded) mixed into a state seeded with the table seed and the length
+// hash of n key bytes (any address space via the byte reader)
 template <class ByteAt>
 IE_HD uint64_t hash_key(uint32_t n, ByteAt at, uint64_t seed) {
   uint64_t h = hash_init(n, seed);
@@ -50,7 +56,9 @@ IE_HD uint32_t fmix32(uint32_t x) {
 }
 
 // pilot group of a key hash (multiply-shift range reduction of the high word)
-IE_HD uint32_t ph_group(uint64_t h, uint32_t nb) { return (uint32_t)(((h >> 32) * (uint64_t)nb) >> 32); }
+IE_HD uint32_t ph_group(uint64_t h, uint32_t nb) {
+  return (uint32_t)(((uint64_t)(uint32_t)(h >> 32) * (uint64_t)nb) >> 32);
+}
 // entry slot of a key hash under its group's pilot
 IE_HD uint32_t ph_slot(uint64_t h, uint32_t pilot, uint32_t mask) {
   return fmix32((uint32_t)h ^ (pilot * 0x9E3779B9u)) & mask;

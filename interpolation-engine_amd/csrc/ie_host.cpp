@@ -277,7 +277,7 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
   x->stamp_tiles = 0;
   if (op == kOpInterp && getenv("IE_DEBUG_STAMPS")) {  // diagnostic build hook, see DESIGN.md
     const uint64_t tiles = (n + kBlock - 1) / kBlock;
-    IE_HIP(x->stamps.ensure(tiles * 64));
+    IE_HIP(x->stamps.ensure(tiles * 128));
     x->stamp_tiles = tiles;
   }
   Batch B{d_bytes, d_off, n, out->offsets, out->status, out->value_id};
@@ -614,7 +614,7 @@ int ie_exec_timing(ie_exec* x, ie_timing* out) {
   if (!x || !out) return fail(IE_ERR_INVALID, "null argument");
   if (x->stamp_tiles && getenv("IE_DEBUG_STAMPS")) {  // dump the last call's phase stamps
     IE_HIP(hipStreamSynchronize(x->stream));
-    std::vector<uint64_t> h(x->stamp_tiles * 8);
+    std::vector<uint64_t> h(x->stamp_tiles * 16);
     IE_HIP(hipMemcpy(h.data(), x->stamps.p, h.size() * 8, hipMemcpyDeviceToHost));
     if (FILE* f = fopen(getenv("IE_DEBUG_STAMPS"), "wb")) {
       fwrite(h.data(), 8, h.size(), f);

@@ -211,6 +211,69 @@ __device__ __forceinline__ void lds_copy(lds_u8* dst, const lds_u8* src, uint32_
 }
 
 // ------------------------------------------------------------------------------------------
+// Unaligned LDS access (gfx950 runs in unaligned mode: ds_read/ds_write_b32/b64/b128 take any
+// byte address). Pieces are moved in 16-byte units; the last partial unit is stored with exact
+// 8/4/2/1-byte stores so no lane ever writes past its own bytes.
+// ------------------------------------------------------------------------------------------
+typedef u32x4 __attribute__((aligned(1))) u32x4_ua;
+typedef uint64_t __attribute__((aligned(1))) u64_ua;
+typedef uint32_t __attribute__((aligned(1))) u32_ua;
+typedef uint16_t __attribute__((aligned(1))) u16_ua;
+typedef __attribute__((address_space(3))) u32x4_ua lds_v4u;
+typedef __attribute__((address_space(3))) u64_ua lds_u64u;
+typedef __attribute__((address_space(3))) u32_ua lds_u32u;
+typedef __attribute__((address_space(3))) u16_ua lds_u16u;
+
+__device__ __forceinline__ u32x4 ld16(const lds_u8* p) { return *(const lds_v4u*)p; }
+__device__ __forceinline__ void st16(lds_u8* p, u32x4 v) { *(lds_v4u*)p = v; }
+
+// the first len (0..16) bytes of v to p
+__device__ __forceinline__ void st_part(lds_u8* p, u32x4 v, uint32_t len) {
+  uint64_t lo = (uint64_t)v.x | ((uint64_t)v.y << 32);
+  const uint64_t hi = (uint64_t)v.z | ((uint64_t)v.w << 32);
+  if (len >= 16) {
+    st16(p, v);
+    return;
+  }
+  if (len & 8) {
+    *(lds_u64u*)p = lo;
+    lo = hi;
+    p += 8;
+  }
+  if (len & 4) {
+    *(lds_u32u*)p = (uint32_t)lo;
+    lo >>= 32;
+    p += 4;
+  }
+  if (len & 2) {
+    *(lds_u16u*)p = (uint16_t)lo;
+    lo >>= 16;
+    p += 2;
+  }
+  if (len & 1) *p = (uint8_t)lo;
+}
+
+// len bytes LDS -> LDS, any alignments (reads up to 15 bytes past the source; the arrays are
+// padded). Wave-uniform call.
+__device__ __forceinline__ void lds_move(lds_u8* dst, const lds_u8* src, uint32_t len) {
+  for (uint32_t k = 0; __any(k + 16 <= len); k += 16)
+    if (k + 16 <= len) st16(dst + k, ld16(src + k));
+  const uint32_t kt = len & ~15u;  // this lane's partial unit
+  if (kt < len) st_part(dst + kt, ld16(src + kt), len - kt);
+}
+
+// v with the bytes at and past len (0..16) cleared
+__device__ __forceinline__ u32x4 keep_bytes(u32x4 v, uint32_t len) {
+  u32x4 r;
+  const int32_t l = (int32_t)len;
+  r.x = l >= 4 ? v.x : l > 0 ? v.x & ((1u << (8 * l)) - 1u) : 0u;
+  r.y = l >= 8 ? v.y : l > 4 ? v.y & ((1u << (8 * (l - 4))) - 1u) : 0u;
+  r.z = l >= 12 ? v.z : l > 8 ? v.z & ((1u << (8 * (l - 8))) - 1u) : 0u;
+  r.w = l >= 16 ? v.w : l > 12 ? v.w & ((1u << (8 * (l - 12))) - 1u) : 0u;
+  return r;
+}
+
+// ------------------------------------------------------------------------------------------
 // Exact evaluator (any string; the reference semantics of SURVEY §3.3). Rounds: every lane scans
 // up to its next closing brace, then all lanes that reached one probe the table together.
 // Scratch is lane-private LDS: the key buffer (kKeyCap bytes, 4-aligned) and the stack
@@ -441,7 +504,7 @@ constexpr uint32_t kChainMax = 112;  // bytes covered by the 128-bit event windo
 
 struct ChainLds {
   lds_u32* pairs;  // [kChainPairs] stride kBlock: open | close << 16 (postorder)
-  lds_u8* kbuf;    // lane-private kMaxTop x 16 B: key prefix (A | child text) of each chain
+  lds_u8* kbuf;    // lane-private 48 B: assembly area of chain keys (A | T | B stores end by byte 32)
 };
 
 struct Probe {
@@ -462,9 +525,15 @@ __device__ __forceinline__ uint32_t w_max32(uint32_t v) {
   return v;
 }
 
+// value texts of the top-level pairs (inline entry texts, <= kInlineText bytes), kept in
+// registers from the lookup to the output build
+struct TopText {
+  uint32_t w[kMaxTop][8];
+};
+
 __device__ bool eval_chains(const DevTable& T, const lds_u8* tile, uint32_t p0, uint32_t n, const lds_u32* cm,
                             const lds_u32* oddbits, bool active, const ChainLds& CL, lds_u8* sink, Desc& d,
-                            uint32_t& out_len) {
+                            TopText& tt, uint32_t& out_len, uint64_t* stamp) {
   bool ok = active && n <= kChainMax;
   const lds_u8* s = tile + p0;
   // ---- 1. the string's open / close events as 128-bit windows ----
@@ -490,16 +559,15 @@ __device__ bool eval_chains(const DevTable& T, const lds_u8* tile, uint32_t p0, 
       C[j] = __builtin_amdgcn_alignbit(Wc[j + 1], Wc[j], o) & keep;
     }
   }
-  // ---- 2. parse: events in order, a 4-deep stack in one 64-bit register ----
+  // ---- 2. parse (branch-free): events in order, a 4-deep stack in one 64-bit register ----
   uint32_t e0 = O[0] | C[0], e1 = O[1] | C[1], e2 = O[2] | C[2], e3 = O[3] | C[3];
   const uint32_t E = __builtin_popcount(e0) + __builtin_popcount(e1) + __builtin_popcount(e2) +
                      __builtin_popcount(e3);
   const uint32_t Ew = w_max32(ok ? E : 0u);
   uint32_t depth = 0, np = 0, nch = 0, cstart = 0, cinfo = 0, maxd = 0;
   uint64_t stk = 0;
-  bool prev_close = false;
+  bool prev_close = false, bad = !ok;
   for (uint32_t k = 0; k < Ew; k++) {
-    const bool valid = ok && k < E;
     const bool z0 = e0 == 0, z1 = e1 == 0, z2 = e2 == 0;
     const uint32_t w = !z0 ? e0 : !z1 ? e1 : !z2 ? e2 : e3;
     const uint32_t ow = !z0 ? O[0] : !z1 ? O[1] : !z2 ? O[2] : O[3];
@@ -510,98 +578,85 @@ __device__ bool eval_chains(const DevTable& T, const lds_u8* tile, uint32_t p0, 
     e1 = z0 && !z1 ? wc : e1;
     e2 = z0 && z1 && !z2 ? wc : e2;
     e3 = z0 && z1 && z2 ? wc : e3;
+    const bool valid = !bad && k < E;
     const bool is_open = (ow >> bit) & 1u;
-    if (valid) {
-      if (is_open) {
-        // a second child (a '{' right after a '}' inside a pair) or too deep: not a chain
-        if (depth == (uint32_t)kChainDepth || (prev_close && depth > 0)) ok = false;
-        if (depth == 0) cstart = np;
-        stk = (stk << 16) | pos;
-        depth++;
-        prev_close = false;
-      } else {
-        if (depth == 0 || np == (uint32_t)kChainPairs) ok = false;  // '}{' / too many pairs
-        const uint32_t open = (uint32_t)stk & 0xFFFFu;
-        stk >>= 16;
-        depth--;
-        if (ok) CL.pairs[np * kBlock] = open | (pos << 16);
-        np++;
-        prev_close = true;
-        if (depth == 0) {
-          const uint32_t dc = np - cstart;
-          if (nch == (uint32_t)kMaxTop) ok = false;
-          cinfo |= (cstart | (dc << 3)) << (6 * nch);
-          maxd = dc > maxd ? dc : maxd;
-          nch++;
-        }
-      }
-    }
+    const bool op = valid && is_open, cl = valid && !is_open;
+    // a second child (a '{' right after a '}' inside a pair), too deep, '}{', too many pairs
+    bad |= op && (depth == (uint32_t)kChainDepth || (prev_close && depth != 0));
+    bad |= cl && (depth == 0 || np == (uint32_t)kChainPairs);
+    cstart = op && depth == 0 ? np : cstart;
+    const uint32_t open = (uint32_t)stk & 0xFFFFu;
+    stk = op ? ((stk << 16) | pos) : cl ? (stk >> 16) : stk;
+    depth = op ? depth + 1 : (cl && depth) ? depth - 1 : depth;
+    prev_close = valid ? !is_open : prev_close;
+    *(cl && !bad ? CL.pairs + np * kBlock : (lds_u32*)sink) = open | (pos << 16);
+    np += cl ? 1u : 0u;
+    const bool cend = cl && depth == 0;
+    const uint32_t dc = np - cstart;
+    bad |= cend && nch == (uint32_t)kMaxTop;
+    cinfo |= cend && !bad ? (cstart | (dc << 3)) << (6 * nch) : 0u;
+    maxd = cend && dc > maxd ? dc : maxd;
+    nch += cend ? 1u : 0u;
   }
-  if (depth) ok = false;  // unbalanced: the exact evaluator reports it
-  if (ok && nch == 1) {   // a whole-string pair: typed result (py:510-514), exact evaluator
+  ok = !bad && depth == 0;  // unbalanced strings: the exact evaluator reports them
+  if (ok && nch == 1) {     // a whole-string pair: typed result (py:510-514), exact evaluator
     const uint32_t top = CL.pairs[(np - 1) * kBlock];
     if ((top & 0xFFFFu) == 0 && (top >> 16) == n - 1) ok = false;
   }
-  // ---- 3. rounds: level r of every chain, all lookups of a round in flight together ----
-  uint32_t kl[kMaxTop] = {0, 0, 0}, pcl[kMaxTop] = {0, 0, 0};
+  if (stamp && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memrealtime();  // diagnostic
+  // ---- 3. rounds: level r of every chain, all lookups of a round in flight together. The key
+  //      of a pair is A | T | B: template up to its child, the child's text, template after the
+  //      child (a leaf: A only); assembled with unaligned 16-byte LDS stores in the lane's area ----
+  uint32_t ct[kMaxTop][4], cl_[kMaxTop], co_[kMaxTop], ctl[kMaxTop];  // child text / close / open / length
+#pragma unroll
+  for (int c = 0; c < kMaxTop; c++) {
+    ct[c][0] = ct[c][1] = ct[c][2] = ct[c][3] = 0;
+    cl_[c] = co_[c] = ctl[c] = 0;
+  }
   uint32_t vsum = 0, span = 0;
   const uint32_t R = w_max32(ok ? maxd : 0u);
   for (uint32_t r = 0; r < R; r++) {
     bool on[kMaxTop];
-    uint32_t idx[kMaxTop], open[kMaxTop], close[kMaxTop], klen[kMaxTop], kw[kMaxTop][4], dcs[kMaxTop];
+    uint32_t open[kMaxTop], close[kMaxTop], klen[kMaxTop], dcs[kMaxTop], first[kMaxTop];
+    u32x4 kw[kMaxTop];
     uint64_t h[kMaxTop];
 #pragma unroll
     for (int c = 0; c < kMaxTop; c++) {
-      const uint32_t first = (cinfo >> (6 * c)) & 7u;
+      first[c] = (cinfo >> (6 * c)) & 7u;
       dcs[c] = (cinfo >> (6 * c + 3)) & 7u;
       on[c] = ok && (uint32_t)c < nch && r < dcs[c];
-      idx[c] = first + r;
-      const uint32_t rec = on[c] ? CL.pairs[idx[c] * kBlock] : 0u;
+      const uint32_t rec = on[c] ? CL.pairs[(first[c] + r) * kBlock] : 0u;
       open[c] = rec & 0xFFFFu;
       close[c] = rec >> 16;
-      kw[c][0] = kw[c][1] = kw[c][2] = kw[c][3] = 0;
+      kw[c] = u32x4{0, 0, 0, 0};
       klen[c] = 0;
       h[c] = 0;
       if (!__any(on[c])) continue;
-      if (r == 0) {  // a leaf: the key is template bytes, read as dwords from the stage
-        const uint32_t len = on[c] ? close[c] - open[c] - 1 : 0u;
-        const uint32_t a = (uint32_t)(uintptr_t)(s + open[c] + 1);
-        const uint32_t sh = a & 3u;
-        const lds_u32* lw = (const lds_u32*)(lds_u8*)(uintptr_t)(a - sh);
-        uint32_t prev = lw[0];
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-          if (!__any(on[c] && 4 * q < (int)len)) break;
-          const uint32_t nx = lw[q + 1];
-          kw[c][q] = __builtin_amdgcn_alignbyte(nx, prev, sh);
-          prev = nx;
+      if (r == 0) {  // a leaf: template bytes straight from the stage
+        klen[c] = on[c] ? close[c] - open[c] - 1 : 0u;
+        kw[c] = ld16(s + open[c] + 1);
+      } else {
+        const uint32_t la = on[c] ? co_[c] - open[c] - 1 : 0u, lb = on[c] ? close[c] - cl_[c] - 1 : 0u;
+        klen[c] = la + ctl[c] + lb;
+        lds_u8* kb = CL.kbuf;  // the lane's 48-byte area (keys are read back before the next chain's)
+        if (klen[c] <= 16u) {
+          st16(kb, ld16(s + open[c] + 1));
+          st16(kb + la, u32x4{ct[c][0], ct[c][1], ct[c][2], ct[c][3]});
+          st16(kb + la + ctl[c], ld16(s + cl_[c] + 1));
+          kw[c] = *(const lds_u128*)kb;
         }
-        klen[c] = len;
-      } else {  // key = A | child text (already in kbuf) | B (template after the child)
-        lds_u8* kb = CL.kbuf + 16 * c;
-        const uint32_t lb = on[c] ? close[c] - pcl[c] - 1 : 0u;
-        const uint32_t len = kl[c] + lb;
-        const bool fit = len <= 16u;
-        if (__any(on[c] && fit && lb)) lds_copy(kb + kl[c], s + pcl[c] + 1, on[c] && fit ? lb : 0u, sink);
-        const u32x4 v = *(const lds_u128*)kb;
-        kw[c][0] = v.x, kw[c][1] = v.y, kw[c][2] = v.z, kw[c][3] = v.w;
-        klen[c] = len;
       }
       if (on[c] && klen[c] > 16u) {  // longer keys live in the arena: exact evaluator
         ok = false;
         on[c] = false;
       }
-#pragma unroll
-      for (int q = 0; q < 4; q++) {  // zero the bytes past the key (entries are zero padded)
-        const int32_t rem = (int32_t)klen[c] - 4 * q;
-        kw[c][q] = rem >= 4 ? kw[c][q] : rem > 0 ? kw[c][q] & ((1u << (8 * rem)) - 1u) : 0u;
-      }
+      kw[c] = keep_bytes(kw[c], klen[c]);
       h[c] = hash_init(klen[c], T.seed);
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        if (!__any(on[c] && 4 * q < (int)klen[c])) break;
-        if (4 * q < (int)klen[c]) h[c] = hash_word(h[c], kw[c][q]);
-      }
+      h[c] = hash_word(h[c], kw[c].x);
+      if (__any(on[c] && klen[c] > 4u)) h[c] = klen[c] > 4u ? hash_word(h[c], kw[c].y) : h[c];
+      if (__any(on[c] && klen[c] > 8u)) h[c] = klen[c] > 8u ? hash_word(h[c], kw[c].z) : h[c];
+      if (__any(on[c] && klen[c] > 12u)) h[c] = klen[c] > 12u ? hash_word(h[c], kw[c].w) : h[c];
+      if (klen[c] == 0) h[c] = hash_init(0, T.seed);
     }
 #pragma unroll
     for (int c = 0; c < kMaxTop; c++) on[c] = on[c] && ok;
@@ -612,38 +667,35 @@ __device__ bool eval_chains(const DevTable& T, const lds_u8* tile, uint32_t p0, 
       const uint32_t pilot = on[c] ? (uint32_t)gld(T.pilots + ph_group(h[c], T.nb)) : 0u;
       slot[c] = on[c] ? ph_slot(h[c], pilot, T.mask) : 0u;
     }
+    if (stamp && threadIdx.x == 0 && r < 3) {  // diagnostic: pilots arrived
+      asm volatile("" ::"v"(slot[0]), "v"(slot[1]), "v"(slot[2]));
+      stamp[2 + 2 * r] = __builtin_amdgcn_s_memrealtime();
+    }
     Probe P[kMaxTop];
 #pragma unroll
     for (int c = 0; c < kMaxTop; c++) {
       if (__any(on[c])) probe_load(T, slot[c], P[c]);
     }
+    if (stamp && threadIdx.x == 0 && r < 3) {  // diagnostic: entries arrived
+      asm volatile("" ::"v"(P[0].q0.x), "v"(P[1].q0.x), "v"(P[2].q0.x), "v"(P[0].q3.x));
+      stamp[3 + 2 * r] = __builtin_amdgcn_s_memrealtime();
+    }
 #pragma unroll
     for (int c = 0; c < kMaxTop; c++) {
       if (!__any(on[c])) continue;
       const Probe& E = P[c];
-      const bool hit = on[c] && (entry_head_ok(E.q0, klen[c]) & (E.q1.x == kw[c][0]) & (E.q1.y == kw[c][1]) &
-                                 (E.q1.z == kw[c][2]) & (E.q1.w == kw[c][3]));
+      const bool hit = on[c] && (entry_head_ok(E.q0, klen[c]) & (E.q1.x == kw[c].x) & (E.q1.y == kw[c].y) &
+                                 (E.q1.z == kw[c].z) & (E.q1.w == kw[c].w));
       const uint32_t flags = E.q0.z, tlen = E.q0.y;
       const bool good = hit && (flags & EF_SPLICE_OK) && (flags & EF_INERT);
       if (on[c] && !good) ok = false;  // a miss or a value needing care: exact evaluator
       const bool top = r + 1 == dcs[c];
-      // inner level: the parent's key prefix = A (template between the parent's '{' and this
-      // pair's '{') | this pair's text; it must fit the 16-byte key
-      const bool inner = on[c] && good && !top;
-      const uint32_t prec = inner ? CL.pairs[(idx[c] + 1) * kBlock] : 0u;
-      const uint32_t la = inner ? open[c] - (prec & 0xFFFFu) - 1 : 0u;
-      const bool fits = la + tlen <= 16u;
-      if (inner && !fits) ok = false;
-      const bool wr = inner && fits;
-      if (__any(wr)) {
-        lds_u8* kb = CL.kbuf + 16 * c;
-        lds_copy(kb, s + (prec & 0xFFFFu) + 1, wr ? la : 0u, sink);
-        const uint32_t tw[5] = {E.q2.y, E.q2.z, E.q2.w, E.q3.x, 0u};
-        put_words<4>(kb + la, tw, wr ? tlen : 0u, sink);
-      }
-      if (wr) {
-        kl[c] = la + tlen;
-        pcl[c] = close[c];
+      if (on[c] && good && !top) {  // inner level: this text goes into the parent's key
+        if (tlen > 16u) ok = false;
+        ct[c][0] = E.q2.y, ct[c][1] = E.q2.z, ct[c][2] = E.q2.w, ct[c][3] = E.q3.x;
+        ctl[c] = tlen;
+        co_[c] = open[c];
+        cl_[c] = close[c];
       }
       if (on[c] && good && top) {
         uint32_t src;
@@ -651,6 +703,8 @@ __device__ bool eval_chains(const DevTable& T, const lds_u8* tile, uint32_t p0, 
         d.vs[c] = src;
         d.open[c] = open[c];
         d.close[c] = close[c];
+        tt.w[c][0] = E.q2.y, tt.w[c][1] = E.q2.z, tt.w[c][2] = E.q2.w, tt.w[c][3] = E.q3.x;
+        tt.w[c][4] = E.q3.y, tt.w[c][5] = E.q3.z, tt.w[c][6] = E.q3.w, tt.w[c][7] = 0;
         vsum += tlen;
         span += close[c] - open[c] + 1;
       }
@@ -772,8 +826,8 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
   }
   __syncthreads();
   const uint32_t tile = s_misc[0];
-  // diagnostic phase stamps (100 MHz s_memrealtime), one row of 8 words per tile
-  uint64_t* const stamp_row = W.stamps ? W.stamps + (uint64_t)tile * 8 : nullptr;
+  // diagnostic phase stamps (100 MHz s_memrealtime), one row of 16 words per tile
+  uint64_t* const stamp_row = W.stamps ? W.stamps + (uint64_t)tile * 16 : nullptr;
 #define IE_STAMP(k)                                                                  \
   do {                                                                               \
     if (stamp_row && tid == 0) stamp_row[k] = __builtin_amdgcn_s_memrealtime();      \
@@ -821,12 +875,13 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
   // ---- 2. evaluate ----
   lds_u8* const sink = (lds_u8*)(s_sink + tid);
   Desc d;
+  TopText tt;
   d.ntop = 0;
 #pragma unroll
   for (int q = 0; q < kMaxTop; q++) d.open[q] = d.close[q] = d.vk[q] = d.vs[q] = 0;
   const uint8_t* s = nullptr;
   const uint32_t p0 = shift + (uint32_t)(so - lo);
-  bool pend = false;
+  bool pend = false, fast_lane = false;
   {
     uint8_t st = IE_OK_STR;
     uint32_t olen = 0, vid = IE_VID_NONE;
@@ -844,8 +899,10 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
     } else if (staged && W.fast_mode) {
       const ChainLds CL{(lds_u32*)(lds_u8*)(s_u + kKbufLds) + tid, (lds_u8*)(s_u + tid * 16 * kMaxTop)};
       const bool fast = eval_chains(T, (const lds_u8*)s_in, p0, (uint32_t)sn, (const lds_u32*)s_cm,
-                                    (const lds_u32*)s_odd, active, CL, sink, d, olen);
+                                    (const lds_u32*)s_odd, active, CL, sink, d, tt, olen,
+                                    stamp_row ? stamp_row + 6 : nullptr);
       slow = active && !fast;
+      fast_lane = fast;
     }
     // the rest: the exact evaluator (scratch: the lane's own chain-evaluator columns)
     const uint64_t slow_m = __ballot(slow);
@@ -917,6 +974,20 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
   const bool in_stage = staged && tile_total <= (uint64_t)kStageBytes;
   const bool mine = i < B.n && st == IE_OK_STR && olen;
   if (in_stage) {
+    // entry texts of values the exact evaluator or the literal path found: into registers first
+    // (the chain evaluator kept its own from the lookup)
+#pragma unroll
+    for (int j = 0; j < kMaxTop; j++) {
+      const bool need = mine && !fast_lane && (uint32_t)j < d.ntop && (d.vk[j] >> 30) == kValEntry;
+      if (__any(need)) {
+        const uint4* tp = (const uint4*)(T.entries + (need ? d.vs[j] : 0u)) + 2;
+        const uint4 t2 = gld4(tp), t3 = gld4(tp + 1);
+        if (need) {
+          tt.w[j][0] = t2.y, tt.w[j][1] = t2.z, tt.w[j][2] = t2.w, tt.w[j][3] = t3.x;
+          tt.w[j][4] = t3.y, tt.w[j][5] = t3.z, tt.w[j][6] = t3.w, tt.w[j][7] = 0;
+        }
+      }
+    }
     lds_u8* const dd = (lds_u8*)(s_u + (mine ? local : 0));
     const lds_u8* const ls = (const lds_u8*)s;
     const uint32_t ntop = mine ? d.ntop : 0u;
@@ -928,14 +999,17 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
       const uint32_t t_lo = j == 0 ? 0u : d.close[j - 1] + 1;
       const uint32_t t_hi = (uint32_t)j < ntop ? d.open[j] : n32;
       const uint32_t tl = ton ? t_hi - t_lo : 0u;
-      if (__any(tl != 0)) lds_copy(dd + w, tl ? ls + t_lo : (const lds_u8*)s_in, tl, sink);
+      if (__any(tl != 0)) lds_move(dd + w, tl ? ls + t_lo : (const lds_u8*)s_in, tl);
       w += tl;
       if (j == kMaxTop) break;
       // value j
       const bool von = mine && (uint32_t)j < ntop;
       const uint32_t kind = d.vk[j] >> 30, len = von ? d.vk[j] & kLenMask : 0u;
       const bool ent = von && kind == kValEntry;
-      if (__any(ent)) put_entry_text(dd + w, T.entries + (ent ? d.vs[j] : 0u), ent ? len : 0u, sink);
+      if (__any(ent)) {
+        if (ent) st_part(dd + w, u32x4{tt.w[j][0], tt.w[j][1], tt.w[j][2], tt.w[j][3]}, len);
+        if (ent && len > 16u) st_part(dd + w + 16, u32x4{tt.w[j][4], tt.w[j][5], tt.w[j][6], tt.w[j][7]}, len - 16);
+      }
       if (von && kind == kValArena)
         copy_bytes<true, false>((uint8_t*)(dd + w), T.arena + d.vs[j], len);
       else if (von && kind == kValPool)
@@ -977,24 +1051,14 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
         gst(g + k, s_u[k]);
       }
       const uint32_t nv = (uint32_t)((b_down - a_up) >> 4);
-      const uint32_t q = head >> 2, sh = head & 3u;  // dword / byte shift of chunk c in the stage
       constexpr int kOutV = (kStageBytes + kBlock * 16 - 1) / (kBlock * 16);
       uint4 v[kOutV];
 #pragma unroll
-      for (int k = 0; k < kOutV; k++) {  // LDS reads first, then the stores
+      for (int k = 0; k < kOutV; k++) {  // LDS reads first (unaligned 16-byte), then the stores
         const uint32_t c = tid + (uint32_t)k * kBlock;
         if (c < nv) {
-          const lds_u128* blk = (const lds_u128*)(lds_u8*)(s_u + 16 * c);
-          const u32x4 x = blk[0], y = blk[1];
-          const uint32_t wv[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
-          uint32_t o4[4];
-#pragma unroll
-          for (int e = 0; e < 4; e++) {
-            const uint32_t lo = q == 0 ? wv[e] : q == 1 ? wv[e + 1] : q == 2 ? wv[e + 2] : wv[e + 3];
-            const uint32_t hi = q == 0 ? wv[e + 1] : q == 1 ? wv[e + 2] : q == 2 ? wv[e + 3] : wv[e + 4];
-            o4[e] = __builtin_amdgcn_alignbyte(hi, lo, sh);
-          }
-          v[k] = make_uint4(o4[0], o4[1], o4[2], o4[3]);
+          const u32x4 x = ld16((const lds_u8*)s_u + head + 16 * c);
+          v[k] = make_uint4(x.x, x.y, x.z, x.w);
         }
       }
       uint4* dstv = (uint4*)a_up;

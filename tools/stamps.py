@@ -3,7 +3,7 @@ import sys
 
 import numpy as np
 
-a = np.fromfile(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/stamps.bin", dtype=np.uint64).reshape(-1, 8)
+a = np.fromfile(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/stamps.bin", dtype=np.uint64).reshape(-1, 16)
 t = a[:, :6].astype(np.int64)
 ph = np.diff(t, axis=1) / 100.0
 for k, nm in enumerate(["stage+classify", "eval", "literal", "scan+lookback", "emit"]):

@@ -4,7 +4,7 @@ import sys
 
 import numpy as np
 
-a = np.fromfile(sys.argv[1], dtype=np.uint64).reshape(-1, 8)
+a = np.fromfile(sys.argv[1], dtype=np.uint64).reshape(-1, 16)
 t = a[:, :6].astype(np.int64)
 t0 = t[:, 0].min()
 ph = np.diff(t, axis=1) / 100.0
@@ -32,3 +32,21 @@ for x in range(8):
     m = xcc == x
     if m.any():
         print("xcc %d tiles %5d life %.1f stage %.2f eval %.2f lookb %.2f emit %.2f" % (x, m.sum(), life[m].mean(), ph[m, 0].mean(), ph[m, 1].mean(), ph[m, 3].mean(), ph[m, 4].mean()))
+# slot 6: end of the chain evaluator's parse (wave 0), when written
+p6 = a[:, 6].astype(np.int64)
+ok = (p6 > t[:, 1]) & (p6 < t[:, 2])
+if ok.any():
+    print("eval: parse %.2f us, rounds+exact %.2f us (tiles with the stamp: %d)" % (((p6 - t[:, 1])[ok] / 100).mean(), ((t[:, 2] - p6)[ok] / 100).mean(), ok.sum()))
+# slots 8..13: round r pilots arrived (8 + 2r), entries arrived (9 + 2r)
+r0 = a[:, 8].astype(np.int64)
+if (r0 > 0).any():
+    prev = p6
+    for r in range(3):
+        pa, ea = a[:, 8 + 2 * r].astype(np.int64), a[:, 9 + 2 * r].astype(np.int64)
+        m = (pa > 0) & (ea > 0) & (prev > 0)
+        if not m.any():
+            break
+        print("round %d: keys+pilot %.2f us, entries %.2f us (tiles %d)" % (r, ((pa - prev)[m] / 100).mean(), ((ea - pa)[m] / 100).mean(), m.sum()))
+        prev = ea
+    m = prev > 0
+    print("after last round -> eval end %.2f us" % (((t[:, 2] - prev)[m]) / 100).mean())
