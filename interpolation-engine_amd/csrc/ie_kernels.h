@@ -9,9 +9,9 @@ namespace ie {
 
 constexpr int kBlock = 256;          // lanes per workgroup = strings per tile
 constexpr int kMaxDepth = 6;         // fast-path nesting limit (deeper: literal path)
-constexpr int kKeyCap = 40;          // fast-path key bytes per lane (longer keys: literal path)
+constexpr int kKeyCap = 32;          // exact-evaluator key bytes per lane (longer keys: literal path)
 
-constexpr int kTileBytes = 17920;    // LDS input stage; larger tiles read global memory directly
+constexpr int kTileBytes = 17664;    // LDS input stage; larger tiles read global memory directly
 constexpr int kStageBytes = 20480;   // LDS output stage; a tile that does not fit goes out in halves
 
 enum { kOpInterp = 0, kOpUnescape = 1, kOpEscape = 2 };

@@ -146,70 +146,6 @@ __device__ __forceinline__ void copy_bytes(uint8_t* __restrict__ dst, const uint
   for (; k < len; k++) wr8(k, rd8(k));
 }
 
-// Branch-free LDS writers: a lane that has nothing to write for some step stores to its own
-// sink dword instead (an address select, no exec-mask branch); trip counts are wave-uniform.
-__device__ __forceinline__ void st8(lds_u8* p, bool on, lds_u8* sink, uint8_t v) { *(on ? p : sink) = v; }
-__device__ __forceinline__ void st32(lds_u32* p, bool on, lds_u8* sink, uint32_t v) {
-  *(on ? p : (lds_u32*)sink) = v;
-}
-
-// len bytes held in registers (w[0..NW-1] little-endian, w[NW] = 0 pad) -> LDS at any byte
-// offset: head bytes until dst is 4-aligned, dwords re-aligned with alignbyte, tail bytes.
-// Wave-uniform call.
-template <int NW>
-__device__ __forceinline__ void put_words(lds_u8* dst, const uint32_t (&w)[NW + 1], uint32_t len, lds_u8* sink) {
-  const uint32_t a = (uint32_t)(uintptr_t)dst & 3u;
-  const uint32_t head = min(len, (4u - a) & 3u);
-#pragma unroll
-  for (uint32_t k = 0; k < 3; k++) st8(dst + k, k < head, sink, (uint8_t)(w[0] >> (8 * k)));
-  // dword q of the aligned body = bytes head + 4q .. head + 4q + 3
-  lds_u32* d32 = (lds_u32*)(dst + head);
-  const uint32_t rest = len - head, nq = rest >> 2, tail = rest & 3u;
-  uint32_t x = 0;
-#pragma unroll
-  for (uint32_t q = 0; q < (uint32_t)NW; q++) {
-    if (!__any(q <= nq)) break;  // wave-uniform exit
-    const uint32_t v = __builtin_amdgcn_alignbyte(w[q + 1], w[q], head);
-    st32(d32 + q, q < nq, sink, v);
-    x = q == nq ? v : x;
-  }
-  lds_u8* t = dst + head + 4 * nq;
-#pragma unroll
-  for (uint32_t k = 0; k < 3; k++) st8(t + k, k < tail, sink, (uint8_t)(x >> (8 * k)));
-}
-
-// an entry's inline text (len <= kInlineText) -> LDS at any byte offset (two 16-byte loads)
-__device__ __forceinline__ void put_entry_text(lds_u8* dst, const Entry* e, uint32_t len, lds_u8* sink) {
-  const uint4* tp = (const uint4*)e + 2;
-  const uint4 t2 = gld4(tp), t3 = gld4(tp + 1);
-  const uint32_t tw[8] = {t2.y, t2.z, t2.w, t3.x, t3.y, t3.z, t3.w, 0u};
-  put_words<7>(dst, tw, len, sink);
-}
-
-// len bytes LDS -> LDS, any alignments: dst-aligned dword body built with alignbyte from the
-// source's aligned dwords (reads may touch up to 3 bytes around the source; the tile is padded)
-__device__ __forceinline__ void lds_copy(lds_u8* dst, const lds_u8* src, uint32_t len, lds_u8* sink) {
-  const uint32_t a = (uint32_t)(uintptr_t)dst & 3u;
-  const uint32_t head = min(len, (4u - a) & 3u);
-#pragma unroll
-  for (uint32_t k = 0; k < 3; k++) st8(dst + k, k < head, sink, src[k]);
-  const uint32_t s2 = (uint32_t)(uintptr_t)(src + head);
-  const uint32_t sh = s2 & 3u;
-  const lds_u32* sw = (const lds_u32*)(lds_u8*)(uintptr_t)(s2 - sh);
-  lds_u32* d32 = (lds_u32*)(dst + head);
-  const uint32_t rest = len - head, nq = rest >> 2, tail = rest & 3u;
-  uint32_t prev = sw[0];
-  for (uint32_t q = 0; __any(q < nq); q++) {  // wave-uniform trip count
-    const uint32_t nx = sw[q + 1];
-    st32(d32 + q, q < nq, sink, __builtin_amdgcn_alignbyte(nx, prev, sh));
-    prev = nx;
-  }
-  const lds_u8* ts = src + head + 4 * nq;
-  lds_u8* td = dst + head + 4 * nq;
-#pragma unroll
-  for (uint32_t k = 0; k < 3; k++) st8(td + k, k < tail, sink, ts[k]);
-}
-
 // ------------------------------------------------------------------------------------------
 // Unaligned LDS access (gfx950 runs in unaligned mode: ds_read/ds_write_b32/b64/b128 take any
 // byte address). Pieces are moved in 16-byte units; the last partial unit is stored with exact
@@ -504,7 +440,7 @@ constexpr uint32_t kChainMax = 112;  // bytes covered by the 128-bit event windo
 
 struct ChainLds {
   lds_u32* pairs;  // [kChainPairs] stride kBlock: open | close << 16 (postorder)
-  lds_u8* kbuf;    // lane-private 48 B: assembly area of chain keys (A | T | B stores end by byte 32)
+  lds_u8* kbuf;    // lane-private kKeyCap B: assembly area of chain keys (A | T | B stores end by byte 32)
 };
 
 struct Probe {
@@ -532,7 +468,7 @@ struct TopText {
 };
 
 __device__ bool eval_chains(const DevTable& T, const lds_u8* tile, uint32_t p0, uint32_t n, const lds_u32* cm,
-                            const lds_u32* oddbits, bool active, const ChainLds& CL, lds_u8* sink, Desc& d,
+                            const lds_u32* oddbits, bool active, const ChainLds& CL, Desc& d,
                             TopText& tt, uint32_t& out_len, uint64_t* stamp) {
   bool ok = active && n <= kChainMax;
   const lds_u8* s = tile + p0;
@@ -589,7 +525,7 @@ __device__ bool eval_chains(const DevTable& T, const lds_u8* tile, uint32_t p0, 
     stk = op ? ((stk << 16) | pos) : cl ? (stk >> 16) : stk;
     depth = op ? depth + 1 : (cl && depth) ? depth - 1 : depth;
     prev_close = valid ? !is_open : prev_close;
-    *(cl && !bad ? CL.pairs + np * kBlock : (lds_u32*)sink) = open | (pos << 16);
+    if (cl && !bad) CL.pairs[np * kBlock] = open | (pos << 16);
     np += cl ? 1u : 0u;
     const bool cend = cl && depth == 0;
     const uint32_t dc = np - cstart;
@@ -753,8 +689,8 @@ __device__ uint64_t look_back(uint64_t* state, uint32_t tile, uint64_t agg, uint
       // backoff: 64 * nap cycles, doubling up to ~1 us
       for (uint32_t k = 0; k < nap; k++) __builtin_amdgcn_s_sleep(1);
       nap = nap < 32 ? 2 * nap : 32;
-      // bounded spin: 60 s of s_memrealtime (100 MHz); a missing predecessor is a bug
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 6000000000ull) {
+      // bounded spin: 10 s of s_memrealtime (100 MHz); a missing predecessor is a bug
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 1000000000ull) {
         if (lane == 0) atomicOr(err, 1u);
         break;
       }
@@ -789,15 +725,66 @@ __device__ uint64_t block_scan(uint64_t v, uint64_t* lds_w, uint64_t* total) {
   return base + inc - v;
 }
 
-// union region: chain-evaluator / exact-evaluator scratch during evaluation, the output stage
-// (tile-relative) after it
-constexpr uint32_t kKbufLds = kBlock * 16 * kMaxTop;
-static_assert(16 * kMaxTop >= kKeyCap && kChainPairs >= kMaxDepth, "exact-evaluator scratch");
+// Union region, by phase:
+//   classification + evaluation: key areas [0, kKbufLds) | pair records / exact-evaluator stacks
+//     [kKbufLds, kEvalLds) | chunk event masks [kCmOff, ..) | odd-chunk bits [kOddOff, ..)
+//     (the masks are read only while building a lane's event window)
+//   literal results: pool offsets at [0, 4 * kBlock)
+//   output: the tile's output bytes (tile-relative), read back for the realigned stream-out
+constexpr uint32_t kKbufLds = kBlock * kKeyCap;
 constexpr uint32_t kPairLds = kBlock * 4 * kChainPairs;
 constexpr uint32_t kEvalLds = kKbufLds + kPairLds;
-constexpr uint32_t kUnionLds = (kEvalLds > (uint32_t)kStageBytes + 32 ? kEvalLds : (uint32_t)kStageBytes + 32);  // +32: the stream-out reads one block past the end
 constexpr uint32_t kChunks = (kTileBytes + 32) / 16;
 constexpr uint32_t kOddWords = ((kChunks + kBlock - 1) / kBlock) * (kBlock / 32) + 2;
+constexpr uint32_t kCmOff = kEvalLds;
+constexpr uint32_t kOddOff = kCmOff + 4 * (kChunks + 10);
+constexpr uint32_t kClassEnd = kOddOff + 4 * kOddWords;
+constexpr uint32_t kUnionLds = kClassEnd > (uint32_t)kStageBytes + 32 ? kClassEnd : (uint32_t)kStageBytes + 32;
+static_assert(kKeyCap >= 32 && kChainPairs >= kMaxDepth, "evaluator scratch");
+
+// where a tile's strings lie: [lo, hi) for the tile, this lane's string at so (sn bytes)
+struct TileGeo {
+  uint64_t lo, hi, so, sn;
+};
+__device__ __forceinline__ TileGeo load_geo(const Batch& B, uint32_t tile, uint32_t tid) {
+  TileGeo g{0, 0, 0, 0};
+  const uint64_t first = (uint64_t)tile * kBlock;
+  if (first >= B.n) return g;
+  const uint64_t last = min(first + (uint64_t)kBlock, B.n), i = first + tid;
+  g.lo = gld(B.in_off + first);
+  g.hi = gld(B.in_off + last);
+  if (i < B.n) {
+    g.so = gld(B.in_off + i);
+    g.sn = gld(B.in_off + i + 1) - g.so;
+  }
+  return g;
+}
+
+// a tile's input chunks in flight into registers, written to the LDS stage later
+template <int MAXV>
+struct TilePrefetch {
+  uint4 v[MAXV];
+  uint32_t nv;
+  __device__ __forceinline__ void issue(const Batch& B, const TileGeo& g, uint32_t tid) {
+    const uintptr_t plo = (uintptr_t)(B.bytes + g.lo);
+    const uint32_t shift = (uint32_t)(plo & 15);
+    const uint4* src = (const uint4*)(plo - shift);  // an aligned chunk never crosses a page
+    nv = (uint32_t)((shift + (g.hi - g.lo) + 15) >> 4);
+#pragma unroll
+    for (int k = 0; k < MAXV; k++) {
+      const uint32_t j = tid + (uint32_t)k * kBlock;
+      if (j < nv) v[k] = gld4(src + j);
+    }
+  }
+  __device__ __forceinline__ void commit(uint4* dst, uint32_t tid) const {
+#pragma unroll
+    for (int k = 0; k < MAXV; k++) {
+      const uint32_t j = tid + (uint32_t)k * kBlock;
+      if (j < nv) dst[j] = v[k];
+    }
+  }
+};
+constexpr int kStageV = ((kTileBytes + 31) / 16 + kBlock - 1) / kBlock;
 
 __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T, uint8_t* out,
                                                     uint64_t cap) {
@@ -805,27 +792,28 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
   __shared__ __attribute__((aligned(16))) uint8_t s_u[kUnionLds];
   __shared__ uint32_t s_olen[kBlock];  // output length; the value id for IE_OK_VALUE strings
   __shared__ uint8_t s_st[kBlock];
-  __shared__ uint16_t s_pend[kBlock];
-  __shared__ uint32_t s_lit[kBlock];   // literal-path result: pool offset >> 4
+  __shared__ uint8_t s_pend[kBlock];
   __shared__ uint32_t s_misc[4];  // tile, pending count
   __shared__ uint64_t s_red[kBlock / 64 + 2];
-  __shared__ uint32_t s_sink[kBlock];     // per-lane write sink of the branch-free LDS writers
-  __shared__ uint32_t s_cm[kChunks + 10];  // event masks of the staged chunks (+ window pad)
-  __shared__ uint32_t s_odd[kOddWords];    // one bit per chunk: '\' or 0xE3 inside
+  lds_u32* const s_cm = (lds_u32*)(lds_u8*)(s_u + kCmOff);    // event masks of the staged chunks (+ pad)
+  lds_u32* const s_odd = (lds_u32*)(lds_u8*)(s_u + kOddOff);  // one bit per chunk: '\' or 0xE3 inside
+  lds_u32* const s_lit = (lds_u32*)(lds_u8*)s_u;              // literal-path results: pool offset >> 4
 
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
+  const uint32_t ntiles = (uint32_t)((B.n + kBlock - 1) / kBlock);
+  // Tile = workgroup index: workgroups are dispatched in index order, so every tile a look-back
+  // waits on is already resident (no ticket: a single-address atomic serializes chip-wide).
+  uint32_t tile = blockIdx.x;
+  const TileGeo geo = load_geo(B, tile, tid);
+  TilePrefetch<kStageV> pre;
+  pre.nv = 0;
+  if (tile < ntiles && geo.hi - geo.lo <= (uint64_t)kTileBytes) pre.issue(B, geo, tid);
+  if (tile < ntiles) {
   uint64_t t_start = 0;
   if (tid == 0) {
     if (W.stamps) t_start = __builtin_amdgcn_s_memrealtime();
-#ifdef IE_EXP_NOTICKET
-    s_misc[0] = blockIdx.x;
-#else
-    s_misc[0] = atomicAdd(W.tile_ticket, 1u);
-#endif
     s_misc[1] = 0;
   }
-  __syncthreads();
-  const uint32_t tile = s_misc[0];
   // diagnostic phase stamps (100 MHz s_memrealtime), one row of 16 words per tile
   uint64_t* const stamp_row = W.stamps ? W.stamps + (uint64_t)tile * 16 : nullptr;
 #define IE_STAMP(k)                                                                  \
@@ -842,38 +830,29 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
   const uint64_t first = (uint64_t)tile * kBlock;
   const uint64_t last = min(first + (uint64_t)kBlock, B.n);
   const uint64_t i = first + tid;
-  const uint64_t lo = gld(B.in_off + first), hi = gld(B.in_off + last);
+  const uint64_t lo = geo.lo, hi = geo.hi, so = geo.so, sn = geo.sn;
   const bool staged = (hi - lo) <= (uint64_t)kTileBytes;
-  const uintptr_t plo = (uintptr_t)(B.bytes + lo);
-  const uint32_t shift = (uint32_t)(plo & 15);
-  uint64_t so = 0, sn = 0;
-  if (i < B.n) {
-    so = gld(B.in_off + i);
-    sn = gld(B.in_off + i + 1) - so;
-  }
-  if (staged) {  // whole 16-byte chunks covering [lo, hi): an aligned chunk never crosses a page
-    const uint4* src = (const uint4*)(plo - shift);
-    uint4* dst = (uint4*)s_in;
-    const uint32_t nv = (uint32_t)((shift + (hi - lo) + 15) >> 4);
-    stage_chunks<kBlock, ((kTileBytes + 31) / 16 + kBlock - 1) / kBlock>(dst, src, nv, tid);
+  const uint32_t shift = (uint32_t)((uintptr_t)(B.bytes + lo) & 15);
+  if (staged) {  // whole 16-byte chunks covering [lo, hi) (loaded during the previous tile)
+    pre.commit((uint4*)s_in, tid);
     __syncthreads();
+    const uint32_t nv = pre.nv;
     for (uint32_t c0 = 0; c0 < nv; c0 += kBlock) {  // uniform trip count: ballots below
       const uint32_t c = c0 + tid;
       bool odd = false;
-      if (c < nv) ((lds_u32*)s_cm)[c] = chunk_classify((const lds_u32*)(lds_u8*)s_in + 4 * c, odd);
+      if (c < nv) s_cm[c] = chunk_classify((const lds_u32*)(lds_u8*)s_in + 4 * c, odd);
       const uint64_t ob = __ballot(odd);
       if (lane == 0) {  // 64 consecutive chunks = two words of the odd bit array
-        ((lds_u32*)s_odd)[(c0 + 64 * wave) >> 5] = (uint32_t)ob;
-        ((lds_u32*)s_odd)[((c0 + 64 * wave) >> 5) + 1] = (uint32_t)(ob >> 32);
+        s_odd[(c0 + 64 * wave) >> 5] = (uint32_t)ob;
+        s_odd[((c0 + 64 * wave) >> 5) + 1] = (uint32_t)(ob >> 32);
       }
     }
-    if (tid < 10) ((lds_u32*)s_cm)[nv + tid] = 0;  // the event windows read past the last chunk
+    if (tid < 10) s_cm[nv + tid] = 0;  // the event windows read past the last chunk
   }
   __syncthreads();
   IE_STAMP(1);
 
   // ---- 2. evaluate ----
-  lds_u8* const sink = (lds_u8*)(s_sink + tid);
   Desc d;
   TopText tt;
   d.ntop = 0;
@@ -897,9 +876,9 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
       olen = (uint32_t)sn;
       slow = false;
     } else if (staged && W.fast_mode) {
-      const ChainLds CL{(lds_u32*)(lds_u8*)(s_u + kKbufLds) + tid, (lds_u8*)(s_u + tid * 16 * kMaxTop)};
-      const bool fast = eval_chains(T, (const lds_u8*)s_in, p0, (uint32_t)sn, (const lds_u32*)s_cm,
-                                    (const lds_u32*)s_odd, active, CL, sink, d, tt, olen,
+      const ChainLds CL{(lds_u32*)(lds_u8*)(s_u + kKbufLds) + tid, (lds_u8*)(s_u + tid * kKeyCap)};
+      const bool fast = eval_chains(T, (const lds_u8*)s_in, p0, (uint32_t)sn, s_cm,
+                                    s_odd, active, CL, d, tt, olen,
                                     stamp_row ? stamp_row + 6 : nullptr);
       slow = active && !fast;
       fast_lane = fast;
@@ -908,7 +887,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
     const uint64_t slow_m = __ballot(slow);
     if (slow_m) {
       if (lane == 0 && W.fast_mode) atomicAdd(W.stats + 3, (uint32_t)__popcll(slow_m));  // rare
-      lds_u8* const kb = (lds_u8*)(s_u + tid * 16 * kMaxTop);
+      lds_u8* const kb = (lds_u8*)(s_u + tid * kKeyCap);
       lds_u32* const stk = (lds_u32*)(lds_u8*)(s_u + kKbufLds) + tid;
       uint32_t o2 = 0;
       uint8_t r2;
@@ -920,7 +899,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
     }
     if (active) st = r;
     pend = i < B.n && st == kStatusPending;
-    if (pend) s_pend[atomicAdd(&s_misc[1], 1u)] = (uint16_t)tid;
+    if (pend) s_pend[atomicAdd(&s_misc[1], 1u)] = (uint8_t)tid;
     s_st[tid] = st;
     s_olen[tid] = st == IE_OK_STR ? olen : (st == IE_OK_VALUE ? vid : 0u);
   }
@@ -1033,12 +1012,12 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
     B.out_off[B.n] = base + tile_total;
     *W.total = base + tile_total;
   }
-  if (base + tile_total > cap) return;  // caller's buffer too small: offsets only
+  const bool write_bytes = base + tile_total <= cap;  // caller's buffer too small: offsets only
 
   // ---- 6. stream out: 16-byte stores at 16-byte aligned addresses, each assembled from the
   //      two stage blocks it straddles (the shift is uniform over the tile) ----
   uint8_t* const g = out + base;
-  if (in_stage) {
+  if (write_bytes && in_stage) {
     const uintptr_t pg = (uintptr_t)g, pe = pg + tile_total;
     const uintptr_t a_up = (pg + 15) & ~(uintptr_t)15, b_down = pe & ~(uintptr_t)15;
     if (a_up >= b_down) {
@@ -1068,7 +1047,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
         if (c < nv) gst4(dstv + c, v[k]);
       }
     }
-  } else if (mine) {  // rare (long strings / large tiles): lanes store their own bytes
+  } else if (write_bytes && mine) {  // rare (long strings / large tiles): lanes store their own bytes
     if (tid == 0) atomicAdd(W.stats + 1, 1u);
     uint8_t* dd = g + local;
     uint32_t w = 0;
@@ -1091,6 +1070,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
   }
   IE_STAMP(5);
 #undef IE_STAMP
+  }
 }
 
 // diagnostic: one key through the device lookups. out[0..1] hash, out[2] slot, out[3] find_bytes,
@@ -1131,7 +1111,9 @@ hipError_t launch_resolve(const Batch& B, const Work& W, const DevTable& T, uint
                           hipStream_t st) {
   const uint64_t tiles = (B.n + kBlock - 1) / kBlock;
   if (!tiles) return hipSuccess;
-  hipLaunchKernelGGL(k_resolve, dim3((uint32_t)tiles), dim3(kBlock), 0, st, B, W, T, out, cap);
+  if (tiles > 0xFFFFFFFFull) return hipErrorInvalidValue;
+  const uint32_t grid = (uint32_t)tiles;
+  hipLaunchKernelGGL(k_resolve, dim3(grid), dim3(kBlock), 0, st, B, W, T, out, cap);
   return hipGetLastError();
 }
 
