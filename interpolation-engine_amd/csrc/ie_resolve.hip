@@ -434,14 +434,37 @@ __device__ __forceinline__ uint32_t chunk_classify(const lds_u32* w, bool& odd) 
 // (from the bottom) of every chain of every lane at once. A lane that breaks any condition
 // returns false with nothing committed; the exact evaluator then decides its result.
 // ------------------------------------------------------------------------------------------
-constexpr int kChainPairs = 8;
 constexpr int kChainDepth = 4;
 constexpr uint32_t kChainMax = 112;  // bytes covered by the 128-bit event window
 
 struct ChainLds {
-  lds_u32* pairs;  // [kChainPairs] stride kBlock: open | close << 16 (postorder)
-  lds_u8* kbuf;    // lane-private kKeyCap B: assembly area of chain keys (A | T | B stores end by byte 32)
+  lds_u8* kbuf;   // lane-private kKeyCap B: assembly area of chain keys (A | T | B stores end by byte 32)
+  lds_u64* ev;    // lane-private event masks (4 words, stride kBlock) for the middle levels of deep chains
 };
+
+// 128-bit event masks of one string (bit i = byte i)
+struct Ev {
+  uint64_t lo, hi;
+};
+__device__ __forceinline__ Ev ev_from(Ev m, uint32_t p) {  // the bits at or after p
+  Ev r;
+  r.lo = p >= 64u ? 0ull : m.lo & (~0ull << p);
+  r.hi = p <= 64u ? m.hi : p >= 128u ? 0ull : m.hi & (~0ull << (p - 64u));
+  return r;
+}
+__device__ __forceinline__ Ev ev_below(Ev m, uint32_t p) {  // the bits before p
+  Ev r;
+  r.lo = p >= 64u ? m.lo : m.lo & ((1ull << p) - 1ull);
+  r.hi = p <= 64u ? 0ull : p >= 128u ? m.hi : m.hi & ((1ull << (p - 64u)) - 1ull);
+  return r;
+}
+__device__ __forceinline__ uint32_t ev_first(Ev m) {  // lowest set bit, 128 if none
+  return m.lo ? (uint32_t)__builtin_ctzll(m.lo) : m.hi ? 64u + (uint32_t)__builtin_ctzll(m.hi) : 128u;
+}
+__device__ __forceinline__ uint32_t ev_last(Ev m) {  // highest set bit, 128 if none
+  return m.hi ? 127u - (uint32_t)__builtin_clzll(m.hi) : m.lo ? 63u - (uint32_t)__builtin_clzll(m.lo) : 128u;
+}
+__device__ __forceinline__ uint32_t ev_count(Ev m) { return (uint32_t)(__popcll(m.lo) + __popcll(m.hi)); }
 
 struct Probe {
   uint4 q0, q1, q2, q3;
@@ -495,49 +518,41 @@ __device__ bool eval_chains(const DevTable& T, const lds_u8* tile, uint32_t p0, 
       C[j] = __builtin_amdgcn_alignbit(Wc[j + 1], Wc[j], o) & keep;
     }
   }
-  // ---- 2. parse (branch-free): events in order, a 4-deep stack in one 64-bit register ----
-  uint32_t e0 = O[0] | C[0], e1 = O[1] | C[1], e2 = O[2] | C[2], e3 = O[3] | C[3];
-  const uint32_t E = __builtin_popcount(e0) + __builtin_popcount(e1) + __builtin_popcount(e2) +
-                     __builtin_popcount(e3);
-  const uint32_t Ew = w_max32(ok ? E : 0u);
-  uint32_t depth = 0, np = 0, nch = 0, cstart = 0, cinfo = 0, maxd = 0;
-  uint64_t stk = 0;
-  bool prev_close = false, bad = !ok;
-  for (uint32_t k = 0; k < Ew; k++) {
-    const bool z0 = e0 == 0, z1 = e1 == 0, z2 = e2 == 0;
-    const uint32_t w = !z0 ? e0 : !z1 ? e1 : !z2 ? e2 : e3;
-    const uint32_t ow = !z0 ? O[0] : !z1 ? O[1] : !z2 ? O[2] : O[3];
-    const uint32_t bit = (uint32_t)__builtin_ctz(w | (w ? 0u : 0x80000000u));
-    const uint32_t pos = (!z0 ? 0u : !z1 ? 32u : !z2 ? 64u : 96u) + bit;
-    const uint32_t wc = w & (w - 1);
-    e0 = !z0 ? wc : e0;
-    e1 = z0 && !z1 ? wc : e1;
-    e2 = z0 && z1 && !z2 ? wc : e2;
-    e3 = z0 && z1 && z2 ? wc : e3;
-    const bool valid = !bad && k < E;
-    const bool is_open = (ow >> bit) & 1u;
-    const bool op = valid && is_open, cl = valid && !is_open;
-    // a second child (a '{' right after a '}' inside a pair), too deep, '}{', too many pairs
-    bad |= op && (depth == (uint32_t)kChainDepth || (prev_close && depth != 0));
-    bad |= cl && (depth == 0 || np == (uint32_t)kChainPairs);
-    cstart = op && depth == 0 ? np : cstart;
-    const uint32_t open = (uint32_t)stk & 0xFFFFu;
-    stk = op ? ((stk << 16) | pos) : cl ? (stk >> 16) : stk;
-    depth = op ? depth + 1 : (cl && depth) ? depth - 1 : depth;
-    prev_close = valid ? !is_open : prev_close;
-    if (cl && !bad) CL.pairs[np * kBlock] = open | (pos << 16);
-    np += cl ? 1u : 0u;
-    const bool cend = cl && depth == 0;
-    const uint32_t dc = np - cstart;
-    bad |= cend && nch == (uint32_t)kMaxTop;
-    cinfo |= cend && !bad ? (cstart | (dc << 3)) << (6 * nch) : 0u;
-    maxd = cend && dc > maxd ? dc : maxd;
-    nch += cend ? 1u : 0u;
+  // ---- 2. chains: the events of a chain-only string are blocks O^d C^d (each pair has at most
+  //      one child), so chain c is located by a few mask scans: its first '{' (a), its first '}'
+  //      (c1), the opens in [a, c1) (its depth), the closes before the next '{' (as many). ----
+  const Ev Om{O[0] | ((uint64_t)O[1] << 32), O[2] | ((uint64_t)O[3] << 32)};
+  const Ev Cm{C[0] | ((uint64_t)C[1] << 32), C[2] | ((uint64_t)C[3] << 32)};
+  // per chain: first open | first close << 8 | innermost open << 16 | last close << 24, depth
+  uint32_t crec[kMaxTop], cdep[kMaxTop];
+  uint32_t pos = 0, nch = 0, maxd = 0;
+  bool bad = !ok, whole = false;
+#pragma unroll
+  for (int c = 0; c < kMaxTop; c++) {
+    crec[c] = cdep[c] = 0;
+    const Ev Oa = ev_from(Om, pos), Ca = ev_from(Cm, pos);
+    const uint32_t a = ev_first(Oa), c1 = ev_first(Ca);
+    const bool has = !bad && (a < 128u || c1 < 128u);
+    if (!__any(has)) continue;
+    const uint32_t dd = ev_count(ev_below(Oa, c1));
+    const Ev Cb = ev_below(Ca, ev_first(ev_from(Om, c1)));
+    const uint32_t end = ev_last(Cb);
+    // a '}' before its '{', a second child or an unbalanced block, too deep: exact evaluator
+    const bool cbad = c1 < a || dd != ev_count(Cb) || dd > (uint32_t)kChainDepth;
+    const bool take = has && !cbad;
+    bad |= has && cbad;
+    if (c == 0) whole = take && a == 0 && end == n - 1;
+    const uint32_t o0 = ev_last(ev_below(Oa, c1));
+    crec[c] = take ? (a | (c1 << 8) | (o0 << 16) | (end << 24)) : 0u;
+    cdep[c] = take ? dd : 0u;
+    maxd = take && dd > maxd ? dd : maxd;
+    nch += take ? 1u : 0u;
+    pos = take ? end + 1u : pos;
   }
-  ok = !bad && depth == 0;  // unbalanced strings: the exact evaluator reports them
-  if (ok && nch == 1) {     // a whole-string pair: typed result (py:510-514), exact evaluator
-    const uint32_t top = CL.pairs[(np - 1) * kBlock];
-    if ((top & 0xFFFFu) == 0 && (top >> 16) == n - 1) ok = false;
+  bad |= ev_first(ev_from(Ev{Om.lo | Cm.lo, Om.hi | Cm.hi}, pos)) < 128u;  // more than kMaxTop chains
+  ok = !bad && !(nch == 1 && whole);  // a whole-string pair: typed result (py:510-514), exact evaluator
+  if (__any(ok && maxd > 2u)) {  // middle levels are found from the masks in their round
+    CL.ev[0] = Om.lo, CL.ev[kBlock] = Om.hi, CL.ev[2 * kBlock] = Cm.lo, CL.ev[3 * kBlock] = Cm.hi;
   }
   if (stamp && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memrealtime();  // diagnostic
   // ---- 3. rounds: level r of every chain, all lookups of a round in flight together. The key
@@ -553,17 +568,27 @@ __device__ bool eval_chains(const DevTable& T, const lds_u8* tile, uint32_t p0, 
   const uint32_t R = w_max32(ok ? maxd : 0u);
   for (uint32_t r = 0; r < R; r++) {
     bool on[kMaxTop];
-    uint32_t open[kMaxTop], close[kMaxTop], klen[kMaxTop], dcs[kMaxTop], first[kMaxTop];
+    uint32_t open[kMaxTop], close[kMaxTop], klen[kMaxTop];
     u32x4 kw[kMaxTop];
     uint64_t h[kMaxTop];
 #pragma unroll
     for (int c = 0; c < kMaxTop; c++) {
-      first[c] = (cinfo >> (6 * c)) & 7u;
-      dcs[c] = (cinfo >> (6 * c + 3)) & 7u;
-      on[c] = ok && (uint32_t)c < nch && r < dcs[c];
-      const uint32_t rec = on[c] ? CL.pairs[(first[c] + r) * kBlock] : 0u;
-      open[c] = rec & 0xFFFFu;
-      close[c] = rec >> 16;
+      on[c] = ok && r < cdep[c];
+      // level r: the innermost pair in round 0, the outermost in the last round; a middle level
+      // is the open before the previous level's and the close after it
+      const bool top_c = r + 1 == cdep[c];
+      uint32_t o = r == 0 ? (crec[c] >> 16) & 0xFFu : top_c ? crec[c] & 0xFFu : 0u;
+      uint32_t q = r == 0 ? (crec[c] >> 8) & 0xFFu : top_c ? crec[c] >> 24 : 0u;
+      const bool mid = on[c] && r != 0 && !top_c;
+      if (__any(mid)) {
+        const Ev Om2{CL.ev[0], CL.ev[kBlock]}, Cm2{CL.ev[2 * kBlock], CL.ev[3 * kBlock]};
+        if (mid) {
+          o = ev_last(ev_below(Om2, co_[c]));
+          q = ev_first(ev_from(Cm2, cl_[c] + 1u));
+        }
+      }
+      open[c] = on[c] ? o : 0u;
+      close[c] = on[c] ? q : 0u;
       kw[c] = u32x4{0, 0, 0, 0};
       klen[c] = 0;
       h[c] = 0;
@@ -625,7 +650,7 @@ __device__ bool eval_chains(const DevTable& T, const lds_u8* tile, uint32_t p0, 
       const uint32_t flags = E.q0.z, tlen = E.q0.y;
       const bool good = hit && (flags & EF_SPLICE_OK) && (flags & EF_INERT);
       if (on[c] && !good) ok = false;  // a miss or a value needing care: exact evaluator
-      const bool top = r + 1 == dcs[c];
+      const bool top = r + 1 == cdep[c];
       if (on[c] && good && !top) {  // inner level: this text goes into the parent's key
         if (tlen > 16u) ok = false;
         ct[c][0] = E.q2.y, ct[c][1] = E.q2.z, ct[c][2] = E.q2.w, ct[c][3] = E.q3.x;
@@ -726,21 +751,21 @@ __device__ uint64_t block_scan(uint64_t v, uint64_t* lds_w, uint64_t* total) {
 }
 
 // Union region, by phase:
-//   classification + evaluation: key areas [0, kKbufLds) | pair records / exact-evaluator stacks
+//   classification + evaluation: key areas [0, kKbufLds) | exact-evaluator stacks
 //     [kKbufLds, kEvalLds) | chunk event masks [kCmOff, ..) | odd-chunk bits [kOddOff, ..)
 //     (the masks are read only while building a lane's event window)
 //   literal results: pool offsets at [0, 4 * kBlock)
 //   output: the tile's output bytes (tile-relative), read back for the realigned stream-out
 constexpr uint32_t kKbufLds = kBlock * kKeyCap;
-constexpr uint32_t kPairLds = kBlock * 4 * kChainPairs;
-constexpr uint32_t kEvalLds = kKbufLds + kPairLds;
+constexpr uint32_t kStackLds = kBlock * 32;  // exact-evaluator stacks (kMaxDepth words) | chain event masks
+constexpr uint32_t kEvalLds = kKbufLds + kStackLds;
 constexpr uint32_t kChunks = (kTileBytes + 32) / 16;
 constexpr uint32_t kOddWords = ((kChunks + kBlock - 1) / kBlock) * (kBlock / 32) + 2;
 constexpr uint32_t kCmOff = kEvalLds;
 constexpr uint32_t kOddOff = kCmOff + 4 * (kChunks + 10);
 constexpr uint32_t kClassEnd = kOddOff + 4 * kOddWords;
 constexpr uint32_t kUnionLds = kClassEnd > (uint32_t)kStageBytes + 32 ? kClassEnd : (uint32_t)kStageBytes + 32;
-static_assert(kKeyCap >= 32 && kChainPairs >= kMaxDepth, "evaluator scratch");
+static_assert(kKeyCap >= 32 && kMaxDepth <= 8, "evaluator scratch");
 
 // where a tile's strings lie: [lo, hi) for the tile, this lane's string at so (sn bytes)
 struct TileGeo {
@@ -786,7 +811,7 @@ struct TilePrefetch {
 };
 constexpr int kStageV = ((kTileBytes + 31) / 16 + kBlock - 1) / kBlock;
 
-__global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T, uint8_t* out,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_resolve(Batch B, Work W, DevTable T, uint8_t* out,
                                                     uint64_t cap) {
   __shared__ __attribute__((aligned(16))) uint8_t s_in[kTileBytes + 48];
   __shared__ __attribute__((aligned(16))) uint8_t s_u[kUnionLds];
@@ -876,7 +901,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Batch B, Work W, DevTable T,
       olen = (uint32_t)sn;
       slow = false;
     } else if (staged && W.fast_mode) {
-      const ChainLds CL{(lds_u32*)(lds_u8*)(s_u + kKbufLds) + tid, (lds_u8*)(s_u + tid * kKeyCap)};
+      const ChainLds CL{(lds_u8*)(s_u + tid * kKeyCap), (lds_u64*)(lds_u8*)(s_u + kKbufLds) + tid};
       const bool fast = eval_chains(T, (const lds_u8*)s_in, p0, (uint32_t)sn, s_cm,
                                     s_odd, active, CL, d, tt, olen,
                                     stamp_row ? stamp_row + 6 : nullptr);

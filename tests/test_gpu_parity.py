@@ -154,6 +154,41 @@ def test_long_strings_and_oversized_tiles():
     assert not bad, [b[:2] for b in bad[:4]]
 
 
+def _chain_table():
+    t = {}
+    for d in range(10):
+        t["x%d" % d] = str(d)
+        t["a-%d" % d] = str(d)
+        t["a-%dz" % d] = str((d + 1) % 10)
+        t["q%d" % d] = "v%d é" % d
+    return t
+
+
+def _chain(rng, depth):
+    s = "x%d" % (rng.randrange(10) if rng.random() < 0.97 else 10)  # x10: an innermost miss
+    for _ in range(depth - 1):
+        s = "{" + s + "}"
+        pre = "a-" if rng.random() < 0.97 else "b-"  # b-: a miss at an outer level
+        s = pre + s + rng.choice(["", "", "z"])
+    return "{" + s + "}"
+
+
+@pytest.mark.parametrize("seed", [11, 12])
+def test_deep_chains_vs_oracle(seed):
+    """Chains of depth 1-5 ({a-{a-{x3}z}}...): the chain evaluator's middle levels, misses at
+    every level, up to three chains per string, and depth 5 (exact evaluator)."""
+    rng = random.Random(seed)
+    strings = []
+    for _ in range(4000):
+        parts = [rng.choice(["", "t ", "é-", "text. "])]
+        for _ in range(rng.randint(1, 3)):
+            parts.append(_chain(rng, rng.choice([1, 2, 3, 4, 4, 5])))
+            parts.append(rng.choice(["", " ", " and ", "😀"]))
+        strings.append("".join(parts))
+    bad = compare_with_oracle(_chain_table(), strings)
+    assert not bad, bad[:4]
+
+
 @pytest.mark.parametrize("n", [0, 1, 255, 256, 257, 511, 1000])
 def test_batch_sizes(n):
     rng = random.Random(n)
