@@ -2,10 +2,12 @@
 //
 // Device data layout of one inserts table (built once per get_interpdata snapshot, read-only):
 //   pilots[nb]      uint16 per pilot group: the displacement that sends every key of the group to
-//                   its own entry (a perfect hash: each key has exactly ONE candidate entry)
+//                   its own entry (a perfect hash: each key has exactly ONE candidate entry).
+//                   Tables of up to kLdsPilotKeys keys use at most kLdsPilots groups, so the kernel
+//                   keeps the pilots in LDS (a lookup is then one memory round trip, not two)
 //   entries[m]      Entry (64 B): lengths, flags, arena offset, value id, and inline copies of the
 //                   key (<= 16 B) and splice text (<= 28 B), so a lookup is one 64-byte read;
-//                   m = next_pow2(1.25 * entries) (load <= 0.8)
+//                   m ~ 1.25 * keys (about 4 keys per group) or 2 * keys (the LDS pilot sizing)
 //   arena[...]      every splice text (4-byte aligned) followed by its key (4-byte aligned)
 // Lookup of key k: h = hash_key(k, seed); group g = ph_group(h, nb); slot = ph_slot(h, pilots[g]);
 // the key is present iff entries[slot] holds it (full byte compare: exact, never a hash test).
@@ -59,10 +61,14 @@ IE_HD uint32_t fmix32(uint32_t x) {
 IE_HD uint32_t ph_group(uint64_t h, uint32_t nb) {
   return (uint32_t)(((uint64_t)(uint32_t)(h >> 32) * (uint64_t)nb) >> 32);
 }
-// entry slot of a key hash under its group's pilot
-IE_HD uint32_t ph_slot(uint64_t h, uint32_t pilot, uint32_t mask) {
-  return fmix32((uint32_t)h ^ (pilot * 0x9E3779B9u)) & mask;
+// entry slot of a key hash under its group's pilot (multiply-shift range reduction to [0, m))
+IE_HD uint32_t ph_slot(uint64_t h, uint32_t pilot, uint32_t m) {
+  return (uint32_t)(((uint64_t)fmix32((uint32_t)h ^ (pilot * 0x9E3779B9u)) * m) >> 32);
 }
+
+// pilot groups the kernel keeps in LDS (12 KB), and the largest table sized for it
+constexpr uint32_t kLdsPilots = 6144;
+constexpr uint32_t kLdsPilotKeys = 20 * kLdsPilots;
 
 // Entry.flags
 enum : uint32_t {
@@ -96,7 +102,7 @@ struct DevTable {
   const uint16_t* pilots;
   const uint8_t* arena;
   uint64_t seed;
-  uint32_t mask;  // entries - 1
+  uint32_t m;     // entries
   uint32_t nb;    // pilot groups
   uint32_t n_entries;
   uint32_t dialect;

@@ -82,7 +82,7 @@ struct Hit {
 
 __device__ __forceinline__ uint32_t ph_lookup_slot(const DevTable& T, uint64_t h) {
   const uint32_t pilot = gld(T.pilots + ph_group(h, T.nb));
-  return ph_slot(h, pilot, T.mask);
+  return ph_slot(h, pilot, T.m);
 }
 
 // the rest of a long key (bytes 16..klen) against the arena copy; b in any address space

@@ -176,7 +176,6 @@ uint64_t key_hash(const std::string_view k, uint64_t seed) {
 // table or changes the seed.
 bool ph_place(const std::vector<uint64_t>& hash, uint64_t m, uint32_t nb, std::vector<uint16_t>& pilots,
               std::vector<uint32_t>& slot_of) {
-  const uint32_t mask = (uint32_t)(m - 1);
   std::vector<uint32_t> start(nb + 1, 0), order(hash.size());
   for (uint64_t h : hash) start[ph_group(h, nb) + 1]++;
   for (uint32_t g = 0; g < nb; g++) start[g + 1] += start[g];
@@ -201,7 +200,7 @@ bool ph_place(const std::vector<uint64_t>& hash, uint64_t m, uint32_t nb, std::v
       cand.clear();
       bool ok = true;
       for (uint32_t k = lo; k < hi && ok; k++) {
-        const uint32_t s = ph_slot(hash[order[k]], p, mask);
+        const uint32_t s = ph_slot(hash[order[k]], p, (uint32_t)m);
         if (taken[s]) ok = false;
         for (uint32_t c : cand) ok &= c != s;
         cand.push_back(s);
@@ -503,11 +502,18 @@ int ie_table_build(const ie_kv* kv, uint64_t n, int32_t dialect, const ie_clock*
     memcpy(b.text, e.text.data(), std::min<size_t>(e.text.size(), kInlineText));
     items.push_back(b);
   }
-  // perfect-hash placement: a failed search grows the table (or, twice in a row at one size,
-  // changes the seed: two keys with one 64-bit hash can never be separated)
-  uint64_t m = 16;
-  while (m < items.size() + items.size() / 4 + 1) m *= 2;
-  const uint32_t nb = (uint32_t)std::max<uint64_t>(1, (items.size() + 3) / 4);
+  // perfect-hash placement. About 4 keys per pilot group at load 0.8; a table too large for that
+  // within kLdsPilots groups but at most kLdsPilotKeys keys packs its keys into kLdsPilots groups
+  // (up to 20 keys each) at load 0.5, where the last, smallest groups still find a pilot. A failed
+  // search changes the seed (two keys with one 64-bit hash can never be separated) and then grows
+  // the table.
+  const uint64_t nk = items.size();
+  uint32_t nb = (uint32_t)std::max<uint64_t>(1, (nk + 3) / 4);
+  uint64_t m = std::max<uint64_t>(16, nk + nk / 4 + 1);
+  if (nb > kLdsPilots && nk <= kLdsPilotKeys) {
+    nb = kLdsPilots;
+    m = 2 * nk;
+  }
   uint64_t seed = 0xA0761D6478BD642Full;
   std::vector<uint16_t> pilots;
   std::vector<uint32_t> slot_of;
@@ -516,7 +522,7 @@ int ie_table_build(const ie_kv* kv, uint64_t n, int32_t dialect, const ie_clock*
     std::vector<uint64_t> hs(items.size());
     for (size_t i = 0; i < items.size(); i++) hs[i] = key_hash(ents[i].key, seed);
     if (ph_place(hs, m, nb, pilots, slot_of)) break;
-    if (attempt & 1) m *= 2;
+    if (attempt & 1) m += m / 4;
     else seed = fmix64_host(seed + 0x9E3779B97F4A7C15ull);
   }
   std::vector<Entry> entries(m);
@@ -544,7 +550,7 @@ int ie_table_build(const ie_kv* kv, uint64_t n, int32_t dialect, const ie_clock*
   t->dev.arena = (const uint8_t*)t->arena.p;
   t->dev.seed = seed;
   t->dev.nb = nb;
-  t->dev.mask = (uint32_t)(m - 1);
+  t->dev.m = (uint32_t)m;
   t->dev.n_entries = (uint32_t)ents.size();
   t->dev.dialect = (uint32_t)dialect;
   t->dev.flags = (flags & IE_TABLE_HAS_INSERTS_DIR) ? TF_HAS_DIR : 0u;
@@ -641,7 +647,7 @@ int ie_exec_timing(ie_exec* x, ie_timing* out) {
 
 // diagnostic (not part of the reference surface): device vs host view of one key's lookup.
 // out[0..1] device hash lo/hi, out[2] device slot, out[3] find_bytes, out[4] find_small (klen <= 16),
-// out[5] mask, out[7..8] host hash lo/hi, out[9] host slot, out[10] the host's entry index holding
+// out[5] entries, out[7..8] host hash lo/hi, out[9] host slot, out[10] the host's entry index holding
 // the key (or -1), out[12] find_bytes by all 64 lanes, out[13] lane agreement ballot
 int ie_debug_probe(const ie_table* t, const char* key, uint64_t len, uint64_t* out) {
   if (!t || !out || (len && !key) || len > 4096) return fail(IE_ERR_INVALID, "bad argument");
@@ -659,9 +665,9 @@ int ie_debug_probe(const ie_table* t, const char* key, uint64_t len, uint64_t* o
   IE_HIP(hipMemcpy(pil.data(), t->dev.pilots, pil.size() * sizeof(uint16_t), hipMemcpyDeviceToHost));
   out[7] = h & 0xFFFFFFFFull;
   out[8] = h >> 32;
-  out[9] = ph_slot(h, pil[ph_group(h, t->dev.nb)], t->dev.mask);
+  out[9] = ph_slot(h, pil[ph_group(h, t->dev.nb)], t->dev.m);
   out[10] = (uint64_t)-1;
-  std::vector<Entry> he((uint64_t)t->dev.mask + 1);
+  std::vector<Entry> he(t->dev.m);
   IE_HIP(hipMemcpy(he.data(), t->dev.entries, he.size() * sizeof(Entry), hipMemcpyDeviceToHost));
   for (uint64_t i = 0; i < he.size(); i++)
     if ((he[i].flags & EF_OCCUPIED) && he[i].key_len == len &&

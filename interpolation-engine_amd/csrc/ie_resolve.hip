@@ -39,6 +39,7 @@ constexpr uint32_t kLenMask = (1u << 30) - 1;
 
 // LDS-typed views: accesses through them compile to ds_* (not flat_*) instructions
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) uint64_t lds_u64;
 typedef __attribute__((address_space(3))) u32x4 lds_u128;
@@ -490,7 +491,7 @@ struct TopText {
   uint32_t w[kMaxTop][8];
 };
 
-__device__ bool eval_chains(const DevTable& T, const lds_u8* tile, uint32_t p0, uint32_t n, const lds_u32* cm,
+__device__ bool eval_chains(const DevTable& T, const lds_u16* pil, const lds_u8* tile, uint32_t p0, uint32_t n, const lds_u32* cm,
                             const lds_u32* oddbits, bool active, const ChainLds& CL, Desc& d,
                             TopText& tt, uint32_t& out_len, uint64_t* stamp) {
   bool ok = active && n <= kChainMax;
@@ -625,8 +626,9 @@ __device__ bool eval_chains(const DevTable& T, const lds_u8* tile, uint32_t p0, 
     uint32_t slot[kMaxTop];
 #pragma unroll
     for (int c = 0; c < kMaxTop; c++) {
-      const uint32_t pilot = on[c] ? (uint32_t)gld(T.pilots + ph_group(h[c], T.nb)) : 0u;
-      slot[c] = on[c] ? ph_slot(h[c], pilot, T.mask) : 0u;
+      const uint32_t grp = ph_group(h[c], T.nb);  // pilot from LDS (small tables) or L2
+      const uint32_t pilot = on[c] ? (pil ? (uint32_t)pil[grp] : (uint32_t)gld(T.pilots + grp)) : 0u;
+      slot[c] = on[c] ? ph_slot(h[c], pilot, T.m) : 0u;
     }
     if (stamp && threadIdx.x == 0 && r < 3) {  // diagnostic: pilots arrived
       asm volatile("" ::"v"(slot[0]), "v"(slot[1]), "v"(slot[2]));
@@ -820,6 +822,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
   __shared__ uint8_t s_pend[kBlock];
   __shared__ uint32_t s_misc[4];  // tile, pending count
   __shared__ uint64_t s_red[kBlock / 64 + 2];
+  __shared__ __attribute__((aligned(16))) uint16_t s_pil[kLdsPilots];  // the table's pilots (small tables)
   lds_u32* const s_cm = (lds_u32*)(lds_u8*)(s_u + kCmOff);    // event masks of the staged chunks (+ pad)
   lds_u32* const s_odd = (lds_u32*)(lds_u8*)(s_u + kOddOff);  // one bit per chunk: '\' or 0xE3 inside
   lds_u32* const s_lit = (lds_u32*)(lds_u8*)s_u;              // literal-path results: pool offset >> 4
@@ -833,6 +836,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
   TilePrefetch<kStageV> pre;
   pre.nv = 0;
   if (tile < ntiles && geo.hi - geo.lo <= (uint64_t)kTileBytes) pre.issue(B, geo, tid);
+  // pilots of a table with at most kLdsPilots groups: one coalesced 12 KB copy per tile, in flight
+  // with the tile's bytes (the scattered per-lookup pilot reads it replaces touch 768 lines)
+  constexpr int kPilV = (kLdsPilots * 2 + 16 * kBlock - 1) / (16 * kBlock);
+  const bool lds_pil = T.nb <= kLdsPilots;
+  const uint32_t npv = lds_pil ? (T.nb * 2u + 15u) / 16u : 0u;
+  uint4 pv[kPilV];
+#pragma unroll
+  for (int k = 0; k < kPilV; k++) {
+    const uint32_t j = tid + (uint32_t)k * kBlock;
+    if (j < npv) pv[k] = gld4((const uint4*)T.pilots + j);
+  }
   if (tile < ntiles) {
   uint64_t t_start = 0;
   if (tid == 0) {
@@ -858,7 +872,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
   const uint64_t lo = geo.lo, hi = geo.hi, so = geo.so, sn = geo.sn;
   const bool staged = (hi - lo) <= (uint64_t)kTileBytes;
   const uint32_t shift = (uint32_t)((uintptr_t)(B.bytes + lo) & 15);
-  if (staged) {  // whole 16-byte chunks covering [lo, hi) (loaded during the previous tile)
+#pragma unroll
+  for (int k = 0; k < kPilV; k++) {
+    const uint32_t j = tid + (uint32_t)k * kBlock;
+    if (j < npv) ((uint4*)s_pil)[j] = pv[k];
+  }
+  if (staged) {  // whole 16-byte chunks covering [lo, hi)
     pre.commit((uint4*)s_in, tid);
     __syncthreads();
     const uint32_t nv = pre.nv;
@@ -902,7 +921,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
       slow = false;
     } else if (staged && W.fast_mode) {
       const ChainLds CL{(lds_u8*)(s_u + tid * kKeyCap), (lds_u64*)(lds_u8*)(s_u + kKbufLds) + tid};
-      const bool fast = eval_chains(T, (const lds_u8*)s_in, p0, (uint32_t)sn, s_cm,
+      const bool fast = eval_chains(T, lds_pil ? (const lds_u16*)s_pil : nullptr, (const lds_u8*)s_in, p0, (uint32_t)sn, s_cm,
                                     s_odd, active, CL, d, tt, olen,
                                     stamp_row ? stamp_row + 6 : nullptr);
       slow = active && !fast;
@@ -1099,7 +1118,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
 }
 
 // diagnostic: one key through the device lookups. out[0..1] hash, out[2] slot, out[3] find_bytes,
-// out[4] find_small (klen <= kInlineKey), out[5] mask, out[12] find_bytes by all 64 lanes,
+// out[4] find_small (klen <= kInlineKey), out[5] entries, out[12] find_bytes by all 64 lanes,
 // out[13] lane agreement ballot
 __global__ void k_debug_probe(DevTable T, const uint8_t* key, uint32_t klen, uint64_t* out) {
   __shared__ uint32_t kb[16];
@@ -1122,7 +1141,7 @@ __global__ void k_debug_probe(DevTable T, const uint8_t* key, uint32_t klen, uin
   out[2] = ph_lookup_slot(T, hash);
   out[3] = (uint64_t)(int64_t)fb;
   out[4] = (uint64_t)(int64_t)fs;
-  out[5] = T.mask;
+  out[5] = T.m;
   out[12] = (uint64_t)(int64_t)fw;
   out[13] = agree;
 }

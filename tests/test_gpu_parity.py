@@ -173,6 +173,28 @@ def _chain(rng, depth):
     return "{" + s + "}"
 
 
+@pytest.mark.parametrize("n_keys", [6000, 30000, 130000])
+def test_table_sizes_vs_oracle(n_keys):
+    """Pilot placement regimes: ~4 keys per group in LDS (6k keys), up to 20 per group in LDS
+    (30k), and a table too large for the LDS copy whose pilots are read from L2 (130k)."""
+    rng = random.Random(n_keys)
+    table = {"k%d" % j: ("v%d" % j if j % 3 else j) for j in range(n_keys)}
+    table.update({"q-%d" % j: "Q%d é" % j for j in range(n_keys // 4)})
+    strings = []
+    for _ in range(3000):
+        parts = ["x "]
+        for _ in range(rng.randint(1, 3)):
+            r = rng.random()
+            if r < 0.5:
+                parts.append("{k%d}" % rng.randrange(n_keys + 50))
+            else:
+                parts.append("{q-{k%d}}" % rng.randrange(n_keys // 4))
+            parts.append(" . ")
+        strings.append("".join(parts))
+    bad = compare_with_oracle(table, strings)
+    assert not bad, bad[:4]
+
+
 @pytest.mark.parametrize("seed", [11, 12])
 def test_deep_chains_vs_oracle(seed):
     """Chains of depth 1-5 ({a-{a-{x3}z}}...): the chain evaluator's middle levels, misses at
