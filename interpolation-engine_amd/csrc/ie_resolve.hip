@@ -813,6 +813,20 @@ struct TilePrefetch {
 };
 constexpr int kStageV = ((kTileBytes + 31) / 16 + kBlock - 1) / kBlock;
 
+// bytes r..r+15 (r wave-uniform, 0..15) of the 32 bytes x | y
+__device__ __forceinline__ uint4 bytes_at(u32x4 x, u32x4 y, uint32_t r) {
+  const uint32_t sb = r & 3u;
+  uint32_t a0, a1, a2, a3, a4;
+  switch (r >> 2) {  // uniform
+    case 0: a0 = x.x, a1 = x.y, a2 = x.z, a3 = x.w, a4 = y.x; break;
+    case 1: a0 = x.y, a1 = x.z, a2 = x.w, a3 = y.x, a4 = y.y; break;
+    case 2: a0 = x.z, a1 = x.w, a2 = y.x, a3 = y.y, a4 = y.z; break;
+    default: a0 = x.w, a1 = y.x, a2 = y.y, a3 = y.z, a4 = y.w; break;
+  }
+  return make_uint4(__builtin_amdgcn_alignbyte(a1, a0, sb), __builtin_amdgcn_alignbyte(a2, a1, sb),
+                    __builtin_amdgcn_alignbyte(a3, a2, sb), __builtin_amdgcn_alignbyte(a4, a3, sb));
+}
+
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_resolve(Batch B, Work W, DevTable T, uint8_t* out,
                                                     uint64_t cap) {
   __shared__ __attribute__((aligned(16))) uint8_t s_in[kTileBytes + 48];
@@ -1077,11 +1091,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
       constexpr int kOutV = (kStageBytes + kBlock * 16 - 1) / (kBlock * 16);
       uint4 v[kOutV];
 #pragma unroll
-      for (int k = 0; k < kOutV; k++) {  // LDS reads first (unaligned 16-byte), then the stores
+      for (int k = 0; k < kOutV; k++) {
         const uint32_t c = tid + (uint32_t)k * kBlock;
         if (c < nv) {
-          const u32x4 x = ld16((const lds_u8*)s_u + head + 16 * c);
-          v[k] = make_uint4(x.x, x.y, x.z, x.w);
+          const lds_u128* blk = (const lds_u128*)(lds_u8*)s_u + c;
+          const u32x4 x = blk[0], y = blk[1];
+          v[k] = bytes_at(x, y, head);
         }
       }
       uint4* dstv = (uint4*)a_up;
