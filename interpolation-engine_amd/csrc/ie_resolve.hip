@@ -210,6 +210,69 @@ __device__ __forceinline__ u32x4 keep_bytes(u32x4 v, uint32_t len) {
   return r;
 }
 
+// 16 bytes at any LDS address from five aligned dword reads and v_alignbyte (a 16-byte access off
+// its natural alignment is replayed at 64 cycles per wave-instruction; aligned dwords are not)
+__device__ __forceinline__ u32x4 ld16a(const lds_u8* p) {
+  const uint32_t sh = (uint32_t)(uintptr_t)p & 3u;
+  const lds_u32* q = (const lds_u32*)(p - sh);
+  const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4];
+  return u32x4{__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+               __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh)};
+}
+
+// the first n (< 16) bytes of v to a 4-aligned LDS address: dwords, then a short and a byte
+__device__ __forceinline__ void put_tail4(lds_u8* p, u32x4 v, uint32_t n) {
+  lds_u32* q = (lds_u32*)p;
+  if (n >= 4) q[0] = v.x;
+  if (n >= 8) q[1] = v.y;
+  if (n >= 12) q[2] = v.z;
+  const uint32_t nw = n >> 2, r = n & 3u;
+  const uint32_t x = nw == 0 ? v.x : nw == 1 ? v.y : nw == 2 ? v.z : v.w;
+  lds_u8* b = p + (n & ~3u);
+  if (r & 2u) *(lds_u16*)b = (uint16_t)x;
+  if (r & 1u) b[r & 2u] = (uint8_t)(x >> (8u * (r & 2u)));
+}
+
+// len bytes LDS -> LDS at any alignments with aligned accesses only: up to 3 head bytes until the
+// destination is 4-aligned, then 4-aligned dwords from aligned source dwords. Wave-uniform call.
+__device__ __forceinline__ void lds_copy(lds_u8* dst, const lds_u8* src, uint32_t len) {
+  const uint32_t h0 = (0u - (uint32_t)(uintptr_t)dst) & 3u, h = h0 < len ? h0 : len;
+  if (h > 0) dst[0] = src[0];
+  if (h > 1) dst[1] = src[1];
+  if (h > 2) dst[2] = src[2];
+  const uint32_t body = (len - h) & ~15u;  // whole 16-byte units after the head
+  for (uint32_t k = 0; __any(k < body); k += 16u) {
+    if (k < body) {
+      const u32x4 v = ld16a(src + h + k);
+      lds_u32* q = (lds_u32*)(dst + h + k);
+      q[0] = v.x, q[1] = v.y, q[2] = v.z, q[3] = v.w;
+    }
+  }
+  const uint32_t kt = h + body;
+  if (kt < len) put_tail4(dst + kt, ld16a(src + kt), len - kt);
+}
+
+// len (<= 28) bytes held as 8 little-endian words (zero past the text) to any LDS address:
+// head bytes, then 4-aligned dwords realigned in registers
+__device__ __forceinline__ void put_words(lds_u8* dst, const uint32_t (&t)[8], uint32_t len) {
+  const uint32_t h0 = (0u - (uint32_t)(uintptr_t)dst) & 3u, h = h0 < len ? h0 : len;
+  if (h > 0) dst[0] = (uint8_t)t[0];
+  if (h > 1) dst[1] = (uint8_t)(t[0] >> 8);
+  if (h > 2) dst[2] = (uint8_t)(t[0] >> 16);
+  const uint32_t rest = len - h, nfull = rest >> 2, r = rest & 3u;
+  lds_u32* q = (lds_u32*)(dst + h);
+  uint32_t last = 0;
+#pragma unroll
+  for (int k = 0; k < 7; k++) {
+    const uint32_t a = __builtin_amdgcn_alignbyte(t[k + 1], t[k], h);  // text bytes h+4k .. h+4k+3
+    if ((uint32_t)k < nfull) q[k] = a;
+    last = (uint32_t)k == nfull ? a : last;
+  }
+  lds_u8* b = dst + h + 4u * nfull;
+  if (r & 2u) *(lds_u16*)b = (uint16_t)last;
+  if (r & 1u) b[r & 2u] = (uint8_t)(last >> (8u * (r & 2u)));
+}
+
 // ------------------------------------------------------------------------------------------
 // Exact evaluator (any string; the reference semantics of SURVEY §3.3). Rounds: every lane scans
 // up to its next closing brace, then all lanes that reached one probe the table together.
@@ -1036,17 +1099,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
       const uint32_t t_lo = j == 0 ? 0u : d.close[j - 1] + 1;
       const uint32_t t_hi = (uint32_t)j < ntop ? d.open[j] : n32;
       const uint32_t tl = ton ? t_hi - t_lo : 0u;
-      if (__any(tl != 0)) lds_move(dd + w, tl ? ls + t_lo : (const lds_u8*)s_in, tl);
+      if (__any(tl != 0)) lds_copy(dd + w, tl ? ls + t_lo : (const lds_u8*)s_in, tl);
       w += tl;
       if (j == kMaxTop) break;
       // value j
       const bool von = mine && (uint32_t)j < ntop;
       const uint32_t kind = d.vk[j] >> 30, len = von ? d.vk[j] & kLenMask : 0u;
       const bool ent = von && kind == kValEntry;
-      if (__any(ent)) {
-        if (ent) st_part(dd + w, u32x4{tt.w[j][0], tt.w[j][1], tt.w[j][2], tt.w[j][3]}, len);
-        if (ent && len > 16u) st_part(dd + w + 16, u32x4{tt.w[j][4], tt.w[j][5], tt.w[j][6], tt.w[j][7]}, len - 16);
-      }
+      if (__any(ent) && ent) put_words(dd + w, tt.w[j], len);
       if (von && kind == kValArena)
         copy_bytes<true, false>((uint8_t*)(dd + w), T.arena + d.vs[j], len);
       else if (von && kind == kValPool)
