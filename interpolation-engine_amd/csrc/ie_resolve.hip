@@ -755,9 +755,17 @@ __device__ __forceinline__ void publish_aggregate(uint64_t* state, uint32_t tile
   if (lane_id() == 0) publish(state, tile, (tile == 0 ? kFlagIncl : kFlagAgg) | agg);
 }
 
-// the exclusive prefix of `tile` from its predecessors' words; publishes the inclusive prefix
+// one poll: the words of the 64 predecessors pos, pos-1, ..., pos-63 (lane l at distance l)
+__device__ __forceinline__ uint64_t lb_poll(const uint64_t* state, int64_t pos) {
+  const int64_t idx = pos - (int64_t)lane_id();
+  return idx >= 0 ? __hip_atomic_load(state + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFlagIncl;
+}
+
+// the exclusive prefix of `tile` from its predecessors' words; publishes the inclusive prefix.
+// `early` is a first poll issued before the output build (its latency hides behind the build);
+// if it shows a gap the window is simply polled again.
 __device__ uint64_t look_back(uint64_t* state, uint32_t tile, uint64_t agg, uint32_t* err,
-                              uint32_t* polls) {
+                              uint32_t* polls, uint64_t early) {
   const uint32_t lane = lane_id();
   if (tile == 0) return 0;
   uint64_t excl = 0;
@@ -766,15 +774,15 @@ __device__ uint64_t look_back(uint64_t* state, uint32_t tile, uint64_t agg, uint
   uint32_t nap = 1, npoll = 0;
   // each poll reads a window of 64 predecessors (lane l at distance l from pos): one 512-byte
   // request; a window with a gap before its first inclusive word is re-read after a backoff
-  for (;;) {
-    const int64_t idx = pos - (int64_t)lane;
-    const uint64_t w = idx >= 0 ? __hip_atomic_load(state + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFlagIncl;
+  for (bool use_early = true;; use_early = false) {
+    const uint64_t w = use_early ? early : lb_poll(state, pos);
     const uint64_t flag = w >> 62;
     const uint64_t incl_m = __ballot(flag == 2);
     const uint64_t wait_m = __ballot(flag == 0);
     const uint32_t first = incl_m ? (uint32_t)__builtin_ctzll(incl_m) : 64u;
     const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);
     if (wait_m & need) {
+      if (use_early) continue;  // the early poll was too early: poll now, no backoff
       npoll++;
       // backoff: 64 * nap cycles, doubling up to ~1 us
       for (uint32_t k = 0; k < nap; k++) __builtin_amdgcn_s_sleep(1);
@@ -1067,7 +1075,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
   }
   uint64_t tile_total;
   const uint64_t local = block_scan(olen, s_red, &tile_total);  // (its barriers also retire s_lit)
-  if (wave == 0) publish_aggregate(W.tile_state, tile, tile_total);
+  uint64_t lb_early = 0;
+  if (wave == 0) {
+    publish_aggregate(W.tile_state, tile, tile_total);
+    if (tile != 0) lb_early = lb_poll(W.tile_state, (int64_t)tile - 1);  // consumed after the build
+  }
 
   // ---- 5. the tile's output bytes into the LDS stage (tile-relative offsets) while the
   //      look-back is pending; tiles whose output does not fit store straight to HBM later ----
@@ -1116,7 +1128,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
   }
   IE_STAMP(4);
   if (wave == 0) {
-    const uint64_t b = look_back(W.tile_state, tile, tile_total, W.err, W.stamps ? W.stats + 2 : nullptr);
+    const uint64_t b = look_back(W.tile_state, tile, tile_total, W.err, W.stamps ? W.stats + 2 : nullptr, lb_early);
     if (tid == 0) s_red[kBlock / 64] = b;
   }
   __syncthreads();
