@@ -60,7 +60,7 @@ enum ie_status {
   IE_E_RS_PANIC = 6,      /* Rust dialect: unwrap() panic on a '}{' leftover (interp.rs:63-66) */
   IE_NEEDS_HOST = 7,      /* key missing and an --inserts-dir is configured (py:452-461)   */
   IE_DIVERGED = 8,        /* iteration cap hit: the reference would loop forever           */
-  IE_E_OVERFLOW = 9       /* device scratch too small for this string (host APIs retry)    */
+  IE_E_OVERFLOW = 9       /* string over its single-pass scratch budget (host APIs retry)  */
 };
 
 /* ---- API return codes ---- */
@@ -163,7 +163,9 @@ void ie_exec_destroy(ie_exec* x);
 int ie_exec_sync(ie_exec* x);
 int ie_exec_set_timing(ie_exec* x, int32_t enabled);
 int ie_exec_timing(ie_exec* x, ie_timing* out); /* syncs */
-int ie_exec_set_scratch(ie_exec* x, uint64_t bytes); /* literal-kernel scratch pool size */
+/* Literal-path scratch pool size. Setting it makes ie_interpolate_device fully asynchronous: it no
+ * longer waits to check the pool's demand, and strings that ran out of it report IE_E_OVERFLOW. */
+int ie_exec_set_scratch(ie_exec* x, uint64_t bytes);
 
 /* Diagnostic (no reference counterpart): one key through the device lookups next to the host's
  * view of the same table; out[12] as documented in ie_host.cpp. */
@@ -182,7 +184,10 @@ int ie_exec_elapsed(ie_exec* x, uint32_t from_slot, uint32_t to_slot, float* ms)
 
 /* ---- interpolate_inserts over a packed batch (py:497-541 / interp.rs:31-89) ----
  * Input: UTF-8 bytes, offsets[n+1] (string i = bytes[offsets[i] .. offsets[i+1])).
- * _device: all pointers device-resident, asynchronous on the exec's stream.
+ * _device: all pointers device-resident, enqueued on the exec's stream; ie_interpolate_device
+ *          then waits for the stream to read the literal path's scratch demand and, when the pool
+ *          was too small, grows it and re-runs the batch once (no IE_E_OVERFLOW from capacity),
+ *          unless ie_exec_set_scratch sized the pool.
  * _batch:  host pointers; H2D + kernels + D2H, synchronous, retries capacity/overflow. */
 int ie_interpolate_device(ie_exec* x, const ie_table* t, const uint8_t* d_bytes,
                           const uint64_t* d_offsets, uint64_t n, const ie_dev_out* out);

@@ -130,7 +130,7 @@ struct SynthParams {
   uint32_t n_keys;    // config 2: k0..k{n_keys-1}
   uint32_t n_q;       // config 3/4: q-0..q-{n_q-1}
   uint32_t n_i;       // config 3/4: i0..i{n_i-1}
-  uint32_t n_chain;   // config 4: a-/b-/c- chain keys
+  uint32_t n_chain;   // config 4: c-0..c-{n_chain-1} (brace-bearing values)
 };
 
 // filler alphabet: ASCII [a-z0-9 .,:;-] plus 5% multibyte code points (é, €, 😀);
@@ -207,7 +207,7 @@ IE_HD uint32_t synth_string(const SynthParams& P, uint64_t i, uint8_t* out) {
       ref[r][w++] = '}';
       rlen[r] = w;
     }
-  } else {
+  } else if (P.config == 3) {
     R = 1 + (uint32_t)(splitmix(st) % 2);
     for (uint32_t r = 0; r < R; r++) {
       uint32_t m = (uint32_t)(splitmix(st) % P.n_i);
@@ -221,6 +221,55 @@ IE_HD uint32_t synth_string(const SynthParams& P, uint64_t i, uint8_t* out) {
       ref[r][w++] = '}';
       ref[r][w++] = '}';
       rlen[r] = w;
+    }
+  } else {
+    // config 4: 1-2 chain refs of depth 1/2/3/4 = 40/30/20/10 %:
+    //   {q-N}  {q-{iM}}  {q-{a-{iM}}}  {q-{a-{b-{iM}}}}
+    // per string: 2 % replace ref 0 by {c-N} (a brace-bearing value: re-resolved, the complex
+    // path), 1 % by a missing key {zz-N} (status row); 10 % add an escaped \{lit\} segment.
+    R = 1 + (uint32_t)(splitmix(st) % 2);
+    for (uint32_t r = 0; r < R; r++) {
+      const uint32_t u = (uint32_t)(splitmix(st) % 100);
+      const uint32_t depth = u < 40 ? 1 : u < 70 ? 2 : u < 90 ? 3 : 4;
+      uint32_t w = 0;
+      ref[r][w++] = '{';
+      ref[r][w++] = 'q';
+      ref[r][w++] = '-';
+      if (depth == 1) {
+        w += put_dec(ref[r] + w, (uint32_t)(splitmix(st) % P.n_q));
+      } else {
+        if (depth >= 3) { ref[r][w++] = '{'; ref[r][w++] = 'a'; ref[r][w++] = '-'; }
+        if (depth == 4) { ref[r][w++] = '{'; ref[r][w++] = 'b'; ref[r][w++] = '-'; }
+        ref[r][w++] = '{';
+        ref[r][w++] = 'i';
+        w += put_dec(ref[r] + w, (uint32_t)(splitmix(st) % P.n_i));
+        for (uint32_t k = 1; k < depth; k++) ref[r][w++] = '}';
+      }
+      ref[r][w++] = '}';
+      rlen[r] = w;
+    }
+    const uint32_t u = (uint32_t)(splitmix(st) % 100);
+    if (u < 3) {
+      uint32_t w = 0;
+      ref[0][w++] = '{';
+      if (u < 2) {
+        ref[0][w++] = 'c';
+        ref[0][w++] = '-';
+        w += put_dec(ref[0] + w, (uint32_t)(splitmix(st) % P.n_chain));
+      } else {
+        ref[0][w++] = 'z';
+        ref[0][w++] = 'z';
+        ref[0][w++] = '-';
+        w += put_dec(ref[0] + w, (uint32_t)(splitmix(st) % 1000));
+      }
+      ref[0][w++] = '}';
+      rlen[0] = w;
+    }
+    if ((uint32_t)(splitmix(st) % 100) < 10) {
+      const char* lit = "\\{lit\\}";
+      for (uint32_t k = 0; k < 7; k++) ref[R][k] = (uint8_t)lit[k];
+      rlen[R] = 7;
+      R++;
     }
   }
   uint32_t refbytes = 0;

@@ -94,6 +94,7 @@ struct ie_exec {
   bool ev_recorded = false;
   uint32_t lit_cap_max = 0;
   uint64_t pool_request = 256ull << 20;
+  bool pool_fixed = false;  // set by ie_exec_set_scratch: the caller sized the pool, no wait/re-run
   // workspace
   DevBuf counters, tile_state, pool, out_len, tile_sum, tile_base;
   // host-API staging
@@ -679,6 +680,7 @@ int ie_debug_probe(const ie_table* t, const char* key, uint64_t len, uint64_t* o
 int ie_exec_set_scratch(ie_exec* x, uint64_t bytes) {
   if (!x) return fail(IE_ERR_INVALID, "null exec");
   x->pool_request = std::max<uint64_t>(bytes, 1 << 20);
+  x->pool_fixed = true;
   return IE_SUCCESS;
 }
 
@@ -734,6 +736,18 @@ int ie_exec_elapsed(ie_exec* x, uint32_t a, uint32_t b, float* ms) {
 
 int ie_interpolate_device(ie_exec* x, const ie_table* t, const uint8_t* d_bytes,
                           const uint64_t* d_offsets, uint64_t n, const ie_dev_out* out) {
+  int rc = run_device(x, kOpInterp, t, d_bytes, d_offsets, n, out);
+  if (rc || !n || x->pool_fixed) return rc;
+  // The literal path reserves scratch with one atomic per string, so the counter ends at the
+  // batch's whole demand even when the pool ran out. A demand above the pool means some strings
+  // report IE_E_OVERFLOW: grow the pool to the demand and re-run the batch once (the look-back
+  // fixed every later offset, so a partial fix-up is impossible). Strings over their own
+  // single-pass budget stay IE_E_OVERFLOW here; ie_interpolate_batch re-runs those in max mode.
+  uint64_t used = 0;
+  IE_HIP(hipMemcpyAsync(&used, (uint64_t*)x->counters.p + 1, 8, hipMemcpyDeviceToHost, x->stream));
+  IE_HIP(hipStreamSynchronize(x->stream));
+  if (used <= x->pool.bytes) return IE_SUCCESS;
+  x->pool_request = std::max<uint64_t>(x->pool_request, used + used / 8 + (1ull << 20));
   return run_device(x, kOpInterp, t, d_bytes, d_offsets, n, out);
 }
 
@@ -801,7 +815,7 @@ int ie_simple_insertkey(const char* s, uint64_t len, int32_t dialect, uint64_t* 
 // ---- synthetic workloads ----
 int ie_synth_create(int32_t config, uint64_t seed, ie_synth** out) {
   if (!out) return fail(IE_ERR_INVALID, "null argument");
-  if (config != 2 && config != 3) return fail(IE_ERR_INVALID, "synthetic config must be 2 or 3");
+  if (config < 2 || config > 4) return fail(IE_ERR_INVALID, "synthetic config must be 2, 3 or 4");
   ie_synth* s = new ie_synth();
   s->P.config = config;
   s->P.seed = seed ? seed : (0x1E5EED00ull + (uint64_t)config);
@@ -820,7 +834,7 @@ int ie_synth_create(int32_t config, uint64_t seed, ie_synth** out) {
       s->keys.push_back("k" + std::to_string(j));
       s->texts.push_back(filler_value());
     }
-  } else {
+  } else if (config == 3) {
     for (uint32_t j = 0; j < s->P.n_q; j++) {
       s->keys.push_back("q-" + std::to_string(j));
       s->texts.push_back(filler_value());
@@ -829,10 +843,38 @@ int ie_synth_create(int32_t config, uint64_t seed, ie_synth** out) {
       s->keys.push_back("i" + std::to_string(j));
       s->texts.push_back(std::to_string(splitmix(st) % s->P.n_q));  // int value, str(int) splice
     }
+  } else {
+    // config 4: 100k entries = q-/a-/b- (32,666 each) + i (1,000) + c (1,000).
+    // q- strings; i, a-, b- ints in [0, n_q) so every chain depth resolves; c- strings that
+    // carry a {q-N} reference (re-resolved after the splice, py:516-535).
+    s->P.n_q = 32666;
+    s->P.n_chain = 1000;
+    for (uint32_t j = 0; j < s->P.n_q; j++) {
+      s->keys.push_back("q-" + std::to_string(j));
+      s->texts.push_back(filler_value());
+    }
+    for (const char* pre : {"a-", "b-"})
+      for (uint32_t j = 0; j < s->P.n_q; j++) {
+        s->keys.push_back(pre + std::to_string(j));
+        s->texts.push_back(std::to_string(splitmix(st) % s->P.n_q));
+      }
+    for (uint32_t j = 0; j < s->P.n_i; j++) {
+      s->keys.push_back("i" + std::to_string(j));
+      s->texts.push_back(std::to_string(splitmix(st) % s->P.n_q));
+    }
+    for (uint32_t j = 0; j < s->P.n_chain; j++) {
+      s->keys.push_back("c-" + std::to_string(j));
+      std::string head(4, '\0'), tail(4, '\0');
+      synth_filler(st, (uint8_t*)&head[0], 4);
+      std::string ref = "{q-" + std::to_string(splitmix(st) % s->P.n_q) + "}";
+      synth_filler(st, (uint8_t*)&tail[0], 4);
+      s->texts.push_back(head + ref + tail);
+    }
   }
   s->kv.resize(s->keys.size());
   for (size_t j = 0; j < s->keys.size(); j++) {
-    const bool is_int = config == 3 && j >= s->P.n_q;
+    const bool is_int = (config == 3 && j >= s->P.n_q) ||
+                        (config == 4 && j >= s->P.n_q && j < 3ull * s->P.n_q + s->P.n_i);
     s->kv[j] = ie_kv{s->keys[j].data(), s->keys[j].size(), s->texts[j].data(), s->texts[j].size(),
                      is_int ? IE_KIND_INT : IE_KIND_STR, 0};
   }

@@ -64,10 +64,10 @@ def _synth(config):
     return h
 
 
-@pytest.mark.parametrize("config", [2, 3])
+@pytest.mark.parametrize("config", [2, 3, 4])
 def test_synthetic_strings_follow_the_spec(config):
     h = _synth(config)
-    n = 2000
+    n = 2000 if config < 4 else 20000
     offs = np.zeros(n + 1, np.uint64)
     total = ctypes.c_uint64()
     N.check(N.lib().ie_synth_strings_host(h, 0, n, None, 0, offs.ctypes.data, ctypes.byref(total)), "len")
@@ -80,14 +80,36 @@ def test_synthetic_strings_follow_the_spec(config):
     blob = buf.tobytes()
     kvp = ctypes.POINTER(N.KV)()
     nkv = N.lib().ie_synth_kv(h, ctypes.byref(kvp))
-    assert nkv == (1000 if config == 2 else 100000)
+    assert nkv == {2: 1000, 3: 100000, 4: 99998}[config]
+    chain = re.compile(r"\{q-(?:\d+|\{i\d+\}|\{a-\{i\d+\}\}|\{a-\{b-\{i\d+\}\}\})\}")
+    depth = [0] * 5
+    esc = brace_val = missing = 0
     for i in range(n):
         s = blob[int(offs[i]):int(offs[i + 1])].decode("utf-8")
         assert not s.startswith("{")
-        assert "\\" not in s and "〠" not in s
-        refs = re.findall(r"\{k\d+\}" if config == 2 else r"\{q-\{i\d+\}\}", s)
-        assert (1 <= len(refs) <= 3) if config == 2 else (1 <= len(refs) <= 2)
-        assert s.count("{") == s.count("}") == (1 if config == 2 else 2) * len(refs)
+        assert "〠" not in s
+        if config < 4:
+            assert "\\" not in s
+            refs = re.findall(r"\{k\d+\}" if config == 2 else r"\{q-\{i\d+\}\}", s)
+            assert (1 <= len(refs) <= 3) if config == 2 else (1 <= len(refs) <= 2)
+            assert s.count("{") == s.count("}") == (1 if config == 2 else 2) * len(refs)
+            continue
+        # config 4: depth mix 40/30/20/10, 10 % escapes, 2 % brace-bearing values, 1 % misses
+        esc += "\\{lit\\}" in s
+        rest = s.replace("\\{lit\\}", "")
+        brace_val += len(re.findall(r"\{c-\d+\}", rest))
+        missing += len(re.findall(r"\{zz-\d+\}", rest))
+        rest = re.sub(r"\{(?:c|zz)-\d+\}", "", rest)
+        refs = chain.findall(rest)
+        for r in refs:
+            depth[r.count("{")] += 1
+        assert "{" not in chain.sub("", rest) and "}" not in chain.sub("", rest), s
+    if config == 4:
+        tot = sum(depth)
+        for d, share in ((1, 0.40), (2, 0.30), (3, 0.20), (4, 0.10)):
+            assert abs(depth[d] / tot - share) < 0.02, depth
+        assert abs(esc / n - 0.10) < 0.01 and abs(brace_val / n - 0.02) < 0.005
+        assert abs(missing / n - 0.01) < 0.004
     # a window is the same bytes as the full stream
     offs2 = np.zeros(11, np.uint64)
     buf2 = np.zeros(2000, np.uint8)
