@@ -78,6 +78,8 @@ enum : uint32_t {
   EF_KEY_STR = 1u << 5,        // raw value usable as a lookup key (py: str only; rs: value_to_string)
   EF_KEY_UNHASHABLE = 1u << 6, // py: list/dict raw value as a dict key raises TypeError
   EF_OCCUPIED = 1u << 7,       // the entry holds a key
+  EF_RAWALT = 1u << 8,         // splice text pre-resolved at build; the raw value sits before it
+                               // in the arena as [raw text, 4-aligned][u32 raw length][text]
 };
 
 // DevTable.flags

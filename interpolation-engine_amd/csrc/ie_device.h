@@ -156,8 +156,13 @@ __device__ int32_t find_raw(const DevTable& T, const Hit& prev, uint8_t& st, Hit
     return -1;
   }
   const uint8_t* k = T.arena + prev.text_off;
-  const int32_t b = find_bytes(T, k, prev.text_len, h);
-  if (b < 0) st = missing_status(T, k, prev.text_len);
+  uint32_t kl = prev.text_len;
+  if (prev.flags & EF_RAWALT) {  // a pre-resolved splice text: the key is the raw value
+    kl = gld((const uint32_t*)(k - 4));
+    k -= 4 + ((kl + 3u) & ~3u);
+  }
+  const int32_t b = find_bytes(T, k, kl, h);
+  if (b < 0) st = missing_status(T, k, kl);
   return b;
 }
 

@@ -437,55 +437,28 @@ int32_t ie_device_count(void) {
   return n;
 }
 
-int ie_table_build(const ie_kv* kv, uint64_t n, int32_t dialect, const ie_clock* now,
-                   uint32_t flags, int32_t device, ie_table** out) {
-  if (!out || (n && !kv)) return fail(IE_ERR_INVALID, "null argument");
-  if (dialect != IE_DIALECT_PY && dialect != IE_DIALECT_RS) return fail(IE_ERR_INVALID, "bad dialect");
-  int rc = set_device(device);
-  if (rc) return rc;
-  // dict semantics: the last duplicate wins; '' is never looked up (py:446 / interp.rs:105)
-  std::unordered_map<std::string_view, uint64_t> last;
-  last.reserve(n * 2 + 4);
-  std::vector<uint64_t> order;
-  for (uint64_t i = 0; i < n; i++) {
-    std::string_view k(kv[i].key ? kv[i].key : "", kv[i].key_len);
-    if (k.empty()) continue;
-    auto it = last.find(k);
-    if (it == last.end()) {
-      last.emplace(k, i);
-      order.push_back(i);
-    } else {
-      it->second = i;
-    }
-  }
-  char hhmm[16], hhmmss[16];
-  const int h = now ? now->hour : 0, mi = now ? now->minute : 0, se = now ? now->second : 0;
-  snprintf(hhmm, sizeof hhmm, "%02d:%02d", h, mi);
-  snprintf(hhmmss, sizeof hhmmss, "%02d:%02d:%02d", h, mi, se);
+struct Ent {
+  std::string_view key, text;
+  uint32_t flags, vid;
+  std::string_view raw;  // EF_RAWALT: the raw value behind a pre-resolved splice text
+};
 
-  struct Ent {
-    std::string_view key, text;
-    uint32_t flags, vid;
-  };
-  std::vector<Ent> ents;
-  ents.reserve(order.size() + 2);
-  for (uint64_t i : order) {
-    std::string_view k(kv[i].key, kv[i].key_len);
-    const uint64_t j = last[k];
-    if (k == "HH:MM" || k == "HH:MM:SS") continue;  // py:433-436: the clock always wins
-    if (kv[j].kind < 0 || kv[j].kind > IE_KIND_DICT) return fail(IE_ERR_INVALID, "bad kind");
-    std::string_view t(kv[j].text ? kv[j].text : "", kv[j].text_len);
-    ents.push_back(Ent{k, t, kind_flags(kv[j].kind, dialect) | text_flags(t), (uint32_t)j});
-  }
-  ents.push_back(Ent{"HH:MM", hhmm, kind_flags(IE_KIND_STR, dialect) | text_flags(hhmm), IE_VID_CLOCK_HHMM});
-  ents.push_back(Ent{"HH:MM:SS", hhmmss, kind_flags(IE_KIND_STR, dialect) | text_flags(hhmmss), IE_VID_CLOCK_HHMMSS});
-
+// Entries -> perfect-hash table on the device.
+int upload_table(const std::vector<Ent>& ents, int32_t dialect, uint32_t flags, int32_t device,
+                 ie_table** out) {
   std::vector<uint8_t> arena;
   std::vector<Entry> items;
   items.reserve(ents.size());
   uint64_t maxtext = 8;
   for (const Ent& e : ents) {
     while (arena.size() & 3) arena.push_back(0);  // texts 4-byte aligned (dword copies)
+    if (e.flags & EF_RAWALT) {  // [raw text][u32 raw length] right before the splice text
+      arena.insert(arena.end(), e.raw.begin(), e.raw.end());
+      while (arena.size() & 3) arena.push_back(0);
+      const uint32_t rl = (uint32_t)e.raw.size();
+      arena.insert(arena.end(), (const uint8_t*)&rl, (const uint8_t*)&rl + 4);
+      maxtext = std::max<uint64_t>(maxtext, e.raw.size());
+    }
     const uint64_t toff = arena.size();
     arena.insert(arena.end(), e.text.begin(), e.text.end());
     while (arena.size() & 3) arena.push_back(0);  // the key follows at key_off_of(toff, len)
@@ -558,6 +531,137 @@ int ie_table_build(const ie_kv* kv, uint64_t n, int32_t dialect, const ie_clock*
   t->dev.maxtext = maxtext;
   *out = t;
   return IE_SUCCESS;
+}
+
+// Pre-resolution of brace-bearing splice texts (device work, at build time).
+// The reference re-resolves a spliced value in place (py:516-535: the loop rescans the content).
+// When the value V is balanced and carries no '\' or U+3020, splicing V and letting the loop
+// continue equals splicing interpolate_inserts(V): rfind('{') always lands inside V until V is
+// brace-free (the suffix after a resolved pair holds no '{', and V's pairs close inside V), no
+// escape or placeholder can form across V's edges, and V's own errors would surface first.
+// So V is resolved once here, on the device through the table itself, as the string "a" + V
+// (never the whole-string simple form), and a result that is inert (no '{', '}', '\', U+3020)
+// replaces the splice text; lookups that need the raw value (py:512 / interp.rs:48) read it
+// from the arena (EF_RAWALT). Values whose resolution fails or stays structural keep the
+// literal path.
+int preresolve(ie_table* t0, std::vector<Ent>& ents, int32_t dialect, uint32_t flags, int32_t device,
+               ie_table** out) {
+  auto clean_value = [](std::string_view v, bool need_brace) {
+    size_t opens = 0;
+    int64_t depth = 0;
+    for (size_t i = 0; i < v.size(); i++) {
+      const uint8_t c = (uint8_t)v[i];
+      if (c == '\\') return false;
+      if (c == 0xE3 && i + 2 < v.size() && (uint8_t)v[i + 1] == 0x80 && (uint8_t)v[i + 2] == 0xA0) return false;
+      if (c == '{') opens++, depth++;
+      if (c == '}' && --depth < 0) return false;
+    }
+    return depth == 0 && (!need_brace || (opens > 0 && opens <= 64));
+  };
+  std::vector<size_t> cand;
+  for (size_t i = 0; i < ents.size(); i++) {
+    const Ent& e = ents[i];
+    if ((e.flags & EF_INERT) || !(e.flags & EF_SPLICE_OK) || e.text.size() > (1u << 16)) continue;
+    if (clean_value(e.text, true)) cand.push_back(i);
+  }
+  if (cand.empty()) return IE_SUCCESS;
+  std::vector<uint8_t> bytes;
+  std::vector<uint64_t> offs(1, 0);
+  for (size_t i : cand) {
+    bytes.push_back('a');
+    bytes.insert(bytes.end(), ents[i].text.begin(), ents[i].text.end());
+    offs.push_back(bytes.size());
+  }
+  ie_exec* x = nullptr;
+  int rc = ie_exec_create(device, nullptr, &x);
+  if (rc) return rc;
+  ie_batch* b = nullptr;
+  rc = ie_interpolate_batch(x, t0, bytes.data(), offs.data(), cand.size(), &b);
+  ie_exec_destroy(x);
+  if (rc) return rc;
+  std::vector<std::string> resolved(cand.size());
+  size_t changed = 0;
+  for (size_t k = 0; k < cand.size(); k++) {
+    if (b->status[k] != IE_OK_STR) continue;
+    const uint64_t o = b->offsets[k], len = b->offsets[k + 1] - o;
+    if (len < 1 || b->bytes[o] != 'a') continue;
+    std::string_view r((const char*)b->bytes + o + 1, len - 1);
+    bool inert = true;
+    for (size_t j = 0; j < r.size() && inert; j++) {
+      const uint8_t c = (uint8_t)r[j];
+      inert = c != '{' && c != '}' && c != '\\' &&
+              !(c == 0xE3 && j + 2 < r.size() && (uint8_t)r[j + 1] == 0x80 && (uint8_t)r[j + 2] == 0xA0);
+    }
+    if (!inert) continue;
+    resolved[k].assign(r);
+    Ent& e = ents[cand[k]];
+    e.raw = e.text;
+    e.text = resolved[k];
+    e.flags = (e.flags & ~EF_INERT) | text_flags(e.text) | EF_RAWALT;
+    changed++;
+  }
+  ie_batch_free(b);
+  if (!changed) return IE_SUCCESS;
+  ie_table* t1 = nullptr;
+  rc = upload_table(ents, dialect, flags, device, &t1);
+  if (rc) return rc;
+  ie_table_free(t0);
+  *out = t1;
+  return IE_SUCCESS;
+}
+
+int ie_table_build(const ie_kv* kv, uint64_t n, int32_t dialect, const ie_clock* now,
+                   uint32_t flags, int32_t device, ie_table** out) {
+  if (!out || (n && !kv)) return fail(IE_ERR_INVALID, "null argument");
+  if (dialect != IE_DIALECT_PY && dialect != IE_DIALECT_RS) return fail(IE_ERR_INVALID, "bad dialect");
+  int rc = set_device(device);
+  if (rc) return rc;
+  // dict semantics: the last duplicate wins; '' is never looked up (py:446 / interp.rs:105)
+  std::unordered_map<std::string_view, uint64_t> last;
+  last.reserve(n * 2 + 4);
+  std::vector<uint64_t> order;
+  for (uint64_t i = 0; i < n; i++) {
+    std::string_view k(kv[i].key ? kv[i].key : "", kv[i].key_len);
+    if (k.empty()) continue;
+    auto it = last.find(k);
+    if (it == last.end()) {
+      last.emplace(k, i);
+      order.push_back(i);
+    } else {
+      it->second = i;
+    }
+  }
+  char hhmm[16], hhmmss[16];
+  const int h = now ? now->hour : 0, mi = now ? now->minute : 0, se = now ? now->second : 0;
+  snprintf(hhmm, sizeof hhmm, "%02d:%02d", h, mi);
+  snprintf(hhmmss, sizeof hhmmss, "%02d:%02d:%02d", h, mi, se);
+
+  std::vector<Ent> ents;
+  ents.reserve(order.size() + 2);
+  for (uint64_t i : order) {
+    std::string_view k(kv[i].key, kv[i].key_len);
+    const uint64_t j = last[k];
+    if (k == "HH:MM" || k == "HH:MM:SS") continue;  // py:433-436: the clock always wins
+    if (kv[j].kind < 0 || kv[j].kind > IE_KIND_DICT) return fail(IE_ERR_INVALID, "bad kind");
+    std::string_view t(kv[j].text ? kv[j].text : "", kv[j].text_len);
+    ents.push_back(Ent{k, t, kind_flags(kv[j].kind, dialect) | text_flags(t), (uint32_t)j});
+  }
+  ents.push_back(Ent{"HH:MM", hhmm, kind_flags(IE_KIND_STR, dialect) | text_flags(hhmm), IE_VID_CLOCK_HHMM});
+  ents.push_back(Ent{"HH:MM:SS", hhmmss, kind_flags(IE_KIND_STR, dialect) | text_flags(hhmmss), IE_VID_CLOCK_HHMMSS});
+
+  ie_table* t0 = nullptr;
+  rc = upload_table(ents, dialect, flags, device, &t0);
+  if (rc || getenv("IE_NO_PRERESOLVE")) {  // diagnostic switch: raw splice texts only
+    *out = t0;
+    return rc;
+  }
+  *out = t0;
+  rc = preresolve(t0, ents, dialect, flags, device, out);
+  if (rc) {
+    ie_table_free(*out);
+    *out = nullptr;
+  }
+  return rc;
 }
 
 void ie_table_free(ie_table* t) {

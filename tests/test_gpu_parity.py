@@ -6,6 +6,7 @@ test_oracle_golden.py). Bar: byte-identical strings, identical status class, ide
 value (same insert) — bit-exact, this is byte/index work.
 """
 import ctypes
+import os
 import random
 
 import numpy as np
@@ -132,6 +133,21 @@ def _rand_string(rng, n_keys, long=False):
     if rng.random() < 0.1:
         s = "{" + s + "}"
     return s
+
+
+@pytest.mark.parametrize("dialect", ["py", "rs"])
+def test_preresolved_values_keep_raw_lookups(dialect):
+    """Brace-bearing values are pre-resolved at table build (splice text = their resolution) while
+    whole-string lookups by value (py:512 / interp.rs:48) still see the raw value: keys equal to
+    both the raw and the resolved text tell the two apart."""
+    table = {"a": "{b}", "b": "x{c}y", "c": "C", "x{c}y": "raw-hit", "xCy": "resolved-hit",
+             "d": "<{b}|{c}>", "e": "{a}{a}", "loop": "{loop}", "m": "{nope}", "n": 7, "w": "{n}",
+             "esc": "\\{b\\}", "half": "}{", "deep": "{e}{d}{e}"}
+    strings = ["{a}", "{{a}}", "{{b}}", "{{{b}}}", "z{b}z", "{x{c}y}", "<{d}>", "{e}", "e={e}!", "{loop}",
+               "x{loop}", "x{m}", "{m}", "{{m}}", "w{w}", "{w}", "{{w}}", "{esc}", "-{esc}-", "{half}",
+               "-{half}-", "{deep}", "a{deep}b{a}", "\\{a\\}{a}", "{q-{c}}", "{x{a}y}"]
+    bad = compare_with_oracle(table, strings, dialect)
+    assert not bad, bad[:4]
 
 
 @pytest.mark.parametrize("seed,brace_values,dialect", [(1, False, "py"), (2, True, "py"), (3, False, "rs"),
@@ -421,9 +437,14 @@ def test_full_size_config4_properties():
 def test_device_scratch_autogrow_and_caller_sized():
     """ie_interpolate_device grows the literal path's scratch pool to the batch's demand and re-runs
     (no IE_E_OVERFLOW from capacity); a pool sized by the caller (ie_exec_set_scratch) keeps the
-    call asynchronous and reports the strings that did not fit as IE_E_OVERFLOW."""
+    call asynchronous and reports the strings that did not fit as IE_E_OVERFLOW. The table keeps
+    its raw brace-bearing values (IE_NO_PRERESOLVE) so config 4's 2 % take the literal path."""
     h, kvp, nkv = _synth(4)
-    table = _table_from_kv(kvp, nkv)
+    os.environ["IE_NO_PRERESOLVE"] = "1"
+    try:
+        table = _table_from_kv(kvp, nkv)
+    finally:
+        del os.environ["IE_NO_PRERESOLVE"]
     n = 300_000
     over = N.STATUS_NAMES.index("E_OVERFLOW")
     x = N.Exec(0)
