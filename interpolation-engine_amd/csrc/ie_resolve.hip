@@ -471,8 +471,8 @@ __device__ uint8_t eval_exact(const DevTable& T, const Src<STAGED> s, uint32_t n
 __device__ __forceinline__ uint32_t nib(uint32_t v) {  // bit k: byte k of v has its top bit
   return ((v & 0x80808080u) * 0x00204081u) >> 28;
 }
-__device__ __forceinline__ uint32_t chunk_classify(const lds_u32* w, bool& odd) {
-  uint32_t op = 0, cl = 0, od = 0;
+__device__ __forceinline__ uint32_t chunk_classify(const lds_u32* w, bool& odd, bool& esc) {
+  uint32_t op = 0, cl = 0, od = 0, bs = 0;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const uint32_t x = w[k];
@@ -482,12 +482,29 @@ __device__ __forceinline__ uint32_t chunk_classify(const lds_u32* w, bool& odd) 
     const uint32_t nc = ((x7 ^ 0x7D7D7D7Du) + 0x7F7F7F7Fu) | x;
     const uint32_t nb = ((x7 ^ 0x5C5C5C5Cu) + 0x7F7F7F7Fu) | x;
     const uint32_t ne = ((x7 ^ 0x63636363u) + 0x7F7F7F7Fu) | ~x;
-    od |= ~(nb & ne);
+    od |= ~ne;
+    bs |= ~nb;
     op |= nib(~no) << (4 * k);
     cl |= nib(~nc) << (4 * k);
   }
   odd = (od & 0x80808080u) != 0;
+  esc = (bs & 0x80808080u) != 0;
   return op | (cl << 16);
+}
+
+// bits 0-15: '\' bytes, bits 16-31: '.' bytes of one staged 16-byte chunk
+__device__ __forceinline__ uint32_t chunk_bs_dot(const lds_u32* w) {
+  uint32_t bs = 0, dt = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t x = w[k];
+    const uint32_t x7 = x & 0x7F7F7F7Fu;
+    const uint32_t nb = ((x7 ^ 0x5C5C5C5Cu) + 0x7F7F7F7Fu) | x;
+    const uint32_t nd = ((x7 ^ 0x2E2E2E2Eu) + 0x7F7F7F7Fu) | x;
+    bs |= nib(~nb) << (4 * k);
+    dt |= nib(~nd) << (4 * k);
+  }
+  return bs | (dt << 16);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -555,7 +572,7 @@ struct TopText {
 };
 
 __device__ bool eval_chains(const DevTable& T, const lds_u16* pil, const lds_u8* tile, uint32_t p0, uint32_t n, const lds_u32* cm,
-                            const lds_u32* oddbits, bool active, const ChainLds& CL, Desc& d,
+                            const lds_u32* oddbits, const lds_u32* escbits, bool active, const ChainLds& CL, Desc& d,
                             TopText& tt, uint32_t& out_len, uint64_t* stamp) {
   bool ok = active && n <= kChainMax;
   const lds_u8* s = tile + p0;
@@ -564,9 +581,12 @@ __device__ bool eval_chains(const DevTable& T, const lds_u16* pil, const lds_u8*
   {
     const uint32_t c0 = ok ? p0 >> 4 : 0u, o = p0 & 15u;
     const uint32_t cl = ok && n ? (p0 + n - 1) >> 4 : c0;
-    // any odd chunk in [c0, cl] (<= 8 chunks): escapes / U+3020 need the exact evaluator
+    // any odd chunk in [c0, cl] (<= 8 chunks): U+3020 needs the exact evaluator
+    const uint64_t span_m = (2ull << (cl - c0)) - 1ull;
     const uint64_t ob = ((uint64_t)oddbits[(c0 >> 5) + 1] << 32) | oddbits[c0 >> 5];
-    if ((ob >> (c0 & 31)) & ((2ull << (cl - c0)) - 1ull)) ok = false;
+    if ((ob >> (c0 & 31)) & span_m) ok = false;
+    const uint64_t eb = ((uint64_t)escbits[(c0 >> 5) + 1] << 32) | escbits[c0 >> 5];
+    const bool esc = ok && ((eb >> (c0 & 31)) & span_m) != 0;
     uint32_t Wo[5], Wc[5];
 #pragma unroll
     for (int j = 0; j < 5; j++) {
@@ -580,6 +600,45 @@ __device__ bool eval_chains(const DevTable& T, const lds_u16* pil, const lds_u8*
       const uint32_t keep = !ok ? 0u : r >= 32 ? 0xFFFFFFFFu : r > 0 ? (1u << r) - 1u : 0u;
       O[j] = __builtin_amdgcn_alignbit(Wo[j + 1], Wo[j], o) & keep;
       C[j] = __builtin_amdgcn_alignbit(Wc[j + 1], Wc[j], o) & keep;
+    }
+    // Escapes (py:505-508): a brace right after a '\' is protected, i.e. plain text to the loop,
+    // and comes back unchanged (py:537-540) unless the restore misreads it: '\}' right after a
+    // '.' or a '}' (a value may end in '.') restores as '\{...' (py:538 runs before py:539), so
+    // such strings stay with the exact evaluator.
+    if (__any(esc)) {
+      uint32_t Wb[5], Wd[5];
+#pragma unroll
+      for (int j = 0; j < 5; j++) {
+        const uint32_t ca = c0 + 2 * j, cb = ca + 1;
+        const uint32_t x = esc && ca <= cl ? chunk_bs_dot(((const lds_u32*)tile) + 4 * ca) : 0u;
+        const uint32_t y = esc && j < 4 && cb <= cl ? chunk_bs_dot(((const lds_u32*)tile) + 4 * cb) : 0u;
+        Wb[j] = (x & 0xFFFFu) | (y << 16);
+        Wd[j] = (x >> 16) | (y & 0xFFFF0000u);
+      }
+      uint32_t B[4], D[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int32_t r = (int32_t)n - 32 * j;
+        const uint32_t keep = !esc ? 0u : r >= 32 ? 0xFFFFFFFFu : r > 0 ? (1u << r) - 1u : 0u;
+        B[j] = __builtin_amdgcn_alignbit(Wb[j + 1], Wb[j], o) & keep;
+        D[j] = __builtin_amdgcn_alignbit(Wd[j + 1], Wd[j], o) & keep;
+      }
+      uint32_t EC[4];
+      bool hazard = false;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t b1 = (B[j] << 1) | (j ? B[j - 1] >> 31 : 0u);  // bytes right after a '\'
+        EC[j] = C[j] & b1;
+        O[j] &= ~b1;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t before = (EC[j] >> 2) | (j < 3 ? EC[j + 1] << 30 : 0u);  // the byte before the '\'
+        hazard |= (before & (D[j] | C[j])) != 0u;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++) C[j] &= ~EC[j];
+      if (hazard) ok = false;
     }
   }
   // ---- 2. chains: the events of a chain-only string are blocks O^d C^d (each pair has at most
@@ -836,7 +895,8 @@ constexpr uint32_t kChunks = (kTileBytes + 32) / 16;
 constexpr uint32_t kOddWords = ((kChunks + kBlock - 1) / kBlock) * (kBlock / 32) + 2;
 constexpr uint32_t kCmOff = kEvalLds;
 constexpr uint32_t kOddOff = kCmOff + 4 * (kChunks + 10);
-constexpr uint32_t kClassEnd = kOddOff + 4 * kOddWords;
+constexpr uint32_t kEscOff = kOddOff + 4 * kOddWords;
+constexpr uint32_t kClassEnd = kEscOff + 4 * kOddWords;
 constexpr uint32_t kUnionLds = kClassEnd > (uint32_t)kStageBytes + 32 ? kClassEnd : (uint32_t)kStageBytes + 32;
 static_assert(kKeyCap >= 32 && kMaxDepth <= 8, "evaluator scratch");
 
@@ -909,7 +969,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
   __shared__ uint64_t s_red[kBlock / 64 + 2];
   __shared__ __attribute__((aligned(16))) uint16_t s_pil[kLdsPilots];  // the table's pilots (small tables)
   lds_u32* const s_cm = (lds_u32*)(lds_u8*)(s_u + kCmOff);    // event masks of the staged chunks (+ pad)
-  lds_u32* const s_odd = (lds_u32*)(lds_u8*)(s_u + kOddOff);  // one bit per chunk: '\' or 0xE3 inside
+  lds_u32* const s_odd = (lds_u32*)(lds_u8*)(s_u + kOddOff);  // one bit per chunk: 0xE3 inside
+  lds_u32* const s_esc = (lds_u32*)(lds_u8*)(s_u + kEscOff);  // one bit per chunk: '\' inside
   lds_u32* const s_lit = (lds_u32*)(lds_u8*)s_u;              // literal-path results: pool offset >> 4
 
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
@@ -968,12 +1029,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
     const uint32_t nv = pre.nv;
     for (uint32_t c0 = 0; c0 < nv; c0 += kBlock) {  // uniform trip count: ballots below
       const uint32_t c = c0 + tid;
-      bool odd = false;
-      if (c < nv) s_cm[c] = chunk_classify((const lds_u32*)(lds_u8*)s_in + 4 * c, odd);
-      const uint64_t ob = __ballot(odd);
-      if (lane == 0) {  // 64 consecutive chunks = two words of the odd bit array
+      bool odd = false, esc = false;
+      if (c < nv) s_cm[c] = chunk_classify((const lds_u32*)(lds_u8*)s_in + 4 * c, odd, esc);
+      const uint64_t ob = __ballot(odd), eb = __ballot(esc);
+      if (lane == 0) {  // 64 consecutive chunks = two words of each bit array
         s_odd[(c0 + 64 * wave) >> 5] = (uint32_t)ob;
         s_odd[((c0 + 64 * wave) >> 5) + 1] = (uint32_t)(ob >> 32);
+        s_esc[(c0 + 64 * wave) >> 5] = (uint32_t)eb;
+        s_esc[((c0 + 64 * wave) >> 5) + 1] = (uint32_t)(eb >> 32);
       }
     }
     if (tid < 10) s_cm[nv + tid] = 0;  // the event windows read past the last chunk
@@ -1007,7 +1070,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
     } else if (staged && W.fast_mode) {
       const ChainLds CL{(lds_u8*)(s_u + tid * kKeyCap), (lds_u64*)(lds_u8*)(s_u + kKbufLds) + tid};
       const bool fast = eval_chains(T, lds_pil ? (const lds_u16*)s_pil : nullptr, (const lds_u8*)s_in, p0, (uint32_t)sn, s_cm,
-                                    s_odd, active, CL, d, tt, olen,
+                                    s_odd, s_esc, active, CL, d, tt, olen,
                                     stamp_row ? stamp_row + 6 : nullptr);
       slow = active && !fast;
       fast_lane = fast;

@@ -136,6 +136,25 @@ def _rand_string(rng, n_keys, long=False):
 
 
 @pytest.mark.parametrize("dialect", ["py", "rs"])
+def test_escapes_next_to_chains(dialect):
+    """Escaped braces inside chain-shaped strings (the chain evaluator treats a brace after '\\' as
+    text) and the restore hazards that must leave it: '\\}' after '.', after a real '}' (a value
+    may end in '.') and after another '\\}'; backslash runs; escapes inside keys."""
+    table = {"k1": "V1", "k2": "dot.", "q-3": "Q3", "i": 3, "a\\}b": "AB", "a\\{b": "AB2", "x.": "XD",
+             "\\{": "BR", "q-V1": "QV"}
+    pieces = ["{k1}", "{k2}", "{q-{i}}", "\\{", "\\}", ".", "\\", "x", "{a\\}b}", "{a\\{b}", "}", "{",
+              "{q-{k1}}", "é", "{\\{}"]
+    rng = random.Random(7)
+    strings = ["a.\\}b{k1}", "{k1}\\}x", "{k2}\\}x", "\\}\\}{k1}", "\\{k1\\}{k2}", "x\\{{k1}\\}",
+               "{a\\}b}", "\\\\{k1}", "\\\\}{k1}", ".\\{{k1}", "{k1}.\\}", "\\}{k1}", "p{k1}\\",
+               "{a\\{b}{q-{i}}\\{", "z{\\{}z"]
+    for _ in range(4000):
+        strings.append("".join(rng.choice(pieces) for _ in range(rng.randint(1, 9))))
+    bad = compare_with_oracle(table, strings, dialect)
+    assert not bad, bad[:4]
+
+
+@pytest.mark.parametrize("dialect", ["py", "rs"])
 def test_preresolved_values_keep_raw_lookups(dialect):
     """Brace-bearing values are pre-resolved at table build (splice text = their resolution) while
     whole-string lookups by value (py:512 / interp.rs:48) still see the raw value: keys equal to
