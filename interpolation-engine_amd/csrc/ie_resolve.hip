@@ -573,7 +573,7 @@ struct TopText {
 
 __device__ bool eval_chains(const DevTable& T, const lds_u16* pil, const lds_u8* tile, uint32_t p0, uint32_t n, const lds_u32* cm,
                             const lds_u32* oddbits, const lds_u32* escbits, bool active, const ChainLds& CL, Desc& d,
-                            TopText& tt, uint32_t& out_len, uint64_t* stamp) {
+                            TopText& tt, uint32_t& out_len, uint8_t& status, uint64_t* stamp) {
   bool ok = active && n <= kChainMax;
   const lds_u8* s = tile + p0;
   // ---- 1. the string's open / close events as 128-bit windows ----
@@ -688,6 +688,10 @@ __device__ bool eval_chains(const DevTable& T, const lds_u16* pil, const lds_u8*
     cl_[c] = co_[c] = ctl[c] = 0;
   }
   uint32_t vsum = 0, span = 0;
+  // failures (a miss, or a hit the dialect cannot splice): the reference stops at the failing pair
+  // with the largest opening offset, and never evaluates the pairs enclosing a failed one (dead)
+  // one word: bits 0-7 the status so far (0 = none), 8-15 its pair's opening offset, 16+ dead chains
+  uint32_t fw = 0;
   const uint32_t R = w_max32(ok ? maxd : 0u);
   for (uint32_t r = 0; r < R; r++) {
     bool on[kMaxTop];
@@ -696,7 +700,7 @@ __device__ bool eval_chains(const DevTable& T, const lds_u16* pil, const lds_u8*
     uint64_t h[kMaxTop];
 #pragma unroll
     for (int c = 0; c < kMaxTop; c++) {
-      on[c] = ok && r < cdep[c];
+      on[c] = ok && r < cdep[c] && !((fw >> (16 + c)) & 1u);
       // level r: the innermost pair in round 0, the outermost in the last round; a middle level
       // is the open before the previous level's and the close after it
       const bool top_c = r + 1 == cdep[c];
@@ -773,7 +777,16 @@ __device__ bool eval_chains(const DevTable& T, const lds_u16* pil, const lds_u8*
                                  (E.q1.z == kw[c].z) & (E.q1.w == kw[c].w));
       const uint32_t flags = E.q0.z, tlen = E.q0.y;
       const bool good = hit && (flags & EF_SPLICE_OK) && (flags & EF_INERT);
-      if (on[c] && !good) ok = false;  // a miss or a value needing care: exact evaluator
+      // a miss (no inserts-dir: py:465 / interp.rs:136) or a hit that cannot be spliced
+      // (py:530 / interp.rs:76-79) fails this pair; a hit on a value needing care, or a miss that
+      // the inserts-dir might resolve, goes to the exact evaluator
+      const bool fail = on[c] && ((!hit && !(T.flags & TF_HAS_DIR)) || (hit && !(flags & EF_SPLICE_OK)));
+      if (on[c] && !good && !fail) ok = false;
+      if (fail) {
+        const uint32_t st = hit ? (uint32_t)IE_E_ASSERT_TYPE : (uint32_t)IE_E_INTERP;
+        const bool newer = (fw & 0xFFu) == 0u || open[c] > ((fw >> 8) & 0xFFu);
+        fw = (fw & ~0xFFFFu) | (newer ? (open[c] << 8) | st : fw & 0xFFFFu) | (1u << (16 + c));
+      }
       const bool top = r + 1 == cdep[c];
       if (on[c] && good && !top) {  // inner level: this text goes into the parent's key
         if (tlen > 16u) ok = false;
@@ -795,8 +808,11 @@ __device__ bool eval_chains(const DevTable& T, const lds_u16* pil, const lds_u8*
       }
     }
   }
-  d.ntop = ok ? nch : 0u;
-  out_len = ok ? n - span + vsum : 0u;
+  const bool failed = (fw & 0xFFu) != 0u;
+  const uint8_t fail_st = (uint8_t)(fw & 0xFFu);
+  d.ntop = ok && !failed ? nch : 0u;
+  out_len = ok && !failed ? n - span + vsum : 0u;
+  if (ok && failed) status = fail_st;
   return ok;
 }
 
@@ -1070,7 +1086,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
     } else if (staged && W.fast_mode) {
       const ChainLds CL{(lds_u8*)(s_u + tid * kKeyCap), (lds_u64*)(lds_u8*)(s_u + kKbufLds) + tid};
       const bool fast = eval_chains(T, lds_pil ? (const lds_u16*)s_pil : nullptr, (const lds_u8*)s_in, p0, (uint32_t)sn, s_cm,
-                                    s_odd, s_esc, active, CL, d, tt, olen,
+                                    s_odd, s_esc, active, CL, d, tt, olen, r,
                                     stamp_row ? stamp_row + 6 : nullptr);
       slow = active && !fast;
       fast_lane = fast;

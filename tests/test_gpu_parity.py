@@ -136,6 +136,24 @@ def _rand_string(rng, n_keys, long=False):
 
 
 @pytest.mark.parametrize("dialect", ["py", "rs"])
+def test_chain_failures_follow_the_reference_order(dialect):
+    """Misses and unspliceable hits inside chain-shaped strings: the reference reports the failing
+    pair with the largest opening offset (rightmost chain, innermost level) and never evaluates
+    the pairs enclosing it."""
+    table = {"a": "A", "i": 2, "q-2": "Q2", "f": 1.5, "n": None, "d": {"z": 1}, "L": ["x", 1], "b": True,
+             "q-A": "QA", "q-1.5": "QF", "i2": "f"}
+    pieces = ["{a}", "{zz}", "{f}", "{n}", "{d}", "{L}", "{b}", "{q-{i}}", "{q-{zz}}", "{q-{f}}", "{zz-{a}}",
+              "{q-{a}}", "{{i2}}", "{q-{q-{i}}}", "{}", "x", "é"]
+    rng = random.Random(11)
+    strings = ["x{zz}{f}", "x{f}{zz}", "x{q-{zz}}{a}", "x{a}{q-{f}}", "x{zz-{f}}", "x{q-{f}}y{zz}",
+               "x{zz}y{q-{n}}", "{q-{zz}}", "x{}{a}"]
+    for _ in range(4000):
+        strings.append("".join(rng.choice(pieces) for _ in range(rng.randint(1, 4))))
+    bad = compare_with_oracle(table, strings, dialect)
+    assert not bad, bad[:4]
+
+
+@pytest.mark.parametrize("dialect", ["py", "rs"])
 def test_escapes_next_to_chains(dialect):
     """Escaped braces inside chain-shaped strings (the chain evaluator treats a brace after '\\' as
     text) and the restore hazards that must leave it: '\\}' after '.', after a real '}' (a value
