@@ -497,6 +497,39 @@ def test_device_scratch_autogrow_and_caller_sized():
     N.lib().ie_table_free(table)
 
 
+@pytest.mark.parametrize("op", ["ie_unescape_device", "ie_escape_device"])
+def test_escape_kernels_on_a_ragged_batch(op):
+    """recursive_unescape / recursive_escape on strings (py:1436-1460) over a ragged batch: empty
+    strings, short strings, strings longer than an LDS tile, backslash runs next to braces."""
+    rng = random.Random(5)
+    alpha = ["a", "{", "}", "\\", "\\{", "\\}", "é", "😀", " "]
+    strs = []
+    for k in range(60_000):
+        r = rng.random()
+        n = 0 if r < 0.05 else rng.randint(1, 20) if r < 0.9 else rng.randint(200, 3000)
+        if k % 9000 == 0:
+            n = 40_000  # a tile beyond the LDS stage
+        strs.append("".join(rng.choice(alpha) for _ in range(n)))
+    enc = [t.encode() for t in strs]
+    offs = np.zeros(len(enc) + 1, np.uint64)
+    offs[1:] = np.cumsum([len(b) for b in enc])
+    buf = np.frombuffer(b"".join(enc) + bytes(16), np.uint8)
+    n = len(enc)
+    x = N.Exec(0)
+    d_b = N.DeviceBuffer.from_numpy(x, buf)
+    d_o = N.DeviceBuffer.from_numpy(x, offs)
+    res = DevResult(x, n, 2 * buf.size + 4096)
+    N.check(getattr(N.lib(), op)(x.h, d_b.ptr, d_o.ptr, n, ctypes.byref(res.out)), op)
+    x.sync()
+    o1 = res.off.to_numpy(np.uint64, n + 1)
+    b1 = res.bytes.to_numpy(np.uint8, res.total()).tobytes()
+    assert int(np.count_nonzero(res.status.to_numpy(np.uint8, n))) == 0
+    for k, t in enumerate(strs):
+        want = (t.replace("\\{", "{").replace("\\}", "}") if op == "ie_unescape_device"
+                else t.replace("{", "\\{").replace("}", "\\}"))
+        assert b1[int(o1[k]):int(o1[k + 1])].decode() == want, k
+
+
 def test_device_api_capacity_contract():
     """bytes_cap too small: offsets/status are valid, *total reports the need, bytes untouched."""
     t = PKG.InsertsTable({"a": "A" * 50}, clock=CLOCK)
