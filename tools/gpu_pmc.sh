@@ -9,6 +9,6 @@ rocprofv3 -L > gpurun_out/pmc_list.txt 2>&1 || true
 k=0
 for set in "$@"; do
   k=$((k+1))
-  timeout -k 10 240 rocprofv3 --pmc $set --output-format csv -d gpurun_out/pmc_$k -o run -- \
-    python3 bench.py --steps 3 --warmup 1 --no-cpu ${BENCH_ARGS:-} > gpurun_out/pmc_$k.log 2>&1 || exit $?
+  timeout -k 10 240 rocprofv3 --pmc $set --output-format csv -d gpurun_out/${PFX:-pmc}_$k -o run -- \
+    python3 bench.py --steps 3 --warmup 1 --no-cpu ${BENCH_ARGS:-} > gpurun_out/${PFX:-pmc}_$k.log 2>&1 || exit $?
 done
