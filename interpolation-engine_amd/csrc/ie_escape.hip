@@ -43,6 +43,35 @@ __device__ uint8_t eval_escape(const uint8_t* __restrict__ s, uint32_t n, uint8_
   return IE_OK_STR;
 }
 
+// Output length of one string staged in LDS, a dword at a time: unescape drops one byte per '\'
+// followed by a brace (such pairs never overlap: the second byte of one is never a '\'), escape
+// adds one per brace. Same result as eval_escape's byte loop (measure mode).
+__device__ __forceinline__ uint32_t nib4(uint32_t v) {  // bit k: byte k of v has its top bit
+  return ((v & 0x80808080u) * 0x00204081u) >> 28;
+}
+template <int OP>
+__device__ uint32_t escape_len_lds(const uint8_t* s, uint32_t n) {
+  const uintptr_t p = (uintptr_t)s;
+  const uint32_t* w = (const uint32_t*)(p & ~(uintptr_t)3);
+  const uint32_t off = (uint32_t)(p & 3), end = off + n;
+  uint32_t cnt = 0, carry = 0;  // carry: a valid '\' in the previous dword's top byte
+  for (uint32_t j = 0; 4 * j < end; j++) {
+    const uint32_t x = w[j], x7 = x & 0x7F7F7F7Fu;
+    const uint32_t bs = nib4(~(((x7 ^ 0x5C5C5C5Cu) + 0x7F7F7F7Fu) | x));
+    const uint32_t br = nib4(~(((x7 ^ 0x7B7B7B7Bu) + 0x7F7F7F7Fu) | x)) | nib4(~(((x7 ^ 0x7D7D7D7Du) + 0x7F7F7F7Fu) | x));
+    const uint32_t lo = 4 * j < off ? off - 4 * j : 0u, hi = end - 4 * j < 4u ? end - 4 * j : 4u;
+    const uint32_t valid = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+    if (OP == kOpUnescape) {
+      const uint32_t b = bs & valid, r = br & valid;
+      cnt += (uint32_t)__popc(b & (r >> 1)) + (carry & r & 1u);
+      carry = b >> 3;
+    } else {
+      cnt += (uint32_t)__popc(br & valid);
+    }
+  }
+  return OP == kOpUnescape ? n - cnt : n + cnt;
+}
+
 // ------------------------------------------------------------------------------------------
 // workgroup helpers
 // ------------------------------------------------------------------------------------------
@@ -112,7 +141,9 @@ __global__ __launch_bounds__(kBlock) void k_measure(Batch B, Work W) {
     const uint64_t so = B.in_off[i], eo = B.in_off[i + 1];
     const uint8_t* s = staged ? s_in + shift + (so - lo) : B.bytes + so;
     uint32_t olen = 0;
-    const uint8_t st = eval_escape<OP>(s, (uint32_t)(eo - so), nullptr, olen, false);
+    uint8_t st = IE_OK_STR;
+    if (staged) olen = escape_len_lds<OP>(s, (uint32_t)(eo - so));
+    else st = eval_escape<OP>(s, (uint32_t)(eo - so), nullptr, olen, false);
     W.out_len[i] = olen;
     my_len = olen;
     B.status[i] = st;
