@@ -95,6 +95,13 @@ struct ie_exec {
   uint32_t lit_cap_max = 0;
   uint64_t pool_request = 256ull << 20;
   bool pool_fixed = false;  // set by ie_exec_set_scratch: the caller sized the pool, no wait/re-run
+  // fail commit (k_resolve<true>): chosen from the exact-path count of an earlier batch, read back
+  // asynchronously (never a wait): a stream with misses or type errors switches to it for good
+  bool fail_commit = false;
+  bool stat_pending = false;
+  uint64_t stat_n = 0;
+  uint32_t* stat_host = nullptr;  // pinned
+  hipEvent_t stat_ev = nullptr;
   // workspace
   DevBuf counters, tile_state, pool, out_len, tile_sum, tile_base;
   // host-API staging
@@ -111,6 +118,8 @@ struct ie_exec {
       if (e) (void)hipEventDestroy(e);
     for (auto& e : marks)
       if (e) (void)hipEventDestroy(e);
+    if (stat_ev) (void)hipEventDestroy(stat_ev);
+    if (stat_host) (void)hipHostFree(stat_host);
     if (own_stream && stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -292,8 +301,25 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
   } else if (op == kOpInterp) {
     const uint64_t tiles = (n + kBlock - 1) / kBlock;
     IE_HIP(hipMemsetAsync(x->tile_state.p, 0, tiles * sizeof(uint64_t), st));
+    // fail commit: forced by IE_FAIL_COMMIT=0/1 (diagnostics, tests), else adaptive
+    const char* fc = getenv("IE_FAIL_COMMIT");
+    if (!fc && x->stat_pending && hipEventQuery(x->stat_ev) == hipSuccess) {
+      x->stat_pending = false;
+      if ((uint64_t)*x->stat_host * 1024 > x->stat_n) x->fail_commit = true;  // > 0.1 % exact-path strings
+    }
+    W.fail_commit = fc ? (uint32_t)(atoi(fc) != 0) : (uint32_t)x->fail_commit;
     if (x->timing) IE_HIP(hipEventRecord(x->ev[1], st));
     IE_HIP(launch_resolve(B, W, t->dev, out->bytes, cap, st));
+    if (!fc && !W.fail_commit && !x->stat_pending) {
+      if (!x->stat_host) {
+        IE_HIP(hipHostMalloc((void**)&x->stat_host, 4, hipHostMallocDefault));
+        IE_HIP(hipEventCreateWithFlags(&x->stat_ev, hipEventDisableTiming));
+      }
+      IE_HIP(hipMemcpyAsync(x->stat_host, W.stats + 3, 4, hipMemcpyDeviceToHost, st));
+      IE_HIP(hipEventRecord(x->stat_ev, st));
+      x->stat_pending = true;
+      x->stat_n = n;
+    }
   } else {
     if (x->timing) IE_HIP(hipEventRecord(x->ev[1], st));
     IE_HIP(launch_escape(op, B, W, out->bytes, cap, st));

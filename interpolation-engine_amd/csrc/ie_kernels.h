@@ -39,6 +39,7 @@ struct Work {
   uint64_t* pool_used;   // 1
   uint64_t pool_bytes;
   uint32_t lit_cap_max;  // 1: literal strings get the full IE_SIZE_CAP working space
+  uint32_t fail_commit;  // 1: chain failures commit in the chain evaluator (k_resolve<true>)
   // escape pipeline
   uint32_t* out_len;     // n
   uint64_t* tile_sum;    // tiles

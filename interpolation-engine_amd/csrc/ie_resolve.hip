@@ -571,6 +571,7 @@ struct TopText {
   uint32_t w[kMaxTop][8];
 };
 
+template <bool FAILC>
 __device__ bool eval_chains(const DevTable& T, const lds_u16* pil, const lds_u8* tile, uint32_t p0, uint32_t n, const lds_u32* cm,
                             const lds_u32* oddbits, const lds_u32* escbits, bool active, const ChainLds& CL, Desc& d,
                             TopText& tt, uint32_t& out_len, uint8_t& status, uint64_t* stamp) {
@@ -780,7 +781,7 @@ __device__ bool eval_chains(const DevTable& T, const lds_u16* pil, const lds_u8*
       // a miss (no inserts-dir: py:465 / interp.rs:136) or a hit that cannot be spliced
       // (py:530 / interp.rs:76-79) fails this pair; a hit on a value needing care, or a miss that
       // the inserts-dir might resolve, goes to the exact evaluator
-      const bool fail = on[c] && ((!hit && !(T.flags & TF_HAS_DIR)) || (hit && !(flags & EF_SPLICE_OK)));
+      const bool fail = FAILC && on[c] && ((!hit && !(T.flags & TF_HAS_DIR)) || (hit && !(flags & EF_SPLICE_OK)));
       if (on[c] && !good && !fail) ok = false;
       if (fail) {
         const uint32_t st = hit ? (uint32_t)IE_E_ASSERT_TYPE : (uint32_t)IE_E_INTERP;
@@ -974,6 +975,9 @@ __device__ __forceinline__ uint4 bytes_at(u32x4 x, u32x4 y, uint32_t r) {
                     __builtin_amdgcn_alignbyte(a3, a2, sb), __builtin_amdgcn_alignbyte(a4, a3, sb));
 }
 
+// FAILC: chain failures commit in the chain evaluator (else they take the exact evaluator). Both
+// give the reference's results; the host picks per batch stream (ie_host.cpp, "fail commit").
+template <bool FAILC>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_resolve(Batch B, Work W, DevTable T, uint8_t* out,
                                                     uint64_t cap) {
   __shared__ __attribute__((aligned(16))) uint8_t s_in[kTileBytes + 48];
@@ -1085,7 +1089,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
       slow = false;
     } else if (staged && W.fast_mode) {
       const ChainLds CL{(lds_u8*)(s_u + tid * kKeyCap), (lds_u64*)(lds_u8*)(s_u + kKbufLds) + tid};
-      const bool fast = eval_chains(T, lds_pil ? (const lds_u16*)s_pil : nullptr, (const lds_u8*)s_in, p0, (uint32_t)sn, s_cm,
+      const bool fast = eval_chains<FAILC>(T, lds_pil ? (const lds_u16*)s_pil : nullptr, (const lds_u8*)s_in, p0, (uint32_t)sn, s_cm,
                                     s_odd, s_esc, active, CL, d, tt, olen, r,
                                     stamp_row ? stamp_row + 6 : nullptr);
       slow = active && !fast;
@@ -1323,7 +1327,8 @@ hipError_t launch_resolve(const Batch& B, const Work& W, const DevTable& T, uint
   if (!tiles) return hipSuccess;
   if (tiles > 0xFFFFFFFFull) return hipErrorInvalidValue;
   const uint32_t grid = (uint32_t)tiles;
-  hipLaunchKernelGGL(k_resolve, dim3(grid), dim3(kBlock), 0, st, B, W, T, out, cap);
+  if (W.fail_commit) hipLaunchKernelGGL(k_resolve<true>, dim3(grid), dim3(kBlock), 0, st, B, W, T, out, cap);
+  else hipLaunchKernelGGL(k_resolve<false>, dim3(grid), dim3(kBlock), 0, st, B, W, T, out, cap);
   return hipGetLastError();
 }
 

@@ -30,6 +30,15 @@ def run_product(table_dict, strings, dialect="py", has_dir=False):
     return t.run(strings), t
 
 
+@pytest.fixture(params=["0", "1"], ids=["chain-fail-exact", "chain-fail-commit"])
+def fail_commit(request):
+    """Both k_resolve variants: chain failures sent to the exact evaluator, or committed in the
+    chain evaluator (the library picks one adaptively; IE_FAIL_COMMIT forces it)."""
+    os.environ["IE_FAIL_COMMIT"] = request.param
+    yield request.param
+    del os.environ["IE_FAIL_COMMIT"]
+
+
 def compare_with_oracle(table_dict, strings, dialect="py", has_dir=False):
     got, t = run_product(table_dict, strings, dialect, has_dir)
     ref = O.Oracle(table_dict, dialect, clock=CLOCK, has_dir=has_dir)
@@ -50,7 +59,7 @@ def compare_with_oracle(table_dict, strings, dialect="py", has_dir=False):
 # ------------------------------------------------------------------------------------------
 # golden vectors from the reference itself
 # ------------------------------------------------------------------------------------------
-def test_reference_golden_vectors(golden_tables, golden_interp):
+def test_reference_golden_vectors(golden_tables, golden_interp, fail_commit):
     by_table = {}
     for row in golden_interp:
         by_table.setdefault(row["t"], []).append(row)
@@ -136,7 +145,7 @@ def _rand_string(rng, n_keys, long=False):
 
 
 @pytest.mark.parametrize("dialect", ["py", "rs"])
-def test_chain_failures_follow_the_reference_order(dialect):
+def test_chain_failures_follow_the_reference_order(dialect, fail_commit):
     """Misses and unspliceable hits inside chain-shaped strings: the reference reports the failing
     pair with the largest opening offset (rightmost chain, innermost level) and never evaluates
     the pairs enclosing it."""
@@ -154,7 +163,7 @@ def test_chain_failures_follow_the_reference_order(dialect):
 
 
 @pytest.mark.parametrize("dialect", ["py", "rs"])
-def test_escapes_next_to_chains(dialect):
+def test_escapes_next_to_chains(dialect, fail_commit):
     """Escaped braces inside chain-shaped strings (the chain evaluator treats a brace after '\\' as
     text) and the restore hazards that must leave it: '\\}' after '.', after a real '}' (a value
     may end in '.') and after another '\\}'; backslash runs; escapes inside keys."""
@@ -189,7 +198,7 @@ def test_preresolved_values_keep_raw_lookups(dialect):
 
 @pytest.mark.parametrize("seed,brace_values,dialect", [(1, False, "py"), (2, True, "py"), (3, False, "rs"),
                                                        (4, True, "rs")])
-def test_random_vs_oracle(seed, brace_values, dialect):
+def test_random_vs_oracle(seed, brace_values, dialect, fail_commit):
     rng = random.Random(seed)
     table = _rand_table(rng, 60, brace_values)
     strings = [_rand_string(rng, 60) for _ in range(3000)]
@@ -361,7 +370,7 @@ def _device_run(x, table, d_bytes, d_off, n, cap=None):
 
 
 @pytest.mark.parametrize("config", [2, 3, 4])
-def test_synthetic_config_vs_oracle(config):
+def test_synthetic_config_vs_oracle(config, fail_commit):
     h, kvp, nkv = _synth(config)
     table = _table_from_kv(kvp, nkv)
     x = N.Exec(0)
@@ -528,6 +537,30 @@ def test_escape_kernels_on_a_ragged_batch(op):
         want = (t.replace("\\{", "{").replace("\\}", "}") if op == "ie_unescape_device"
                 else t.replace("{", "\\{").replace("}", "\\}"))
         assert b1[int(o1[k]):int(o1[k + 1])].decode() == want, k
+
+
+def test_fail_commit_is_adopted_after_a_batch_with_misses():
+    """Adaptive variant choice: an exec starts with chain failures on the exact evaluator and
+    switches once an earlier batch showed exact-path strings; results are identical throughout."""
+    h, kvp, nkv = _synth(4)
+    table = _table_from_kv(kvp, nkv)
+    x = N.Exec(0)
+    n = 200_000
+    d_off, d_bytes, _ = _device_strings(x, h, 0, n)
+    runs = []
+    for _ in range(3):
+        x.set_timing(True)
+        r = _device_run(x, table, d_bytes, d_off, n)
+        tm = x.timing()
+        x.set_timing(False)
+        runs.append((int(tm.n_exact), r.off.to_numpy(np.uint64, n + 1), r.bytes.to_numpy(np.uint8, r.total()),
+                     r.status.to_numpy(np.uint8, n)))
+    assert runs[0][0] > n // 1024  # misses went to the exact evaluator
+    assert runs[2][0] == 0  # ... and are committed by the chain evaluator later
+    for k in (1, 2):
+        assert np.array_equal(runs[k][1], runs[0][1]) and np.array_equal(runs[k][2], runs[0][2])
+        assert np.array_equal(runs[k][3], runs[0][3])
+    N.lib().ie_table_free(table)
 
 
 def test_device_api_capacity_contract():
