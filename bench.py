@@ -76,7 +76,12 @@ def main():
         dist.init_process_group("gloo")
 
     import __graft_entry__ as G
-    G.build()
+    if local == 0:  # one build per node (ranks share the in-tree library)
+        G.build()
+    if dist:
+        dist.barrier()
+    if local != 0:
+        G.build()  # up to date by now: only loads the library
     pkg = G.load_package()
     N = pkg._native
     L = N.lib()
