@@ -6,6 +6,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
@@ -32,7 +33,7 @@ def _shard_bytes(N, L, synth, first, n):
     return buf[:int(tot.value)].tobytes()
 
 
-def _worker(rank, world, port, result_dir):
+def _worker(rank, world, port, result_dir, config=3):
     import bench
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -40,7 +41,7 @@ def _worker(rank, world, port, result_dir):
     N = pkg._native
     L = N.lib()
     synth = ctypes.c_void_p()
-    N.check(L.ie_synth_create(3, 0, ctypes.byref(synth)), "synth")
+    N.check(L.ie_synth_create(config, 0, ctypes.byref(synth)), "synth")
     mine = _shard_bytes(N, L, synth, bench.shard_first(rank, N_PER_RANK), N_PER_RANK)
     gathered = [None] * world
     dist.all_gather_object(gathered, mine)
@@ -53,7 +54,8 @@ def _worker(rank, world, port, result_dir):
     dist.destroy_process_group()
 
 
-def test_two_rank_shards_tile_the_stream(tmp_path):
+@pytest.mark.parametrize("config", [3, 4])
+def test_two_rank_shards_tile_the_stream(tmp_path, config):
     G.build()
-    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path), config), nprocs=2, join=True)
     assert (tmp_path / "ok").read_text() == "1"
