@@ -183,14 +183,15 @@ def main():
         cpu = cpu_baseline(args, L, N, synth, kvp, nkv, d_ooff, d_out, d_st)
 
     traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc_path):
-        try:
-            pm = json.load(open(pmc_path))
-            if pm.get("config") == cfg and pm.get("n") == n:
-                traffic = pm.get("hbm_bytes_per_step")
-        except Exception:
-            traffic = None
+    for name in ("pmc_traffic.json", "pmc_traffic_cfg%d.json" % cfg):  # PMC passes of this workload
+        pmc_path = os.path.join(ROOT, "profiles", name)
+        if traffic is None and os.path.exists(pmc_path):
+            try:
+                pm = json.load(open(pmc_path))
+                if pm.get("config") == cfg and pm.get("n") == n:
+                    traffic = pm.get("hbm_bytes_per_step")
+            except Exception:
+                traffic = None
 
     if rank == 0:
         line = {
