@@ -76,12 +76,7 @@ def main():
         dist.init_process_group("gloo")
 
     import __graft_entry__ as G
-    if local == 0:  # one build per node (ranks share the in-tree library)
-        G.build()
-    if dist:
-        dist.barrier()
-    if local != 0:
-        G.build()  # up to date by now: only loads the library
+    G.check_built()  # never compiles here (this process may already hold the GPU, e.g. under rocprofv3)
     pkg = G.load_package()
     N = pkg._native
     L = N.lib()

@@ -142,10 +142,12 @@ typedef struct ie_timing {
   uint64_t n_direct;     /* tiles that bypassed the LDS stages (long strings / many segments) */
   uint64_t n_polls;      /* look-back poll rounds that found a predecessor not yet published */
   uint64_t n_exact;      /* strings the level evaluator handed to the exact event evaluator */
+  uint64_t n_chain_fail; /* strings whose chain evaluation met a miss or an unspliceable hit */
 } ie_timing;
 
 /* ---- library ---- */
 int32_t ie_abi_version(void);
+const char* ie_build_id(void); /* hash of the sources the library was built from */
 const char* ie_last_error(void);
 int32_t ie_device_count(void);
 
@@ -163,6 +165,13 @@ void ie_exec_destroy(ie_exec* x);
 int ie_exec_sync(ie_exec* x);
 int ie_exec_set_timing(ie_exec* x, int32_t enabled);
 int ie_exec_timing(ie_exec* x, ie_timing* out); /* syncs */
+/* Exec options (defaults from the environment at ie_exec_create: IE_FAIL_COMMIT, IE_FAST,
+ * IE_DEBUG_NOEVAL). IE_OPT_FAIL_COMMIT: -1 adaptive (default), 0 / 1 forces the k_resolve variant
+ * (both give the reference's results; tests run under both). */
+#define IE_OPT_FAIL_COMMIT 1
+#define IE_OPT_FAST 2
+#define IE_OPT_DEBUG_NOEVAL 3
+int ie_exec_set_option(ie_exec* x, int32_t option, int64_t value);
 /* Literal-path scratch pool size. Setting it makes ie_interpolate_device fully asynchronous: it no
  * longer waits to check the pool's demand, and strings that ran out of it report IE_E_OVERFLOW. */
 int ie_exec_set_scratch(ie_exec* x, uint64_t bytes);

@@ -18,13 +18,14 @@ STATUS_NAMES = ["OK_STR", "OK_VALUE", "E_INTERP", "E_ASSERT_BRACES", "E_ASSERT_T
                 "E_UNHASHABLE", "E_RS_PANIC", "NEEDS_HOST", "DIVERGED", "E_OVERFLOW"]
 VID_NONE, VID_HHMM, VID_HHMMSS = 0xFFFFFFFF, 0xFFFFFFFE, 0xFFFFFFFD
 TABLE_HAS_INSERTS_DIR = 1
+OPT_FAIL_COMMIT, OPT_FAST, OPT_DEBUG_NOEVAL = 1, 2, 3
 
 # every symbol include/ie_amd.h declares (tests check the .so exports exactly these)
 EXPORTS = [
-    "ie_abi_version", "ie_last_error", "ie_device_count",
+    "ie_abi_version", "ie_build_id", "ie_last_error", "ie_device_count",
     "ie_table_build", "ie_table_free", "ie_table_entries", "ie_table_dialect",
     "ie_exec_create", "ie_exec_destroy", "ie_exec_sync", "ie_exec_set_timing", "ie_exec_timing",
-    "ie_exec_set_scratch",
+    "ie_exec_set_scratch", "ie_exec_set_option",
     "ie_dev_alloc", "ie_dev_free", "ie_copy_h2d", "ie_copy_d2h", "ie_memset_d", "ie_exec_mark",
     "ie_exec_elapsed",
     "ie_interpolate_device", "ie_interpolate_batch", "ie_interpolate",
@@ -60,7 +61,7 @@ class BatchRes(ctypes.Structure):
 class Timing(ctypes.Structure):
     _fields_ = [("resolve_ms", ctypes.c_float), ("complex_ms", ctypes.c_float),
                 ("total_ms", ctypes.c_float), ("n_complex", ctypes.c_uint64), ("n_direct", ctypes.c_uint64),
-                ("n_polls", ctypes.c_uint64), ("n_exact", ctypes.c_uint64)]
+                ("n_polls", ctypes.c_uint64), ("n_exact", ctypes.c_uint64), ("n_chain_fail", ctypes.c_uint64)]
 
 
 _lib = None
@@ -79,6 +80,7 @@ def lib():
     pvp = ctypes.POINTER(ctypes.c_void_p)
     sig = {
         "ie_abi_version": (i32, []),
+        "ie_build_id": (ctypes.c_char_p, []),
         "ie_last_error": (ctypes.c_char_p, []),
         "ie_device_count": (i32, []),
         "ie_table_build": (ctypes.c_int, [vp, u64, i32, ctypes.POINTER(Clock), u32, i32, pvp]),
@@ -91,6 +93,7 @@ def lib():
         "ie_exec_set_timing": (ctypes.c_int, [vp, i32]),
         "ie_exec_timing": (ctypes.c_int, [vp, ctypes.POINTER(Timing)]),
         "ie_exec_set_scratch": (ctypes.c_int, [vp, u64]),
+        "ie_exec_set_option": (ctypes.c_int, [vp, i32, ctypes.c_int64]),
         "ie_dev_alloc": (ctypes.c_int, [i32, u64, pvp]),
         "ie_dev_free": (None, [vp]),
         "ie_copy_h2d": (ctypes.c_int, [vp, vp, vp, u64]),
@@ -156,6 +159,9 @@ class Exec:
 
     def set_timing(self, on):
         check(lib().ie_exec_set_timing(self.h, 1 if on else 0), "ie_exec_set_timing")
+
+    def set_option(self, option, value):
+        check(lib().ie_exec_set_option(self.h, option, value), "ie_exec_set_option")
 
     def timing(self):
         t = Timing()

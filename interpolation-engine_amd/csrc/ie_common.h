@@ -5,8 +5,9 @@
 //                   its own entry (a perfect hash: each key has exactly ONE candidate entry).
 //                   Tables of up to kLdsPilotKeys keys use at most kLdsPilots groups, so the kernel
 //                   keeps the pilots in LDS (a lookup is then one memory round trip, not two)
-//   entries[m]      Entry (64 B): lengths, flags, arena offset, value id, and inline copies of the
-//                   key (<= 16 B) and splice text (<= 28 B), so a lookup is one 64-byte read;
+//   entries[m]      Entry (64 B): lengths, flags, arena offset, inline copies of the key (<= 16 B)
+//                   and splice text (<= 28 B), value id; a lookup reads the first 48 bytes (the
+//                   first 16 text bytes are all an inner nesting level needs);
 //                   m ~ 1.25 * keys (about 4 keys per group) or 2 * keys (the LDS pilot sizing)
 //   arena[...]      every splice text (4-byte aligned) followed by its key (4-byte aligned)
 // Lookup of key k: h = hash_key(k, seed); group g = ph_group(h, nb); slot = ph_slot(h, pilots[g]);
@@ -91,8 +92,8 @@ constexpr uint32_t kInlineText = 28;  // bytes of splice text kept inline in an 
 struct Entry {
   uint32_t key_len, text_len, flags, text_off;  // 16-byte word 0
   uint8_t key[kInlineKey];                      // word 1: zero padded
-  uint32_t vid;                                 // word 2.x
-  uint8_t text[kInlineText];                    // words 2.yzw, 3: zero padded
+  uint8_t text[kInlineText];                    // words 2, 3.xyz: zero padded (a <= 16 B text is word 2)
+  uint32_t vid;                                 // word 3.w
 };
 static_assert(sizeof(Entry) == 64, "Entry must stay one 64-byte block");
 

@@ -95,8 +95,13 @@ struct ie_exec {
   uint32_t lit_cap_max = 0;
   uint64_t pool_request = 256ull << 20;
   bool pool_fixed = false;  // set by ie_exec_set_scratch: the caller sized the pool, no wait/re-run
-  // fail commit (k_resolve<true>): chosen from the exact-path count of an earlier batch, read back
-  // asynchronously (never a wait): a stream with misses or type errors switches to it for good
+  // options (ie_exec_set_option); defaults read once from the environment at ie_exec_create
+  int32_t opt_fail_commit = -1;   // -1 adaptive, 0 / 1 forced (IE_FAIL_COMMIT)
+  uint32_t opt_fast = 1;          // 0: exact evaluator only (IE_FAST)
+  uint32_t opt_noeval = 0;        // diagnostic verbatim copy (IE_DEBUG_NOEVAL)
+  std::string stamps_path;        // diagnostic phase stamps (IE_DEBUG_STAMPS)
+  // fail commit (k_resolve<true>): chosen from the chain-failure count of an earlier batch, read
+  // back asynchronously (never a wait): > 0.1 % of a batch switches to it, a batch with none back
   bool fail_commit = false;
   bool stat_pending = false;
   uint64_t stat_n = 0;
@@ -235,7 +240,8 @@ int set_device(int32_t dev) {
 }
 
 // workspace for a batch of n strings. counters (u32 words): [0] tile ticket, [1] look-back error,
-// [2..3] pool bytes used (u64), [4..6] telemetry; zeroed with the tile states on every call.
+// [2..3] pool bytes used (u64), [4..8] telemetry (literal strings, direct tiles, look-back polls,
+// exact-path strings, chain failures); zeroed with the tile states on every call.
 int ensure_work(ie_exec* x, int op, uint64_t n) {
   const uint64_t tiles = (n + kBlock - 1) / kBlock + 1;
   IE_HIP(x->counters.ensure(64));
@@ -257,8 +263,8 @@ Work make_work(ie_exec* x, uint64_t* total) {
   W.err = (uint32_t*)x->counters.p + 1;
   W.stats = (uint32_t*)x->counters.p + 4;
   W.stamps = x->stamp_tiles ? (uint64_t*)x->stamps.p : nullptr;
-  W.debug_noeval = getenv("IE_DEBUG_NOEVAL") ? 1u : 0u;  // diagnostic hooks, see DESIGN.md
-  W.fast_mode = getenv("IE_FAST") ? (uint32_t)atoi(getenv("IE_FAST")) : 1u;  // 0: exact evaluator only
+  W.debug_noeval = x->opt_noeval;  // diagnostic hooks, see DESIGN.md
+  W.fast_mode = x->opt_fast;       // 0: exact evaluator only
   W.pool_used = (uint64_t*)x->counters.p + 1;
   W.tile_state = (uint64_t*)x->tile_state.p;
   W.pool = (uint8_t*)x->pool.p;
@@ -284,7 +290,7 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
   rc = ensure_work(x, op, n);
   if (rc) return rc;
   x->stamp_tiles = 0;
-  if (op == kOpInterp && getenv("IE_DEBUG_STAMPS")) {  // diagnostic build hook, see DESIGN.md
+  if (op == kOpInterp && !x->stamps_path.empty()) {  // diagnostic build hook, see DESIGN.md
     const uint64_t tiles = (n + kBlock - 1) / kBlock;
     IE_HIP(x->stamps.ensure(tiles * 128));
     x->stamp_tiles = tiles;
@@ -301,21 +307,24 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
   } else if (op == kOpInterp) {
     const uint64_t tiles = (n + kBlock - 1) / kBlock;
     IE_HIP(hipMemsetAsync(x->tile_state.p, 0, tiles * sizeof(uint64_t), st));
-    // fail commit: forced by IE_FAIL_COMMIT=0/1 (diagnostics, tests), else adaptive
-    const char* fc = getenv("IE_FAIL_COMMIT");
-    if (!fc && x->stat_pending && hipEventQuery(x->stat_ev) == hipSuccess) {
+    // fail commit: forced by the option (diagnostics, tests), else adaptive on the count of chain
+    // failures (misses / unspliceable hits) an earlier batch saw, in either variant
+    const bool forced = x->opt_fail_commit >= 0;
+    if (!forced && x->stat_pending && hipEventQuery(x->stat_ev) == hipSuccess) {
       x->stat_pending = false;
-      if ((uint64_t)*x->stat_host * 1024 > x->stat_n) x->fail_commit = true;  // > 0.1 % exact-path strings
+      const uint64_t fails = *x->stat_host;
+      if (fails * 1024 > x->stat_n) x->fail_commit = true;  // > 0.1 % of the strings
+      else if (fails == 0) x->fail_commit = false;
     }
-    W.fail_commit = fc ? (uint32_t)(atoi(fc) != 0) : (uint32_t)x->fail_commit;
+    W.fail_commit = forced ? (uint32_t)x->opt_fail_commit : (uint32_t)x->fail_commit;
     if (x->timing) IE_HIP(hipEventRecord(x->ev[1], st));
     IE_HIP(launch_resolve(B, W, t->dev, out->bytes, cap, st));
-    if (!fc && !W.fail_commit && !x->stat_pending) {
+    if (!forced && !x->stat_pending) {
       if (!x->stat_host) {
         IE_HIP(hipHostMalloc((void**)&x->stat_host, 4, hipHostMallocDefault));
         IE_HIP(hipEventCreateWithFlags(&x->stat_ev, hipEventDisableTiming));
       }
-      IE_HIP(hipMemcpyAsync(x->stat_host, W.stats + 3, 4, hipMemcpyDeviceToHost, st));
+      IE_HIP(hipMemcpyAsync(x->stat_host, W.stats + 4, 4, hipMemcpyDeviceToHost, st));
       IE_HIP(hipEventRecord(x->stat_ev, st));
       x->stat_pending = true;
       x->stat_n = n;
@@ -453,9 +462,16 @@ int run_host(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, const 
 
 }  // namespace
 
+#ifndef IE_BUILD_ID
+#define IE_BUILD_ID "unstamped-build!"
+#endif
+// the source id __graft_entry__.build() stamps into the library (found in the file by its marker)
+static const char kBuildId[] = "IE_BUILD_ID:" IE_BUILD_ID;
+
 extern "C" {
 
 int32_t ie_abi_version(void) { return IE_ABI_VERSION; }
+const char* ie_build_id(void) { return kBuildId + 12; }
 const char* ie_last_error(void) { return g_err.c_str(); }
 int32_t ie_device_count(void) {
   int n = 0;
@@ -705,6 +721,10 @@ int ie_exec_create(int32_t device, void* hip_stream, ie_exec** out) {
   if (rc) return rc;
   ie_exec* x = new ie_exec();
   x->device = device;
+  if (const char* e = getenv("IE_FAIL_COMMIT")) x->opt_fail_commit = atoi(e) != 0 ? 1 : 0;
+  if (const char* e = getenv("IE_FAST")) x->opt_fast = (uint32_t)atoi(e);
+  if (getenv("IE_DEBUG_NOEVAL")) x->opt_noeval = 1;
+  if (const char* e = getenv("IE_DEBUG_STAMPS")) x->stamps_path = e;
   if (hip_stream) {
     x->stream = (hipStream_t)hip_stream;
   } else {
@@ -749,11 +769,11 @@ int ie_exec_set_timing(ie_exec* x, int32_t enabled) {
 
 int ie_exec_timing(ie_exec* x, ie_timing* out) {
   if (!x || !out) return fail(IE_ERR_INVALID, "null argument");
-  if (x->stamp_tiles && getenv("IE_DEBUG_STAMPS")) {  // dump the last call's phase stamps
+  if (x->stamp_tiles && !x->stamps_path.empty()) {  // dump the last call's phase stamps
     IE_HIP(hipStreamSynchronize(x->stream));
     std::vector<uint64_t> h(x->stamp_tiles * 16);
     IE_HIP(hipMemcpy(h.data(), x->stamps.p, h.size() * 8, hipMemcpyDeviceToHost));
-    if (FILE* f = fopen(getenv("IE_DEBUG_STAMPS"), "wb")) {
+    if (FILE* f = fopen(x->stamps_path.c_str(), "wb")) {
       fwrite(h.data(), 8, h.size(), f);
       fclose(f);
     }
@@ -767,12 +787,13 @@ int ie_exec_timing(ie_exec* x, ie_timing* out) {
   out->resolve_ms = kern;   // the resolve (or escape) kernels
   out->complex_ms = 0.0f;   // literal strings are resolved inside k_resolve
   out->total_ms = setup + kern;
-  uint32_t st[4] = {0, 0, 0, 0};
-  if (x->counters.p) IE_HIP(hipMemcpy(st, (uint32_t*)x->counters.p + 4, 16, hipMemcpyDeviceToHost));
+  uint32_t st[5] = {0, 0, 0, 0, 0};
+  if (x->counters.p) IE_HIP(hipMemcpy(st, (uint32_t*)x->counters.p + 4, 20, hipMemcpyDeviceToHost));
   out->n_complex = st[0];
   out->n_direct = st[1];
   out->n_polls = st[2];
   out->n_exact = st[3];
+  out->n_chain_fail = st[4];
   return check_device_error(x);
 }
 
@@ -805,6 +826,25 @@ int ie_debug_probe(const ie_table* t, const char* key, uint64_t len, uint64_t* o
         memcmp(he[i].key, key, std::min<uint64_t>(len, kInlineKey)) == 0)
       out[10] = i;
   return IE_SUCCESS;
+}
+
+int ie_exec_set_option(ie_exec* x, int32_t option, int64_t value) {
+  if (!x) return fail(IE_ERR_INVALID, "null exec");
+  switch (option) {
+    case IE_OPT_FAIL_COMMIT:
+      if (value < -1 || value > 1) return fail(IE_ERR_INVALID, "fail commit must be -1, 0 or 1");
+      x->opt_fail_commit = (int32_t)value;
+      x->stat_pending = false;
+      return IE_SUCCESS;
+    case IE_OPT_FAST:
+      x->opt_fast = value ? 1u : 0u;
+      return IE_SUCCESS;
+    case IE_OPT_DEBUG_NOEVAL:
+      x->opt_noeval = value ? 1u : 0u;
+      return IE_SUCCESS;
+    default:
+      return fail(IE_ERR_INVALID, "unknown exec option");
+  }
 }
 
 int ie_exec_set_scratch(ie_exec* x, uint64_t bytes) {

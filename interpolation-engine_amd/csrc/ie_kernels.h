@@ -12,7 +12,7 @@ constexpr int kMaxDepth = 6;         // fast-path nesting limit (deeper: literal
 constexpr int kKeyCap = 32;          // exact-evaluator key bytes per lane (longer keys: literal path)
 
 constexpr int kTileBytes = 17664;    // LDS input stage; larger tiles read global memory directly
-constexpr int kStageBytes = 20480;   // LDS output stage; a tile that does not fit goes out in halves
+constexpr int kStageBytes = 20480;   // LDS output stage; a larger tile's lanes store their own bytes
 
 enum { kOpInterp = 0, kOpUnescape = 1, kOpEscape = 2 };
 
@@ -31,7 +31,8 @@ struct Work {
   uint32_t* tile_ticket; // 1   dynamic tile ids (zeroed per call)
   uint64_t* tile_state;  // tiles: look-back words (zeroed per call)
   uint32_t* err;         // 1   look-back timeout flag
-  uint32_t* stats;       // 4   telemetry: literal strings, direct tiles, look-back polls, exact-path strings
+  uint32_t* stats;       // 5   telemetry: literal strings, direct tiles, look-back polls, exact-path
+                         //     strings, chain failures (the adaptive variant choice)
   uint64_t* stamps;      // diagnostic (IE_DEBUG_STAMPS): 8 words per tile, or null
   uint32_t debug_noeval; // diagnostic (IE_DEBUG_NOEVAL): copy strings verbatim (pipeline floor)
   uint32_t fast_mode;    // level evaluator: 1 on (default), 0 off; diagnostics 2 = parse only, 3 = no probes

@@ -1,9 +1,12 @@
 // ie_resolve.hip — k_resolve: interpolate_inserts (py:497-541 / rust-project/src/interp.rs:31-89)
 // over a packed batch in ONE pass over HBM.
 //
-// One 256-lane workgroup per tile of 256 consecutive strings; tiles are taken from an atomic
-// ticket (so every tile a workgroup waits on is already running) and chained with a decoupled
-// look-back over 8-byte {flag, value} words published by agent-scope atomics. Per tile:
+// One 256-lane workgroup per tile of 256 consecutive strings; the tile is the workgroup index and
+// tiles are chained with a decoupled look-back over 8-byte {flag, value} words published by
+// agent-scope atomics. Forward progress relies on the dispatcher starting workgroups in index
+// order (observed on gfx950; HIP does not promise it): a tile only waits on lower-numbered tiles,
+// which are then already resident. The wait is bounded (10 s): a violation sets the exec's error
+// word, which ie_exec_sync / the host APIs report as IE_ERR_TIMEOUT. Per tile:
 //   1. stage the tile's input bytes in LDS (16-byte loads) and classify every 16-byte chunk into
 //      an open-brace and a close-brace mask (plus one "odd byte" bit per chunk: '\' or 0xE3);
 //   2. every lane evaluates its string. Clean strings (no odd byte, brace pairs forming chains
@@ -29,6 +32,10 @@
 #include "ie_device.h"
 #include "ie_kernels.h"
 #include "ie_literal.h"
+
+#ifndef IE_WAVES_PER_EU
+#define IE_WAVES_PER_EU 3
+#endif
 
 namespace ie {
 
@@ -556,7 +563,9 @@ __device__ __forceinline__ void probe_load(const DevTable& T, uint32_t slot, Pro
   P.q0 = gld4(e);
   P.q1 = gld4(e + 1);
   P.q2 = gld4(e + 2);
+#ifndef IE_EXP_NOTT
   P.q3 = gld4(e + 3);
+#endif
 }
 
 __device__ __forceinline__ uint32_t w_max32(uint32_t v) {
@@ -574,7 +583,7 @@ struct TopText {
 template <bool FAILC>
 __device__ bool eval_chains(const DevTable& T, const lds_u16* pil, const lds_u8* tile, uint32_t p0, uint32_t n, const lds_u32* cm,
                             const lds_u32* oddbits, const lds_u32* escbits, bool active, const ChainLds& CL, Desc& d,
-                            TopText& tt, uint32_t& out_len, uint8_t& status, uint64_t* stamp) {
+                            TopText& tt, uint32_t& out_len, uint8_t& status, bool& chain_fail, uint64_t* stamp) {
   bool ok = active && n <= kChainMax;
   const lds_u8* s = tile + p0;
   // ---- 1. the string's open / close events as 128-bit windows ----
@@ -767,7 +776,7 @@ __device__ bool eval_chains(const DevTable& T, const lds_u16* pil, const lds_u8*
       if (__any(on[c])) probe_load(T, slot[c], P[c]);
     }
     if (stamp && threadIdx.x == 0 && r < 3) {  // diagnostic: entries arrived
-      asm volatile("" ::"v"(P[0].q0.x), "v"(P[1].q0.x), "v"(P[2].q0.x), "v"(P[0].q3.x));
+      asm volatile("" ::"v"(P[0].q0.x), "v"(P[1].q0.x), "v"(P[2].q0.x), "v"(P[0].q2.x));
       stamp[3 + 2 * r] = __builtin_amdgcn_s_memrealtime();
     }
 #pragma unroll
@@ -781,7 +790,9 @@ __device__ bool eval_chains(const DevTable& T, const lds_u16* pil, const lds_u8*
       // a miss (no inserts-dir: py:465 / interp.rs:136) or a hit that cannot be spliced
       // (py:530 / interp.rs:76-79) fails this pair; a hit on a value needing care, or a miss that
       // the inserts-dir might resolve, goes to the exact evaluator
-      const bool fail = FAILC && on[c] && ((!hit && !(T.flags & TF_HAS_DIR)) || (hit && !(flags & EF_SPLICE_OK)));
+      const bool would_fail = on[c] && ((!hit && !(T.flags & TF_HAS_DIR)) || (hit && !(flags & EF_SPLICE_OK)));
+      chain_fail |= would_fail;  // the adaptive variant choice counts these (either variant)
+      const bool fail = FAILC && would_fail;
       if (on[c] && !good && !fail) ok = false;
       if (fail) {
         const uint32_t st = hit ? (uint32_t)IE_E_ASSERT_TYPE : (uint32_t)IE_E_INTERP;
@@ -791,7 +802,7 @@ __device__ bool eval_chains(const DevTable& T, const lds_u16* pil, const lds_u8*
       const bool top = r + 1 == cdep[c];
       if (on[c] && good && !top) {  // inner level: this text goes into the parent's key
         if (tlen > 16u) ok = false;
-        ct[c][0] = E.q2.y, ct[c][1] = E.q2.z, ct[c][2] = E.q2.w, ct[c][3] = E.q3.x;
+        ct[c][0] = E.q2.x, ct[c][1] = E.q2.y, ct[c][2] = E.q2.z, ct[c][3] = E.q2.w;
         ctl[c] = tlen;
         co_[c] = open[c];
         cl_[c] = close[c];
@@ -802,8 +813,10 @@ __device__ bool eval_chains(const DevTable& T, const lds_u16* pil, const lds_u8*
         d.vs[c] = src;
         d.open[c] = open[c];
         d.close[c] = close[c];
-        tt.w[c][0] = E.q2.y, tt.w[c][1] = E.q2.z, tt.w[c][2] = E.q2.w, tt.w[c][3] = E.q3.x;
-        tt.w[c][4] = E.q3.y, tt.w[c][5] = E.q3.z, tt.w[c][6] = E.q3.w, tt.w[c][7] = 0;
+#ifndef IE_EXP_NOTT
+        tt.w[c][0] = E.q2.x, tt.w[c][1] = E.q2.y, tt.w[c][2] = E.q2.z, tt.w[c][3] = E.q2.w;
+        tt.w[c][4] = E.q3.x, tt.w[c][5] = E.q3.y, tt.w[c][6] = E.q3.z, tt.w[c][7] = 0;
+#endif
         vsum += tlen;
         span += close[c] - open[c] + 1;
       }
@@ -978,7 +991,7 @@ __device__ __forceinline__ uint4 bytes_at(u32x4 x, u32x4 y, uint32_t r) {
 // FAILC: chain failures commit in the chain evaluator (else they take the exact evaluator). Both
 // give the reference's results; the host picks per batch stream (ie_host.cpp, "fail commit").
 template <bool FAILC>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_resolve(Batch B, Work W, DevTable T, uint8_t* out,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES_PER_EU))) void k_resolve(Batch B, Work W, DevTable T, uint8_t* out,
                                                     uint64_t cap) {
   __shared__ __attribute__((aligned(16))) uint8_t s_in[kTileBytes + 48];
   __shared__ __attribute__((aligned(16))) uint8_t s_u[kUnionLds];
@@ -1072,7 +1085,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
   for (int q = 0; q < kMaxTop; q++) d.open[q] = d.close[q] = d.vk[q] = d.vs[q] = 0;
   const uint8_t* s = nullptr;
   const uint32_t p0 = shift + (uint32_t)(so - lo);
-  bool pend = false, fast_lane = false;
+  bool pend = false, fast_lane = false, chain_fail = false;
   {
     uint8_t st = IE_OK_STR;
     uint32_t olen = 0, vid = IE_VID_NONE;
@@ -1090,11 +1103,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
     } else if (staged && W.fast_mode) {
       const ChainLds CL{(lds_u8*)(s_u + tid * kKeyCap), (lds_u64*)(lds_u8*)(s_u + kKbufLds) + tid};
       const bool fast = eval_chains<FAILC>(T, lds_pil ? (const lds_u16*)s_pil : nullptr, (const lds_u8*)s_in, p0, (uint32_t)sn, s_cm,
-                                    s_odd, s_esc, active, CL, d, tt, olen, r,
+                                    s_odd, s_esc, active, CL, d, tt, olen, r, chain_fail,
                                     stamp_row ? stamp_row + 6 : nullptr);
       slow = active && !fast;
       fast_lane = fast;
     }
+    const uint64_t fail_m = __ballot(chain_fail);
+    if (fail_m && lane == 0) atomicAdd(W.stats + 4, (uint32_t)__popcll(fail_m));  // misses: rare
     // the rest: the exact evaluator (scratch: the lane's own chain-evaluator columns)
     const uint64_t slow_m = __ballot(slow);
     if (slow_m) {
@@ -1103,10 +1118,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
       lds_u32* const stk = (lds_u32*)(lds_u8*)(s_u + kKbufLds) + tid;
       uint32_t o2 = 0;
       uint8_t r2;
+#ifdef IE_EXP_NOEXACT
+      r2 = kStatusPending;
+#else
       if (staged)
         r2 = eval_exact<true>(T, Src<true>{s}, (uint32_t)sn, slow, kb, stk, d, o2, vid);
       else
         r2 = eval_exact<false>(T, Src<false>{s}, (uint32_t)sn, slow, kb, stk, d, o2, vid);
+#endif
       if (slow) r = r2, olen = o2;
     }
     if (active) st = r;
@@ -1132,7 +1151,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
     if (lane == 0) pbase = atomicAdd((unsigned long long*)W.pool_used, (unsigned long long)(4 * rcap));
     pbase = __shfl(pbase, 0, 64);
     LitOut r{IE_E_OVERFLOW, 0, 0, IE_VID_NONE};
+#ifndef IE_EXP_NOLIT
     if (pbase + 4 * rcap <= W.pool_bytes)
+#else
+    if (false)
+#endif
       r = w_literal(T, B.bytes + po, pn, W.pool + pbase, rcap, pbase, W.lit_cap_max != 0);
     if (r.status == IE_OK_STR && (r.res_len > kLenMask || (r.res_off >> 4) > 0xFFFFFFFFull))
       r.status = IE_E_OVERFLOW;
@@ -1173,13 +1196,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
     // (the chain evaluator kept its own from the lookup)
 #pragma unroll
     for (int j = 0; j < kMaxTop; j++) {
-      const bool need = mine && !fast_lane && (uint32_t)j < d.ntop && (d.vk[j] >> 30) == kValEntry;
+      #ifdef IE_EXP_NOTT
+      const bool need = mine && (uint32_t)j
+#else
+      const bool need = mine && !fast_lane && (uint32_t)j
+#endif
+                         < d.ntop && (d.vk[j] >> 30) == kValEntry;
       if (__any(need)) {
         const uint4* tp = (const uint4*)(T.entries + (need ? d.vs[j] : 0u)) + 2;
         const uint4 t2 = gld4(tp), t3 = gld4(tp + 1);
         if (need) {
-          tt.w[j][0] = t2.y, tt.w[j][1] = t2.z, tt.w[j][2] = t2.w, tt.w[j][3] = t3.x;
-          tt.w[j][4] = t3.y, tt.w[j][5] = t3.z, tt.w[j][6] = t3.w, tt.w[j][7] = 0;
+          tt.w[j][0] = t2.x, tt.w[j][1] = t2.y, tt.w[j][2] = t2.z, tt.w[j][3] = t2.w;
+          tt.w[j][4] = t3.x, tt.w[j][5] = t3.y, tt.w[j][6] = t3.z, tt.w[j][7] = 0;
         }
       }
     }

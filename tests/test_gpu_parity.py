@@ -31,12 +31,14 @@ def run_product(table_dict, strings, dialect="py", has_dir=False):
 
 
 @pytest.fixture(params=["0", "1"], ids=["chain-fail-exact", "chain-fail-commit"])
-def fail_commit(request):
+def fail_commit(request, monkeypatch):
     """Both k_resolve variants: chain failures sent to the exact evaluator, or committed in the
-    chain evaluator (the library picks one adaptively; IE_FAIL_COMMIT forces it)."""
-    os.environ["IE_FAIL_COMMIT"] = request.param
+    chain evaluator (the library picks one adaptively; IE_FAIL_COMMIT / IE_OPT_FAIL_COMMIT force it).
+    Execs read the environment when they are created; the mirror's cached exec is set directly."""
+    monkeypatch.setenv("IE_FAIL_COMMIT", request.param)
+    PKG.get_exec(0).set_option(N.OPT_FAIL_COMMIT, int(request.param))
     yield request.param
-    del os.environ["IE_FAIL_COMMIT"]
+    PKG.get_exec(0).set_option(N.OPT_FAIL_COMMIT, -1)
 
 
 def compare_with_oracle(table_dict, strings, dialect="py", has_dir=False):
@@ -539,9 +541,11 @@ def test_escape_kernels_on_a_ragged_batch(op):
         assert b1[int(o1[k]):int(o1[k + 1])].decode() == want, k
 
 
-def test_fail_commit_is_adopted_after_a_batch_with_misses():
-    """Adaptive variant choice: an exec starts with chain failures on the exact evaluator and
-    switches once an earlier batch showed exact-path strings; results are identical throughout."""
+def test_fail_commit_is_adopted_after_a_batch_with_misses(monkeypatch):
+    """Adaptive variant choice: an exec starts with chain failures on the exact evaluator, switches
+    once an earlier batch showed chain failures, and switches back after a batch without any;
+    results are identical throughout."""
+    monkeypatch.delenv("IE_FAIL_COMMIT", raising=False)
     h, kvp, nkv = _synth(4)
     table = _table_from_kv(kvp, nkv)
     x = N.Exec(0)
@@ -560,6 +564,18 @@ def test_fail_commit_is_adopted_after_a_batch_with_misses():
     for k in (1, 2):
         assert np.array_equal(runs[k][1], runs[0][1]) and np.array_equal(runs[k][2], runs[0][2])
         assert np.array_equal(runs[k][3], runs[0][3])
+    # a stream without chain failures (config 3) switches back to the lean variant
+    h3, kvp3, nkv3 = _synth(3)
+    t3 = _table_from_kv(kvp3, nkv3)
+    d_off3, d_bytes3, _ = _device_strings(x, h3, 0, n)
+    fails = []
+    for _ in range(3):
+        x.set_timing(True)
+        _device_run(x, t3, d_bytes3, d_off3, n)
+        fails.append(int(x.timing().n_chain_fail))
+        x.set_timing(False)
+    assert fails == [0, 0, 0]
+    N.lib().ie_table_free(t3)
     N.lib().ie_table_free(table)
 
 
