@@ -154,8 +154,19 @@ int32_t ie_device_count(void);
 /* ---- table: get_interpdata (py:430-467 / interp.rs:91-137) ---- */
 int ie_table_build(const ie_kv* kv, uint64_t n, int32_t dialect, const ie_clock* now,
                    uint32_t flags, int32_t device, ie_table** out);
+/* A table set: n_tables inserts dicts in one device table, table t = kv[kv_start[t] .. kv_start[t+1]).
+ * Strings pick their dict with a table id (ie_interpolate_*_ids); value ids index kv as a whole.
+ * This is SURVEY §8b's `tables[] + table_id[]` batch for config 5's forked states (one dict per
+ * state, the per-task map clone of rust-project/src/runtime.rs:700-701 made unnecessary) and for
+ * replace_map's `inserts | extra_inserts` (py:1734). ie_table_build is the one-dict case. */
+int ie_table_set_build(const ie_kv* kv, const uint64_t* kv_start, uint32_t n_tables, int32_t dialect,
+                       const ie_clock* now, uint32_t flags, int32_t device, ie_table** out);
 void ie_table_free(ie_table* t);
+/* Re-read the clock (py:433-436) without a rebuild: rewrites the 'HH:MM' / 'HH:MM:SS' entries in
+ * place. IE_ERR_INVALID when a brace-bearing value pre-resolved at build read the clock (rebuild). */
+int ie_table_set_clock(ie_table* t, const ie_clock* now);
 uint64_t ie_table_entries(const ie_table* t);
+uint32_t ie_table_tables(const ie_table* t);
 int32_t ie_table_dialect(const ie_table* t);
 
 /* ---- exec context ---- */
@@ -202,6 +213,12 @@ int ie_interpolate_device(ie_exec* x, const ie_table* t, const uint8_t* d_bytes,
                           const uint64_t* d_offsets, uint64_t n, const ie_dev_out* out);
 int ie_interpolate_batch(ie_exec* x, const ie_table* t, const uint8_t* bytes,
                          const uint64_t* offsets, uint64_t n, ie_batch** out);
+/* The same over a table set: string i resolves against table table_id[i] (_device: a device array;
+ * an id beyond the set finds no key, so such strings report IE_E_INTERP; _batch checks the ids). */
+int ie_interpolate_device_ids(ie_exec* x, const ie_table* t, const uint32_t* d_table_id, const uint8_t* d_bytes,
+                              const uint64_t* d_offsets, uint64_t n, const ie_dev_out* out);
+int ie_interpolate_batch_ids(ie_exec* x, const ie_table* t, const uint32_t* table_id, const uint8_t* bytes,
+                             const uint64_t* offsets, uint64_t n, ie_batch** out);
 /* scalar drop-in: one string (a batch of one on the device) */
 int ie_interpolate(ie_exec* x, const ie_table* t, const char* s, uint64_t len, ie_batch** out);
 

@@ -7,11 +7,14 @@ see __graft_entry__.load_package().
 from . import _native  # noqa: F401
 from .interpolation_engine import (  # noqa: F401
     InsertsTable,
+    InsertsTableSet,
     InterpolationException,
+    VersionedInserts,
     get_interpdata,
     get_simple_insertkey,
     interpolate_batch,
     interpolate_inserts,
+    interpolate_states,
     recursive_escape,
     recursive_interpolate,
     recursive_unescape,

@@ -23,12 +23,14 @@ OPT_FAIL_COMMIT, OPT_FAST, OPT_DEBUG_NOEVAL = 1, 2, 3
 # every symbol include/ie_amd.h declares (tests check the .so exports exactly these)
 EXPORTS = [
     "ie_abi_version", "ie_build_id", "ie_last_error", "ie_device_count",
-    "ie_table_build", "ie_table_free", "ie_table_entries", "ie_table_dialect",
+    "ie_table_build", "ie_table_set_build", "ie_table_set_clock", "ie_table_free", "ie_table_entries", "ie_table_tables",
+    "ie_table_dialect",
     "ie_exec_create", "ie_exec_destroy", "ie_exec_sync", "ie_exec_set_timing", "ie_exec_timing",
     "ie_exec_set_scratch", "ie_exec_set_option",
     "ie_dev_alloc", "ie_dev_free", "ie_copy_h2d", "ie_copy_d2h", "ie_memset_d", "ie_exec_mark",
     "ie_exec_elapsed",
-    "ie_interpolate_device", "ie_interpolate_batch", "ie_interpolate",
+    "ie_interpolate_device", "ie_interpolate_batch", "ie_interpolate", "ie_interpolate_device_ids",
+    "ie_interpolate_batch_ids",
     "ie_unescape_device", "ie_escape_device", "ie_unescape_batch", "ie_escape_batch",
     "ie_batch_free", "ie_simple_insertkey",
     "ie_synth_create", "ie_synth_free", "ie_synth_kv", "ie_synth_strings_host",
@@ -84,7 +86,10 @@ def lib():
         "ie_last_error": (ctypes.c_char_p, []),
         "ie_device_count": (i32, []),
         "ie_table_build": (ctypes.c_int, [vp, u64, i32, ctypes.POINTER(Clock), u32, i32, pvp]),
+        "ie_table_set_build": (ctypes.c_int, [vp, vp, u32, i32, ctypes.POINTER(Clock), u32, i32, pvp]),
         "ie_table_free": (None, [vp]),
+        "ie_table_set_clock": (ctypes.c_int, [vp, ctypes.POINTER(Clock)]),
+        "ie_table_tables": (u32, [vp]),
         "ie_table_entries": (u64, [vp]),
         "ie_table_dialect": (i32, [vp]),
         "ie_exec_create": (ctypes.c_int, [i32, vp, pvp]),
@@ -104,6 +109,8 @@ def lib():
         "ie_interpolate_device": (ctypes.c_int, [vp, vp, vp, vp, u64, ctypes.POINTER(DevOut)]),
         "ie_interpolate_batch": (ctypes.c_int, [vp, vp, vp, vp, u64, ctypes.POINTER(ctypes.POINTER(BatchRes))]),
         "ie_interpolate": (ctypes.c_int, [vp, vp, ctypes.c_char_p, u64, ctypes.POINTER(ctypes.POINTER(BatchRes))]),
+        "ie_interpolate_device_ids": (ctypes.c_int, [vp, vp, vp, vp, vp, u64, ctypes.POINTER(DevOut)]),
+        "ie_interpolate_batch_ids": (ctypes.c_int, [vp, vp, vp, vp, vp, u64, ctypes.POINTER(ctypes.POINTER(BatchRes))]),
         "ie_unescape_device": (ctypes.c_int, [vp, vp, vp, u64, ctypes.POINTER(DevOut)]),
         "ie_escape_device": (ctypes.c_int, [vp, vp, vp, u64, ctypes.POINTER(DevOut)]),
         "ie_unescape_batch": (ctypes.c_int, [vp, vp, vp, u64, ctypes.POINTER(ctypes.POINTER(BatchRes))]),

@@ -10,8 +10,9 @@
 //                   first 16 text bytes are all an inner nesting level needs);
 //                   m ~ 1.25 * keys (about 4 keys per group) or 2 * keys (the LDS pilot sizing)
 //   arena[...]      every splice text (4-byte aligned) followed by its key (4-byte aligned)
-// Lookup of key k: h = hash_key(k, seed); group g = ph_group(h, nb); slot = ph_slot(h, pilots[g]);
-// the key is present iff entries[slot] holds it (full byte compare: exact, never a hash test).
+// Lookup of key k in table t of the set: h = hash_key(k, seed, t); group g = ph_group(h, nb);
+// slot = ph_slot(h, pilots[g]); the key is present iff entries[slot] holds it for table t (full
+// byte compare and table index compare: exact, never a hash test).
 #pragma once
 #include <stdint.h>
 
@@ -33,14 +34,18 @@ IE_HD uint64_t hash_word(uint64_t h, uint32_t w) {
   return ((uint64_t)a << 32) | b;
 }
 
-IE_HD uint64_t hash_init(uint32_t n, uint64_t seed) {
-  return seed ^ (((uint64_t)n << 32) | (uint64_t)(n * 0x85EBCA77u));
+// start of a key's hash: the table seed, the key length and the index of the table the key belongs
+// to in a table set (0 for a single table), so one device table can hold many inserts dicts
+IE_HD uint64_t hash_init(uint32_t n, uint64_t seed, uint32_t tid) {
+  // the table index enters both lanes: equal keys of different tables must differ in the high
+  // lane (their pilot group) and in the low lane (their slot under a shared pilot)
+  return seed ^ (((uint64_t)(n ^ (tid << 11)) << 32) | (uint64_t)((n * 0x85EBCA77u) ^ tid));
 }
 
 // hash of n key bytes (any address space via the byte reader)
 template <class ByteAt>
-IE_HD uint64_t hash_key(uint32_t n, ByteAt at, uint64_t seed) {
-  uint64_t h = hash_init(n, seed);
+IE_HD uint64_t hash_key(uint32_t n, ByteAt at, uint64_t seed, uint32_t tid) {
+  uint64_t h = hash_init(n, seed, tid);
   for (uint32_t j = 0; j < n; j += 4) {
     uint32_t w = 0;
     for (uint32_t b = 0; b < 4 && j + b < n; b++) w |= (uint32_t)at(j + b) << (8 * b);
@@ -82,6 +87,9 @@ enum : uint32_t {
   EF_RAWALT = 1u << 8,         // splice text pre-resolved at build; the raw value sits before it
                                // in the arena as [raw text, 4-aligned][u32 raw length][text]
 };
+// bits 12-31 of Entry.flags: the index of the entry's table within its table set
+constexpr uint32_t kTidShift = 12;
+constexpr uint32_t kMaxTables = 1u << (32 - kTidShift);
 
 // DevTable.flags
 enum : uint32_t { TF_HAS_DIR = 1u };
@@ -108,6 +116,7 @@ struct DevTable {
   uint32_t m;     // entries
   uint32_t nb;    // pilot groups
   uint32_t n_entries;
+  uint32_t n_tables;  // inserts dicts in the set (strings pick one with Batch.table_id)
   uint32_t dialect;
   uint32_t flags;
   uint64_t maxtext;

@@ -93,19 +93,19 @@ __device__ __forceinline__ bool long_key_eq(const DevTable& T, uint4 q0, const u
   return eq;
 }
 
-__device__ __forceinline__ bool entry_head_ok(uint4 q0, uint32_t klen) {
-  return ((q0.z & EF_OCCUPIED) != 0) & (q0.x == klen);
+__device__ __forceinline__ bool entry_head_ok(uint4 q0, uint32_t klen, uint32_t tid) {
+  return ((q0.z & EF_OCCUPIED) != 0) & (q0.x == klen) & ((q0.z >> kTidShift) == tid);
 }
 
-// Lookup of a key whose bytes are at `key` (generic pointer: LDS or global). Returns the entry
-// index or -1.
-__device__ int32_t find_bytes(const DevTable& T, const uint8_t* key, uint32_t klen, Hit& h) {
-  const uint64_t hash = hash_key(klen, [&](uint32_t j) { return key[j]; }, T.seed);
+// Lookup of a key whose bytes are at `key` (generic pointer: LDS or global) in table `tid` of the
+// set. Returns the entry index or -1.
+__device__ int32_t find_bytes(const DevTable& T, uint32_t tid, const uint8_t* key, uint32_t klen, Hit& h) {
+  const uint64_t hash = hash_key(klen, [&](uint32_t j) { return key[j]; }, T.seed, tid);
   const uint32_t slot = ph_lookup_slot(T, hash);
   const Entry* e = T.entries + slot;
   const uint4 q0 = gld4((const uint4*)e), q1 = gld4((const uint4*)e + 1);
   const uint32_t kw[4] = {q1.x, q1.y, q1.z, q1.w};
-  bool eq = entry_head_ok(q0, klen);
+  bool eq = entry_head_ok(q0, klen, tid);
   const uint32_t ni = klen < kInlineKey ? klen : kInlineKey;
   for (uint32_t j = 0; j < ni; j++) eq &= (uint8_t)(kw[j >> 2] >> (8 * (j & 3))) == key[j];
   if (eq && klen > kInlineKey) eq = long_key_eq(T, q0, key, klen);
@@ -115,8 +115,9 @@ __device__ int32_t find_bytes(const DevTable& T, const uint8_t* key, uint32_t kl
 
 // Lookup of a key held as dwords at a 4-byte aligned address (generic pointer),
 // klen <= kInlineKey: hashed word-wise, compared against the entry's inline key in registers.
-__device__ __forceinline__ int32_t find_small(const DevTable& T, const uint32_t* key32, uint32_t klen, Hit& h) {
-  uint64_t hash = hash_init(klen, T.seed);
+__device__ __forceinline__ int32_t find_small(const DevTable& T, uint32_t tid, const uint32_t* key32, uint32_t klen,
+                                             Hit& h) {
+  uint64_t hash = hash_init(klen, T.seed, tid);
   uint32_t kw[4];
 #pragma unroll
   for (int d = 0; d < 4; d++) {
@@ -131,7 +132,7 @@ __device__ __forceinline__ int32_t find_small(const DevTable& T, const uint32_t*
   const uint32_t slot = ph_lookup_slot(T, hash);
   const Entry* e = T.entries + slot;
   const uint4 q0 = gld4((const uint4*)e), q1 = gld4((const uint4*)e + 1);
-  const bool eq = entry_head_ok(q0, klen) & (q1.x == kw[0]) & (q1.y == kw[1]) & (q1.z == kw[2]) & (q1.w == kw[3]);
+  const bool eq = entry_head_ok(q0, klen, tid) & (q1.x == kw[0]) & (q1.y == kw[1]) & (q1.z == kw[2]) & (q1.w == kw[3]);
   h = Hit{q0.y, q0.w, gld(&e->vid), q0.z};
   return eq ? (int32_t)slot : -1;
 }
@@ -148,7 +149,7 @@ __device__ uint8_t missing_status(const DevTable& T, const uint8_t* k, uint32_t 
 
 // lookup with the RAW value of bucket `prev` as the key (nested whole-string form,
 // py:511-512: the object itself; interp.rs:47-48: value_to_string of it)
-__device__ int32_t find_raw(const DevTable& T, const Hit& prev, uint8_t& st, Hit& h) {
+__device__ int32_t find_raw(const DevTable& T, uint32_t tid, const Hit& prev, uint8_t& st, Hit& h) {
   if (!(prev.flags & EF_KEY_STR)) {
     st = (prev.flags & EF_KEY_UNHASHABLE) ? (uint8_t)IE_E_UNHASHABLE
          : (T.flags & TF_HAS_DIR)         ? (uint8_t)IE_NEEDS_HOST
@@ -161,7 +162,7 @@ __device__ int32_t find_raw(const DevTable& T, const Hit& prev, uint8_t& st, Hit
     kl = gld((const uint32_t*)(k - 4));
     k -= 4 + ((kl + 3u) & ~3u);
   }
-  const int32_t b = find_bytes(T, k, kl, h);
+  const int32_t b = find_bytes(T, tid, k, kl, h);
   if (b < 0) st = missing_status(T, k, kl);
   return b;
 }

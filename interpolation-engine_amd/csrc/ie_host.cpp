@@ -75,7 +75,11 @@ struct ie_table {
   int32_t dialect = 0;
   uint32_t flags = 0;
   uint64_t n_entries = 0;
+  uint32_t n_tables = 1;  // inserts dicts in the set
   DevTable dev{};
+  // the clock entries ('HH:MM', 'HH:MM:SS' of every table): slot, host copy (ie_table_set_clock)
+  std::vector<std::pair<uint32_t, Entry>> clock_entries;
+  bool clock_dependent = false;  // a pre-resolved value read the clock: a new clock needs a rebuild
   DevBuf entries, pilots, arena;
   ~ie_table() {
     entries.release();
@@ -110,14 +114,14 @@ struct ie_exec {
   // workspace
   DevBuf counters, tile_state, pool, out_len, tile_sum, tile_base;
   // host-API staging
-  DevBuf in_bytes, in_off, o_bytes, o_off, o_status, o_vid, o_total;
+  DevBuf in_bytes, in_off, in_tid, o_bytes, o_off, o_status, o_vid, o_total;
   // synth scratch
   DevBuf s_lens, s_part;
   DevBuf stamps;        // diagnostic phase stamps (env IE_DEBUG_STAMPS=<file>)
   uint64_t stamp_tiles = 0;
   ~ie_exec() {
     for (DevBuf* b : {&counters, &tile_state, &pool, &out_len, &tile_sum, &tile_base, &in_bytes,
-                      &in_off, &o_bytes, &o_off, &o_status, &o_vid, &o_total, &s_lens, &s_part, &stamps})
+                      &in_off, &in_tid, &o_bytes, &o_off, &o_status, &o_vid, &o_total, &s_lens, &s_part, &stamps})
       b->release();
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
@@ -181,8 +185,8 @@ uint64_t fmix64_host(uint64_t k) {
   return k;
 }
 
-uint64_t key_hash(const std::string_view k, uint64_t seed) {
-  return hash_key((uint32_t)k.size(), [&](uint32_t j) { return (uint8_t)k[j]; }, seed);
+uint64_t key_hash(const std::string_view k, uint64_t seed, uint32_t tid) {
+  return hash_key((uint32_t)k.size(), [&](uint32_t j) { return (uint8_t)k[j]; }, seed, tid);
 }
 
 // Perfect-hash placement (hash-and-displace): keys are grouped by ph_group (about 4 per group);
@@ -277,7 +281,7 @@ Work make_work(ie_exec* x, uint64_t* total) {
 }
 
 int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, const uint64_t* d_off,
-               uint64_t n, const ie_dev_out* out) {
+               uint64_t n, const ie_dev_out* out, const uint32_t* d_tid = nullptr) {
   if (!x || !d_off || !out || !out->offsets || !out->status || !out->total || (op == kOpInterp && !t))
     return fail(IE_ERR_INVALID, "null argument");
   if (n && !d_bytes) return fail(IE_ERR_INVALID, "null input bytes");
@@ -295,7 +299,7 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
     IE_HIP(x->stamps.ensure(tiles * 128));
     x->stamp_tiles = tiles;
   }
-  Batch B{d_bytes, d_off, n, out->offsets, out->status, out->value_id};
+  Batch B{d_bytes, d_off, n, out->offsets, out->status, out->value_id, d_tid};
   Work W = make_work(x, out->total);
   hipStream_t st = x->stream;
   const uint64_t cap = out->bytes ? out->bytes_cap : 0;
@@ -352,10 +356,19 @@ int check_device_error(ie_exec* x) {
 // synchronous host batch: H2D, run, D2H; grows the output buffer and re-runs overflowed
 // literal-path strings with the full working space until every status is final.
 int run_host(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, const uint64_t* offsets,
-             uint64_t n, ie_batch** outp) {
+             uint64_t n, ie_batch** outp, const uint32_t* table_id = nullptr) {
   if (!x || !outp || (n && (!bytes || !offsets))) return fail(IE_ERR_INVALID, "null argument");
   int rc = set_device(x->device);
   if (rc) return rc;
+  if (table_id && t)
+    for (uint64_t i = 0; i < n; i++)
+      if (table_id[i] >= t->n_tables) return fail(IE_ERR_INVALID, "table id beyond the table set");
+  const uint32_t* d_tid = nullptr;
+  if (table_id && n) {
+    IE_HIP(x->in_tid.ensure(n * 4));
+    IE_HIP(hipMemcpyAsync(x->in_tid.p, table_id, n * 4, hipMemcpyHostToDevice, x->stream));
+    d_tid = (const uint32_t*)x->in_tid.p;
+  }
   const uint64_t base = n ? offsets[0] : 0;
   const uint64_t in_bytes = n ? offsets[n] - base : 0;
   std::vector<uint64_t> off(n + 1);
@@ -373,7 +386,7 @@ int run_host(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, const 
   cap = x->o_bytes.bytes;
   ie_dev_out o{(uint8_t*)x->o_bytes.p, cap, (uint64_t*)x->o_off.p, (uint8_t*)x->o_status.p,
                (uint32_t*)x->o_vid.p, (uint64_t*)x->o_total.p};
-  rc = run_device(x, op, t, (const uint8_t*)x->in_bytes.p, (const uint64_t*)x->in_off.p, n, &o);
+  rc = run_device(x, op, t, (const uint8_t*)x->in_bytes.p, (const uint64_t*)x->in_off.p, n, &o, d_tid);
   if (rc) return rc;
   uint64_t total = 0;
   IE_HIP(hipMemcpyAsync(&total, o.total, 8, hipMemcpyDeviceToHost, x->stream));
@@ -383,7 +396,7 @@ int run_host(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, const 
     IE_HIP(x->o_bytes.ensure(total + 4096));
     o.bytes = (uint8_t*)x->o_bytes.p;
     o.bytes_cap = x->o_bytes.bytes;
-    rc = run_device(x, op, t, (const uint8_t*)x->in_bytes.p, (const uint64_t*)x->in_off.p, n, &o);
+    rc = run_device(x, op, t, (const uint8_t*)x->in_bytes.p, (const uint64_t*)x->in_off.p, n, &o, d_tid);
     if (rc) return rc;
     IE_HIP(hipMemcpyAsync(&total, o.total, 8, hipMemcpyDeviceToHost, x->stream));
     IE_HIP(hipStreamSynchronize(x->stream));
@@ -413,18 +426,20 @@ int run_host(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, const 
     if (!redo.empty() && !x->lit_cap_max) {
       std::vector<uint8_t> rb;
       std::vector<uint64_t> ro(1, 0);
+      std::vector<uint32_t> rt;
       uint64_t need = 0;
       for (uint64_t i : redo) {
         const uint64_t len = offsets[i + 1] - offsets[i];
         rb.insert(rb.end(), bytes + offsets[i], bytes + offsets[i + 1]);
         ro.push_back(rb.size());
+        rt.push_back(table_id ? table_id[i] : 0u);
         need += 4 * (IE_SIZE_CAP(len, t->dev.maxtext) + 4 * t->dev.maxtext + 80);
       }
       const uint64_t saved_pool = x->pool_request;
       x->lit_cap_max = 1;
       x->pool_request = std::max<uint64_t>(need + (1 << 20), saved_pool);
       ie_batch* sub = nullptr;
-      rc = run_host(x, op, t, rb.data(), ro.data(), redo.size(), &sub);
+      rc = run_host(x, op, t, rb.data(), ro.data(), redo.size(), &sub, table_id ? rt.data() : nullptr);
       x->lit_cap_max = 0;
       x->pool_request = saved_pool;
       if (rc) {
@@ -482,12 +497,13 @@ int32_t ie_device_count(void) {
 struct Ent {
   std::string_view key, text;
   uint32_t flags, vid;
+  uint32_t tid;          // the entry's table within the set
   std::string_view raw;  // EF_RAWALT: the raw value behind a pre-resolved splice text
 };
 
 // Entries -> perfect-hash table on the device.
-int upload_table(const std::vector<Ent>& ents, int32_t dialect, uint32_t flags, int32_t device,
-                 ie_table** out) {
+int upload_table(const std::vector<Ent>& ents, uint32_t n_tables, int32_t dialect, uint32_t flags,
+                 int32_t device, ie_table** out) {
   std::vector<uint8_t> arena;
   std::vector<Entry> items;
   items.reserve(ents.size());
@@ -512,7 +528,7 @@ int upload_table(const std::vector<Ent>& ents, int32_t dialect, uint32_t flags, 
     b.key_len = (uint32_t)e.key.size();
     b.text_len = (uint32_t)e.text.size();
     b.vid = e.vid;
-    b.flags = e.flags | EF_OCCUPIED;
+    b.flags = e.flags | EF_OCCUPIED | (e.tid << kTidShift);
     b.text_off = (uint32_t)toff;
     memcpy(b.key, e.key.data(), std::min<size_t>(e.key.size(), kInlineKey));
     memcpy(b.text, e.text.data(), std::min<size_t>(e.text.size(), kInlineText));
@@ -536,19 +552,29 @@ int upload_table(const std::vector<Ent>& ents, int32_t dialect, uint32_t flags, 
   for (int attempt = 0;; attempt++) {
     if (m > (1ull << 31)) return fail(IE_ERR_INVALID, "table too large");
     std::vector<uint64_t> hs(items.size());
-    for (size_t i = 0; i < items.size(); i++) hs[i] = key_hash(ents[i].key, seed);
+    for (size_t i = 0; i < items.size(); i++) hs[i] = key_hash(ents[i].key, seed, ents[i].tid);
     if (ph_place(hs, m, nb, pilots, slot_of)) break;
     if (attempt & 1) m += m / 4;
     else seed = fmix64_host(seed + 0x9E3779B97F4A7C15ull);
   }
   std::vector<Entry> entries(m);
   for (size_t i = 0; i < items.size(); i++) entries[slot_of[i]] = items[i];
+  std::vector<std::pair<uint32_t, Entry>> clock_entries;
+  bool clock_dependent = false;
+  for (size_t i = 0; i < items.size(); i++) {
+    if (items[i].vid == IE_VID_CLOCK_HHMM || items[i].vid == IE_VID_CLOCK_HHMMSS)
+      clock_entries.emplace_back(slot_of[i], items[i]);
+    if ((ents[i].flags & EF_RAWALT) && ents[i].raw.find("HH:MM") != std::string_view::npos) clock_dependent = true;
+  }
   for (int pad = 0; pad < 16; pad++) arena.push_back(0);  // dword reads past the last text
   ie_table* t = new ie_table();
   t->device = device;
   t->dialect = dialect;
   t->flags = flags;
   t->n_entries = ents.size();
+  t->n_tables = n_tables;
+  t->clock_entries = std::move(clock_entries);
+  t->clock_dependent = clock_dependent;
   auto up = [&](DevBuf& b, const void* src, uint64_t bytes) -> hipError_t {
     hipError_t e = b.ensure(bytes + 16);
     if (e != hipSuccess) return e;
@@ -568,6 +594,7 @@ int upload_table(const std::vector<Ent>& ents, int32_t dialect, uint32_t flags, 
   t->dev.nb = nb;
   t->dev.m = (uint32_t)m;
   t->dev.n_entries = (uint32_t)ents.size();
+  t->dev.n_tables = n_tables;
   t->dev.dialect = (uint32_t)dialect;
   t->dev.flags = (flags & IE_TABLE_HAS_INSERTS_DIR) ? TF_HAS_DIR : 0u;
   t->dev.maxtext = maxtext;
@@ -586,8 +613,8 @@ int upload_table(const std::vector<Ent>& ents, int32_t dialect, uint32_t flags, 
 // replaces the splice text; lookups that need the raw value (py:512 / interp.rs:48) read it
 // from the arena (EF_RAWALT). Values whose resolution fails or stays structural keep the
 // literal path.
-int preresolve(ie_table* t0, std::vector<Ent>& ents, int32_t dialect, uint32_t flags, int32_t device,
-               ie_table** out) {
+int preresolve(ie_table* t0, std::vector<Ent>& ents, uint32_t n_tables, int32_t dialect, uint32_t flags,
+               int32_t device, ie_table** out) {
   auto clean_value = [](std::string_view v, bool need_brace) {
     size_t opens = 0;
     int64_t depth = 0;
@@ -609,16 +636,18 @@ int preresolve(ie_table* t0, std::vector<Ent>& ents, int32_t dialect, uint32_t f
   if (cand.empty()) return IE_SUCCESS;
   std::vector<uint8_t> bytes;
   std::vector<uint64_t> offs(1, 0);
+  std::vector<uint32_t> tids;
   for (size_t i : cand) {
     bytes.push_back('a');
     bytes.insert(bytes.end(), ents[i].text.begin(), ents[i].text.end());
     offs.push_back(bytes.size());
+    tids.push_back(ents[i].tid);  // a value resolves against its own table of the set
   }
   ie_exec* x = nullptr;
   int rc = ie_exec_create(device, nullptr, &x);
   if (rc) return rc;
   ie_batch* b = nullptr;
-  rc = ie_interpolate_batch(x, t0, bytes.data(), offs.data(), cand.size(), &b);
+  rc = run_host(x, kOpInterp, t0, bytes.data(), offs.data(), cand.size(), &b, tids.data());
   ie_exec_destroy(x);
   if (rc) return rc;
   std::vector<std::string> resolved(cand.size());
@@ -645,65 +674,78 @@ int preresolve(ie_table* t0, std::vector<Ent>& ents, int32_t dialect, uint32_t f
   ie_batch_free(b);
   if (!changed) return IE_SUCCESS;
   ie_table* t1 = nullptr;
-  rc = upload_table(ents, dialect, flags, device, &t1);
+  rc = upload_table(ents, n_tables, dialect, flags, device, &t1);
   if (rc) return rc;
   ie_table_free(t0);
   *out = t1;
   return IE_SUCCESS;
 }
 
-int ie_table_build(const ie_kv* kv, uint64_t n, int32_t dialect, const ie_clock* now,
-                   uint32_t flags, int32_t device, ie_table** out) {
-  if (!out || (n && !kv)) return fail(IE_ERR_INVALID, "null argument");
+int ie_table_set_build(const ie_kv* kv, const uint64_t* kv_start, uint32_t n_tables, int32_t dialect,
+                       const ie_clock* now, uint32_t flags, int32_t device, ie_table** out) {
+  if (!out || !kv_start || (kv_start[n_tables] && !kv)) return fail(IE_ERR_INVALID, "null argument");
   if (dialect != IE_DIALECT_PY && dialect != IE_DIALECT_RS) return fail(IE_ERR_INVALID, "bad dialect");
+  if (n_tables == 0 || n_tables > kMaxTables) return fail(IE_ERR_INVALID, "table count must be in [1, 2^20]");
+  for (uint32_t t = 0; t < n_tables; t++)
+    if (kv_start[t + 1] < kv_start[t]) return fail(IE_ERR_INVALID, "kv_start must be non-decreasing");
   int rc = set_device(device);
   if (rc) return rc;
-  // dict semantics: the last duplicate wins; '' is never looked up (py:446 / interp.rs:105)
-  std::unordered_map<std::string_view, uint64_t> last;
-  last.reserve(n * 2 + 4);
-  std::vector<uint64_t> order;
-  for (uint64_t i = 0; i < n; i++) {
-    std::string_view k(kv[i].key ? kv[i].key : "", kv[i].key_len);
-    if (k.empty()) continue;
-    auto it = last.find(k);
-    if (it == last.end()) {
-      last.emplace(k, i);
-      order.push_back(i);
-    } else {
-      it->second = i;
-    }
-  }
   char hhmm[16], hhmmss[16];
   const int h = now ? now->hour : 0, mi = now ? now->minute : 0, se = now ? now->second : 0;
   snprintf(hhmm, sizeof hhmm, "%02d:%02d", h, mi);
   snprintf(hhmmss, sizeof hhmmss, "%02d:%02d:%02d", h, mi, se);
-
   std::vector<Ent> ents;
-  ents.reserve(order.size() + 2);
-  for (uint64_t i : order) {
-    std::string_view k(kv[i].key, kv[i].key_len);
-    const uint64_t j = last[k];
-    if (k == "HH:MM" || k == "HH:MM:SS") continue;  // py:433-436: the clock always wins
-    if (kv[j].kind < 0 || kv[j].kind > IE_KIND_DICT) return fail(IE_ERR_INVALID, "bad kind");
-    std::string_view t(kv[j].text ? kv[j].text : "", kv[j].text_len);
-    ents.push_back(Ent{k, t, kind_flags(kv[j].kind, dialect) | text_flags(t), (uint32_t)j});
+  ents.reserve(kv_start[n_tables] - kv_start[0] + 2ull * n_tables);
+  std::unordered_map<std::string_view, uint64_t> last;
+  std::vector<uint64_t> order;
+  for (uint32_t tb = 0; tb < n_tables; tb++) {
+    // dict semantics per table: the last duplicate wins; '' is never looked up (py:446 / interp.rs:105)
+    last.clear();
+    order.clear();
+    for (uint64_t i = kv_start[tb]; i < kv_start[tb + 1]; i++) {
+      std::string_view k(kv[i].key ? kv[i].key : "", kv[i].key_len);
+      if (k.empty()) continue;
+      auto it = last.find(k);
+      if (it == last.end()) {
+        last.emplace(k, i);
+        order.push_back(i);
+      } else {
+        it->second = i;
+      }
+    }
+    for (uint64_t i : order) {
+      std::string_view k(kv[i].key, kv[i].key_len);
+      const uint64_t j = last[k];
+      if (k == "HH:MM" || k == "HH:MM:SS") continue;  // py:433-436: the clock always wins
+      if (kv[j].kind < 0 || kv[j].kind > IE_KIND_DICT) return fail(IE_ERR_INVALID, "bad kind");
+      if (j >= IE_VID_CLOCK_HHMMSS) return fail(IE_ERR_INVALID, "more inserts than value ids");
+      std::string_view t(kv[j].text ? kv[j].text : "", kv[j].text_len);
+      ents.push_back(Ent{k, t, kind_flags(kv[j].kind, dialect) | text_flags(t), (uint32_t)j, tb, {}});
+    }
+    ents.push_back(Ent{"HH:MM", hhmm, kind_flags(IE_KIND_STR, dialect) | text_flags(hhmm), IE_VID_CLOCK_HHMM, tb, {}});
+    ents.push_back(Ent{"HH:MM:SS", hhmmss, kind_flags(IE_KIND_STR, dialect) | text_flags(hhmmss), IE_VID_CLOCK_HHMMSS,
+                       tb, {}});
   }
-  ents.push_back(Ent{"HH:MM", hhmm, kind_flags(IE_KIND_STR, dialect) | text_flags(hhmm), IE_VID_CLOCK_HHMM});
-  ents.push_back(Ent{"HH:MM:SS", hhmmss, kind_flags(IE_KIND_STR, dialect) | text_flags(hhmmss), IE_VID_CLOCK_HHMMSS});
-
   ie_table* t0 = nullptr;
-  rc = upload_table(ents, dialect, flags, device, &t0);
+  rc = upload_table(ents, n_tables, dialect, flags, device, &t0);
   if (rc || getenv("IE_NO_PRERESOLVE")) {  // diagnostic switch: raw splice texts only
     *out = t0;
     return rc;
   }
   *out = t0;
-  rc = preresolve(t0, ents, dialect, flags, device, out);
+  rc = preresolve(t0, ents, n_tables, dialect, flags, device, out);
   if (rc) {
     ie_table_free(*out);
     *out = nullptr;
   }
   return rc;
+}
+
+int ie_table_build(const ie_kv* kv, uint64_t n, int32_t dialect, const ie_clock* now,
+                   uint32_t flags, int32_t device, ie_table** out) {
+  if (!out || (n && !kv)) return fail(IE_ERR_INVALID, "null argument");
+  const uint64_t start[2] = {0, n};
+  return ie_table_set_build(kv, start, 1, dialect, now, flags, device, out);
 }
 
 void ie_table_free(ie_table* t) {
@@ -712,7 +754,27 @@ void ie_table_free(ie_table* t) {
     delete t;
   }
 }
+int ie_table_set_clock(ie_table* t, const ie_clock* now) {
+  if (!t || !now) return fail(IE_ERR_INVALID, "null argument");
+  if (t->clock_dependent) return fail(IE_ERR_INVALID, "a pre-resolved value depends on the clock: rebuild the table");
+  int rc = set_device(t->device);
+  if (rc) return rc;
+  char hhmm[16], hhmmss[16];
+  snprintf(hhmm, sizeof hhmm, "%02d:%02d", now->hour, now->minute);
+  snprintf(hhmmss, sizeof hhmmss, "%02d:%02d:%02d", now->hour, now->minute, now->second);
+  for (auto& ce : t->clock_entries) {
+    Entry& e = ce.second;
+    const char* txt = e.vid == IE_VID_CLOCK_HHMM ? hhmm : hhmmss;
+    if (strlen(txt) != e.text_len) return fail(IE_ERR_INVALID, "clock field out of range");
+    memcpy(e.text, txt, e.text_len);
+    IE_HIP(hipMemcpy((Entry*)t->entries.p + ce.first, &e, sizeof(Entry), hipMemcpyHostToDevice));
+    IE_HIP(hipMemcpy((uint8_t*)t->arena.p + e.text_off, txt, e.text_len, hipMemcpyHostToDevice));
+  }
+  return IE_SUCCESS;
+}
+
 uint64_t ie_table_entries(const ie_table* t) { return t ? t->n_entries : 0; }
+uint32_t ie_table_tables(const ie_table* t) { return t ? t->n_tables : 0; }
 int32_t ie_table_dialect(const ie_table* t) { return t ? t->dialect : -1; }
 
 int ie_exec_create(int32_t device, void* hip_stream, ie_exec** out) {
@@ -812,7 +874,7 @@ int ie_debug_probe(const ie_table* t, const char* key, uint64_t len, uint64_t* o
   IE_HIP(launch_debug_probe(t->dev, (const uint8_t*)dk.p, (uint32_t)len, (uint64_t*)dout.p, 0));
   IE_HIP(hipDeviceSynchronize());
   IE_HIP(hipMemcpy(out, dout.p, 16 * 8, hipMemcpyDeviceToHost));
-  const uint64_t h = key_hash(std::string_view(key ? key : "", len), t->dev.seed);
+  const uint64_t h = key_hash(std::string_view(key ? key : "", len), t->dev.seed, 0);
   std::vector<uint16_t> pil(t->dev.nb);
   IE_HIP(hipMemcpy(pil.data(), t->dev.pilots, pil.size() * sizeof(uint16_t), hipMemcpyDeviceToHost));
   out[7] = h & 0xFFFFFFFFull;
@@ -822,7 +884,7 @@ int ie_debug_probe(const ie_table* t, const char* key, uint64_t len, uint64_t* o
   std::vector<Entry> he(t->dev.m);
   IE_HIP(hipMemcpy(he.data(), t->dev.entries, he.size() * sizeof(Entry), hipMemcpyDeviceToHost));
   for (uint64_t i = 0; i < he.size(); i++)
-    if ((he[i].flags & EF_OCCUPIED) && he[i].key_len == len &&
+    if ((he[i].flags & EF_OCCUPIED) && he[i].key_len == len && (he[i].flags >> kTidShift) == 0 &&
         memcmp(he[i].key, key, std::min<uint64_t>(len, kInlineKey)) == 0)
       out[10] = i;
   return IE_SUCCESS;
@@ -904,9 +966,9 @@ int ie_exec_elapsed(ie_exec* x, uint32_t a, uint32_t b, float* ms) {
   return IE_SUCCESS;
 }
 
-int ie_interpolate_device(ie_exec* x, const ie_table* t, const uint8_t* d_bytes,
-                          const uint64_t* d_offsets, uint64_t n, const ie_dev_out* out) {
-  int rc = run_device(x, kOpInterp, t, d_bytes, d_offsets, n, out);
+int ie_interpolate_device_ids(ie_exec* x, const ie_table* t, const uint32_t* d_table_id, const uint8_t* d_bytes,
+                              const uint64_t* d_offsets, uint64_t n, const ie_dev_out* out) {
+  int rc = run_device(x, kOpInterp, t, d_bytes, d_offsets, n, out, d_table_id);
   if (rc || !n || x->pool_fixed) return rc;
   // The literal path reserves scratch with one atomic per string, so the counter ends at the
   // batch's whole demand even when the pool ran out. A demand above the pool means some strings
@@ -918,7 +980,19 @@ int ie_interpolate_device(ie_exec* x, const ie_table* t, const uint8_t* d_bytes,
   IE_HIP(hipStreamSynchronize(x->stream));
   if (used <= x->pool.bytes) return IE_SUCCESS;
   x->pool_request = std::max<uint64_t>(x->pool_request, used + used / 8 + (1ull << 20));
-  return run_device(x, kOpInterp, t, d_bytes, d_offsets, n, out);
+  return run_device(x, kOpInterp, t, d_bytes, d_offsets, n, out, d_table_id);
+}
+
+int ie_interpolate_device(ie_exec* x, const ie_table* t, const uint8_t* d_bytes,
+                          const uint64_t* d_offsets, uint64_t n, const ie_dev_out* out) {
+  return ie_interpolate_device_ids(x, t, nullptr, d_bytes, d_offsets, n, out);
+}
+
+int ie_interpolate_batch_ids(ie_exec* x, const ie_table* t, const uint32_t* table_id, const uint8_t* bytes,
+                             const uint64_t* offsets, uint64_t n, ie_batch** out) {
+  if (!t) return fail(IE_ERR_INVALID, "null table");
+  if (n && !table_id) return fail(IE_ERR_INVALID, "null table ids");
+  return run_host(x, kOpInterp, t, bytes, offsets, n, out, table_id);
 }
 
 int ie_interpolate_batch(ie_exec* x, const ie_table* t, const uint8_t* bytes,

@@ -23,6 +23,7 @@ struct Batch {
   uint64_t* out_off;        // n + 1 output offsets
   uint8_t* status;          // n
   uint32_t* value_id;       // n
+  const uint32_t* table_id; // n: the table of the set each string is resolved against, or null (0)
 };
 
 struct Work {

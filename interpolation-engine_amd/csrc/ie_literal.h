@@ -157,7 +157,7 @@ struct LitOut {
 
 // One complex string, executed by all 64 lanes of a wave with uniform control flow.
 // Scratch: four regions of `cap` bytes at R[0..3] (pool offset `pool_off` of R[0]).
-__device__ LitOut w_literal(const DevTable& T, const uint8_t* s, uint64_t n, uint8_t* R0,
+__device__ LitOut w_literal(const DevTable& T, uint32_t tid, const uint8_t* s, uint64_t n, uint8_t* R0,
                             uint64_t cap, uint64_t pool_off, bool max_mode) {
   LitOut r{0, 0, 0, IE_VID_NONE};
   uint8_t* R[4] = {R0, R0 + cap, R0 + 2 * cap, R0 + 3 * cap};
@@ -203,7 +203,7 @@ __device__ LitOut w_literal(const DevTable& T, const uint8_t* s, uint64_t n, uin
     const uint64_t k1 = w_replace<kPatRestoreOpen>(src + outer_from + 1, (uint64_t)inner_to - outer_from - 1, K, cap);
     const uint64_t k2 = w_replace<kPatRestoreClose>(K, k1, K2, cap);
     Hit E;
-    const int32_t e = find_bytes(T, K2, (uint32_t)k2, E);                // py:529
+    const int32_t e = find_bytes(T, tid, K2, (uint32_t)k2, E);                // py:529
     if (e < 0) { r.status = missing_status(T, K2, (uint32_t)k2); return r; }
     if (!(E.flags & EF_SPLICE_OK)) { r.status = IE_E_ASSERT_TYPE; return r; }  // py:530
     // py:531-535: prefix (protected already, never ends in '\') + protect(text | seam) + suffix
@@ -236,11 +236,11 @@ __device__ LitOut w_literal(const DevTable& T, const uint8_t* s, uint64_t n, uin
   // typed result: W lookups, the first on the string, then on raw values (py:512 / interp.rs:48)
   uint8_t st = 0;
   Hit cur_hit;
-  int32_t e = find_bytes(T, K, (uint32_t)f2, cur_hit);
+  int32_t e = find_bytes(T, tid, K, (uint32_t)f2, cur_hit);
   if (e < 0) { r.status = missing_status(T, K, (uint32_t)f2); return r; }
   for (uint32_t k = 1; k < W; k++) {
     Hit nh;
-    e = find_raw(T, cur_hit, st, nh);  // rs: every raw value has EF_KEY_STR (value_to_string)
+    e = find_raw(T, tid, cur_hit, st, nh);  // rs: every raw value has EF_KEY_STR (value_to_string)
     if (e < 0) { r.status = st; return r; }
     cur_hit = nh;
   }

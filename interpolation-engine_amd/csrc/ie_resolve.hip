@@ -287,7 +287,7 @@ __device__ __forceinline__ void put_words(lds_u8* dst, const uint32_t (&t)[8], u
 // (kMaxDepth words, stride kBlock) reuse the lane's own chain-evaluator columns.
 // ------------------------------------------------------------------------------------------
 template <bool STAGED>
-__device__ uint8_t eval_exact(const DevTable& T, const Src<STAGED> s, uint32_t n, bool active, lds_u8* kbuf,
+__device__ uint8_t eval_exact(const DevTable& T, uint32_t tid, const Src<STAGED> s, uint32_t n, bool active, lds_u8* kbuf,
                               lds_u32* stack, Desc& d, uint32_t& out_len, uint32_t& vid) {
   constexpr uint8_t kRunning = 0xFF;
   uint8_t status = active ? kRunning : (uint8_t)IE_OK_STR;
@@ -414,10 +414,10 @@ __device__ uint8_t eval_exact(const DevTable& T, const Src<STAGED> s, uint32_t n
       Hit h;
       int32_t b;
       if (c_wrapping && wrapped) {
-        b = find_raw(T, wrap_h, est, h);  // the key is the inner level's raw value
+        b = find_raw(T, tid, wrap_h, est, h);  // the key is the inner level's raw value
       } else {
         const uint8_t* kg = (const uint8_t*)(kbuf + c_ks);  // generic view of the LDS key
-        b = c_kl <= kInlineKey ? find_small(T, (const uint32_t*)kg, c_kl, h) : find_bytes(T, kg, c_kl, h);
+        b = c_kl <= kInlineKey ? find_small(T, tid, (const uint32_t*)kg, c_kl, h) : find_bytes(T, tid, kg, c_kl, h);
         if (b < 0) est = missing_status(T, kg, c_kl);
       }
       if (b >= 0 && !c_wrapping) {
@@ -581,7 +581,7 @@ struct TopText {
 };
 
 template <bool FAILC>
-__device__ bool eval_chains(const DevTable& T, const lds_u16* pil, const lds_u8* tile, uint32_t p0, uint32_t n, const lds_u32* cm,
+__device__ bool eval_chains(const DevTable& T, uint32_t tid, const lds_u16* pil, const lds_u8* tile, uint32_t p0, uint32_t n, const lds_u32* cm,
                             const lds_u32* oddbits, const lds_u32* escbits, bool active, const ChainLds& CL, Desc& d,
                             TopText& tt, uint32_t& out_len, uint8_t& status, bool& chain_fail, uint64_t* stamp) {
   bool ok = active && n <= kChainMax;
@@ -749,12 +749,12 @@ __device__ bool eval_chains(const DevTable& T, const lds_u16* pil, const lds_u8*
         on[c] = false;
       }
       kw[c] = keep_bytes(kw[c], klen[c]);
-      h[c] = hash_init(klen[c], T.seed);
+      h[c] = hash_init(klen[c], T.seed, tid);
       h[c] = hash_word(h[c], kw[c].x);
       if (__any(on[c] && klen[c] > 4u)) h[c] = klen[c] > 4u ? hash_word(h[c], kw[c].y) : h[c];
       if (__any(on[c] && klen[c] > 8u)) h[c] = klen[c] > 8u ? hash_word(h[c], kw[c].z) : h[c];
       if (__any(on[c] && klen[c] > 12u)) h[c] = klen[c] > 12u ? hash_word(h[c], kw[c].w) : h[c];
-      if (klen[c] == 0) h[c] = hash_init(0, T.seed);
+      if (klen[c] == 0) h[c] = hash_init(0, T.seed, tid);
     }
 #pragma unroll
     for (int c = 0; c < kMaxTop; c++) on[c] = on[c] && ok;
@@ -783,7 +783,7 @@ __device__ bool eval_chains(const DevTable& T, const lds_u16* pil, const lds_u8*
     for (int c = 0; c < kMaxTop; c++) {
       if (!__any(on[c])) continue;
       const Probe& E = P[c];
-      const bool hit = on[c] && (entry_head_ok(E.q0, klen[c]) & (E.q1.x == kw[c].x) & (E.q1.y == kw[c].y) &
+      const bool hit = on[c] && (entry_head_ok(E.q0, klen[c], tid) & (E.q1.x == kw[c].x) & (E.q1.y == kw[c].y) &
                                  (E.q1.z == kw[c].z) & (E.q1.w == kw[c].w));
       const uint32_t flags = E.q0.z, tlen = E.q0.y;
       const bool good = hit && (flags & EF_SPLICE_OK) && (flags & EF_INERT);
@@ -990,7 +990,7 @@ __device__ __forceinline__ uint4 bytes_at(u32x4 x, u32x4 y, uint32_t r) {
 
 // FAILC: chain failures commit in the chain evaluator (else they take the exact evaluator). Both
 // give the reference's results; the host picks per batch stream (ie_host.cpp, "fail commit").
-template <bool FAILC>
+template <bool FAILC, bool MULTI>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES_PER_EU))) void k_resolve(Batch B, Work W, DevTable T, uint8_t* out,
                                                     uint64_t cap) {
   __shared__ __attribute__((aligned(16))) uint8_t s_in[kTileBytes + 48];
@@ -1086,6 +1086,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES
   const uint8_t* s = nullptr;
   const uint32_t p0 = shift + (uint32_t)(so - lo);
   bool pend = false, fast_lane = false, chain_fail = false;
+  // this string's table in the set (MULTI: a table-id batch; else every key lives in table 0)
+  const uint32_t tid_s = (MULTI && i < B.n) ? gld(B.table_id + i) : 0u;
   {
     uint8_t st = IE_OK_STR;
     uint32_t olen = 0, vid = IE_VID_NONE;
@@ -1102,7 +1104,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES
       slow = false;
     } else if (staged && W.fast_mode) {
       const ChainLds CL{(lds_u8*)(s_u + tid * kKeyCap), (lds_u64*)(lds_u8*)(s_u + kKbufLds) + tid};
-      const bool fast = eval_chains<FAILC>(T, lds_pil ? (const lds_u16*)s_pil : nullptr, (const lds_u8*)s_in, p0, (uint32_t)sn, s_cm,
+      const bool fast = eval_chains<FAILC>(T, tid_s, lds_pil ? (const lds_u16*)s_pil : nullptr, (const lds_u8*)s_in, p0, (uint32_t)sn, s_cm,
                                     s_odd, s_esc, active, CL, d, tt, olen, r, chain_fail,
                                     stamp_row ? stamp_row + 6 : nullptr);
       slow = active && !fast;
@@ -1122,9 +1124,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES
       r2 = kStatusPending;
 #else
       if (staged)
-        r2 = eval_exact<true>(T, Src<true>{s}, (uint32_t)sn, slow, kb, stk, d, o2, vid);
+        r2 = eval_exact<true>(T, tid_s, Src<true>{s}, (uint32_t)sn, slow, kb, stk, d, o2, vid);
       else
-        r2 = eval_exact<false>(T, Src<false>{s}, (uint32_t)sn, slow, kb, stk, d, o2, vid);
+        r2 = eval_exact<false>(T, tid_s, Src<false>{s}, (uint32_t)sn, slow, kb, stk, d, o2, vid);
 #endif
       if (slow) r = r2, olen = o2;
     }
@@ -1156,7 +1158,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES
 #else
     if (false)
 #endif
-      r = w_literal(T, B.bytes + po, pn, W.pool + pbase, rcap, pbase, W.lit_cap_max != 0);
+      r = w_literal(T, MULTI ? gld(B.table_id + gi) : 0u, B.bytes + po, pn, W.pool + pbase, rcap, pbase,
+                    W.lit_cap_max != 0);
     if (r.status == IE_OK_STR && (r.res_len > kLenMask || (r.res_off >> 4) > 0xFFFFFFFFull))
       r.status = IE_E_OVERFLOW;
     if (lane == 0) {
@@ -1327,13 +1330,13 @@ __global__ void k_debug_probe(DevTable T, const uint8_t* key, uint32_t klen, uin
     for (uint32_t j = 0; j < klen && j < 64; j++) ((uint8_t*)kb)[j] = key[j];
   __syncthreads();
   Hit hw{0, 0, 0, 0};
-  const int32_t fw = find_bytes(T, key, klen, hw);
+  const int32_t fw = find_bytes(T, 0, key, klen, hw);
   const uint64_t agree = __ballot(fw == __shfl(fw, 0, 64) && hw.text_off == __shfl(hw.text_off, 0, 64));
   if (lane != 0) return;
-  const uint64_t hash = hash_key(klen, [&](uint32_t j) { return key[j]; }, T.seed);
+  const uint64_t hash = hash_key(klen, [&](uint32_t j) { return key[j]; }, T.seed, 0u);
   Hit h;
-  const int32_t fb = find_bytes(T, key, klen, h);
-  const int32_t fs = klen <= kInlineKey ? find_small(T, (const uint32_t*)kb, klen, h) : -2;
+  const int32_t fb = find_bytes(T, 0, key, klen, h);
+  const int32_t fs = klen <= kInlineKey ? find_small(T, 0, (const uint32_t*)kb, klen, h) : -2;
   out[0] = hash & 0xFFFFFFFFull;
   out[1] = hash >> 32;
   out[2] = ph_lookup_slot(T, hash);
@@ -1355,8 +1358,11 @@ hipError_t launch_resolve(const Batch& B, const Work& W, const DevTable& T, uint
   if (!tiles) return hipSuccess;
   if (tiles > 0xFFFFFFFFull) return hipErrorInvalidValue;
   const uint32_t grid = (uint32_t)tiles;
-  if (W.fail_commit) hipLaunchKernelGGL(k_resolve<true>, dim3(grid), dim3(kBlock), 0, st, B, W, T, out, cap);
-  else hipLaunchKernelGGL(k_resolve<false>, dim3(grid), dim3(kBlock), 0, st, B, W, T, out, cap);
+  const bool multi = B.table_id != nullptr;
+  if (W.fail_commit && multi) hipLaunchKernelGGL((k_resolve<true, true>), dim3(grid), dim3(kBlock), 0, st, B, W, T, out, cap);
+  else if (W.fail_commit) hipLaunchKernelGGL((k_resolve<true, false>), dim3(grid), dim3(kBlock), 0, st, B, W, T, out, cap);
+  else if (multi) hipLaunchKernelGGL((k_resolve<false, true>), dim3(grid), dim3(kBlock), 0, st, B, W, T, out, cap);
+  else hipLaunchKernelGGL((k_resolve<false, false>), dim3(grid), dim3(kBlock), 0, st, B, W, T, out, cap);
   return hipGetLastError();
 }
 

@@ -87,18 +87,25 @@ def get_exec(device=0):
     return x
 
 
-class InsertsTable:
-    """An immutable device snapshot of an inserts dict (get_interpdata's view of it)."""
+class InsertsTableSet:
+    """Immutable device snapshots of several inserts dicts in ONE device table (a table set,
+    include/ie_amd.h ie_table_set_build): every string names the dict it resolves against.
+    This is the batch form of get_interpdata for many forked interpreter states (config 5)."""
 
-    def __init__(self, inserts, dialect="py", clock=None, device=0, has_inserts_dir=False):
+    def __init__(self, dicts, dialect="py", clock=None, device=0, has_inserts_dir=False):
         if clock is None:
             now = _dt.datetime.now()
             clock = (now.hour, now.minute, now.second)
         self.clock = tuple(clock)
         self.dialect = dialect
         self.device = device
-        self.keys = list(inserts.keys())
-        self.values = list(inserts.values())
+        self.dicts = list(dicts)
+        self.keys, self.values, starts = [], [], [0]
+        for d in self.dicts:
+            self.keys.extend(d.keys())
+            self.values.extend(d.values())
+            starts.append(len(self.keys))
+        self.starts = starts
         n = len(self.keys)
         arr = (N.KV * max(1, n))()
         keep = []
@@ -111,13 +118,12 @@ class InsertsTable:
             arr[i] = N.KV(kb, len(kb), tb, len(tb), kind, 0)
         h = ctypes.c_void_p()
         clk = N.Clock(*self.clock)
-        N.check(N.lib().ie_table_build(ctypes.cast(arr, ctypes.c_void_p), n, N.IE_DIALECT[dialect],
-                                       ctypes.byref(clk), N.TABLE_HAS_INSERTS_DIR if has_inserts_dir else 0,
-                                       device, ctypes.byref(h)), "ie_table_build")
+        st = (ctypes.c_uint64 * len(starts))(*starts)
+        N.check(N.lib().ie_table_set_build(ctypes.cast(arr, ctypes.c_void_p), st, len(self.dicts),
+                                           N.IE_DIALECT[dialect], ctypes.byref(clk),
+                                           N.TABLE_HAS_INSERTS_DIR if has_inserts_dir else 0, device,
+                                           ctypes.byref(h)), "ie_table_set_build")
         self.h = h
-        self._snapshot = (dict(inserts), {k: text for k, text in
-                                          ((k, render(v, dialect)[1]) for k, v in inserts.items()
-                                           if isinstance(v, (list, dict)))})
 
     def close(self):
         if getattr(self, "h", None):
@@ -126,16 +132,12 @@ class InsertsTable:
 
     __del__ = close
 
-    def matches(self, inserts, clock):
-        snap, mutable = self._snapshot
-        if clock != self.clock or len(inserts) != len(snap):
+    def set_clock(self, clock):
+        """Re-read the clock without a rebuild; False when the table must be rebuilt instead."""
+        clk = N.Clock(*clock)
+        if N.lib().ie_table_set_clock(self.h, ctypes.byref(clk)) != 0:
             return False
-        for k, v in inserts.items():
-            if k not in snap or snap[k] is not v:
-                return False
-        for k, text in mutable.items():  # lists/dicts may have been mutated in place
-            if render(inserts[k], self.dialect)[1] != text:
-                return False
+        self.clock = tuple(clock)
         return True
 
     def value(self, vid):
@@ -145,33 +147,71 @@ class InsertsTable:
             return "%02d:%02d:%02d" % self.clock
         return self.values[vid]
 
+    def table_keys(self, t):
+        return self.keys[self.starts[t]:self.starts[t + 1]]
+
     # --------------------------------------------------------------------------------------
-    def run(self, strings):
-        """Resolve a list of str on the device -> list of (status, payload)."""
+    def run(self, strings, table_ids=None):
+        """Resolve a list of str on the device -> list of (status, payload); string i against dict
+        table_ids[i] (all against dict 0 when table_ids is None)."""
         blob, offs = N.pack(strings)
         x = get_exec(self.device)
         res = ctypes.POINTER(N.BatchRes)()
         bp = ctypes.c_char_p(blob)
-        N.check(N.lib().ie_interpolate_batch(x.h, self.h, ctypes.cast(bp, ctypes.c_void_p),
-                                             offs.ctypes.data, len(strings), ctypes.byref(res)),
-                "ie_interpolate_batch")
+        if table_ids is None:
+            N.check(N.lib().ie_interpolate_batch(x.h, self.h, ctypes.cast(bp, ctypes.c_void_p),
+                                                 offs.ctypes.data, len(strings), ctypes.byref(res)),
+                    "ie_interpolate_batch")
+        else:
+            import numpy as np
+            ids = np.ascontiguousarray(table_ids, dtype=np.uint32)
+            if ids.size != len(strings):
+                raise ValueError("one table id per string")
+            N.check(N.lib().ie_interpolate_batch_ids(x.h, self.h, ids.ctypes.data, ctypes.cast(bp, ctypes.c_void_p),
+                                                     offs.ctypes.data, len(strings), ctypes.byref(res)),
+                    "ie_interpolate_batch_ids")
         outs, sts, vids = N.batch_to_python(res)
         return [(st, N.dec(o) if st == N.OK_STR else (vids[i] if st == N.OK_VALUE else None))
                 for i, (o, st) in enumerate(zip(outs, sts))]
 
-    def results(self, strings):
+    def results(self, strings, table_ids=None):
         """Like interpolate_inserts on each string; failures come back as exception instances."""
+        ids = [0] * len(strings) if table_ids is None else list(table_ids)
         out = []
-        for s, (st, payload) in zip(strings, self.run(strings)):
-            out.append(self._result(s, st, payload))
+        for s, t, (st, payload) in zip(strings, ids, self.run(strings, table_ids)):
+            if st == N.OK_STR:
+                out.append(payload)
+            elif st == N.OK_VALUE:
+                out.append(self.value(payload))
+            else:
+                out.append(_exception(s, st, self.table_keys(t)))
         return out
 
-    def _result(self, s, st, payload):
-        if st == N.OK_STR:
-            return payload
-        if st == N.OK_VALUE:
-            return self.value(payload)
-        return _exception(s, st, self.keys)
+
+class InsertsTable(InsertsTableSet):
+    """An immutable device snapshot of one inserts dict (get_interpdata's view of it)."""
+
+    def __init__(self, inserts, dialect="py", clock=None, device=0, has_inserts_dir=False):
+        super().__init__([inserts], dialect=dialect, clock=clock, device=device, has_inserts_dir=has_inserts_dir)
+        self._snapshot = (dict(inserts), {k: render(v, dialect)[1] for k, v in inserts.items()
+                                          if isinstance(v, (list, dict))})
+        self._version = getattr(inserts, "version", None)
+
+    def matches(self, inserts):
+        """Is this still a snapshot of `inserts`? O(1) for a VersionedInserts, else O(len)."""
+        v = getattr(inserts, "version", None)
+        if v is not None:
+            return v == self._version
+        snap, mutable = self._snapshot
+        if len(inserts) != len(snap):
+            return False
+        for k, v in inserts.items():
+            if k not in snap or snap[k] is not v:
+                return False
+        for k, text in mutable.items():  # lists/dicts may have been mutated in place
+            if render(inserts[k], self.dialect)[1] != text:
+                return False
+        return True
 
 
 def _exception(s, st, keys):
@@ -193,20 +233,70 @@ def _exception(s, st, keys):
     return RuntimeError("device status %s for %r" % (N.STATUS_NAMES[st] if st < len(N.STATUS_NAMES) else st, s))
 
 
-_cache = {}
+class VersionedInserts(dict):
+    """A dict that counts its mutations, so table_for() recognises an unchanged inserts dict in
+    O(1) instead of comparing every value (use it as the runner's `state['inserts']`). Mutating a
+    list or dict value in place is not a mutation of this dict: bump() after doing that."""
+    __slots__ = ("version",)
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.version = 0
+
+    def bump(self):
+        self.version += 1
+
+    def _mut(name):
+        base = getattr(dict, name)
+
+        def f(self, *a, **k):
+            self.version += 1
+            return base(self, *a, **k)
+        f.__name__ = name
+        return f
+
+    for _n in ("__setitem__", "__delitem__", "update", "pop", "popitem", "clear", "setdefault", "__ior__"):
+        locals()[_n] = _mut(_n)
+    del _n, _mut
+
+
+_CACHE_SIZE = 8
+_cache = {}  # (id(inserts), dialect, device) -> (inserts, InsertsTable), least recently used first
 
 
 def table_for(inserts, dialect="py", device=0):
-    """The device table for this dict, rebuilt only when the dict or the clock changed."""
+    """The device table for this dict: rebuilt only when the dict changed; a new clock second
+    rewrites the two clock entries in place (ie_table_set_clock). At most _CACHE_SIZE tables stay
+    alive (the dict is held with its table, so its id cannot be reused while cached)."""
     now = _dt.datetime.now()
     clock = (now.hour, now.minute, now.second)
     key = (id(inserts), dialect, device)
-    t = _cache.get(key)
-    if t is None or not t.matches(inserts, clock):
-        t = InsertsTable(inserts, dialect=dialect, clock=clock, device=device,
-                         has_inserts_dir=bool(inserts_dir))
-        _cache[key] = t
+    hit = _cache.pop(key, None)
+    t = hit[1] if hit is not None and hit[0] is inserts else None
+    if t is not None and not t.matches(inserts):
+        t.close()
+        t = None
+    if t is not None and t.clock != clock and not t.set_clock(clock):
+        t.close()
+        t = None
+    if t is None:
+        t = InsertsTable(inserts, dialect=dialect, clock=clock, device=device, has_inserts_dir=bool(inserts_dir))
+    _cache[key] = (inserts, t)
+    while len(_cache) > _CACHE_SIZE:
+        _, old = _cache.pop(next(iter(_cache)))
+        old.close()
     return t
+
+
+def interpolate_states(states, items, dialect="py", device=0):
+    """Batch interpolate_inserts over many inserts dicts (forked interpreter states, config 5):
+    `items` is a list of (state index, content); one device table set, one batch. Failures are
+    returned as exception instances, results in item order."""
+    tset = InsertsTableSet(states, dialect=dialect, device=device, has_inserts_dir=bool(inserts_dir))
+    try:
+        return tset.results([c for _, c in items], [i for i, _ in items])
+    finally:
+        tset.close()
 
 
 # ------------------------------------------------------------------------------------------

@@ -36,9 +36,9 @@ def fail_commit(request, monkeypatch):
     chain evaluator (the library picks one adaptively; IE_FAIL_COMMIT / IE_OPT_FAIL_COMMIT force it).
     Execs read the environment when they are created; the mirror's cached exec is set directly."""
     monkeypatch.setenv("IE_FAIL_COMMIT", request.param)
-    PKG.get_exec(0).set_option(N.OPT_FAIL_COMMIT, int(request.param))
+    PKG.interpolation_engine.get_exec(0).set_option(N.OPT_FAIL_COMMIT, int(request.param))
     yield request.param
-    PKG.get_exec(0).set_option(N.OPT_FAIL_COMMIT, -1)
+    PKG.interpolation_engine.get_exec(0).set_option(N.OPT_FAIL_COMMIT, -1)
 
 
 def compare_with_oracle(table_dict, strings, dialect="py", has_dir=False):
@@ -665,3 +665,96 @@ def test_recursive_interpolate_golden():
         else:
             assert PKG.recursive_escape(row["esc_in"]) == row["esc"]
             assert PKG.recursive_unescape(row["esc_in"]) == row["unesc"]
+
+
+# ------------------------------------------------------------------------------------------
+# table sets: many inserts dicts in one device table, a table id per string (config 5, §8b)
+# ------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("dialect", ["py", "rs"])
+def test_table_set_matches_per_table_oracle(dialect, fail_commit):
+    """Every string resolves against its own dict: same keys with different values in different
+    tables, brace-bearing values pre-resolved against their own table, clock entries per table."""
+    rng = random.Random(99)
+    tables = [_rand_table(rng, rng.randint(5, 40), brace_values=(k % 2 == 0)) for k in range(37)]
+    tables[3] = {}  # an empty dict in the set
+    tables[5]["k1"] = "{HH:MM}-{k2}"
+    items = []
+    for _ in range(6000):
+        t = rng.randrange(len(tables))
+        items.append((t, _rand_string(rng, 40)))
+    items += [(t, "{HH:MM:SS}") for t in range(len(tables))] + [(5, "x{k1}")]
+    tset = PKG.InsertsTableSet(tables, dialect=dialect, clock=CLOCK)
+    got = tset.run([s for _, s in items], [t for t, _ in items])
+    oracles = [O.Oracle(tb, dialect, clock=CLOCK) for tb in tables]
+    bad = []
+    for (t, s), (st, payload) in zip(items, got):
+        rst, rout, rvid = oracles[t].interpolate(s)
+        name = N.STATUS_NAMES[st]
+        ok = name == rst
+        if ok and rst == "OK_STR":
+            ok = payload == rout
+        if ok and rst == "OK_VALUE":  # value ids index the concatenated kv list of the set
+            ok = payload == (rvid if rvid >= 0xFFFFFFF0 else rvid + tset.starts[t])
+        if not ok:
+            bad.append((t, s, name, payload, rst, rout, rvid))
+    assert not bad, (len(bad), bad[:4])
+
+
+def test_table_set_device_ids_out_of_range_find_nothing():
+    """Device API: an id beyond the set reports missing keys (no memory is indexed by the id);
+    the host API refuses such ids."""
+    tset = PKG.InsertsTableSet([{"a": "A"}, {"a": "B"}], clock=CLOCK)
+    x = N.Exec(0)
+    strings = ["x{a}", "x{a}", "x{a}", "plain"]
+    ids = np.array([0, 1, 7, 7], np.uint32)
+    blob, offs = N.pack(strings)
+    d_bytes = N.DeviceBuffer.from_numpy(x, np.frombuffer(blob, np.uint8))
+    d_off = N.DeviceBuffer.from_numpy(x, offs)
+    d_ids = N.DeviceBuffer.from_numpy(x, ids)
+    r = DevResult(x, len(strings), 256)
+    N.check(N.lib().ie_interpolate_device_ids(x.h, tset.h, d_ids.ptr, d_bytes.ptr, d_off.ptr, len(strings),
+                                              ctypes.byref(r.out)), "ids")
+    x.sync()
+    st = [N.STATUS_NAMES[v] for v in r.status.to_numpy(np.uint8, 4)]
+    assert st == ["OK_STR", "OK_STR", "E_INTERP", "OK_STR"]
+    oo = r.off.to_numpy(np.uint64, 5)
+    ob = r.bytes.to_numpy(np.uint8, r.total()).tobytes()
+    assert [ob[int(oo[i]):int(oo[i + 1])] for i in (0, 1, 3)] == [b"xA", b"xB", b"plain"]
+    with pytest.raises(RuntimeError):
+        tset.run(strings, [0, 1, 7, 7])
+
+
+def test_table_clock_rewritten_in_place():
+    t = PKG.InsertsTable({"k": "v", "w": "{k}"}, clock=(1, 2, 3))
+    assert t.results(["{HH:MM}", "x{HH:MM:SS}", "{w}"]) == ["01:02", "x01:02:03", "{k}"]
+    assert t.set_clock((23, 59, 58))
+    assert t.results(["{HH:MM}", "x{HH:MM:SS}", "x{w}"]) == ["23:59", "x23:59:58", "xv"]
+    dep = PKG.InsertsTable({"w": "at {HH:MM}"}, clock=(1, 2, 3))  # pre-resolved with the old clock
+    assert dep.results(["x{w}"]) == ["xat 01:02"]
+    assert not dep.set_clock((4, 5, 6))
+
+
+def test_mirror_table_cache_versioned_and_bounded():
+    ins = PKG.VersionedInserts(name="tom", n=1)
+    assert PKG.interpolate_inserts(ins, "hi {name}") == "hi tom"
+    t1 = PKG.interpolation_engine.table_for(ins)
+    assert PKG.interpolation_engine.table_for(ins) is t1  # unchanged: no rebuild
+    ins["name"] = "ann"
+    assert PKG.interpolate_inserts(ins, "hi {name}") == "hi ann"
+    dicts = [{"k": str(j)} for j in range(20)]
+    for d in dicts:
+        assert PKG.interpolate_inserts(d, "{k}") == d["k"]
+    assert len(PKG.interpolation_engine._cache) <= PKG.interpolation_engine._CACHE_SIZE
+
+
+def test_interpolate_states_batch():
+    states = [{"scenario": "s%d" % j, "stage": "first", "L": [j]} for j in range(50)]
+    items = [(j % 50, c) for j, c in enumerate(["{scenario}", "x{stage}|{scenario}", "{L}", "{nope}"] * 50)]
+    res = PKG.interpolate_states(states, items)
+    for (j, c), r in zip(items, res):
+        if c == "{nope}":
+            assert isinstance(r, PKG.InterpolationException)
+        elif c == "{L}":
+            assert r is states[j]["L"]
+        else:
+            assert r == c.replace("{scenario}", states[j]["scenario"]).replace("{stage}", "first")
