@@ -229,6 +229,14 @@ int ie_escape_device(ie_exec* x, const uint8_t* d_bytes, const uint64_t* d_offse
                      const ie_dev_out* out);
 int ie_unescape_batch(ie_exec* x, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
                       ie_batch** out);
+/* The `unescape` command's transform of its item (py:1660-1667 / rust-project/src/runtime.rs:
+ * 1044-1050): recursive_unescape, then recursive_interpolate, on a batch of strings (table ids
+ * nullable). tmp receives the unescaped strings (caller-sized; IE_ERR_CAPACITY when too small).
+ * d_status_in (nullable): the statuses of the step that produced the input; a string that failed
+ * there keeps that status (a failed item never reaches the command). Synchronous once (capacity). */
+int ie_unescape_cmd_device(ie_exec* x, const ie_table* t, const uint32_t* d_table_id, const uint8_t* d_bytes,
+                           const uint64_t* d_offsets, uint64_t n, const uint8_t* d_status_in, const ie_dev_out* tmp,
+                           const ie_dev_out* out);
 int ie_escape_batch(ie_exec* x, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
                     ie_batch** out);
 

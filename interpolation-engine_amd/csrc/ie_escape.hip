@@ -295,9 +295,35 @@ __global__ __launch_bounds__(kBlock) void k_scan_c(const uint64_t* in, uint64_t 
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = run;
 }
 
+// A step of a multi-step batch that failed earlier stays failed: strings whose earlier status
+// is not IE_OK_STR take that status (their bytes are empty: a failed string has no output)
+__global__ void k_status_carry(const uint8_t* before, uint8_t* after, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint8_t b = before[i];
+    if (b != IE_OK_STR) after[i] = b;
+  }
+}
+
+// device-side capacity check between two steps: flags the exec's error word (reported at sync)
+__global__ void k_cap_check(const uint64_t* total, uint64_t cap, uint32_t* err) {
+  if (threadIdx.x == 0 && *total > cap) atomicOr(err, 2u);
+}
+
 // ------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------
+hipError_t launch_cap_check(const uint64_t* total, uint64_t cap, uint32_t* err, hipStream_t st) {
+  hipLaunchKernelGGL(k_cap_check, dim3(1), dim3(64), 0, st, total, cap, err);
+  return hipGetLastError();
+}
+
+hipError_t launch_status_carry(const uint8_t* before, uint8_t* after, uint64_t n, hipStream_t st) {
+  if (!n) return hipSuccess;
+  const uint64_t g0 = (n + 255) / 256;
+  hipLaunchKernelGGL(k_status_carry, dim3((uint32_t)(g0 < 8192 ? g0 : 8192)), dim3(256), 0, st, before, after, n);
+  return hipGetLastError();
+}
+
 hipError_t launch_escape(int op, const Batch& B, const Work& W, uint8_t* out, uint64_t cap, hipStream_t st) {
   const uint64_t tiles = (B.n + kBlock - 1) / kBlock;
   if (!tiles) return hipSuccess;

@@ -112,7 +112,7 @@ struct ie_exec {
   uint32_t* stat_host = nullptr;  // pinned
   hipEvent_t stat_ev = nullptr;
   // workspace
-  DevBuf counters, tile_state, pool, out_len, tile_sum, tile_base;
+  DevBuf counters, tile_state, pool, out_len, tile_sum, tile_base, defer_tiles, defer_desc;
   // host-API staging
   DevBuf in_bytes, in_off, in_tid, o_bytes, o_off, o_status, o_vid, o_total;
   // synth scratch
@@ -120,7 +120,7 @@ struct ie_exec {
   DevBuf stamps;        // diagnostic phase stamps (env IE_DEBUG_STAMPS=<file>)
   uint64_t stamp_tiles = 0;
   ~ie_exec() {
-    for (DevBuf* b : {&counters, &tile_state, &pool, &out_len, &tile_sum, &tile_base, &in_bytes,
+    for (DevBuf* b : {&counters, &tile_state, &pool, &out_len, &tile_sum, &tile_base, &defer_tiles, &defer_desc, &in_bytes,
                       &in_off, &in_tid, &o_bytes, &o_off, &o_status, &o_vid, &o_total, &s_lens, &s_part, &stamps})
       b->release();
     for (auto& e : ev)
@@ -244,14 +244,18 @@ int set_device(int32_t dev) {
 }
 
 // workspace for a batch of n strings. counters (u32 words): [0] tile ticket, [1] look-back error,
-// [2..3] pool bytes used (u64), [4..8] telemetry (literal strings, direct tiles, look-back polls,
-// exact-path strings, chain failures); zeroed with the tile states on every call.
+// [2..3] pool bytes used (u64), [4..8] telemetry (literal strings, deferred tiles, look-back polls,
+// exact-path strings, chain failures), [9] deferred-tile count; zeroed on every call.
 int ensure_work(ie_exec* x, int op, uint64_t n) {
   const uint64_t tiles = (n + kBlock - 1) / kBlock + 1;
   IE_HIP(x->counters.ensure(64));
   if (op == kOpInterp) {
     IE_HIP(x->tile_state.ensure(tiles * sizeof(uint64_t)));
     IE_HIP(x->pool.ensure(x->pool_request));
+    // room for every tile to be deferred (64 B of descriptor per string; grow-only, never read
+    // unless written, so only HBM capacity is spent)
+    IE_HIP(x->defer_tiles.ensure(tiles * sizeof(uint32_t)));
+    IE_HIP(x->defer_desc.ensure(tiles * kBlock * 64));
   } else {
     IE_HIP(x->out_len.ensure((n + 1) * sizeof(uint32_t)));
     IE_HIP(x->tile_sum.ensure(tiles * sizeof(uint64_t)));
@@ -270,6 +274,9 @@ Work make_work(ie_exec* x, uint64_t* total) {
   W.debug_noeval = x->opt_noeval;  // diagnostic hooks, see DESIGN.md
   W.fast_mode = x->opt_fast;       // 0: exact evaluator only
   W.pool_used = (uint64_t*)x->counters.p + 1;
+  W.defer_count = (uint32_t*)x->counters.p + 9;
+  W.defer_tiles = (uint32_t*)x->defer_tiles.p;
+  W.defer_desc = (uint4*)x->defer_desc.p;
   W.tile_state = (uint64_t*)x->tile_state.p;
   W.pool = (uint8_t*)x->pool.p;
   W.pool_bytes = x->pool.bytes;
@@ -349,6 +356,7 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
 int check_device_error(ie_exec* x) {
   uint32_t err = 0;
   if (x->counters.p) IE_HIP(hipMemcpy(&err, (uint32_t*)x->counters.p + 1, 4, hipMemcpyDeviceToHost));
+  if (err & 2u) return fail(IE_ERR_CAPACITY, "a step's output did not fit its caller-sized buffer");
   if (err) return fail(IE_ERR_TIMEOUT, "look-back spin timed out (a predecessor tile never published)");
   return IE_SUCCESS;
 }
@@ -849,10 +857,10 @@ int ie_exec_timing(ie_exec* x, ie_timing* out) {
   out->resolve_ms = kern;   // the resolve (or escape) kernels
   out->complex_ms = 0.0f;   // literal strings are resolved inside k_resolve
   out->total_ms = setup + kern;
-  uint32_t st[5] = {0, 0, 0, 0, 0};
-  if (x->counters.p) IE_HIP(hipMemcpy(st, (uint32_t*)x->counters.p + 4, 20, hipMemcpyDeviceToHost));
+  uint32_t st[6] = {0, 0, 0, 0, 0, 0};
+  if (x->counters.p) IE_HIP(hipMemcpy(st, (uint32_t*)x->counters.p + 4, 24, hipMemcpyDeviceToHost));
   out->n_complex = st[0];
-  out->n_direct = st[1];
+  out->n_direct = st[5];  // tiles deferred to the windowed emit (counter word 9)
   out->n_polls = st[2];
   out->n_exact = st[3];
   out->n_chain_fail = st[4];
@@ -1004,6 +1012,22 @@ int ie_interpolate_batch(ie_exec* x, const ie_table* t, const uint8_t* bytes,
 int ie_interpolate(ie_exec* x, const ie_table* t, const char* s, uint64_t len, ie_batch** out) {
   uint64_t off[2] = {0, len};
   return ie_interpolate_batch(x, t, (const uint8_t*)s, off, 1, out);
+}
+
+int ie_unescape_cmd_device(ie_exec* x, const ie_table* t, const uint32_t* d_table_id, const uint8_t* d_bytes,
+                           const uint64_t* d_offsets, uint64_t n, const uint8_t* d_status_in, const ie_dev_out* tmp,
+                           const ie_dev_out* out) {
+  if (!tmp || !out || !tmp->bytes || !out->status) return fail(IE_ERR_INVALID, "null argument");
+  int rc = run_device(x, kOpUnescape, nullptr, d_bytes, d_offsets, n, tmp);  // py:1665
+  if (rc) return rc;
+  // the unescaped bytes feed the interpolation (py:1666). Unescaping never lengthens a string, so
+  // a tmp as large as the input always fits; a smaller one that overflowed is flagged on the
+  // device (no wait here) and reported by ie_exec_sync as IE_ERR_CAPACITY
+  rc = ie_interpolate_device_ids(x, t, d_table_id, tmp->bytes, tmp->offsets, n, out);
+  if (rc) return rc;
+  IE_HIP(launch_cap_check(tmp->total, tmp->bytes_cap, (uint32_t*)x->counters.p + 1, x->stream));
+  if (d_status_in) IE_HIP(launch_status_carry(d_status_in, out->status, n, x->stream));
+  return IE_SUCCESS;
 }
 
 int ie_unescape_device(ie_exec* x, const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t n,

@@ -42,6 +42,10 @@ struct Work {
   uint64_t pool_bytes;
   uint32_t lit_cap_max;  // 1: literal strings get the full IE_SIZE_CAP working space
   uint32_t fail_commit;  // 1: chain failures commit in the chain evaluator (k_resolve<true>)
+  // tiles whose output does not fit the LDS stage: k_emit_windows writes their bytes
+  uint32_t* defer_count; // 1
+  uint32_t* defer_tiles; // tiles
+  uint4* defer_desc;     // tiles * kBlock * 4: each string's descriptor
   // escape pipeline
   uint32_t* out_len;     // n
   uint64_t* tile_sum;    // tiles
@@ -52,6 +56,8 @@ hipError_t launch_resolve(const Batch& B, const Work& W, const DevTable& T, uint
                           uint64_t cap, hipStream_t st);
 hipError_t launch_escape(int op, const Batch& B, const Work& W, uint8_t* out, uint64_t cap,
                          hipStream_t st);
+hipError_t launch_cap_check(const uint64_t* total, uint64_t cap, uint32_t* err, hipStream_t st);
+hipError_t launch_status_carry(const uint8_t* before, uint8_t* after, uint64_t n, hipStream_t st);
 hipError_t launch_debug_probe(const DevTable& T, const uint8_t* key, uint32_t klen, uint64_t* out,
                               hipStream_t st);
 hipError_t launch_synth(const SynthParams& P, uint64_t first, uint64_t n, uint64_t* d_lens,

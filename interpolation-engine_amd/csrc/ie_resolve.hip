@@ -988,6 +988,151 @@ __device__ __forceinline__ uint4 bytes_at(u32x4 x, u32x4 y, uint32_t r) {
                     __builtin_amdgcn_alignbyte(a3, a2, sb), __builtin_amdgcn_alignbyte(a4, a3, sb));
 }
 
+// stream the LDS stage [0, len) to g (any alignment): 16-byte stores at 16-byte aligned
+// addresses, each assembled from the two stage blocks it straddles; byte stores at the ends
+__device__ __forceinline__ void stream_stage(uint8_t* g, const uint8_t* stage, uint32_t len, uint32_t tid) {
+  const uintptr_t pg = (uintptr_t)g, pe = pg + len;
+  const uintptr_t a_up = (pg + 15) & ~(uintptr_t)15, b_down = pe & ~(uintptr_t)15;
+  if (a_up >= b_down) {
+    for (uint32_t k = tid; k < len; k += kBlock) gst(g + k, ((const lds_u8*)stage)[k]);
+    return;
+  }
+  const uint32_t head = (uint32_t)(a_up - pg), tail = (uint32_t)(pe - b_down);
+  if (tid < head) gst(g + tid, ((const lds_u8*)stage)[tid]);
+  if (tid < tail) {
+    const uint32_t k = (uint32_t)(b_down - pg) + tid;
+    gst(g + k, ((const lds_u8*)stage)[k]);
+  }
+  const uint32_t nv = (uint32_t)((b_down - a_up) >> 4);
+  constexpr int kOutV = (kStageBytes + kBlock * 16 - 1) / (kBlock * 16);
+  uint4 v[kOutV];
+#pragma unroll
+  for (int k = 0; k < kOutV; k++) {
+    const uint32_t c = tid + (uint32_t)k * kBlock;
+    if (c < nv) {
+      const lds_u128* blk = (const lds_u128*)(const lds_u8*)stage + c;
+      const u32x4 x = blk[0], y = blk[1];
+      v[k] = bytes_at(x, y, head);
+    }
+  }
+  uint4* dstv = (uint4*)a_up;
+#pragma unroll
+  for (int k = 0; k < kOutV; k++) {
+    const uint32_t c = tid + (uint32_t)k * kBlock;
+    if (c < nv) gst4(dstv + c, v[k]);
+  }
+}
+
+// the whole wave copies len bytes src -> dst (LDS; arguments uniform): lane k moves destination
+// dwords k, k+64, ... realigned from the source's aligned dwords (reads at most 3 bytes past the
+// source end, inside an aligned dword)
+template <bool SRC_LDS>
+__device__ void wave_copy(lds_u8* dst, const uint8_t* src, uint32_t len) {
+  auto rd8 = [&](const uint8_t* p) -> uint8_t {
+    if (SRC_LDS) return *(const lds_u8*)p;
+    return gld(p);
+  };
+  auto rd32 = [&](const uint32_t* p) -> uint32_t {
+    if (SRC_LDS) return *(const lds_u32*)(const lds_u8*)(const uint8_t*)p;
+    return gld(p);
+  };
+  const uint32_t lane = lane_id();
+  const uint32_t h0 = (0u - (uint32_t)(uintptr_t)dst) & 3u, h = h0 < len ? h0 : len;
+  if (lane < h) dst[lane] = rd8(src + lane);
+  const uint32_t nw = (len - h) >> 2;
+  const uintptr_t sa = (uintptr_t)(src + h);
+  const uint32_t sh = (uint32_t)(sa & 3u);
+  const uint32_t* s32 = (const uint32_t*)(sa - sh);
+  lds_u32* d32 = (lds_u32*)(dst + h);
+  for (uint32_t q = lane; q < nw; q += 64) {
+    const uint32_t w0 = rd32(s32 + q);
+    d32[q] = sh ? __builtin_amdgcn_alignbyte(rd32(s32 + q + 1), w0, sh) : w0;
+  }
+  const uint32_t t0 = h + 4 * nw;
+  if (lane < len - t0) dst[t0 + lane] = rd8(src + t0 + lane);
+}
+
+// the part of one output piece (len bytes at src, first byte at window position rel) inside the
+// window [0, wl): short parts by their own lane, long ones by the whole wave
+template <bool SRC_LDS>
+__device__ __forceinline__ void window_piece(lds_u8* win, int64_t rel, const uint8_t* src, uint32_t len, uint32_t wl) {
+  const int64_t a = rel > 0 ? rel : 0, b = rel + (int64_t)len < (int64_t)wl ? rel + (int64_t)len : (int64_t)wl;
+  const uint32_t n = a < b ? (uint32_t)(b - a) : 0u;
+  const uint8_t* from = src + (a - rel);
+  const bool big = n > 96u;
+  if (n && !big) copy_bytes<true, SRC_LDS>((uint8_t*)(win + a), from, n);
+  for (uint64_t m = __ballot(big); m; m &= m - 1) {
+    const int l = __builtin_ctzll(m);
+    const uint64_t f = (uint64_t)(uintptr_t)from;
+    const uint32_t fl = __shfl((uint32_t)f, l, 64), fh = __shfl((uint32_t)(f >> 32), l, 64);
+    const uint32_t aa = __shfl((uint32_t)a, l, 64), nn = __shfl(n, l, 64);
+    wave_copy<SRC_LDS>(win + aa, (const uint8_t*)(uintptr_t)(((uint64_t)fh << 32) | fl), nn);
+  }
+}
+
+// The deferred tiles' bytes (see k_resolve): one workgroup per deferred tile at a time. Each
+// lane rebuilds its string's pieces from the stored descriptor (template runs from the input in
+// global memory, values from the table or the literal pool) and the tile's output goes through
+// the LDS stage in windows of kStageBytes (long pieces copied by a whole wave).
+__global__ __launch_bounds__(kBlock) void k_emit_windows(Batch B, Work W, DevTable T, uint8_t* out) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_win[kStageBytes + 48];
+  const uint32_t count = __hip_atomic_load(W.defer_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t slot = blockIdx.x; slot < count; slot += gridDim.x) {
+    const uint32_t tile = gld(W.defer_tiles + slot);
+    const uint64_t first = (uint64_t)tile * kBlock, last = min(first + (uint64_t)kBlock, B.n), i = first + tid;
+    const uint64_t base = gld(B.out_off + first), tile_total = gld(B.out_off + last) - base;
+    const uint4* dd = W.defer_desc + ((uint64_t)slot * kBlock + tid) * 4;
+    Desc d;
+    uint32_t olen = 0, n32 = 0;
+    uint64_t local = 0;
+    const uint8_t* s = B.bytes;
+    if (i < B.n) {
+      const uint4 a = gld4(dd), b = gld4(dd + 1), c = gld4(dd + 2), e = gld4(dd + 3);
+      d.ntop = a.x, d.open[0] = a.y, d.open[1] = a.z, d.open[2] = a.w;
+      d.close[0] = b.x, d.close[1] = b.y, d.close[2] = b.z, n32 = b.w;
+      d.vk[0] = c.x, d.vk[1] = c.y, d.vk[2] = c.z;
+      d.vs[0] = e.x, d.vs[1] = e.y, d.vs[2] = e.z;
+      const uint64_t o = gld(B.out_off + i);
+      local = o - base;
+      olen = gld(B.status + i) == IE_OK_STR ? (uint32_t)(gld(B.out_off + i + 1) - o) : 0u;
+      s = B.bytes + gld(B.in_off + i);
+    } else {
+      d.ntop = 0;
+#pragma unroll
+      for (int q = 0; q < kMaxTop; q++) d.open[q] = d.close[q] = d.vk[q] = d.vs[q] = 0;
+    }
+    const bool mine = olen != 0;
+    lds_u8* const win = (lds_u8*)s_win;
+    for (uint64_t w0 = 0; w0 < tile_total; w0 += (uint64_t)kStageBytes) {
+      const uint32_t wl = (uint32_t)min((uint64_t)kStageBytes, tile_total - w0);
+      const int64_t rel0 = (int64_t)local - (int64_t)w0;  // this lane's output, window-relative
+      const bool on = mine && rel0 < (int64_t)wl && rel0 + (int64_t)olen > 0;
+      const uint32_t ntop = mine ? d.ntop : 0u;
+      uint32_t w = 0;
+#pragma unroll
+      for (int j = 0; j <= kMaxTop; j++) {
+        const uint32_t t_lo = j == 0 ? 0u : d.close[j - 1] + 1;
+        const uint32_t t_hi = (uint32_t)j < ntop ? d.open[j] : n32;
+        const uint32_t tl = on && (uint32_t)j <= ntop ? t_hi - t_lo : 0u;
+        window_piece<false>(win, rel0 + w, s + t_lo, tl, wl);
+        w += tl;
+        if (j == kMaxTop) break;
+        const bool von = on && (uint32_t)j < ntop;
+        const uint32_t kind = d.vk[j] >> 30, len = von ? d.vk[j] & kLenMask : 0u;
+        const uint8_t* p = kind == kValEntry ? T.entries[von ? d.vs[j] : 0u].text
+                           : kind == kValArena ? T.arena + d.vs[j]
+                                               : W.pool + ((uint64_t)d.vs[j] << 4);
+        window_piece<false>(win, rel0 + w, p, len, wl);
+        w += len;
+      }
+      __syncthreads();
+      stream_stage(out + base + w0, s_win, wl, tid);
+      __syncthreads();
+    }
+  }
+}
+
 // FAILC: chain failures commit in the chain evaluator (else they take the exact evaluator). Both
 // give the reference's results; the host picks per batch stream (ie_host.cpp, "fail commit").
 template <bool FAILC, bool MULTI>
@@ -998,7 +1143,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES
   __shared__ uint32_t s_olen[kBlock];  // output length; the value id for IE_OK_VALUE strings
   __shared__ uint8_t s_st[kBlock];
   __shared__ uint8_t s_pend[kBlock];
-  __shared__ uint32_t s_misc[4];  // tile, pending count
+  __shared__ uint32_t s_misc[4];  // tile, pending count, defer slot
   __shared__ uint64_t s_red[kBlock / 64 + 2];
   __shared__ __attribute__((aligned(16))) uint16_t s_pil[kLdsPilots];  // the table's pilots (small tables)
   lds_u32* const s_cm = (lds_u32*)(lds_u8*)(s_u + kCmOff);    // event masks of the staged chunks (+ pad)
@@ -1262,56 +1407,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES
   //      two stage blocks it straddles (the shift is uniform over the tile) ----
   uint8_t* const g = out + base;
   if (write_bytes && in_stage) {
-    const uintptr_t pg = (uintptr_t)g, pe = pg + tile_total;
-    const uintptr_t a_up = (pg + 15) & ~(uintptr_t)15, b_down = pe & ~(uintptr_t)15;
-    if (a_up >= b_down) {
-      for (uint32_t k = tid; k < tile_total; k += kBlock) gst(g + k, s_u[k]);
-    } else {
-      const uint32_t head = (uint32_t)(a_up - pg), tail = (uint32_t)(pe - b_down);
-      if (tid < head) gst(g + tid, s_u[tid]);
-      if (tid < tail) {
-        const uint32_t k = (uint32_t)(b_down - pg) + tid;
-        gst(g + k, s_u[k]);
-      }
-      const uint32_t nv = (uint32_t)((b_down - a_up) >> 4);
-      constexpr int kOutV = (kStageBytes + kBlock * 16 - 1) / (kBlock * 16);
-      uint4 v[kOutV];
-#pragma unroll
-      for (int k = 0; k < kOutV; k++) {
-        const uint32_t c = tid + (uint32_t)k * kBlock;
-        if (c < nv) {
-          const lds_u128* blk = (const lds_u128*)(lds_u8*)s_u + c;
-          const u32x4 x = blk[0], y = blk[1];
-          v[k] = bytes_at(x, y, head);
-        }
-      }
-      uint4* dstv = (uint4*)a_up;
-#pragma unroll
-      for (int k = 0; k < kOutV; k++) {
-        const uint32_t c = tid + (uint32_t)k * kBlock;
-        if (c < nv) gst4(dstv + c, v[k]);
-      }
-    }
-  } else if (write_bytes && mine) {  // rare (long strings / large tiles): lanes store their own bytes
-    if (tid == 0) atomicAdd(W.stats + 1, 1u);
-    uint8_t* dd = g + local;
-    uint32_t w = 0;
-    for (uint32_t j = 0; j <= d.ntop; j++) {
-      uint32_t t_lo = 0, t_hi = n32, vk = 0, vs = 0;
-#pragma unroll
-      for (int q = 0; q < kMaxTop; q++) {
-        if (j == (uint32_t)q + 1) t_lo = d.close[q] + 1;
-        if (j == (uint32_t)q && j < d.ntop) t_hi = d.open[q], vk = d.vk[q], vs = d.vs[q];
-      }
-      for (uint32_t q = t_lo; q < t_hi; q++) gst(dd + w++, staged ? ((const lds_u8*)s)[q] : gld(s + q));
-      if (j < d.ntop) {
-        const uint32_t kind = vk >> 30, len = vk & kLenMask;
-        const uint8_t* p = kind == kValEntry ? T.entries[vs].text
-                           : kind == kValArena ? T.arena + vs
-                                               : W.pool + ((uint64_t)vs << 4);
-        for (uint32_t q = 0; q < len; q++) gst(dd + w++, gld(p + q));
-      }
-    }
+    stream_stage(g, s_u, (uint32_t)tile_total, tid);
+  } else if (write_bytes) {
+    // a tile whose output exceeds the stage (long strings, large expansions) or whose input was
+    // not staged: its descriptors go to the defer list and k_emit_windows writes its bytes
+    // (offsets and statuses are final already); the windowed copy is kept out of this kernel so
+    // that its registers do not weigh on the common path
+    if (tid == 0) s_misc[2] = atomicAdd(W.defer_count, 1u);
+    __syncthreads();
+    const uint32_t slot = s_misc[2];
+    uint4* dd = W.defer_desc + ((uint64_t)slot * kBlock + tid) * 4;
+    const uint32_t nt = mine ? d.ntop : 0u;
+    gst4(dd, make_uint4(nt, d.open[0], d.open[1], d.open[2]));
+    gst4(dd + 1, make_uint4(d.close[0], d.close[1], d.close[2], n32));
+    gst4(dd + 2, make_uint4(d.vk[0], d.vk[1], d.vk[2], 0u));
+    gst4(dd + 3, make_uint4(d.vs[0], d.vs[1], d.vs[2], 0u));
+    if (tid == 0) gst(W.defer_tiles + slot, tile);
   }
   IE_STAMP(5);
 #undef IE_STAMP
@@ -1363,6 +1474,8 @@ hipError_t launch_resolve(const Batch& B, const Work& W, const DevTable& T, uint
   else if (W.fail_commit) hipLaunchKernelGGL((k_resolve<true, false>), dim3(grid), dim3(kBlock), 0, st, B, W, T, out, cap);
   else if (multi) hipLaunchKernelGGL((k_resolve<false, true>), dim3(grid), dim3(kBlock), 0, st, B, W, T, out, cap);
   else hipLaunchKernelGGL((k_resolve<false, false>), dim3(grid), dim3(kBlock), 0, st, B, W, T, out, cap);
+  // the deferred (oversized) tiles' bytes; exits at once when there are none
+  if (out) hipLaunchKernelGGL(k_emit_windows, dim3(grid < 512u ? grid : 512u), dim3(kBlock), 0, st, B, W, T, out);
   return hipGetLastError();
 }
 
