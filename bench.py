@@ -1,21 +1,30 @@
 #!/usr/bin/env python3
 """Benchmark of the `{key}` interpolation hot path on MI355X (BASELINE.json metric).
 
-One step = one ie_interpolate_device call over one batch of synthetic strings already resident
-in HBM (SURVEY §8d config 3 by default: 10M strings of 48-80 B, 1-2 nested `{q-{iM}}` refs each,
-100k-entry inserts table). Multi-GPU: one process per GPU, each resolving its own shard of the
-string index space (weak scaling; the table is replicated, no data-path collective — only the
-barrier and the max-over-ranks timing use torch.distributed).
+One step = one pass of the hot path over one batch of synthetic strings already resident in HBM:
+  config 3 (default): 10M strings of 48-80 B, 1-2 nested `{q-{iM}}` refs, 100k-entry inserts
+  config 2: 1M strings, 1-3 single-level `{kJ}` refs, 1k-entry inserts
+  config 4: 12.5M strings per GPU (the 100M batch over 8), mixed-depth chains, escapes,
+            brace-bearing values, misses; step = interpolate, then the `unescape` command
+            (recursive_unescape + recursive_interpolate, py:1660-1667) on the results
+  config 5: text_adventure.json5 forked states (10k per GPU): the per-iteration pre-pass stream
+            recorded from the reference (tests/golden/config5_stream.json) against one inserts
+            dict per state, all states in one table set, a table id per string
+Multi-GPU: one process per GPU, each resolving its own shard (weak scaling; the table is built
+per rank, no data-path collective — only the barrier and the max-over-ranks time go over
+torch.distributed, gloo on the host).
 
-Prints ONE JSON line (rank 0). `value` is interpolated MB/s (input payload, 1 MB = 1e6 B) over all
-ranks; `roofline` prices the resolve pipeline against HBM (algorithmic bytes |in|+|out|+17 per
-string); `cpu_baseline` times the C oracle (a literal restatement of the reference
-algorithm, oracle/ie_oracle.c) on a bounded sample of the same workload on this host.
+Prints ONE JSON line (rank 0): `value` = interpolated MB/s (input payload, 1 MB = 1e6 B) over
+all ranks; `roofline` prices the resolve pipeline against HBM (algorithmic bytes
+|in| + |out| + 17 per string); `cpu_baseline` times the C oracle (a literal
+restatement of the reference algorithm, oracle/ie_oracle.c) on a bounded sample of the same
+workload on this host, single-thread and on every core of this rank's CPU share.
 """
 import argparse
 import ctypes
 import json
 import os
+import platform
 import sys
 import time
 
@@ -31,13 +40,15 @@ WORKLOADS = {
     3: "cfg3: 10M strings/GPU, 48-80 B, 1-2 nested {q-{iM}} refs, 100k-entry inserts",
     4: "cfg4: 12.5M strings/GPU (100M over 8), 48-80 B, 1-2 chain refs of depth 1-4 (40/30/20/10 %), "
        "10 % \\{lit\\} escapes, 2 % brace-bearing values, 1 % missing keys, 100k-entry inserts; "
-       "step = resolve + unescape pass",
+       "step = interpolate + the unescape command (unescape, interpolate again)",
+    5: "cfg5: text_adventure.json5 agent-loop states (10k/GPU), the recorded per-iteration pre-pass "
+       "stream per state, one inserts dict per state in one table set",
 }
-DEFAULT_N = {2: 1_000_000, 3: 10_000_000, 4: 12_500_000}
+DEFAULT_N = {2: 1_000_000, 3: 10_000_000, 4: 12_500_000, 5: 10_000}  # strings (configs 2-4) / states (5)
 
 
 def shard_first(rank, n_per_rank):
-    """First global string index of a rank's shard (weak scaling: every rank owns n strings)."""
+    """First global index (string or state) of a rank's shard: every rank owns n (weak scaling)."""
     return rank * n_per_rank
 
 
@@ -51,17 +62,115 @@ def max_over_ranks(x, dist):
     return float(t.item())
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4])
-    ap.add_argument("--n", type=int, default=0, help="strings per GPU (default: the config's size)")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline budget (thread-seconds)")
+    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4, 5])
+    ap.add_argument("--n", type=int, default=0, help="strings (configs 2-4) or states (config 5) per GPU")
+    ap.add_argument("--device", type=int, default=-1, help="HIP device (default: LOCAL_RANK)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (wall seconds)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def cpu_share():
+    """Threads this rank may use (the box sets OMP_NUM_THREADS to its CPU share; os.cpu_count()
+    shows the whole machine there), and the host's CPU model."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        n = min(n, int(os.environ["OMP_NUM_THREADS"]))
+    model = platform.processor() or "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return max(1, n), model
+
+
+# ------------------------------------------------------------------------------------------
+# workloads: device-resident inputs + what the CPU baseline needs
+# ------------------------------------------------------------------------------------------
+class Synth:
+    """Configs 2-4: the library's counter-based generator writes the shard straight into HBM."""
+
+    def __init__(self, N, L, x, cfg, first, n, dev):
+        self.N, self.L, self.cfg, self.n = N, L, cfg, n
+        self.synth = ctypes.c_void_p()
+        N.check(L.ie_synth_create(cfg, 0, ctypes.byref(self.synth)), "ie_synth_create")
+        self.kvp = ctypes.POINTER(N.KV)()
+        self.nkv = L.ie_synth_kv(self.synth, ctypes.byref(self.kvp))
+        self.table = ctypes.c_void_p()
+        clk = N.Clock(*CLOCK)
+        t0 = time.perf_counter()
+        N.check(L.ie_table_build(ctypes.cast(self.kvp, ctypes.c_void_p), self.nkv, 0, ctypes.byref(clk), 0, dev,
+                                 ctypes.byref(self.table)), "ie_table_build")
+        self.build_s = time.perf_counter() - t0
+        self.d_off = N.DeviceBuffer(x, (n + 1) * 8)
+        tot = ctypes.c_uint64()
+        N.check(L.ie_synth_strings_device(x.h, self.synth, first, n, None, 0, self.d_off.ptr, ctypes.byref(tot)), "synth")
+        self.in_bytes = int(tot.value)
+        self.d_in = N.DeviceBuffer(x, self.in_bytes + 16)
+        N.check(L.ie_synth_strings_device(x.h, self.synth, first, n, self.d_in.ptr, self.d_in.nbytes, self.d_off.ptr,
+                                          ctypes.byref(tot)), "synth")
+        self.first = first
+        self.inserts = int(self.nkv)
+        self.d_ids = None
+
+    def host_sample(self, m):
+        N, L = self.N, self.L
+        offs = np.zeros(m + 1, np.uint64)
+        tot = ctypes.c_uint64()
+        N.check(L.ie_synth_strings_host(self.synth, self.first, m, None, 0, offs.ctypes.data, ctypes.byref(tot)), "len")
+        buf = np.zeros(int(tot.value) + 1, np.uint8)
+        N.check(L.ie_synth_strings_host(self.synth, self.first, m, buf.ctypes.data, buf.size, offs.ctypes.data,
+                                        ctypes.byref(tot)), "fill")
+        return buf, offs
+
+    def close(self):
+        self.L.ie_table_free(self.table)
+        self.L.ie_synth_free(self.synth)
+
+
+class States:
+    """Config 5: one inserts dict per agent-loop state (interpolation-engine_amd/workloads.py) in
+    one table set, and per state the pre-pass strings the reference resolved in one loop
+    iteration with that stage (recorded, tests/golden/config5_stream.json)."""
+
+    def __init__(self, N, L, x, pkg, first, n, dev):
+        from interpolation_engine_amd import workloads as Wk
+        c5 = json.load(open(os.path.join(ROOT, "tests", "golden", "config5_stream.json"), encoding="utf-8"))
+        self.stream = {}
+        for st in c5["states"]:  # the pre-pass templates of the first recorded state of each stage
+            if st["stage"] not in self.stream:
+                self.stream[st["stage"]] = [c["s"] for c in st["calls"] if c["by"] == "recursive_interpolate"]
+        self.states = [Wk.state_inserts(c5["defaults"], first + j) for j in range(n)]
+        strings, ids = [], []
+        for j, ins in enumerate(self.states):
+            tpl = self.stream[ins["stage"]]
+            strings.extend(tpl)
+            ids.extend([j] * len(tpl))
+        self.ids = np.asarray(ids, dtype=np.uint32)
+        self.n = len(strings)
+        t0 = time.perf_counter()
+        self.tset = pkg.InsertsTableSet(self.states, clock=CLOCK, device=dev)
+        self.build_s = time.perf_counter() - t0
+        self.table = self.tset.h
+        blob, offs = N.pack(strings)
+        self.in_bytes = len(blob)
+        self.d_in = N.DeviceBuffer.from_numpy(x, np.frombuffer(blob + bytes(16), np.uint8))
+        self.d_off = N.DeviceBuffer.from_numpy(x, offs)
+        self.d_ids = N.DeviceBuffer.from_numpy(x, self.ids)
+        self.blob, self.offs = blob, offs
+        self.inserts = len(self.tset.keys)
+
+    def close(self):
+        self.tset.close()
 
 
 def main():
@@ -69,70 +178,67 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        # control plane only (barrier + max-over-ranks timing): the string shards are independent
-        import torch.distributed as dist
-        dist.init_process_group("gloo")
 
+    # the library (and with it the HIP runtime it links) is loaded before anything imports torch:
+    # torch bundles a HIP runtime of the same soname, and which one binds depends on load order
     import __graft_entry__ as G
     G.check_built()  # never compiles here (this process may already hold the GPU, e.g. under rocprofv3)
     pkg = G.load_package()
     N = pkg._native
     L = N.lib()
-    dev = local
+    ndev = L.ie_device_count()
+    dev = args.device if args.device >= 0 else local
+    if ndev <= 0 or dev >= ndev:
+        raise SystemExit("device %d requested, %d visible" % (dev, ndev))
+
+    dist = None
+    if world > 1:
+        # control plane only (barrier + max-over-ranks time): the shards are independent
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
 
     cfg = args.config
-    n = args.n or DEFAULT_N[cfg]
-    first = shard_first(rank, n)  # this rank's shard of the global string index space
-
-    synth = ctypes.c_void_p()
-    N.check(L.ie_synth_create(cfg, 0, ctypes.byref(synth)), "ie_synth_create")
-    kvp = ctypes.POINTER(N.KV)()
-    nkv = L.ie_synth_kv(synth, ctypes.byref(kvp))
+    n_units = args.n or DEFAULT_N[cfg]
+    first = shard_first(rank, n_units)  # this rank's shard of the global string / state index space
     x = N.Exec(dev)
-    # literal-path scratch sized for the workload (2 % of config 4's strings carry brace-bearing
-    # values, ~2.4 KB of working space each): the device call then stays asynchronous, and the
-    # statuses below prove no string ran out of it
+    # literal-path scratch sized for the workload (the call stays asynchronous; the statuses below
+    # prove no string ran out of it)
     N.check(L.ie_exec_set_scratch(x.h, (2 << 30) if cfg == 4 else (256 << 20)), "ie_exec_set_scratch")
-    table = ctypes.c_void_p()
-    clk = N.Clock(*CLOCK)
-    N.check(L.ie_table_build(ctypes.cast(kvp, ctypes.c_void_p), nkv, 0, ctypes.byref(clk), 0, dev,
-                             ctypes.byref(table)), "ie_table_build")
-
-    # inputs generated straight into HBM (counter-based splitmix64: rank r owns strings [r*n, (r+1)*n))
-    d_off = N.DeviceBuffer(x, (n + 1) * 8)
-    tot = ctypes.c_uint64()
-    N.check(L.ie_synth_strings_device(x.h, synth, first, n, None, 0, d_off.ptr, ctypes.byref(tot)), "synth")
-    in_bytes = int(tot.value)
-    d_in = N.DeviceBuffer(x, in_bytes + 16)
-    N.check(L.ie_synth_strings_device(x.h, synth, first, n, d_in.ptr, d_in.nbytes, d_off.ptr, ctypes.byref(tot)),
-            "synth")
-    out_cap = 2 * in_bytes + (1 << 20)
+    W = Synth(N, L, x, cfg, first, n_units, dev) if cfg != 5 else States(N, L, x, pkg, first, n_units, dev)
+    n = W.n
+    in_bytes = W.in_bytes
+    out_cap = 3 * in_bytes + (64 << 20) if cfg != 5 else 16 * in_bytes + (64 << 20)
     d_out = N.DeviceBuffer(x, out_cap)
     d_ooff = N.DeviceBuffer(x, (n + 1) * 8)
     d_st = N.DeviceBuffer(x, n + 1)
     d_vid = N.DeviceBuffer(x, 4 * n + 4)
     d_tot = N.DeviceBuffer(x, 8)
     o = N.DevOut(d_out.ptr, out_cap, d_ooff.ptr, d_st.ptr, d_vid.ptr, d_tot.ptr)
+    ids = W.d_ids.ptr if W.d_ids is not None else None
 
-    unesc = cfg == 4  # config 4: the unescape pass (recursive_unescape py:1448-1460) over the outputs
-    if unesc:
-        d_uout = N.DeviceBuffer(x, out_cap)
+    cmd = cfg == 4  # the unescape command on the results (py:1660-1667): unescape, interpolate again
+    if cmd:
+        d_u = N.DeviceBuffer(x, out_cap)
         d_uoff = N.DeviceBuffer(x, (n + 1) * 8)
         d_ust = N.DeviceBuffer(x, n + 1)
         d_utot = N.DeviceBuffer(x, 8)
-        uo = N.DevOut(d_uout.ptr, out_cap, d_uoff.ptr, d_ust.ptr, d_vid.ptr, d_utot.ptr)
+        tmp = N.DevOut(d_u.ptr, out_cap, d_uoff.ptr, d_ust.ptr, d_vid.ptr, d_utot.ptr)
+        d_out2 = N.DeviceBuffer(x, out_cap)
+        d_ooff2 = N.DeviceBuffer(x, (n + 1) * 8)
+        d_st2 = N.DeviceBuffer(x, n + 1)
+        d_tot2 = N.DeviceBuffer(x, 8)
+        o2 = N.DevOut(d_out2.ptr, out_cap, d_ooff2.ptr, d_st2.ptr, d_vid.ptr, d_tot2.ptr)
 
     def step(k=None):
         if k is not None:
             x.mark(3 * k)
-        N.check(L.ie_interpolate_device(x.h, table, d_in.ptr, d_off.ptr, n, ctypes.byref(o)),
-                "ie_interpolate_device")
+        N.check(L.ie_interpolate_device_ids(x.h, W.table, ids, W.d_in.ptr, W.d_off.ptr, n, ctypes.byref(o)),
+                "ie_interpolate_device_ids")
         if k is not None:
             x.mark(3 * k + 1)
-        if unesc:
-            N.check(L.ie_unescape_device(x.h, d_out.ptr, d_ooff.ptr, n, ctypes.byref(uo)), "ie_unescape_device")
+        if cmd:
+            N.check(L.ie_unescape_cmd_device(x.h, W.table, None, d_out.ptr, d_ooff.ptr, n, d_st.ptr,
+                                             ctypes.byref(tmp), ctypes.byref(o2)), "ie_unescape_cmd_device")
         if k is not None:
             x.mark(3 * k + 2)
 
@@ -141,9 +247,10 @@ def main():
     x.sync()
     out_bytes = int(d_tot.to_numpy(np.uint64, 1)[0])
     assert out_bytes <= out_cap
-    st_host = d_st.to_numpy(np.uint8, n)
-    n_bad = int(np.count_nonzero(st_host))
-    assert int(np.count_nonzero(st_host == N.STATUS_NAMES.index("E_OVERFLOW"))) == 0, "scratch too small"
+    st_final = (d_st2 if cmd else d_st).to_numpy(np.uint8, n)
+    names = N.STATUS_NAMES
+    status_counts = {names[k]: int(c) for k, c in enumerate(np.bincount(st_final, minlength=len(names))[:len(names)]) if c}
+    assert "E_OVERFLOW" not in status_counts, "scratch too small"
 
     if dist:
         dist.barrier()
@@ -156,37 +263,37 @@ def main():
     if dist:
         dist.barrier()
     wall = time.perf_counter() - t0
-    step_ms = [x.elapsed(3 * k, 3 * k + 1) for k in range(args.steps)]
-    unesc_ms = [x.elapsed(3 * k + 1, 3 * k + 2) for k in range(args.steps)] if unesc else None
+    res_ms = [x.elapsed(3 * k, 3 * k + 1) for k in range(args.steps)]
+    cmd_ms = [x.elapsed(3 * k + 1, 3 * k + 2) for k in range(args.steps)] if cmd else None
     wall_max = max_over_ranks(wall, dist)
 
-    # one timed call with the library's own HIP events for the kernel split
-    x.set_timing(True)
-    N.check(L.ie_interpolate_device(x.h, table, d_in.ptr, d_off.ptr, n, ctypes.byref(o)), "ie_interpolate_device")
+    x.set_timing(True)  # one more call with the library's own events for the telemetry
+    N.check(L.ie_interpolate_device_ids(x.h, W.table, ids, W.d_in.ptr, W.d_off.ptr, n, ctypes.byref(o)), "timing")
     tm = x.timing()
     x.set_timing(False)
 
-    gpu_ms = float(np.mean(step_ms))
-    alg_bytes = in_bytes + out_bytes + 17 * n  # |in| + |out| + 16 (offsets) + 1 (status)
+    gpu_ms = float(np.mean(res_ms))
+    id_bytes = 4 * n if ids is not None else 0
+    alg_bytes = in_bytes + out_bytes + 17 * n + id_bytes  # |in| + |out| + 16 (offsets) + 1 (status)
     achieved_gbs = alg_bytes / (gpu_ms * 1e-3) / 1e9
-    total_in = in_bytes * world
-    value = total_in / wall_max * args.steps / 1e6  # MB/s over all ranks
+    value = in_bytes * world / wall_max * args.steps / 1e6  # MB/s over all ranks
     strings_per_s = n * world * args.steps / wall_max
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(args, L, N, synth, kvp, nkv, d_ooff, d_out, d_st)
+    if rank == 0 and not args.no_cpu:
+        cpu = cpu_baseline(args, W, N, d_ooff2 if cmd else d_ooff, d_out2 if cmd else d_out, d_st2 if cmd else d_st)
 
     traffic = None
-    for name in ("pmc_traffic.json", "pmc_traffic_cfg%d.json" % cfg):  # PMC passes of this workload
-        pmc_path = os.path.join(ROOT, "profiles", name)
-        if traffic is None and os.path.exists(pmc_path):
-            try:
-                pm = json.load(open(pmc_path))
-                if pm.get("config") == cfg and pm.get("n") == n:
-                    traffic = pm.get("hbm_bytes_per_step")
-            except Exception:
-                traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic_cfg%d.json" % cfg)
+    if cfg == 3 and not os.path.exists(pmc_path):
+        pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_path):
+        try:
+            pm = json.load(open(pmc_path))
+            if pm.get("config") == cfg and pm.get("n") == n:
+                traffic = pm.get("hbm_bytes_per_step")
+        except (OSError, ValueError):
+            traffic = None
 
     if rank == 0:
         line = {
@@ -201,74 +308,113 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (SURVEY §8d generator, splitmix64 seed 0x1E5EED00+config, generated in HBM)",
+            "data": "synthetic (SURVEY §8d generators; configs 2-4 splitmix64 seed 0x1E5EED00+config generated in "
+                    "HBM; config 5 seeded states + the reference-recorded call stream)",
             "config": {"workload": WORKLOADS[cfg], "strings_per_gpu": n, "input_bytes_per_gpu": in_bytes,
-                       "output_bytes_per_gpu": out_bytes, "inserts": int(nkv), "parallelism": "shard%d" % world,
-                       "non_ok_statuses": n_bad},
+                       "output_bytes_per_gpu": out_bytes, "inserts": W.inserts, "parallelism": "shard%d" % world,
+                       "statuses": status_counts, "table_build_s": round(W.build_s, 3)},
             "strings_per_s": round(strings_per_s, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "k_resolve (single pass: stage, evaluate, look-back, emit)",
+                         "kernel": "k_resolve (single pass: stage, evaluate, look-back, emit) + k_emit_windows",
                          "launch_ms": round(gpu_ms, 4), "alg_bytes_per_launch": alg_bytes,
                          "telemetry": {"kernel_ms": round(tm.resolve_ms, 4), "literal_strings": int(tm.n_complex),
-                                       "direct_tiles": int(tm.n_direct), "lookback_polls": int(tm.n_polls),
-                                       "exact_strings": int(tm.n_exact)}},
+                                       "windowed_tiles": int(tm.n_direct), "exact_strings": int(tm.n_exact),
+                                       "chain_failures": int(tm.n_chain_fail)}},
             "cpu_baseline": cpu,
         }
-        if unesc:
-            ubytes = int(d_utot.to_numpy(np.uint64, 1)[0])
-            ums = float(np.mean(unesc_ms))
-            ualg = out_bytes + ubytes + 16 * n + n  # read outputs + offsets, write unescaped + offsets + status
-            line["unescape"] = {"kernel_ms": round(ums, 4), "out_bytes": ubytes,
-                                "achieved_gbs": round(ualg / (ums * 1e-3) / 1e9, 1)}
+        if cfg == 5:
+            line["config"]["states_per_gpu"] = n_units
+        if cmd:
+            ub = int(d_utot.to_numpy(np.uint64, 1)[0])
+            ob2 = int(d_tot2.to_numpy(np.uint64, 1)[0])
+            ums = float(np.mean(cmd_ms))
+            ualg = out_bytes + ub + ub + ob2 + 2 * 17 * n  # unescape: read out1, write tmp; interpolate: read tmp, write out2
+            line["unescape_cmd"] = {"ms": round(ums, 4), "unescaped_bytes": ub, "output_bytes": ob2,
+                                    "achieved_gbs": round(ualg / (ums * 1e-3) / 1e9, 1)}
         print(json.dumps(line), flush=True)
-    L.ie_table_free(table)
-    L.ie_synth_free(synth)
+    W.close()
     if dist:
         dist.destroy_process_group()
 
 
-def cpu_baseline(args, L, N, synth, kvp, nkv, d_ooff, d_out, d_st):
-    """The oracle (a literal C restatement of interpolate_inserts) on a bounded sample of the same
-    workload, timed on this host; the sample's GPU results are checked against it."""
+def cpu_baseline(args, W, N, d_ooff, d_out, d_st):
+    """The oracle (a literal C restatement of interpolate_inserts, kind "port") timed on this host
+    over a bounded sample of the same workload, single-thread and on every core of this rank's
+    share; the GPU's results on the sample are checked against it string by string."""
     from oracle import oracle as O
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-    ref = O.Oracle.from_kv(ctypes.cast(kvp, ctypes.c_void_p), nkv, "py", clock=CLOCK)
-
-    def host_sample(m):
-        offs = np.zeros(m + 1, np.uint64)
-        tot = ctypes.c_uint64()
-        N.check(L.ie_synth_strings_host(synth, 0, m, None, 0, offs.ctypes.data, ctypes.byref(tot)), "len")
-        buf = np.zeros(int(tot.value) + 1, np.uint8)
-        N.check(L.ie_synth_strings_host(synth, 0, m, buf.ctypes.data, buf.size, offs.ctypes.data,
-                                        ctypes.byref(tot)), "fill")
-        return buf, offs
-
-    buf, offs = host_sample(20000)  # calibrate single-thread speed
-    dt = ref.run_batch(buf, offs, 20000, 1)
-    per_string = max(dt / 20000, 1e-9)
-    m = int(min(args.n or DEFAULT_N[args.config], max(20000, args.cpu_seconds / per_string)))
-    buf, offs = host_sample(m)
+    threads, model = cpu_share()
+    if args.cpu_threads:
+        threads = args.cpu_threads
+    budget = args.cpu_seconds
+    if args.config == 5:
+        return cpu_baseline_states(args, W, N, d_ooff, d_out, d_st, model, budget)
+    ref = O.Oracle.from_kv(ctypes.cast(W.kvp, ctypes.c_void_p), W.nkv, "py", clock=CLOCK)
+    cmd = args.config == 4
+    buf, offs = W.host_sample(20000)
+    dt1 = ref.run_batch(buf, offs, 20000, 1, unescape_cmd=cmd)  # single-thread calibration
+    per_string = max(dt1 / 20000, 1e-9)
+    m = int(min(W.n, max(20000, budget * 0.5 * threads / per_string)))
+    buf, offs = W.host_sample(m)
+    m1 = int(min(m, max(20000, budget * 0.25 / per_string)))
+    wall1 = ref.run_batch(buf, offs, m1, 1, unescape_cmd=cmd)
     st = np.zeros(m, np.uint8)
     ln = np.zeros(m, np.uint64)
     hs = np.zeros(m, np.uint64)
-    wall = ref.run_batch(buf, offs, m, threads, st, ln, hs, None)
-    sample_bytes = int(offs[m])
-    # parity of the GPU's first m results with the oracle on the same strings
-    gst = d_st.to_numpy(np.uint8, m)
-    goff = d_ooff.to_numpy(np.uint64, m + 1)
-    gout = d_out.to_numpy(np.uint8, int(goff[m])).tobytes()
-    same = bool(np.array_equal(gst, st)) and bool(np.array_equal(np.diff(goff.astype(np.int64)), ln.astype(np.int64)))
-    if same:
-        k = min(m, 20000)
-        gh = np.array([O.fnv1a(gout[int(goff[i]):int(goff[i + 1])]) if gst[i] == 0 else 0 for i in range(k)],
-                      dtype=np.uint64)  # the oracle hashes OK_STR outputs only
-        same = bool(np.array_equal(gh, hs[:k]))
-    return {"value": round(sample_bytes / wall / 1e6, 2), "unit": "MB/s", "cores": threads, "kind": "port",
-            "strings_per_s": round(m / wall, 1),
-            "sample": "first %d strings (%d B) of the same workload; oracle/ie_oracle.c, %d threads, %.2f s wall; "
-                      "GPU output identical on the sample: %s%s" % (m, sample_bytes, threads, wall, same,
-                      "; interpolate_inserts only (the unescape pass is not timed on the CPU)" if args.config == 4 else "")}
+    wall = ref.run_batch(buf, offs, m, threads, st, ln, hs, None, unescape_cmd=cmd)
+    same = compare_sample(N, d_ooff, d_out, d_st, 0, m, st, ln, hs)
+    return {"value": round(int(offs[m]) / wall / 1e6, 2), "unit": "MB/s", "cores": threads, "kind": "port",
+            "value_1t": round(int(offs[m1]) / wall1 / 1e6, 2), "threads_all": threads, "cpu_model": model,
+            "nproc_visible": os.cpu_count(), "strings_per_s": round(m / wall, 1),
+            "sample": "first %d strings (%d B) of this rank's shard, oracle/ie_oracle.c on %d threads (%.2f s), "
+                      "single-thread on the first %d (%.2f s)%s; GPU results identical on all %d: %s"
+                      % (m, int(offs[m]), threads, wall, m1, wall1,
+                         "; each OK result then through the unescape command" if cmd else "", m, same)}
+
+
+def compare_sample(N, d_ooff, d_out, d_st, lo, m, st, ln, hs):
+    """GPU strings [lo, lo+m) against the oracle's statuses, lengths and FNV-1a hashes."""
+    from oracle import oracle as O
+    gst = d_st.to_numpy(np.uint8, lo + m)[lo:]
+    goff = d_ooff.to_numpy(np.uint64, lo + m + 1)[lo:]
+    if not (np.array_equal(gst, st) and np.array_equal(np.diff(goff.astype(np.int64)), ln.astype(np.int64))):
+        return False
+    base = int(goff[0])
+    gout = d_out.to_numpy(np.uint8, int(goff[m]) - base, offset_bytes=base).tobytes()
+    for i in range(m):  # the oracle hashes OK_STR outputs only (0 for status rows)
+        h = O.fnv1a(gout[int(goff[i]) - base:int(goff[i + 1]) - base]) if gst[i] == 0 else 0
+        if h != int(hs[i]):
+            return False
+    return True
+
+
+def cpu_baseline_states(args, W, N, d_ooff, d_out, d_st, model, budget):
+    """Config 5: per state, the oracle over that state's inserts and strings (states in order,
+    single-thread: one oracle table per state is built on the host each time, as the reference
+    interpreter resolves one state at a time)."""
+    from oracle import oracle as O
+    t_start = time.perf_counter()
+    k, nbytes, wall, j = 0, 0, 0.0, 0
+    st_all = np.zeros(W.n, np.uint8)
+    ln_all = np.zeros(W.n, np.uint64)
+    hs_all = np.zeros(W.n, np.uint64)
+    buf = np.frombuffer(W.blob, np.uint8)
+    while j < len(W.states) and time.perf_counter() - t_start < budget:
+        ref = O.Oracle(W.states[j], "py", clock=CLOCK)
+        cnt = int(np.count_nonzero(W.ids == j))
+        offs = np.ascontiguousarray(W.offs[k:k + cnt + 1])
+        s_, l_, h_ = np.zeros(cnt, np.uint8), np.zeros(cnt, np.uint64), np.zeros(cnt, np.uint64)
+        wall += ref.run_batch(buf, offs, cnt, 1, s_, l_, h_)
+        st_all[k:k + cnt], ln_all[k:k + cnt], hs_all[k:k + cnt] = s_, l_, h_
+        nbytes += int(offs[-1] - offs[0])
+        k += cnt
+        j += 1
+    same = compare_sample(N, d_ooff, d_out, d_st, 0, k, st_all[:k], ln_all[:k], hs_all[:k])
+    return {"value": round(nbytes / max(wall, 1e-9) / 1e6, 2), "unit": "MB/s", "cores": 1, "kind": "port",
+            "value_1t": round(nbytes / max(wall, 1e-9) / 1e6, 2), "threads_all": 1, "cpu_model": model,
+            "nproc_visible": os.cpu_count(), "strings_per_s": round(k / max(wall, 1e-9), 1),
+            "sample": "the first %d states (%d strings, %d B), one oracle table per state, single-thread "
+                      "(%.2f s of interpolation); GPU results identical on all: %s" % (j, k, nbytes, wall, same)}
 
 
 if __name__ == "__main__":

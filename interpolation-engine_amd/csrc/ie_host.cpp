@@ -1130,6 +1130,10 @@ int ie_synth_create(int32_t config, uint64_t seed, ie_synth** out) {
       s->keys.push_back("i" + std::to_string(j));
       s->texts.push_back(std::to_string(splitmix(st) % s->P.n_q));
     }
+    // the escaped segment \{lit\} of 10 % of the strings: after the unescape command's
+    // recursive_unescape it is a live {lit} reference, resolved by its recursive_interpolate
+    s->keys.push_back("lit");
+    s->texts.push_back("LIT");
     for (uint32_t j = 0; j < s->P.n_chain; j++) {
       s->keys.push_back("c-" + std::to_string(j));
       std::string head(4, '\0'), tail(4, '\0');

@@ -507,6 +507,7 @@ typedef struct {
   uint64_t* out_len;
   uint64_t* out_hash; /* FNV-1a of each output (0 if not OK_STR) */
   uint32_t* vid;
+  int32_t mode; /* 0: interpolate_inserts; 1: then the `unescape` command on the result (py:1660-1667) */
 } job;
 
 static void* run_job(void* p) {
@@ -514,6 +515,17 @@ static void* run_job(void* p) {
   for (uint64_t i = j->lo; i < j->hi; i++) {
     result r = {0};
     interpolate(j->c, (const char*)j->bytes + j->offsets[i], j->offsets[i + 1] - j->offsets[i], &r, 0);
+    if (j->mode == 1 && r.status == IE_OK_STR) {
+      /* recursive_unescape (py:1665) then recursive_interpolate of the string (py:1666) */
+      sb a = {0}, b = {0};
+      str_replace(&a, r.str.p ? r.str.p : "", r.str.n, ESC_START, 2, "{", 1);
+      str_replace(&b, a.p ? a.p : "", a.n, ESC_STOP, 2, "}", 1);
+      sb_free(&a);
+      sb_free(&r.str);
+      memset(&r, 0, sizeof r);
+      interpolate(j->c, b.p ? b.p : "", b.n, &r, 0);
+      sb_free(&b);
+    }
     if (j->status) j->status[i] = (uint8_t)r.status;
     if (j->out_len) j->out_len[i] = r.status == IE_OK_STR ? r.str.n : 0;
     if (j->out_hash) j->out_hash[i] = r.status == IE_OK_STR ? fnv(r.str.p ? r.str.p : "", r.str.n) : 0;
@@ -524,9 +536,9 @@ static void* run_job(void* p) {
 }
 
 /* returns wall seconds; threads split the batch into contiguous, byte-balanced shards */
-double ieo_run_batch(const ieo_ctx* c, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
-                     int32_t nthreads, uint8_t* status, uint64_t* out_len, uint64_t* out_hash,
-                     uint32_t* vid) {
+double ieo_run_batch_mode(const ieo_ctx* c, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                          int32_t nthreads, uint8_t* status, uint64_t* out_len, uint64_t* out_hash,
+                          uint32_t* vid, int32_t mode) {
   if (nthreads < 1) nthreads = 1;
   if (nthreads > 256) nthreads = 256;
   job jobs[256];
@@ -546,7 +558,7 @@ double ieo_run_batch(const ieo_ctx* c, const uint8_t* bytes, const uint64_t* off
       }
       hi = a;
     }
-    jobs[t] = (job){c, bytes, offsets, lo, hi, status, out_len, out_hash, vid};
+    jobs[t] = (job){c, bytes, offsets, lo, hi, status, out_len, out_hash, vid, mode};
     lo = hi;
   }
   struct timespec t0, t1;
@@ -555,6 +567,12 @@ double ieo_run_batch(const ieo_ctx* c, const uint8_t* bytes, const uint64_t* off
   for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
   clock_gettime(CLOCK_MONOTONIC, &t1);
   return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
+double ieo_run_batch(const ieo_ctx* c, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                     int32_t nthreads, uint8_t* status, uint64_t* out_len, uint64_t* out_hash,
+                     uint32_t* vid) {
+  return ieo_run_batch_mode(c, bytes, offsets, n, nthreads, status, out_len, out_hash, vid, 0);
 }
 
 uint64_t ieo_fnv1a(const uint8_t* p, uint64_t n) { return fnv((const char*)p, n); }

@@ -69,6 +69,8 @@ def lib():
         L.ieo_run_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                     ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_void_p]
+        L.ieo_run_batch_mode.restype = ctypes.c_double
+        L.ieo_run_batch_mode.argtypes = L.ieo_run_batch.argtypes + [ctypes.c_int32]
         L.ieo_fnv1a.restype = ctypes.c_uint64
         L.ieo_fnv1a.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
         _lib = L
@@ -155,12 +157,14 @@ class Oracle:
         lib().ieo_out_free(ctypes.byref(o))
         return st, out, vid
 
-    def run_batch(self, bytes_arr, offsets_arr, n, nthreads=1, status=None, out_len=None, out_hash=None, vid=None):
-        """numpy arrays in/out; returns wall seconds."""
+    def run_batch(self, bytes_arr, offsets_arr, n, nthreads=1, status=None, out_len=None, out_hash=None, vid=None,
+                  unescape_cmd=False):
+        """numpy arrays in/out; returns wall seconds. unescape_cmd: each OK result then goes through
+        the `unescape` command (unescape, interpolate again: py:1660-1667), as config 4's step."""
         def p(a):
             return None if a is None else a.ctypes.data
-        return lib().ieo_run_batch(self.h, p(bytes_arr), p(offsets_arr), n, nthreads,
-                                   p(status), p(out_len), p(out_hash), p(vid))
+        return lib().ieo_run_batch_mode(self.h, p(bytes_arr), p(offsets_arr), n, nthreads,
+                                        p(status), p(out_len), p(out_hash), p(vid), 1 if unescape_cmd else 0)
 
 
 def escape(s, unescape=False):

@@ -433,13 +433,55 @@ def test_full_size_config3_properties():
     N.lib().ie_table_free(table)
 
 
+def _unescape_cmd(x, table, r, n, cap):
+    """The `unescape` command (py:1660-1667) over a resolved batch r: recursive_unescape, then
+    recursive_interpolate; strings that failed in r keep their status."""
+    tmp = DevResult(x, n, cap)
+    out = DevResult(x, n, cap)
+    N.check(N.lib().ie_unescape_cmd_device(x.h, table, None, r.bytes.ptr, r.off.ptr, n, r.status.ptr,
+                                           ctypes.byref(tmp.out), ctypes.byref(out.out)), "ie_unescape_cmd_device")
+    x.sync()
+    return tmp, out
+
+
+def test_config4_step_vs_oracle(fail_commit):
+    """Config 4's whole step on 200k strings, string for string against the oracle running
+    interpolate, then the unescape command (unescape, interpolate again: py:1660-1667)."""
+    h, kvp, nkv = _synth(4)
+    table = _table_from_kv(kvp, nkv)
+    x = N.Exec(0)
+    n = 200_000
+    buf, offs = _host_strings(h, 5_000_000, n)
+    d_bytes = N.DeviceBuffer.from_numpy(x, buf)
+    d_off = N.DeviceBuffer.from_numpy(x, offs)
+    r = _device_run(x, table, d_bytes, d_off, n)
+    _, u = _unescape_cmd(x, table, r, n, 2 * r.total() + 4096)
+    ref = O.Oracle.from_kv(ctypes.cast(kvp, ctypes.c_void_p), nkv, "py", clock=CLOCK)
+    rst = np.zeros(n, np.uint8)
+    rlen = np.zeros(n, np.uint64)
+    rhash = np.zeros(n, np.uint64)
+    ref.run_batch(buf, offs, n, 8, rst, rlen, rhash, None, unescape_cmd=True)
+    st = u.status.to_numpy(np.uint8, n)
+    oo = u.off.to_numpy(np.uint64, n + 1)
+    ob = u.bytes.to_numpy(np.uint8, u.total()).tobytes()
+    assert np.array_equal(st, rst)
+    assert np.array_equal(np.diff(oo.astype(np.int64)), rlen.astype(np.int64))
+    hashes = np.array([O.fnv1a(ob[int(oo[i]):int(oo[i + 1])]) if st[i] == 0 else 0 for i in range(n)],
+                      dtype=np.uint64)
+    assert np.array_equal(hashes, rhash)
+    # the escaped {lit} of ~10 % of the strings is live after the unescape and resolves to LIT
+    assert 0.08 < ob.count(b"LIT") / n < 0.12
+    N.lib().ie_table_free(table)
+
+
 def test_full_size_config4_properties():
     """Config 4 at its per-GPU size (100M strings sharded 8 ways = 12.5M; this is rank 3's shard):
-    mixed-depth chains, escapes, brace-bearing values and misses, then the unescape pass
-    (recursive_unescape py:1448-1460) over the outputs. Properties: statuses are OK_STR or
-    E_INTERP only, misses ~1 %, OK outputs carry no unescaped brace, the unescaped outputs carry
-    no backslash-brace pair and equal the resolved ones with the escapes removed; plus a sampled
-    oracle check of both passes."""
+    mixed-depth chains, escapes, brace-bearing values and misses, then the `unescape` command
+    (recursive_unescape, then recursive_interpolate: py:1660-1667) over the outputs. Properties:
+    statuses are OK_STR or E_INTERP only, misses ~1 %, the unescaped text is the resolved text with
+    every backslash-brace pair's backslash removed, the command's outputs carry no brace (the
+    un-escaped {lit} resolved again), idempotence of the second resolve; plus a sampled oracle
+    check of both passes."""
     h, kvp, nkv = _synth(4)
     table = _table_from_kv(kvp, nkv)
     x = N.Exec(0)
@@ -458,17 +500,19 @@ def test_full_size_config4_properties():
     oo = r.off.to_numpy(np.uint64, n + 1)
     assert int(oo[-1]) == tot and np.all(np.diff(oo.astype(np.int64)) >= 0)
     ob = r.bytes.to_numpy(np.uint8, tot)
-    # unescape pass over the resolved batch
-    u = DevResult(x, n, tot + 4096)
-    N.check(N.lib().ie_unescape_device(x.h, r.bytes.ptr, r.off.ptr, n, ctypes.byref(u.out)), "unescape")
-    x.sync()
-    utot = u.total()
-    ub = u.bytes.to_numpy(np.uint8, utot)
-    uo = u.off.to_numpy(np.uint64, n + 1)
+    tmp, u = _unescape_cmd(x, table, r, n, tot + 4096)
+    utot = tmp.total()
+    ub = tmp.bytes.to_numpy(np.uint8, utot)
     n_esc = int(np.count_nonzero((ob[:-1] == ord("\\")) & (ob[1:] == ord("{"))))
     n_esc += int(np.count_nonzero((ob[:-1] == ord("\\")) & (ob[1:] == ord("}"))))
     assert n_esc > 0 and utot == tot - n_esc
     assert int(np.count_nonzero(ub == ord("\\"))) == 0
+    ust = u.status.to_numpy(np.uint8, n)
+    assert np.array_equal(ust, st)  # the un-escaped {lit} always resolves; failures carry through
+    uo = u.off.to_numpy(np.uint64, n + 1)
+    ftot = u.total()
+    fb = u.bytes.to_numpy(np.uint8, ftot)
+    assert int(np.count_nonzero(fb == ord("{"))) == 0 and int(np.count_nonzero(fb == ord("}"))) == 0
     rng = np.random.default_rng(4)
     ref = O.Oracle.from_kv(ctypes.cast(kvp, ctypes.c_void_p), nkv, "py", clock=CLOCK)
     for i in np.sort(rng.choice(n, 500, replace=False)):
@@ -477,8 +521,9 @@ def test_full_size_config4_properties():
         assert rs == names[st[i]]
         if rs == "OK_STR":
             assert ob[int(oo[i]):int(oo[i + 1])].tobytes().decode("utf-8") == rout
-            un = rout.replace("\\{", "{").replace("\\}", "}")
-            assert ub[int(uo[i]):int(uo[i + 1])].tobytes().decode("utf-8") == un
+            rs2, rout2, _ = ref.interpolate(rout.replace("\\{", "{").replace("\\}", "}").encode())
+            assert rs2 == "OK_STR"
+            assert fb[int(uo[i]):int(uo[i + 1])].tobytes().decode("utf-8") == rout2
     N.lib().ie_table_free(table)
 
 

@@ -29,7 +29,7 @@ __device__ __forceinline__ uint4 gld4(const uint4* p) { const u32x4 v = *(const 
 __device__ __forceinline__ void gst4(uint4* p, uint4 v) { u32x4 w; w.x=v.x; w.y=v.y; w.z=v.z; w.w=v.w; *(__attribute__((address_space(1))) u32x4*)(void*)p = w; }
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
-struct Args { const uint8_t* in; const uint64_t* off; uint64_t n; uint8_t* out; uint64_t* ooff; uint8_t* st; uint64_t* state; uint32_t* err; uint64_t* stamps; };
+struct Args { const uint8_t* in; const uint64_t* off; uint64_t n; uint8_t* out; uint64_t* ooff; uint8_t* st; uint64_t* state; uint32_t* err; uint64_t* stamps; uint64_t* sstate; };
 __device__ uint32_t g_polls;
 
 constexpr uint64_t kFlagAgg = 1ull << 62, kFlagIncl = 2ull << 62, kValMask = (1ull << 62) - 1;
@@ -153,6 +153,53 @@ __device__ uint64_t look_back_rows(uint64_t* state, uint32_t tile, uint64_t agg,
   if (lane == 0) publish(state, tile, kFlagIncl | (excl + agg));
   return excl;
 }
+// two-level look-back: tiles publish only aggregates; the last tile of each super-tile of 64
+// publishes the super-tile's aggregate, then its inclusive prefix. A tile's exclusive prefix =
+// (the aggregates of its super-tile's earlier tiles: one 64-word window) + (the super-tile's
+// exclusive prefix: a look-back over super words, 64 super-tiles = 4096 tiles per poll).
+constexpr uint32_t kSuper = 64;
+__device__ uint32_t g_polls2;
+template <int NAPMAX>
+__device__ uint64_t look_back2(uint64_t* state, uint64_t* sstate, uint32_t tile, uint32_t ntiles, uint64_t agg, uint32_t* err) {
+  const uint32_t lane = lane_id();
+  const uint32_t S = tile / kSuper, j = tile % kSuper;
+  const bool last = j == kSuper - 1 || tile == ntiles - 1;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  // in-super prefix: tiles S*64 .. tile-1 (lane l reads tile-1-l, l < j)
+  uint64_t in_s = 0, ex_s = 0;
+  bool have_in = j == 0, have_ex = S == 0;
+  int64_t spos = (int64_t)S - 1;
+  uint32_t nap = 1, npoll = 0;
+  for (;;) {
+    uint64_t w = 0, v = 0;
+    if (!have_in) w = lane < j ? __hip_atomic_load(state + tile - 1 - lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFlagAgg;
+    if (!have_ex) v = spos - (int64_t)lane >= 0 ? __hip_atomic_load(sstate + spos - lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFlagIncl;
+    bool again = false;
+    if (!have_in) {
+      if (__ballot((w >> 62) == 0)) again = true;
+      else { in_s = w_sum(w & kValMask); have_in = true;
+        if (last && lane == 0) publish(sstate, S, (S == 0 ? kFlagIncl : kFlagAgg) | (in_s + agg)); }
+    }
+    if (!have_ex) {
+      const uint64_t flag = v >> 62;
+      const uint64_t incl_m = __ballot(flag == 2), wait_m = __ballot(flag == 0);
+      const uint32_t first = incl_m ? (uint32_t)__builtin_ctzll(incl_m) : 64u;
+      const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);
+      if (wait_m & need) again = true;
+      else { ex_s += w_sum(lane <= first ? (v & kValMask) : 0ull); if (first < 64) have_ex = true; else spos -= 64; }
+    }
+    if (have_in && have_ex) break;
+    if (again) {
+      npoll++;
+      for (uint32_t k = 0; k < nap; k++) __builtin_amdgcn_s_sleep(1);
+      nap = nap < NAPMAX ? 2 * nap : NAPMAX;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) { if (lane == 0) atomicOr(err, 1u); break; }
+    }
+  }
+  if (last && S > 0 && lane == 0) publish(sstate, S, kFlagIncl | (ex_s + in_s + agg));
+  if (lane == 0 && npoll) atomicAdd(&g_polls2, npoll);
+  return ex_s + in_s;
+}
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
   const uint32_t lane = lane_id();
   for (int d = 1; d < 64; d <<= 1) { const uint64_t t = __shfl_up(v, d, 64); if (lane >= (uint32_t)d) v += t; }
@@ -241,7 +288,7 @@ __global__ __launch_bounds__(kBlock) void kA(Args a) {
   if (i < a.n) { so = gld(a.off + i); sn = gld(a.off + i + 1) - so; }
   uint64_t early0 = 0;
   if (EARLYPUB && wave == 0) {  // the aggregate is known from the offsets alone (verbatim copy)
-    if (lane_id() == 0) publish(a.state, tile, (tile == 0 ? kFlagIncl : kFlagAgg) | (hi - lo));
+    if (lane_id() == 0) publish(a.state, tile, (tile == 0 && LBW != 2 ? kFlagIncl : kFlagAgg) | (hi - lo));
     if (EARLYPUB == 2 && tile) early0 = lb_poll(a.state, (int64_t)tile - 1);
   }
   const uintptr_t plo = (uintptr_t)(a.in + lo); const uint32_t shift = plo & 15;
@@ -257,12 +304,12 @@ __global__ __launch_bounds__(kBlock) void kA(Args a) {
   uint64_t tot; const uint64_t local = block_scan<false>(sn, s_red, &tot);
   uint64_t early = 0;
   if (LB && wave == 0) {
-    if (!EARLYPUB && lane_id() == 0) publish(a.state, tile, (tile == 0 ? kFlagIncl : kFlagAgg) | tot);
-    if (tile) early = EARLYPUB == 2 ? early0 : lb_poll(a.state, (int64_t)tile - 1);
+    if (!EARLYPUB && lane_id() == 0) publish(a.state, tile, (tile == 0 && LBW != 2 ? kFlagIncl : kFlagAgg) | tot);
+    if (tile && LBW != 2) early = EARLYPUB == 2 ? early0 : lb_poll(a.state, (int64_t)tile - 1);
   }
   if (BUILD && __any(sn != 0)) lds_copy((lds_u8*)s_out + local, (const lds_u8*)s_in + shift + (so - lo), (uint32_t)sn);
   const uint64_t tlb0 = __builtin_amdgcn_s_memrealtime();
-  if (LB && wave == 0) { const uint64_t b = LBW == 4 ? look_back4<SLEEP>(a.state, tile, tot, a.err) : LBW > 4 ? look_back_rows<(LBW >= 64 ? LBW / 64 : 1), SLEEP>(a.state, tile, tot, a.err, early) : look_back(a.state, tile, tot, a.err, early); if (tid == 0) s_red[4] = b; }
+  if (LB && wave == 0) { const uint64_t b = LBW == 2 ? look_back2<SLEEP>(a.state, a.sstate, tile, (uint32_t)((a.n + kBlock - 1) / kBlock), tot, a.err) : LBW == 4 ? look_back4<SLEEP>(a.state, tile, tot, a.err) : LBW > 4 ? look_back_rows<(LBW >= 64 ? LBW / 64 : 1), SLEEP>(a.state, tile, tot, a.err, early) : look_back(a.state, tile, tot, a.err, early); if (tid == 0) s_red[4] = b; }
   if (!LB && tid == 0) s_red[4] = lo;
   __syncthreads();
   const uint64_t base = s_red[4];
@@ -360,11 +407,11 @@ int main(int argc, char** argv) {
   uint8_t *din, *dout, *dst; uint64_t *doff, *dooff, *dstate; uint32_t* derr;
   const uint64_t ntiles = (n + kBlock - 1) / kBlock;
   CHECK(hipMalloc(&din, tot + 64)); CHECK(hipMalloc(&dout, tot + 64)); CHECK(hipMalloc(&dst, n + 16));
-  CHECK(hipMalloc(&doff, (n + 1) * 8)); CHECK(hipMalloc(&dooff, (n + 1) * 8)); CHECK(hipMalloc(&dstate, ntiles * 8)); CHECK(hipMalloc(&derr, 4));
+  CHECK(hipMalloc(&doff, (n + 1) * 8)); CHECK(hipMalloc(&dooff, (n + 1) * 8)); CHECK(hipMalloc(&dstate, ntiles * 8)); uint64_t* dsstate; CHECK(hipMalloc(&dsstate, (ntiles / kSuper + 2) * 8)); CHECK(hipMalloc(&derr, 4));
   CHECK(hipMemcpy(din, in.data(), tot, hipMemcpyHostToDevice)); CHECK(hipMemcpy(doff, off.data(), (n + 1) * 8, hipMemcpyHostToDevice));
   CHECK(hipMemset(derr, 0, 4));
   uint64_t* dstamps; CHECK(hipMalloc(&dstamps, ntiles * 32));
-  a = Args{din, doff, n, dout, dooff, dst, dstate, derr, nullptr};
+  a = Args{din, doff, n, dout, dooff, dst, dstate, derr, nullptr, dsstate};
   int dev = 0, cus = 0; CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   int occB = 0; CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occB, kB, kBlock, 0));
   int occA = 0; CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occA, kA<true, true>, kBlock, 0));
@@ -375,7 +422,7 @@ int main(int argc, char** argv) {
   auto run = [&](const char* name, auto launch) {
     float sum = 0, best = 1e9;
     for (int r = 0; r < reps + 2; r++) {
-      CHECK(hipMemsetAsync(dstate, 0, ntiles * 8)); CHECK(hipMemsetAsync(dout, 0, 64));
+      CHECK(hipMemsetAsync(dstate, 0, ntiles * 8)); CHECK(hipMemsetAsync(dsstate, 0, (ntiles / kSuper + 2) * 8)); CHECK(hipMemsetAsync(dout, 0, 64));
       CHECK(hipEventRecord(e0)); launch(); CHECK(hipEventRecord(e1)); CHECK(hipEventSynchronize(e1));
       float ms; CHECK(hipEventElapsedTime(&ms, e0, e1));
       if (r >= 2) { best = ms < best ? ms : best; sum += ms; }
@@ -390,7 +437,7 @@ int main(int argc, char** argv) {
   const uint32_t gA = (uint32_t)ntiles;
   auto stamped = [&](const char* name, auto launch) {
     a.stamps = dstamps; uint32_t z = 0; CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_polls), &z, 4));
-    CHECK(hipMemsetAsync(dstate, 0, ntiles * 8)); launch(); CHECK(hipDeviceSynchronize());
+    CHECK(hipMemsetAsync(dstate, 0, ntiles * 8)); CHECK(hipMemsetAsync(dsstate, 0, (ntiles / kSuper + 2) * 8)); launch(); CHECK(hipDeviceSynchronize());
     std::vector<uint64_t> h(ntiles * 4); CHECK(hipMemcpy(h.data(), dstamps, ntiles * 32, hipMemcpyDeviceToHost));
     uint32_t polls; CHECK(hipMemcpyFromSymbol(&polls, HIP_SYMBOL(g_polls), 4));
     double pre = 0, lb = 0, post = 0; uint64_t t0 = ~0ull, t1 = 0;
@@ -402,6 +449,11 @@ int main(int argc, char** argv) {
   stamped("lookback+build", [&] { hipLaunchKernelGGL((kA<true, true>), dim3(gA), dim3(kBlock), 0, 0, a); });
   stamped("early publish, poll late", [&] { hipLaunchKernelGGL((kA<true, true, 1, 1, 1>), dim3(gA), dim3(kBlock), 0, 0, a); });
   stamped("no lookback", [&] { hipLaunchKernelGGL((kA<false, true>), dim3(gA), dim3(kBlock), 0, 0, a); });
+  stamped("2level+build", [&] { hipLaunchKernelGGL((kA<true, true, 2, 32>), dim3(gA), dim3(kBlock), 0, 0, a); });
+  run("A 2level nap32 +build", [&] { hipLaunchKernelGGL((kA<true, true, 2, 32>), dim3(gA), dim3(kBlock), 0, 0, a); });
+  run("A 2level nap4 +build", [&] { hipLaunchKernelGGL((kA<true, true, 2, 4>), dim3(gA), dim3(kBlock), 0, 0, a); });
+  run("A 2level nap1 +build", [&] { hipLaunchKernelGGL((kA<true, true, 2, 1>), dim3(gA), dim3(kBlock), 0, 0, a); });
+  run("A 2level early publish", [&] { hipLaunchKernelGGL((kA<true, true, 2, 4, 1>), dim3(gA), dim3(kBlock), 0, 0, a); });
   run("A lookback+build", [&] { hipLaunchKernelGGL((kA<true, true>), dim3(gA), dim3(kBlock), 0, 0, a); });
   run("A early publish, poll late", [&] { hipLaunchKernelGGL((kA<true, true, 1, 1, 1>), dim3(gA), dim3(kBlock), 0, 0, a); });
   run("A early publish+poll", [&] { hipLaunchKernelGGL((kA<true, true, 1, 1, 2>), dim3(gA), dim3(kBlock), 0, 0, a); });
