@@ -9,11 +9,14 @@
  *     get_simple_insertkey(content)                py:477-495   -> ie_simple_insertkey
  *     recursive_unescape / recursive_escape        py:1436-1460 -> ie_unescape_batch / ie_escape_batch
  *     InterpolationException / AssertionError      py:426, 519, 530 -> ie_status codes
+ *     is_wildcard_match / get_wildcard_matches     py:553-567   -> ie_wildcards_build + ie_wildcard_match_*
  *   Rust    rust-project/src/interp.rs
  *     interpolate_inserts(&Map, &str, &ctx)        interp.rs:31-89  -> ie_interpolate (dialect IE_DIALECT_RS)
  *     get_interpdata                               interp.rs:91-137 -> ie_table_build
  *     get_simple_insertkey                         interp.rs:11-29  -> ie_simple_insertkey
  *     recursive_unescape / recursive_escape        interp.rs:147-177 -> ie_unescape_batch / ie_escape_batch
+ *   Rust    rust-project/src/runtime.rs
+ *     wildcard match / captures                    runtime.rs:1633-1647, 1754-1775 -> ie_wildcard_match_*
  *
  * Plain pointers and sizes only; no torch or HIP types appear in a signature (streams are void*).
  * Every entry point returns 0 (IE_SUCCESS) or a negative IE_ERR_* code; ie_last_error() gives text.
@@ -241,6 +244,26 @@ int ie_escape_batch(ie_exec* x, const uint8_t* bytes, const uint64_t* offsets, u
                     ie_batch** out);
 
 void ie_batch_free(ie_batch* b);
+
+/* ---- wildcard match / capture (py:553-567 is_wildcard_match / get_wildcard_matches; the matcher
+ * of goto_map / replace_map / delete_except, py:1688-1773; rust-project/src/runtime.rs:1633-1647,
+ * 1754-1775). A wildcard is literal text with '*' (and, as in the reference, U+3020) standing for
+ * a DOTALL greedy group; the match is anchored at both ends ('$' also before a trailing '\n').
+ * ie_wildcards_build compiles a LIST of wildcards (packed UTF-8, offsets[n_patterns + 1]) onto a
+ * device. ie_wildcard_match_*: for each string i, the FIRST wildcard p of the list (or of
+ * [range[2i], range[2i+1]) when range is given) that matches; match[i] = p or -1, ncap[i] the
+ * number of captures and caps[i * 2 * IE_WC_MAX_CAP + 2c .. +1] = {byte start, byte length} of
+ * capture c within string i (re.findall's groups; a wildcard without '*' captures its whole match,
+ * as re.findall returns it). Wildcards with more than IE_WC_MAX_CAP groups are rejected. ---- */
+#define IE_WC_MAX_CAP 16
+typedef struct ie_wildcards ie_wildcards;
+int ie_wildcards_build(const uint8_t* bytes, const uint64_t* offsets, uint32_t n_patterns, int32_t device,
+                       ie_wildcards** out);
+void ie_wildcards_free(ie_wildcards* w);
+int ie_wildcard_match_device(ie_exec* x, const ie_wildcards* w, const uint8_t* d_bytes, const uint64_t* d_offsets,
+                             uint64_t n, const uint32_t* d_range, int32_t* d_match, uint8_t* d_ncap, uint32_t* d_caps);
+int ie_wildcard_match_batch(ie_exec* x, const ie_wildcards* w, const uint8_t* bytes, const uint64_t* offsets,
+                            uint64_t n, const uint32_t* range, int32_t* match, uint8_t* ncap, uint32_t* caps);
 
 /* ---- get_simple_insertkey (py:477-495 / interp.rs:11-29), host-side classifier used by the
  * callers' control flow (recursive_interpolate, validate_program). Returns 1 when the reference

@@ -19,5 +19,6 @@ from .interpolation_engine import (  # noqa: F401
     recursive_interpolate,
     recursive_unescape,
 )
+from .wildcard import Wildcards, get_wildcard_matches, is_wildcard_match  # noqa: F401
 
 __version__ = "0.1.0"

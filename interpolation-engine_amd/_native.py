@@ -35,7 +35,9 @@ EXPORTS = [
     "ie_batch_free", "ie_simple_insertkey",
     "ie_synth_create", "ie_synth_free", "ie_synth_kv", "ie_synth_strings_host",
     "ie_synth_strings_device", "ie_debug_probe",
+    "ie_wildcards_build", "ie_wildcards_free", "ie_wildcard_match_device", "ie_wildcard_match_batch",
 ]
+WC_MAX_CAP = 16
 
 
 class KV(ctypes.Structure):
@@ -119,6 +121,10 @@ def lib():
         "ie_escape_batch": (ctypes.c_int, [vp, vp, vp, u64, ctypes.POINTER(ctypes.POINTER(BatchRes))]),
         "ie_batch_free": (None, [ctypes.POINTER(BatchRes)]),
         "ie_simple_insertkey": (ctypes.c_int, [ctypes.c_char_p, u64, i32, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
+        "ie_wildcards_build": (ctypes.c_int, [vp, vp, u32, i32, pvp]),
+        "ie_wildcards_free": (None, [vp]),
+        "ie_wildcard_match_device": (ctypes.c_int, [vp, vp, vp, vp, u64, vp, vp, vp, vp]),
+        "ie_wildcard_match_batch": (ctypes.c_int, [vp, vp, vp, vp, u64, vp, vp, vp, vp]),
         "ie_synth_create": (ctypes.c_int, [i32, u64, pvp]),
         "ie_synth_free": (None, [vp]),
         "ie_synth_kv": (u64, [vp, ctypes.POINTER(ctypes.POINTER(KV))]),

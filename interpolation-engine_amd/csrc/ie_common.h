@@ -72,9 +72,6 @@ IE_HD uint32_t ph_slot(uint64_t h, uint32_t pilot, uint32_t m) {
   return (uint32_t)(((uint64_t)fmix32((uint32_t)h ^ (pilot * 0x9E3779B9u)) * m) >> 32);
 }
 
-// pilot groups the kernel keeps in LDS (12 KB), and the largest table sized for it
-constexpr uint32_t kLdsPilots = 6144;
-constexpr uint32_t kLdsPilotKeys = 20 * kLdsPilots;
 
 // Entry.flags
 enum : uint32_t {

@@ -114,14 +114,15 @@ struct ie_exec {
   // workspace
   DevBuf counters, tile_state, pool, out_len, tile_sum, tile_base, defer_tiles, defer_desc;
   // host-API staging
-  DevBuf in_bytes, in_off, in_tid, o_bytes, o_off, o_status, o_vid, o_total;
+  DevBuf in_bytes, in_off, in_tid, o_bytes, o_off, o_status, o_vid, o_total, wc_range, wc_match, wc_ncap, wc_caps;
   // synth scratch
   DevBuf s_lens, s_part;
   DevBuf stamps;        // diagnostic phase stamps (env IE_DEBUG_STAMPS=<file>)
   uint64_t stamp_tiles = 0;
   ~ie_exec() {
     for (DevBuf* b : {&counters, &tile_state, &pool, &out_len, &tile_sum, &tile_base, &defer_tiles, &defer_desc, &in_bytes,
-                      &in_off, &in_tid, &o_bytes, &o_off, &o_status, &o_vid, &o_total, &s_lens, &s_part, &stamps})
+                      &in_off, &in_tid, &o_bytes, &o_off, &o_status, &o_vid, &o_total, &wc_range, &wc_match, &wc_ncap, &wc_caps,
+                      &s_lens, &s_part, &stamps})
       b->release();
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
@@ -130,6 +131,16 @@ struct ie_exec {
     if (stat_ev) (void)hipEventDestroy(stat_ev);
     if (stat_host) (void)hipHostFree(stat_host);
     if (own_stream && stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+struct ie_wildcards {
+  int32_t device = 0;
+  uint32_t n_pat = 0;
+  DevBuf bytes, lit_off, lit_len, pat_lit;
+  WcSet dev{};
+  ~ie_wildcards() {
+    for (DevBuf* b : {&bytes, &lit_off, &lit_len, &pat_lit}) b->release();
   }
 };
 
@@ -542,18 +553,12 @@ int upload_table(const std::vector<Ent>& ents, uint32_t n_tables, int32_t dialec
     memcpy(b.text, e.text.data(), std::min<size_t>(e.text.size(), kInlineText));
     items.push_back(b);
   }
-  // perfect-hash placement. About 4 keys per pilot group at load 0.8; a table too large for that
-  // within kLdsPilots groups but at most kLdsPilotKeys keys packs its keys into kLdsPilots groups
-  // (up to 20 keys each) at load 0.5, where the last, smallest groups still find a pilot. A failed
-  // search changes the seed (two keys with one 64-bit hash can never be separated) and then grows
-  // the table.
+  // perfect-hash placement: about 4 keys per pilot group at load 0.8 (entries 64 B: a 100k-key
+  // table is 8 MB of entries and 50 KB of L2-resident pilots). A failed search changes the seed
+  // (two keys with one 64-bit hash can never be separated) and then grows the table.
   const uint64_t nk = items.size();
-  uint32_t nb = (uint32_t)std::max<uint64_t>(1, (nk + 3) / 4);
+  const uint32_t nb = (uint32_t)std::max<uint64_t>(1, (nk + 3) / 4);
   uint64_t m = std::max<uint64_t>(16, nk + nk / 4 + 1);
-  if (nb > kLdsPilots && nk <= kLdsPilotKeys) {
-    nb = kLdsPilots;
-    m = 2 * nk;
-  }
   uint64_t seed = 0xA0761D6478BD642Full;
   std::vector<uint16_t> pilots;
   std::vector<uint32_t> slot_of;
@@ -1045,6 +1050,109 @@ int ie_unescape_batch(ie_exec* x, const uint8_t* bytes, const uint64_t* offsets,
 int ie_escape_batch(ie_exec* x, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
                     ie_batch** out) {
   return run_host(x, kOpEscape, nullptr, bytes, offsets, n, out);
+}
+
+// ---- wildcard match / capture (py:553-567; ie_wildcard.hip) ----
+// A wildcard compiles to its literals: the text between consecutive group markers, where a marker
+// is '*' or U+3020 (the reference's w.replace('*', '〠') then '〠' -> '(.*)', so a literal U+3020
+// is a group as well); re.escape makes every other byte literal.
+int ie_wildcards_build(const uint8_t* bytes, const uint64_t* offsets, uint32_t n_patterns, int32_t device,
+                       ie_wildcards** out) {
+  if (!out || (n_patterns && (!offsets || (!bytes && offsets[n_patterns])))) return fail(IE_ERR_INVALID, "null argument");
+  *out = nullptr;
+  int rc = set_device(device);
+  if (rc) return rc;
+  std::vector<uint32_t> lit_off, lit_len, pat_lit;
+  const uint64_t base = n_patterns ? offsets[0] : 0;
+  for (uint32_t p = 0; p < n_patterns; p++) {
+    pat_lit.push_back((uint32_t)lit_off.size());
+    const uint64_t a = offsets[p] - base, b = offsets[p + 1] - base;
+    if (b < a || b >= 0xFFFFFFF0ull) return fail(IE_ERR_INVALID, "bad wildcard offsets");
+    uint64_t start = a;
+    uint32_t groups = 0;
+    for (uint64_t k = a; k < b;) {
+      const uint8_t* c = bytes + base + k;
+      const uint32_t mk = c[0] == '*' ? 1u : (k + 2 < b && c[0] == 0xE3 && c[1] == 0x80 && c[2] == 0xA0) ? 3u : 0u;
+      if (!mk) {
+        k++;
+        continue;
+      }
+      lit_off.push_back((uint32_t)start);
+      lit_len.push_back((uint32_t)(k - start));
+      groups++;
+      k += mk;
+      start = k;
+    }
+    lit_off.push_back((uint32_t)start);
+    lit_len.push_back((uint32_t)(b - start));
+    if (groups > IE_WC_MAX_CAP) return fail(IE_ERR_INVALID, "wildcard with more than IE_WC_MAX_CAP groups");
+  }
+  pat_lit.push_back((uint32_t)lit_off.size());
+  ie_wildcards* w = new ie_wildcards();
+  w->device = device;
+  w->n_pat = n_patterns;
+  const uint64_t nb = n_patterns ? offsets[n_patterns] - base : 0;
+  auto up = [&](DevBuf& d, const void* src, uint64_t n) -> hipError_t {
+    hipError_t e = d.ensure(n + 16);
+    return e != hipSuccess ? e : n ? hipMemcpy(d.p, src, n, hipMemcpyHostToDevice) : hipSuccess;
+  };
+  hipError_t e = up(w->bytes, bytes ? bytes + base : nullptr, nb);
+  if (e == hipSuccess) e = up(w->lit_off, lit_off.data(), lit_off.size() * 4);
+  if (e == hipSuccess) e = up(w->lit_len, lit_len.data(), lit_len.size() * 4);
+  if (e == hipSuccess) e = up(w->pat_lit, pat_lit.data(), pat_lit.size() * 4);
+  if (e != hipSuccess) {
+    delete w;
+    return fail(IE_ERR_HIP, std::string("wildcard upload: ") + hipGetErrorString(e));
+  }
+  w->dev = WcSet{(const uint8_t*)w->bytes.p, (const uint32_t*)w->lit_off.p, (const uint32_t*)w->lit_len.p,
+                 (const uint32_t*)w->pat_lit.p, n_patterns};
+  *out = w;
+  return IE_SUCCESS;
+}
+
+void ie_wildcards_free(ie_wildcards* w) { delete w; }
+
+int ie_wildcard_match_device(ie_exec* x, const ie_wildcards* w, const uint8_t* d_bytes, const uint64_t* d_offsets,
+                             uint64_t n, const uint32_t* d_range, int32_t* d_match, uint8_t* d_ncap, uint32_t* d_caps) {
+  if (!x || !w || !d_offsets || !d_match || !d_ncap || !d_caps || (n && !d_bytes)) return fail(IE_ERR_INVALID, "null argument");
+  if (w->device != x->device) return fail(IE_ERR_INVALID, "wildcards and exec live on different devices");
+  int rc = set_device(x->device);
+  if (rc) return rc;
+  IE_HIP(launch_wildcard(w->dev, d_bytes, d_offsets, n, d_range, d_match, d_ncap, d_caps, x->stream));
+  return IE_SUCCESS;
+}
+
+int ie_wildcard_match_batch(ie_exec* x, const ie_wildcards* w, const uint8_t* bytes, const uint64_t* offsets,
+                            uint64_t n, const uint32_t* range, int32_t* match, uint8_t* ncap, uint32_t* caps) {
+  if (!x || !w || !offsets || !match || !ncap || !caps || (n && !bytes && offsets[n] > offsets[0]))
+    return fail(IE_ERR_INVALID, "null argument");
+  int rc = set_device(x->device);
+  if (rc) return rc;
+  if (n == 0) return IE_SUCCESS;
+  const uint64_t base = offsets[0], nb = offsets[n] - base;
+  std::vector<uint64_t> off(offsets, offsets + n + 1);
+  for (auto& o : off) o -= base;
+  IE_HIP(x->in_bytes.ensure(nb + 16));
+  IE_HIP(x->in_off.ensure((n + 1) * 8));
+  IE_HIP(x->wc_match.ensure(n * 4));
+  IE_HIP(x->wc_ncap.ensure(n));
+  IE_HIP(x->wc_caps.ensure(n * 8 * IE_WC_MAX_CAP));
+  if (nb) IE_HIP(hipMemcpyAsync(x->in_bytes.p, bytes + base, nb, hipMemcpyHostToDevice, x->stream));
+  IE_HIP(hipMemcpyAsync(x->in_off.p, off.data(), (n + 1) * 8, hipMemcpyHostToDevice, x->stream));
+  const uint32_t* d_range = nullptr;
+  if (range) {
+    IE_HIP(x->wc_range.ensure(n * 8));
+    IE_HIP(hipMemcpyAsync(x->wc_range.p, range, n * 8, hipMemcpyHostToDevice, x->stream));
+    d_range = (const uint32_t*)x->wc_range.p;
+  }
+  rc = ie_wildcard_match_device(x, w, (const uint8_t*)x->in_bytes.p, (const uint64_t*)x->in_off.p, n, d_range,
+                                (int32_t*)x->wc_match.p, (uint8_t*)x->wc_ncap.p, (uint32_t*)x->wc_caps.p);
+  if (rc) return rc;
+  IE_HIP(hipMemcpyAsync(match, x->wc_match.p, n * 4, hipMemcpyDeviceToHost, x->stream));
+  IE_HIP(hipMemcpyAsync(ncap, x->wc_ncap.p, n, hipMemcpyDeviceToHost, x->stream));
+  IE_HIP(hipMemcpyAsync(caps, x->wc_caps.p, n * 8 * IE_WC_MAX_CAP, hipMemcpyDeviceToHost, x->stream));
+  IE_HIP(hipStreamSynchronize(x->stream));
+  return IE_SUCCESS;
 }
 
 void ie_batch_free(ie_batch* b) {

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/ie_amd.h"
 #include "ie_common.h"
 
 namespace ie {
@@ -51,6 +52,19 @@ struct Work {
   uint64_t* tile_sum;    // tiles
   uint64_t* tile_base;   // tiles
 };
+
+// compiled wildcard patterns (ie_wildcard.hip): pattern p = literals [pat_lit[p], pat_lit[p+1]),
+// literal l = bytes[lit_off[l] .. lit_off[l] + lit_len[l]); the groups sit between the literals
+constexpr uint32_t kWcMaxCap = IE_WC_MAX_CAP;
+struct WcSet {
+  const uint8_t* bytes;
+  const uint32_t* lit_off;
+  const uint32_t* lit_len;
+  const uint32_t* pat_lit;  // n_pat + 1
+  uint32_t n_pat;
+};
+hipError_t launch_wildcard(const WcSet& P, const uint8_t* bytes, const uint64_t* off, uint64_t n,
+                           const uint32_t* range, int32_t* match, uint8_t* ncap, uint32_t* caps, hipStream_t st);
 
 hipError_t launch_resolve(const Batch& B, const Work& W, const DevTable& T, uint8_t* out,
                           uint64_t cap, hipStream_t st);

@@ -34,7 +34,7 @@
 #include "ie_literal.h"
 
 #ifndef IE_WAVES_PER_EU
-#define IE_WAVES_PER_EU 3
+#define IE_WAVES_PER_EU 4
 #endif
 
 namespace ie {
@@ -215,6 +215,20 @@ __device__ __forceinline__ u32x4 keep_bytes(u32x4 v, uint32_t len) {
   r.z = l >= 12 ? v.z : l > 8 ? v.z & ((1u << (8 * (l - 8))) - 1u) : 0u;
   r.w = l >= 16 ? v.w : l > 12 ? v.w & ((1u << (8 * (l - 12))) - 1u) : 0u;
   return r;
+}
+
+// v moved up by sh (0..16) bytes: byte i of the result is byte i - sh of v (zero below sh; bytes
+// moved past 16 are dropped)
+__device__ __forceinline__ u32x4 shl_bytes(u32x4 v, uint32_t sh) {
+  const uint32_t q = sh >> 2, r = sh & 3u;
+  const uint32_t w0 = q == 0 ? v.x : 0u;
+  const uint32_t w1 = q == 0 ? v.y : q == 1 ? v.x : 0u;
+  const uint32_t w2 = q == 0 ? v.z : q == 1 ? v.y : q == 2 ? v.x : 0u;
+  const uint32_t w3 = q == 0 ? v.w : q == 1 ? v.z : q == 2 ? v.y : q == 3 ? v.x : 0u;
+  if (r == 0) return u32x4{w0, w1, w2, w3};
+  const uint32_t a = 4u - r;  // v_alignbyte: ({hi, lo} >> 8a)[31:0] = hi << 8r | lo >> (32 - 8r)
+  return u32x4{__builtin_amdgcn_alignbyte(w0, 0u, a), __builtin_amdgcn_alignbyte(w1, w0, a),
+               __builtin_amdgcn_alignbyte(w2, w1, a), __builtin_amdgcn_alignbyte(w3, w2, a)};
 }
 
 // 16 bytes at any LDS address from five aligned dword reads and v_alignbyte (a 16-byte access off
@@ -525,11 +539,6 @@ __device__ __forceinline__ uint32_t chunk_bs_dot(const lds_u32* w) {
 constexpr int kChainDepth = 4;
 constexpr uint32_t kChainMax = 112;  // bytes covered by the 128-bit event window
 
-struct ChainLds {
-  lds_u8* kbuf;   // lane-private kKeyCap B: assembly area of chain keys (A | T | B stores end by byte 32)
-  lds_u64* ev;    // lane-private event masks (4 words, stride kBlock) for the middle levels of deep chains
-};
-
 // 128-bit event masks of one string (bit i = byte i)
 struct Ev {
   uint64_t lo, hi;
@@ -555,18 +564,8 @@ __device__ __forceinline__ uint32_t ev_last(Ev m) {  // highest set bit, 128 if 
 __device__ __forceinline__ uint32_t ev_count(Ev m) { return (uint32_t)(__popcll(m.lo) + __popcll(m.hi)); }
 
 struct Probe {
-  uint4 q0, q1, q2, q3;
+  uint4 q0, q1, q2;
 };
-
-__device__ __forceinline__ void probe_load(const DevTable& T, uint32_t slot, Probe& P) {
-  const uint4* e = (const uint4*)(T.entries + slot);
-  P.q0 = gld4(e);
-  P.q1 = gld4(e + 1);
-  P.q2 = gld4(e + 2);
-#ifndef IE_EXP_NOTT
-  P.q3 = gld4(e + 3);
-#endif
-}
 
 __device__ __forceinline__ uint32_t w_max32(uint32_t v) {
 #pragma unroll
@@ -574,16 +573,45 @@ __device__ __forceinline__ uint32_t w_max32(uint32_t v) {
   return v;
 }
 
-// value texts of the top-level pairs (inline entry texts, <= kInlineText bytes), kept in
-// registers from the lookup to the output build
-struct TopText {
-  uint32_t w[kMaxTop][8];
+// Chain evaluation in two steps. parse_chains (per lane = per string) locates the string's chains
+// from the staged event masks; every chain then becomes a JOB, and resolve_jobs runs the jobs of
+// the whole tile chain-parallel (a lane per job, two jobs per lane in flight), level by level,
+// innermost first; combine_chains (per string) gathers its jobs' results into the descriptor.
+// Per-job state is one chain (not a string's three), which keeps the register budget small.
+struct ChainJobs {  // LDS views, tile-wide
+  lds_u32* crec;    // kJobCap: the chain's record (first open | first close << 8 | innermost open << 16 | last close << 24)
+  lds_u16* meta;    // kJobCap: string lane | depth << 12
+  lds_u32* res_k;   // kJobCap: the job's result: value kind << 30 | text length; kResFail | status | open << 8; kResReject
+  lds_u32* res_s;   // kJobCap: value source (entry index / arena offset)
+  lds_u16* p0;      // kBlock: each string's first byte in the stage
+  lds_u32* tbl;     // kBlock: each string's table in the set
+  lds_u64* ev;      // kBlock x 4 columns: the event masks of strings with chains deeper than 2
 };
+constexpr uint32_t kJobCap = kMaxTop * kBlock;
+constexpr uint32_t kResFail = 1u << 29, kResReject = 1u << 28;
 
-template <bool FAILC>
-__device__ bool eval_chains(const DevTable& T, uint32_t tid, const lds_u16* pil, const lds_u8* tile, uint32_t p0, uint32_t n, const lds_u32* cm,
-                            const lds_u32* oddbits, const lds_u32* escbits, bool active, const ChainLds& CL, Desc& d,
-                            TopText& tt, uint32_t& out_len, uint8_t& status, bool& chain_fail, uint64_t* stamp) {
+// the string's chains (<= kMaxTop, depth <= kChainDepth; records as in ChainJobs::crec). False:
+// the string is not a chain-only clean string (the exact evaluator decides it).
+__device__ bool parse_chains(const lds_u8* tile, uint32_t p0, uint32_t n, const lds_u32* cm, const lds_u32* oddbits,
+                             const lds_u32* escbits, bool active, lds_u64* ev, uint32_t (&crec)[kMaxTop],
+                             uint32_t (&cdep)[kMaxTop], uint32_t& nch) {
+  if (active && n > kChainMax) {
+    // a long string is copied verbatim when none of its bytes is a brace and its chunks hold no
+    // U+3020 lead byte (no pair to resolve, no placeholder to collide with: py:505-540 leave it
+    // unchanged); otherwise the exact evaluator decides it
+    nch = 0;
+#pragma unroll
+    for (int c = 0; c < kMaxTop; c++) crec[c] = cdep[c] = 0;
+    const uint32_t c0 = p0 >> 4, cl = (p0 + n - 1) >> 4;
+    bool clean = true;
+    for (uint32_t c = c0; c <= cl && clean; c++) {
+      const uint32_t m = cm[c];  // bits 0-15 '{', 16-31 '}' of the chunk's bytes
+      const uint32_t b_lo = c == c0 ? (p0 & 15u) : 0u, b_hi = c == cl ? ((p0 + n - 1) & 15u) : 15u;
+      const uint32_t bm = ((2u << b_hi) - 1u) & ~((1u << b_lo) - 1u);  // the string's bytes in the chunk
+      clean = (((m | (m >> 16)) & bm) == 0u) && !((oddbits[c >> 5] >> (c & 31u)) & 1u);
+    }
+    return clean;
+  }
   bool ok = active && n <= kChainMax;
   const lds_u8* s = tile + p0;
   // ---- 1. the string's open / close events as 128-bit windows ----
@@ -657,8 +685,8 @@ __device__ bool eval_chains(const DevTable& T, uint32_t tid, const lds_u16* pil,
   const Ev Om{O[0] | ((uint64_t)O[1] << 32), O[2] | ((uint64_t)O[3] << 32)};
   const Ev Cm{C[0] | ((uint64_t)C[1] << 32), C[2] | ((uint64_t)C[3] << 32)};
   // per chain: first open | first close << 8 | innermost open << 16 | last close << 24, depth
-  uint32_t crec[kMaxTop], cdep[kMaxTop];
-  uint32_t pos = 0, nch = 0, maxd = 0;
+  uint32_t pos = 0, maxd = 0;
+  nch = 0;
   bool bad = !ok, whole = false;
 #pragma unroll
   for (int c = 0; c < kMaxTop; c++) {
@@ -684,149 +712,198 @@ __device__ bool eval_chains(const DevTable& T, uint32_t tid, const lds_u16* pil,
   }
   bad |= ev_first(ev_from(Ev{Om.lo | Cm.lo, Om.hi | Cm.hi}, pos)) < 128u;  // more than kMaxTop chains
   ok = !bad && !(nch == 1 && whole);  // a whole-string pair: typed result (py:510-514), exact evaluator
-  if (__any(ok && maxd > 2u)) {  // middle levels are found from the masks in their round
-    CL.ev[0] = Om.lo, CL.ev[kBlock] = Om.hi, CL.ev[2 * kBlock] = Cm.lo, CL.ev[3 * kBlock] = Cm.hi;
+  if (__any(ok && maxd > 2u)) {  // middle levels are found from these masks in their round
+    ev[0] = Om.lo, ev[kBlock] = Om.hi, ev[2 * kBlock] = Cm.lo, ev[3 * kBlock] = Cm.hi;
   }
-  if (stamp && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memrealtime();  // diagnostic
-  // ---- 3. rounds: level r of every chain, all lookups of a round in flight together. The key
-  //      of a pair is A | T | B: template up to its child, the child's text, template after the
-  //      child (a leaf: A only); assembled with unaligned 16-byte LDS stores in the lane's area ----
-  uint32_t ct[kMaxTop][4], cl_[kMaxTop], co_[kMaxTop], ctl[kMaxTop];  // child text / close / open / length
+  return ok;
+}
+
+// The jobs [j0, j0 + 2 * kBlock) of the tile: lane t takes jobs j0 + t and j0 + kBlock + t. Round r
+// resolves level r of each job (the innermost pair in round 0); the key of a level is A | T | B
+// (template before the child, the child's splice text, template after it; a leaf: A only),
+// assembled in registers and looked up with one pilot and one 48-byte entry read. A job ends at
+// its top level (the value goes to res_k / res_s), at a failure (FAILC: a miss without an
+// inserts-dir or an unspliceable hit, recorded with its pair's opening offset) or at anything the
+// exact evaluator must decide (kResReject: a long key or text, a non-inert value, a failure when
+// !FAILC, a miss an inserts-dir might resolve).
+template <bool FAILC>
+__device__ void resolve_jobs(const DevTable& T, const lds_u8* tile, const ChainJobs& J, uint32_t j0, uint32_t njobs,
+                             bool& chain_fail, uint64_t* stamp) {
+  constexpr int NJ = 2;
+  const uint32_t tid = threadIdx.x;
+  bool on[NJ], done[NJ];
+  uint32_t job[NJ], cr[NJ], dep[NJ], ls[NJ], tb[NJ], res_k[NJ], res_s[NJ];
+  const lds_u8* s[NJ];
+  uint32_t ct[NJ][4], ctl[NJ], co_[NJ], cl_[NJ];
+  uint32_t maxd = 0;
 #pragma unroll
-  for (int c = 0; c < kMaxTop; c++) {
-    ct[c][0] = ct[c][1] = ct[c][2] = ct[c][3] = 0;
-    cl_[c] = co_[c] = ctl[c] = 0;
+  for (int q = 0; q < NJ; q++) {
+    job[q] = j0 + (uint32_t)q * kBlock + tid;
+    const bool valid = job[q] < njobs;
+    cr[q] = valid ? J.crec[job[q]] : 0u;
+    const uint32_t mt = valid ? (uint32_t)J.meta[job[q]] : 0u;
+    ls[q] = mt & 0xFFFu;
+    dep[q] = valid ? mt >> 12 : 0u;
+    s[q] = tile + (valid ? (uint32_t)J.p0[ls[q]] : 0u);
+    tb[q] = valid ? J.tbl[ls[q]] : 0u;
+    done[q] = !valid;
+    res_k[q] = kResReject;
+    res_s[q] = 0;
+    ct[q][0] = ct[q][1] = ct[q][2] = ct[q][3] = 0;
+    ctl[q] = co_[q] = cl_[q] = 0;
+    maxd = dep[q] > maxd ? dep[q] : maxd;
   }
-  uint32_t vsum = 0, span = 0;
-  // failures (a miss, or a hit the dialect cannot splice): the reference stops at the failing pair
-  // with the largest opening offset, and never evaluates the pairs enclosing a failed one (dead)
-  // one word: bits 0-7 the status so far (0 = none), 8-15 its pair's opening offset, 16+ dead chains
-  uint32_t fw = 0;
-  const uint32_t R = w_max32(ok ? maxd : 0u);
+  const uint32_t R = w_max32(maxd);
   for (uint32_t r = 0; r < R; r++) {
-    bool on[kMaxTop];
-    uint32_t open[kMaxTop], close[kMaxTop], klen[kMaxTop];
-    u32x4 kw[kMaxTop];
-    uint64_t h[kMaxTop];
+    uint32_t open[NJ], close[NJ], la[NJ], lb[NJ], klen[NJ], slot[NJ];
+    u32x4 ka[NJ], kb[NJ], kw[NJ];
+    uint64_t h[NJ];
 #pragma unroll
-    for (int c = 0; c < kMaxTop; c++) {
-      on[c] = ok && r < cdep[c] && !((fw >> (16 + c)) & 1u);
-      // level r: the innermost pair in round 0, the outermost in the last round; a middle level
-      // is the open before the previous level's and the close after it
-      const bool top_c = r + 1 == cdep[c];
-      uint32_t o = r == 0 ? (crec[c] >> 16) & 0xFFu : top_c ? crec[c] & 0xFFu : 0u;
-      uint32_t q = r == 0 ? (crec[c] >> 8) & 0xFFu : top_c ? crec[c] >> 24 : 0u;
-      const bool mid = on[c] && r != 0 && !top_c;
+    for (int q = 0; q < NJ; q++) {
+      on[q] = !done[q] && r < dep[q];
+      // level r: the innermost pair in round 0, the outermost in the last round; a middle level is
+      // the open before the previous level's and the close after it (from the string's masks)
+      const bool top = r + 1 == dep[q];
+      uint32_t o = r == 0 ? (cr[q] >> 16) & 0xFFu : top ? cr[q] & 0xFFu : 0u;
+      uint32_t c = r == 0 ? (cr[q] >> 8) & 0xFFu : top ? cr[q] >> 24 : 0u;
+      const bool mid = on[q] && r != 0 && !top;
       if (__any(mid)) {
-        const Ev Om2{CL.ev[0], CL.ev[kBlock]}, Cm2{CL.ev[2 * kBlock], CL.ev[3 * kBlock]};
         if (mid) {
-          o = ev_last(ev_below(Om2, co_[c]));
-          q = ev_first(ev_from(Cm2, cl_[c] + 1u));
+          const lds_u64* e = J.ev + ls[q];
+          o = ev_last(ev_below(Ev{e[0], e[kBlock]}, co_[q]));
+          c = ev_first(ev_from(Ev{e[2 * kBlock], e[3 * kBlock]}, cl_[q] + 1u));
         }
       }
-      open[c] = on[c] ? o : 0u;
-      close[c] = on[c] ? q : 0u;
-      kw[c] = u32x4{0, 0, 0, 0};
-      klen[c] = 0;
-      h[c] = 0;
-      if (!__any(on[c])) continue;
-      if (r == 0) {  // a leaf: template bytes straight from the stage
-        klen[c] = on[c] ? close[c] - open[c] - 1 : 0u;
-        kw[c] = ld16(s + open[c] + 1);
-      } else {
-        const uint32_t la = on[c] ? co_[c] - open[c] - 1 : 0u, lb = on[c] ? close[c] - cl_[c] - 1 : 0u;
-        klen[c] = la + ctl[c] + lb;
-        lds_u8* kb = CL.kbuf;  // the lane's 48-byte area (keys are read back before the next chain's)
-        if (klen[c] <= 16u) {
-          st16(kb, ld16(s + open[c] + 1));
-          st16(kb + la, u32x4{ct[c][0], ct[c][1], ct[c][2], ct[c][3]});
-          st16(kb + la + ctl[c], ld16(s + cl_[c] + 1));
-          kw[c] = *(const lds_u128*)kb;
-        }
+      open[q] = on[q] ? o : 0u;
+      close[q] = on[q] ? c : 0u;
+      la[q] = on[q] ? (r == 0 ? close[q] : co_[q]) - open[q] - 1 : 0u;
+      lb[q] = on[q] && r != 0 ? close[q] - cl_[q] - 1 : 0u;
+      ka[q] = ld16a(s[q] + open[q] + 1);
+      kb[q] = r != 0 ? ld16a(s[q] + cl_[q] + 1) : u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int q = 0; q < NJ; q++) {
+      klen[q] = la[q] + (r != 0 ? ctl[q] + lb[q] : 0u);
+      if (on[q] && klen[q] > 16u) {  // longer keys live in the arena: exact evaluator
+        on[q] = false;
+        done[q] = true;
       }
-      if (on[c] && klen[c] > 16u) {  // longer keys live in the arena: exact evaluator
-        ok = false;
-        on[c] = false;
+      u32x4 k = keep_bytes(ka[q], la[q]);
+      if (r != 0) {
+        const u32x4 t = shl_bytes(u32x4{ct[q][0], ct[q][1], ct[q][2], ct[q][3]}, la[q]);
+        const u32x4 b = shl_bytes(keep_bytes(kb[q], lb[q]), la[q] + ctl[q]);
+        k = u32x4{k.x | t.x | b.x, k.y | t.y | b.y, k.z | t.z | b.z, k.w | t.w | b.w};
       }
-      kw[c] = keep_bytes(kw[c], klen[c]);
-      h[c] = hash_init(klen[c], T.seed, tid);
-      h[c] = hash_word(h[c], kw[c].x);
-      if (__any(on[c] && klen[c] > 4u)) h[c] = klen[c] > 4u ? hash_word(h[c], kw[c].y) : h[c];
-      if (__any(on[c] && klen[c] > 8u)) h[c] = klen[c] > 8u ? hash_word(h[c], kw[c].z) : h[c];
-      if (__any(on[c] && klen[c] > 12u)) h[c] = klen[c] > 12u ? hash_word(h[c], kw[c].w) : h[c];
-      if (klen[c] == 0) h[c] = hash_init(0, T.seed, tid);
+      kw[q] = keep_bytes(k, klen[q]);
+      uint64_t hh = hash_init(klen[q], T.seed, tb[q]);
+      if (klen[q] > 0u) hh = hash_word(hh, kw[q].x);
+      if (klen[q] > 4u) hh = hash_word(hh, kw[q].y);
+      if (klen[q] > 8u) hh = hash_word(hh, kw[q].z);
+      if (klen[q] > 12u) hh = hash_word(hh, kw[q].w);
+      h[q] = hh;
+    }
+    if (stamp && threadIdx.x == 0 && r == 0) {  // diagnostic: keys hashed
+      asm volatile("" ::"v"(h[0]), "v"(h[1]));
+      stamp[6] = __builtin_amdgcn_s_memrealtime();
+    }
+    // pilots, then entries: two memory latencies per round, every job's in flight together
+#pragma unroll
+    for (int q = 0; q < NJ; q++) {
+      const uint32_t pilot = on[q] ? (uint32_t)gld(T.pilots + ph_group(h[q], T.nb)) : 0u;
+      slot[q] = on[q] ? ph_slot(h[q], pilot, T.m) : 0u;
+    }
+    if (stamp && threadIdx.x == 0 && r == 0) {  // diagnostic: pilots arrived
+      asm volatile("" ::"v"(slot[0]), "v"(slot[1]));
+      stamp[13] = __builtin_amdgcn_s_memrealtime();
+    }
+    Probe P[NJ];
+#pragma unroll
+    for (int q = 0; q < NJ; q++) {
+      if (__any(on[q])) {
+        const uint4* e = (const uint4*)(T.entries + slot[q]);
+        P[q].q0 = gld4(e);
+        P[q].q1 = gld4(e + 1);
+        P[q].q2 = gld4(e + 2);
+      }
+    }
+    if (stamp && threadIdx.x == 0 && r < 2) {  // diagnostic: entries arrived
+      asm volatile("" ::"v"(P[0].q0.x), "v"(P[1].q0.x), "v"(P[0].q2.x));
+      stamp[14 + r] = __builtin_amdgcn_s_memrealtime();
     }
 #pragma unroll
-    for (int c = 0; c < kMaxTop; c++) on[c] = on[c] && ok;
-    // pilots of every chain, then every entry: two memory latencies per round
-    uint32_t slot[kMaxTop];
-#pragma unroll
-    for (int c = 0; c < kMaxTop; c++) {
-      const uint32_t grp = ph_group(h[c], T.nb);  // pilot from LDS (small tables) or L2
-      const uint32_t pilot = on[c] ? (pil ? (uint32_t)pil[grp] : (uint32_t)gld(T.pilots + grp)) : 0u;
-      slot[c] = on[c] ? ph_slot(h[c], pilot, T.m) : 0u;
-    }
-    if (stamp && threadIdx.x == 0 && r < 3) {  // diagnostic: pilots arrived
-      asm volatile("" ::"v"(slot[0]), "v"(slot[1]), "v"(slot[2]));
-      stamp[2 + 2 * r] = __builtin_amdgcn_s_memrealtime();
-    }
-    Probe P[kMaxTop];
-#pragma unroll
-    for (int c = 0; c < kMaxTop; c++) {
-      if (__any(on[c])) probe_load(T, slot[c], P[c]);
-    }
-    if (stamp && threadIdx.x == 0 && r < 3) {  // diagnostic: entries arrived
-      asm volatile("" ::"v"(P[0].q0.x), "v"(P[1].q0.x), "v"(P[2].q0.x), "v"(P[0].q2.x));
-      stamp[3 + 2 * r] = __builtin_amdgcn_s_memrealtime();
-    }
-#pragma unroll
-    for (int c = 0; c < kMaxTop; c++) {
-      if (!__any(on[c])) continue;
-      const Probe& E = P[c];
-      const bool hit = on[c] && (entry_head_ok(E.q0, klen[c], tid) & (E.q1.x == kw[c].x) & (E.q1.y == kw[c].y) &
-                                 (E.q1.z == kw[c].z) & (E.q1.w == kw[c].w));
+    for (int q = 0; q < NJ; q++) {
+      if (!__any(on[q])) continue;
+      const Probe& E = P[q];
+      const bool hit = on[q] && (entry_head_ok(E.q0, klen[q], tb[q]) & (E.q1.x == kw[q].x) & (E.q1.y == kw[q].y) &
+                                 (E.q1.z == kw[q].z) & (E.q1.w == kw[q].w));
       const uint32_t flags = E.q0.z, tlen = E.q0.y;
       const bool good = hit && (flags & EF_SPLICE_OK) && (flags & EF_INERT);
       // a miss (no inserts-dir: py:465 / interp.rs:136) or a hit that cannot be spliced
       // (py:530 / interp.rs:76-79) fails this pair; a hit on a value needing care, or a miss that
       // the inserts-dir might resolve, goes to the exact evaluator
-      const bool would_fail = on[c] && ((!hit && !(T.flags & TF_HAS_DIR)) || (hit && !(flags & EF_SPLICE_OK)));
+      const bool would_fail = on[q] && ((!hit && !(T.flags & TF_HAS_DIR)) || (hit && !(flags & EF_SPLICE_OK)));
       chain_fail |= would_fail;  // the adaptive variant choice counts these (either variant)
       const bool fail = FAILC && would_fail;
-      if (on[c] && !good && !fail) ok = false;
+      const bool top = r + 1 == dep[q];
+      if (on[q] && !good && !fail) done[q] = true;  // kResReject
       if (fail) {
-        const uint32_t st = hit ? (uint32_t)IE_E_ASSERT_TYPE : (uint32_t)IE_E_INTERP;
-        const bool newer = (fw & 0xFFu) == 0u || open[c] > ((fw >> 8) & 0xFFu);
-        fw = (fw & ~0xFFFFu) | (newer ? (open[c] << 8) | st : fw & 0xFFFFu) | (1u << (16 + c));
+        res_k[q] = kResFail | (hit ? (uint32_t)IE_E_ASSERT_TYPE : (uint32_t)IE_E_INTERP) | (open[q] << 8);
+        done[q] = true;
       }
-      const bool top = r + 1 == cdep[c];
-      if (on[c] && good && !top) {  // inner level: this text goes into the parent's key
-        if (tlen > 16u) ok = false;
-        ct[c][0] = E.q2.x, ct[c][1] = E.q2.y, ct[c][2] = E.q2.z, ct[c][3] = E.q2.w;
-        ctl[c] = tlen;
-        co_[c] = open[c];
-        cl_[c] = close[c];
+      if (on[q] && good && !top) {  // inner level: this text goes into the parent's key
+        if (tlen > 16u) done[q] = true;  // kResReject
+        ct[q][0] = E.q2.x, ct[q][1] = E.q2.y, ct[q][2] = E.q2.z, ct[q][3] = E.q2.w;
+        ctl[q] = tlen;
+        co_[q] = open[q];
+        cl_[q] = close[q];
       }
-      if (on[c] && good && top) {
+      if (on[q] && good && top) {
         uint32_t src;
-        d.vk[c] = value_kl(tlen, E.q0.w, slot[c], src);
-        d.vs[c] = src;
-        d.open[c] = open[c];
-        d.close[c] = close[c];
-#ifndef IE_EXP_NOTT
-        tt.w[c][0] = E.q2.x, tt.w[c][1] = E.q2.y, tt.w[c][2] = E.q2.z, tt.w[c][3] = E.q2.w;
-        tt.w[c][4] = E.q3.x, tt.w[c][5] = E.q3.y, tt.w[c][6] = E.q3.z, tt.w[c][7] = 0;
-#endif
-        vsum += tlen;
-        span += close[c] - open[c] + 1;
+        res_k[q] = value_kl(tlen, E.q0.w, slot[q], src);
+        res_s[q] = src;
+        done[q] = true;
       }
     }
   }
+#pragma unroll
+  for (int q = 0; q < NJ; q++) {
+    if (job[q] < njobs) {
+      J.res_k[job[q]] = res_k[q];
+      J.res_s[job[q]] = res_s[q];
+    }
+  }
+}
+
+// a string's descriptor from its jobs [jb, jb + nch): false when any job needs the exact evaluator;
+// a failed job (FAILC) makes the string fail with the status of the failing pair with the largest
+// opening offset (the reference resolves the rightmost chain first and stops at its first failure)
+__device__ bool combine_chains(const ChainJobs& J, uint32_t jb, uint32_t nch, const uint32_t (&crec)[kMaxTop],
+                               uint32_t n, Desc& d, uint32_t& out_len, uint8_t& status) {
+  bool ok = true;
+  uint32_t fw = 0, vsum = 0, span = 0;
+#pragma unroll
+  for (int c = 0; c < kMaxTop; c++) {
+    if ((uint32_t)c >= nch) continue;
+    const uint32_t rk = J.res_k[jb + c], rs = J.res_s[jb + c];
+    const uint32_t a = crec[c] & 0xFFu, e = crec[c] >> 24;
+    if (rk & kResReject) {
+      ok = false;
+    } else if ((rk >> 30) == 0u) {  // failed at the pair opening at (rk >> 8) & 0xFF
+      const uint32_t op = (rk >> 8) & 0xFFu;
+      if ((fw & 0xFFu) == 0u || op > (fw >> 8)) fw = (op << 8) | (rk & 0xFFu);
+    } else {
+      d.open[c] = a;
+      d.close[c] = e;
+      d.vk[c] = rk;
+      d.vs[c] = rs;
+      vsum += rk & kLenMask;
+      span += e - a + 1;
+    }
+  }
   const bool failed = (fw & 0xFFu) != 0u;
-  const uint8_t fail_st = (uint8_t)(fw & 0xFFu);
   d.ntop = ok && !failed ? nch : 0u;
   out_len = ok && !failed ? n - span + vsum : 0u;
-  if (ok && failed) status = fail_st;
+  if (ok && failed) status = (uint8_t)(fw & 0xFFu);
   return ok;
 }
 
@@ -948,6 +1025,8 @@ __device__ __forceinline__ TileGeo load_geo(const Batch& B, uint32_t tile, uint3
   return g;
 }
 
+constexpr uint32_t kStageChunks = (kTileBytes + 31) / 16;  // the input stage: the tile's first chunks
+
 // a tile's input chunks in flight into registers, written to the LDS stage later
 template <int MAXV>
 struct TilePrefetch {
@@ -957,7 +1036,7 @@ struct TilePrefetch {
     const uintptr_t plo = (uintptr_t)(B.bytes + g.lo);
     const uint32_t shift = (uint32_t)(plo & 15);
     const uint4* src = (const uint4*)(plo - shift);  // an aligned chunk never crosses a page
-    nv = (uint32_t)((shift + (g.hi - g.lo) + 15) >> 4);
+    nv = (uint32_t)min((uint64_t)((shift + (g.hi - g.lo) + 15) >> 4), (uint64_t)kStageChunks);
 #pragma unroll
     for (int k = 0; k < MAXV; k++) {
       const uint32_t j = tid + (uint32_t)k * kBlock;
@@ -972,7 +1051,7 @@ struct TilePrefetch {
     }
   }
 };
-constexpr int kStageV = ((kTileBytes + 31) / 16 + kBlock - 1) / kBlock;
+constexpr int kStageV = (kStageChunks + kBlock - 1) / kBlock;
 
 // bytes r..r+15 (r wave-uniform, 0..15) of the 32 bytes x | y
 __device__ __forceinline__ uint4 bytes_at(u32x4 x, u32x4 y, uint32_t r) {
@@ -1145,7 +1224,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES
   __shared__ uint8_t s_pend[kBlock];
   __shared__ uint32_t s_misc[4];  // tile, pending count, defer slot
   __shared__ uint64_t s_red[kBlock / 64 + 2];
-  __shared__ __attribute__((aligned(16))) uint16_t s_pil[kLdsPilots];  // the table's pilots (small tables)
   lds_u32* const s_cm = (lds_u32*)(lds_u8*)(s_u + kCmOff);    // event masks of the staged chunks (+ pad)
   lds_u32* const s_odd = (lds_u32*)(lds_u8*)(s_u + kOddOff);  // one bit per chunk: 0xE3 inside
   lds_u32* const s_esc = (lds_u32*)(lds_u8*)(s_u + kEscOff);  // one bit per chunk: '\' inside
@@ -1159,18 +1237,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES
   const TileGeo geo = load_geo(B, tile, tid);
   TilePrefetch<kStageV> pre;
   pre.nv = 0;
-  if (tile < ntiles && geo.hi - geo.lo <= (uint64_t)kTileBytes) pre.issue(B, geo, tid);
-  // pilots of a table with at most kLdsPilots groups: one coalesced 12 KB copy per tile, in flight
-  // with the tile's bytes (the scattered per-lookup pilot reads it replaces touch 768 lines)
-  constexpr int kPilV = (kLdsPilots * 2 + 16 * kBlock - 1) / (16 * kBlock);
-  const bool lds_pil = T.nb <= kLdsPilots;
-  const uint32_t npv = lds_pil ? (T.nb * 2u + 15u) / 16u : 0u;
-  uint4 pv[kPilV];
-#pragma unroll
-  for (int k = 0; k < kPilV; k++) {
-    const uint32_t j = tid + (uint32_t)k * kBlock;
-    if (j < npv) pv[k] = gld4((const uint4*)T.pilots + j);
-  }
+  if (tile < ntiles) pre.issue(B, geo, tid);
   if (tile < ntiles) {
   uint64_t t_start = 0;
   if (tid == 0) {
@@ -1194,17 +1261,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES
   const uint64_t last = min(first + (uint64_t)kBlock, B.n);
   const uint64_t i = first + tid;
   const uint64_t lo = geo.lo, hi = geo.hi, so = geo.so, sn = geo.sn;
-  const bool staged = (hi - lo) <= (uint64_t)kTileBytes;
   const uint32_t shift = (uint32_t)((uintptr_t)(B.bytes + lo) & 15);
-#pragma unroll
-  for (int k = 0; k < kPilV; k++) {
-    const uint32_t j = tid + (uint32_t)k * kBlock;
-    if (j < npv) ((uint4*)s_pil)[j] = pv[k];
-  }
-  if (staged) {  // whole 16-byte chunks covering [lo, hi)
+  // the stage holds the tile's first kStageChunks 16-byte chunks: strings that end inside it are
+  // evaluated from LDS, the rest (a tile of long strings) from global memory
+  const uint32_t nv = pre.nv;
+  const uint32_t p0 = shift + (uint32_t)(so - lo);
+  const bool lane_staged = p0 + sn <= 16ull * nv;
+  {
     pre.commit((uint4*)s_in, tid);
     __syncthreads();
-    const uint32_t nv = pre.nv;
     for (uint32_t c0 = 0; c0 < nv; c0 += kBlock) {  // uniform trip count: ballots below
       const uint32_t c = c0 + tid;
       bool odd = false, esc = false;
@@ -1224,13 +1289,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES
 
   // ---- 2. evaluate ----
   Desc d;
-  TopText tt;
   d.ntop = 0;
 #pragma unroll
   for (int q = 0; q < kMaxTop; q++) d.open[q] = d.close[q] = d.vk[q] = d.vs[q] = 0;
   const uint8_t* s = nullptr;
-  const uint32_t p0 = shift + (uint32_t)(so - lo);
-  bool pend = false, fast_lane = false, chain_fail = false;
+  bool pend = false, chain_fail = false;
   // this string's table in the set (MULTI: a table-id batch; else every key lives in table 0)
   const uint32_t tid_s = (MULTI && i < B.n) ? gld(B.table_id + i) : 0u;
   {
@@ -1238,7 +1301,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES
     uint32_t olen = 0, vid = IE_VID_NONE;
     bool active = false;
     if (i < B.n) {
-      s = staged ? s_in + p0 : B.bytes + so;
+      s = lane_staged ? s_in + p0 : B.bytes + so;
       active = sn < 0xFFFF0000ull;
       if (!active) st = kStatusPending;
     }
@@ -1247,13 +1310,43 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES
     if (W.debug_noeval) {  // diagnostic: copy verbatim (the pipeline floor)
       olen = (uint32_t)sn;
       slow = false;
-    } else if (staged && W.fast_mode) {
-      const ChainLds CL{(lds_u8*)(s_u + tid * kKeyCap), (lds_u64*)(lds_u8*)(s_u + kKbufLds) + tid};
-      const bool fast = eval_chains<FAILC>(T, tid_s, lds_pil ? (const lds_u16*)s_pil : nullptr, (const lds_u8*)s_in, p0, (uint32_t)sn, s_cm,
-                                    s_odd, s_esc, active, CL, d, tt, olen, r, chain_fail,
-                                    stamp_row ? stamp_row + 6 : nullptr);
+    } else if (W.fast_mode) {
+      // chains: parse per string, resolve per chain job (tile-wide), gather per string. The job
+      // arrays live in the union (results and string starts in the exact evaluator's key area,
+      // records in the chunk masks once every string has read its event windows).
+      lds_u64* const ev = (lds_u64*)(lds_u8*)(s_u + kKbufLds) + tid;
+      uint32_t crec[kMaxTop], cdep[kMaxTop], nch = 0;
+      const bool pok = parse_chains((const lds_u8*)s_in, p0, (uint32_t)sn, s_cm, s_odd, s_esc, active && lane_staged, ev,
+                                    crec, cdep, nch);
+      uint64_t njobs64;
+      const uint32_t jb = (uint32_t)block_scan(pok ? nch : 0u, s_red, &njobs64);  // barriers: masks read
+      const uint32_t njobs = (uint32_t)njobs64;
+      IE_STAMP(8);
+      const ChainJobs J{(lds_u32*)(lds_u8*)(s_u + kCmOff), (lds_u16*)(lds_u8*)(s_u + 8 * kJobCap),
+                        (lds_u32*)(lds_u8*)s_u, (lds_u32*)(lds_u8*)(s_u + 4 * kJobCap),
+                        (lds_u16*)(lds_u8*)(s_u + 10 * kJobCap), (lds_u32*)(lds_u8*)s_olen,
+                        (lds_u64*)(lds_u8*)(s_u + kKbufLds)};
+      if (pok) {
+#pragma unroll
+        for (int c = 0; c < kMaxTop; c++) {
+          if ((uint32_t)c < nch) {
+            J.crec[jb + c] = crec[c];
+            J.meta[jb + c] = (uint16_t)(tid | (cdep[c] << 12));
+          }
+        }
+      }
+      J.p0[tid] = (uint16_t)p0;
+      J.tbl[tid] = tid_s;
+      __syncthreads();
+      IE_STAMP(9);
+      for (uint32_t j0 = 0; j0 < njobs; j0 += 2 * kBlock) resolve_jobs<FAILC>(T, (const lds_u8*)s_in, J, j0, njobs, chain_fail, j0 == 0 ? stamp_row : nullptr);
+      IE_STAMP(10);
+      __syncthreads();
+      IE_STAMP(11);
+      const bool fast = pok && combine_chains(J, jb, nch, crec, (uint32_t)sn, d, olen, r);
+      __syncthreads();  // the job arrays are free (the exact evaluator's scratch)
+      IE_STAMP(12);
       slow = active && !fast;
-      fast_lane = fast;
     }
     const uint64_t fail_m = __ballot(chain_fail);
     if (fail_m && lane == 0) atomicAdd(W.stats + 4, (uint32_t)__popcll(fail_m));  // misses: rare
@@ -1263,17 +1356,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES
       if (lane == 0 && W.fast_mode) atomicAdd(W.stats + 3, (uint32_t)__popcll(slow_m));  // rare
       lds_u8* const kb = (lds_u8*)(s_u + tid * kKeyCap);
       lds_u32* const stk = (lds_u32*)(lds_u8*)(s_u + kKbufLds) + tid;
-      uint32_t o2 = 0;
-      uint8_t r2;
-#ifdef IE_EXP_NOEXACT
-      r2 = kStatusPending;
-#else
-      if (staged)
-        r2 = eval_exact<true>(T, tid_s, Src<true>{s}, (uint32_t)sn, slow, kb, stk, d, o2, vid);
-      else
-        r2 = eval_exact<false>(T, tid_s, Src<false>{s}, (uint32_t)sn, slow, kb, stk, d, o2, vid);
+      uint32_t o2 = 0, o3 = 0;
+      uint8_t r2 = kStatusPending, r3 = kStatusPending;
+#ifndef IE_EXP_NOEXACT
+      if (__any(slow && lane_staged))
+        r2 = eval_exact<true>(T, tid_s, Src<true>{s}, (uint32_t)sn, slow && lane_staged, kb, stk, d, o2, vid);
+      if (__any(slow && !lane_staged))
+        r3 = eval_exact<false>(T, tid_s, Src<false>{s}, (uint32_t)sn, slow && !lane_staged, kb, stk, d, o3, vid);
 #endif
-      if (slow) r = r2, olen = o2;
+      if (slow) r = lane_staged ? r2 : r3, olen = lane_staged ? o2 : o3;
     }
     if (active) st = r;
     pend = i < B.n && st == kStatusPending;
@@ -1337,26 +1428,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES
 
   // ---- 5. the tile's output bytes into the LDS stage (tile-relative offsets) while the
   //      look-back is pending; tiles whose output does not fit store straight to HBM later ----
-  const bool in_stage = staged && tile_total <= (uint64_t)kStageBytes;
+  const bool in_stage = tile_total <= (uint64_t)kStageBytes;
   const bool mine = i < B.n && st == IE_OK_STR && olen;
   if (in_stage) {
-    // entry texts of values the exact evaluator or the literal path found: into registers first
-    // (the chain evaluator kept its own from the lookup)
+    // entry texts of the values (inline, <= kInlineText bytes): into registers first, all in flight
+    uint32_t tt[kMaxTop][8];
 #pragma unroll
     for (int j = 0; j < kMaxTop; j++) {
-      #ifdef IE_EXP_NOTT
-      const bool need = mine && (uint32_t)j
-#else
-      const bool need = mine && !fast_lane && (uint32_t)j
-#endif
-                         < d.ntop && (d.vk[j] >> 30) == kValEntry;
+      const bool need = mine && (uint32_t)j < d.ntop && (d.vk[j] >> 30) == kValEntry;
       if (__any(need)) {
         const uint4* tp = (const uint4*)(T.entries + (need ? d.vs[j] : 0u)) + 2;
         const uint4 t2 = gld4(tp), t3 = gld4(tp + 1);
-        if (need) {
-          tt.w[j][0] = t2.x, tt.w[j][1] = t2.y, tt.w[j][2] = t2.z, tt.w[j][3] = t2.w;
-          tt.w[j][4] = t3.x, tt.w[j][5] = t3.y, tt.w[j][6] = t3.z, tt.w[j][7] = 0;
-        }
+        tt[j][0] = t2.x, tt[j][1] = t2.y, tt[j][2] = t2.z, tt[j][3] = t2.w;
+        tt[j][4] = t3.x, tt[j][5] = t3.y, tt[j][6] = t3.z, tt[j][7] = 0;
       }
     }
     lds_u8* const dd = (lds_u8*)(s_u + (mine ? local : 0));
@@ -1370,14 +1454,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES
       const uint32_t t_lo = j == 0 ? 0u : d.close[j - 1] + 1;
       const uint32_t t_hi = (uint32_t)j < ntop ? d.open[j] : n32;
       const uint32_t tl = ton ? t_hi - t_lo : 0u;
-      if (__any(tl != 0)) lds_copy(dd + w, tl ? ls + t_lo : (const lds_u8*)s_in, tl);
+      if (__any(tl != 0)) {
+        if (lane_staged) lds_copy(dd + w, tl ? ls + t_lo : (const lds_u8*)s_in, tl);
+        else if (tl) copy_bytes<true, false>((uint8_t*)(dd + w), s + t_lo, tl);  // a string past the stage
+      }
       w += tl;
       if (j == kMaxTop) break;
       // value j
       const bool von = mine && (uint32_t)j < ntop;
       const uint32_t kind = d.vk[j] >> 30, len = von ? d.vk[j] & kLenMask : 0u;
       const bool ent = von && kind == kValEntry;
-      if (__any(ent) && ent) put_words(dd + w, tt.w[j], len);
+      if (__any(ent) && ent) put_words(dd + w, tt[j], len);
       if (von && kind == kValArena)
         copy_bytes<true, false>((uint8_t*)(dd + w), T.arena + d.vs[j], len);
       else if (von && kind == kValPool)

@@ -185,3 +185,39 @@ def simple_insertkey(s, dialect="py"):
 
 def fnv1a(b):
     return lib().ieo_fnv1a(b, len(b))
+
+
+# ---------------------------------------------------------------------------------------------
+# wildcard match / capture: a restatement of the reference's construction (py:553-567) on
+# Python's `re` (stdlib: available here and on the GPU box), the checker of k_wildcard
+# ---------------------------------------------------------------------------------------------
+def wildcard_regex(wildcard_s):
+    """py:554 / py:558: '*' -> '〠' -> re.escape -> '(.*)', anchored"""
+    import re
+    return "^" + re.escape(wildcard_s.replace("*", "〠")).replace("〠", "(.*)") + "$"
+
+
+def is_wildcard_match(wildcard_s, s):
+    """py:553-555 (DOTALL)"""
+    import re
+    return bool(re.match(wildcard_regex(wildcard_s), s, re.DOTALL))
+
+
+def get_wildcard_matches(wildcard_s, s):
+    """py:557-567: re.findall's groups (a tuple is flattened; a group-less pattern gives the match)"""
+    import re
+    result = []
+    for x in re.findall(wildcard_regex(wildcard_s), s, re.DOTALL):
+        if type(x) == tuple:
+            result.extend(x)
+        else:
+            result.append(x)
+    return result
+
+
+def first_wildcard_match(patterns, s):
+    """goto_map / replace_map order (py:1704, 1735-1742): the first matching wildcard and its captures"""
+    for p, w in enumerate(patterns):
+        if is_wildcard_match(w, s):
+            return p, get_wildcard_matches(w, s)
+    return -1, []

@@ -10,5 +10,5 @@ name=$1; src=$(readlink -f "$2"); shift 2
 tmp=$(mktemp -d)
 cp "$src" $tmp/ie_resolve.hip
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wno-unused-result -I$C "$@" \
-  $tmp/ie_resolve.hip $C/ie_escape.hip $C/ie_host.cpp -o interpolation-engine_amd/libie_amd_$name.so
+  $tmp/ie_resolve.hip $C/ie_escape.hip $C/ie_wildcard.hip $C/ie_host.cpp -o interpolation-engine_amd/libie_amd_$name.so
 rm -rf $tmp
