@@ -68,17 +68,18 @@ __device__ __forceinline__ uint32_t value_kl(uint32_t text_len, uint32_t text_of
   return ((inl ? kValEntry : kValArena) << 30) | text_len;
 }
 
-// the string being evaluated: in the tile's LDS stage (STAGED) or in global memory
+// the string being evaluated: in the tile's LDS stage (STAGED) or anywhere (a generic pointer:
+// flat loads, so one instance serves staged strings and strings past the stage alike)
 template <bool STAGED>
 struct Src {
   const uint8_t* p;
   __device__ __forceinline__ uint8_t operator[](uint32_t i) const {
     if (STAGED) return ((const lds_u8*)p)[i];
-    return gld(p + i);
+    return p[i];
   }
   __device__ __forceinline__ uint32_t word_at(uintptr_t aligned_addr) const {
     if (STAGED) return *(const lds_u32*)(const lds_u8*)(const uint8_t*)aligned_addr;
-    return gld((const uint32_t*)aligned_addr);
+    return *(const uint32_t*)aligned_addr;
   }
 };
 
@@ -1356,15 +1357,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES
       if (lane == 0 && W.fast_mode) atomicAdd(W.stats + 3, (uint32_t)__popcll(slow_m));  // rare
       lds_u8* const kb = (lds_u8*)(s_u + tid * kKeyCap);
       lds_u32* const stk = (lds_u32*)(lds_u8*)(s_u + kKbufLds) + tid;
-      uint32_t o2 = 0, o3 = 0;
-      uint8_t r2 = kStatusPending, r3 = kStatusPending;
+      uint32_t o2 = 0;
+      uint8_t r2 = kStatusPending;
 #ifndef IE_EXP_NOEXACT
-      if (__any(slow && lane_staged))
-        r2 = eval_exact<true>(T, tid_s, Src<true>{s}, (uint32_t)sn, slow && lane_staged, kb, stk, d, o2, vid);
-      if (__any(slow && !lane_staged))
-        r3 = eval_exact<false>(T, tid_s, Src<false>{s}, (uint32_t)sn, slow && !lane_staged, kb, stk, d, o3, vid);
+      // staged strings through a generic pointer into the stage, the rest in global memory
+      r2 = eval_exact<false>(T, tid_s, Src<false>{s}, (uint32_t)sn, slow, kb, stk, d, o2, vid);
 #endif
-      if (slow) r = lane_staged ? r2 : r3, olen = lane_staged ? o2 : o3;
+      if (slow) r = r2, olen = o2;
     }
     if (active) st = r;
     pend = i < B.n && st == kStatusPending;
