@@ -137,14 +137,28 @@ __device__ __forceinline__ int32_t find_small(const DevTable& T, uint32_t tid, c
   return eq ? (int32_t)slot : -1;
 }
 
-// status of a key that is not in the table (py:437-467 / interp.rs:105-136)
+// status of a key that is not in the table (py:437-467 / interp.rs:105-136). A table built with
+// IE_TABLE_HAS_INSERTS_DIR holds the inserts directory's snapshot after the inserts
+// (get_interpdata's file fallback, py:452-461, for every key a file answers), so a key it lacks
+// is missing there too, unless it is not a canonical relative file name (absolute, an empty, '.'
+// or '..' component, a NUL): os.path.join may then reach outside the directory, and the host
+// decides (IE_NEEDS_HOST).
 __device__ uint8_t missing_status(const DevTable& T, const uint8_t* k, uint32_t n) {
-  if (n == 0) return IE_E_INTERP;
-  if (!(T.flags & TF_HAS_DIR)) return IE_E_INTERP;
-  bool is_arg = n >= 3 && k[0] == 'A' && k[1] == 'R' && k[2] == 'G';
-  if (T.dialect == IE_DIALECT_PY && n == 3) is_arg = false;  // ''.isdigit() is False
-  for (uint32_t j = 3; is_arg && j < n; j++) is_arg = k[j] >= '0' && k[j] <= '9';
-  return is_arg ? (uint8_t)IE_E_INTERP : (uint8_t)IE_NEEDS_HOST;
+  if (n == 0 || !(T.flags & TF_HAS_DIR)) return IE_E_INTERP;
+  // a canonical relative path (components separated by single '/', none empty, '.' or '..',
+  // no NUL) names a file inside the directory, which the snapshot covers; anything else is
+  // the host's
+  bool odd = false;
+  uint32_t c0 = 0;
+  for (uint32_t j = 0; j <= n && !odd; j++) {
+    if (j < n && k[j] == 0) odd = true;
+    if (j == n || k[j] == '/') {
+      const uint32_t cl = j - c0;
+      odd |= cl == 0 || (cl == 1 && k[c0] == '.') || (cl == 2 && k[c0] == '.' && k[c0 + 1] == '.');
+      c0 = j + 1;
+    }
+  }
+  return odd ? (uint8_t)IE_NEEDS_HOST : (uint8_t)IE_E_INTERP;
 }
 
 // lookup with the RAW value of bucket `prev` as the key (nested whole-string form,

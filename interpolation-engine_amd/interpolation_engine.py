@@ -24,13 +24,15 @@ import copy
 import ctypes
 import datetime as _dt
 import json
+import os
+import time
 
 from . import _native as N
 
 insert_start = "{"
 insert_stop = "}"
 escape = "\\"
-inserts_dir = None  # py:44 — a set inserts directory makes missing keys NEEDS_HOST (not supported)
+inserts_dir = None  # py:44 — when set, get_interpdata falls back to its files (py:452-461)
 
 
 class InterpolationException(Exception):
@@ -191,8 +193,11 @@ class InsertsTableSet:
 class InsertsTable(InsertsTableSet):
     """An immutable device snapshot of one inserts dict (get_interpdata's view of it)."""
 
-    def __init__(self, inserts, dialect="py", clock=None, device=0, has_inserts_dir=False):
-        super().__init__([inserts], dialect=dialect, clock=clock, device=device, has_inserts_dir=has_inserts_dir)
+    dir_key = None
+
+    def __init__(self, inserts, dialect="py", clock=None, device=0, has_inserts_dir=False, extra=None):
+        merged = inserts if not extra else {**extra, **inserts}  # the inserts win (py:450 before 452)
+        super().__init__([merged], dialect=dialect, clock=clock, device=device, has_inserts_dir=has_inserts_dir)
         self._snapshot = (dict(inserts), {k: render(v, dialect)[1] for k, v in inserts.items()
                                           if isinstance(v, (list, dict))})
         self._version = getattr(inserts, "version", None)
@@ -229,7 +234,8 @@ def _exception(s, st, keys):
     if st == N.DIVERGED:
         return RecursionError("interpolation of %r does not terminate (self-referential inserts)" % s)
     if st == N.NEEDS_HOST:
-        return NotImplementedError("key lookup needs the inserts directory (not supported on the device path)")
+        return NotImplementedError("a key of %r names a path outside the inserts directory's snapshot "
+                                   "('/', '.', '..' or NUL in the key): not resolved on the device path" % s)
     return RuntimeError("device status %s for %r" % (N.STATUS_NAMES[st] if st < len(N.STATUS_NAMES) else st, s))
 
 
@@ -262,25 +268,87 @@ class VersionedInserts(dict):
 
 _CACHE_SIZE = 8
 _cache = {}  # (id(inserts), dialect, device) -> (inserts, InsertsTable), least recently used first
+_DIR_TTL = 1.0  # seconds a directory snapshot is reused before the directory is read again
+_dir_snap = {}  # path -> (time read, version, {key: value})
+
+
+def _is_arg_key(k):
+    return k.startswith("ARG") and k[3:].isdigit()  # py:437 (str.isdigit: Unicode digits too)
+
+
+def read_inserts_dir(path):
+    """The values get_interpdata's file fallback (py:452-461) finds, before recursive_escape:
+    {key: json5.loads(<key>.json5)} or {key: <key> text stripped} for every file under `path`
+    (nested files as 'sub/name'; `<key>.json5` first, as py:455-459 tries it first). Keys the
+    lookup never sends to the directory ('', 'HH:MM', 'HH:MM:SS', ARGn) are left out."""
+    from .program import loads as json5_loads  # the builder's JSON5 reader (json5 is absent here)
+    plain, j5 = {}, {}
+    seen = set()
+    for root, dirs, files in os.walk(path, followlinks=True):  # open() follows links too
+        real = os.path.realpath(root)
+        if real in seen:  # a link cycle
+            dirs[:] = []
+            continue
+        seen.add(real)
+        rel_root = os.path.relpath(root, path)
+        for f in files:
+            rel = f if rel_root == "." else "/".join(rel_root.split(os.sep) + [f])
+            plain[rel] = os.path.join(root, f)
+            if rel.endswith(".json5"):
+                j5[rel[:-len(".json5")]] = os.path.join(root, f)
+    raw = {}
+    for key in sorted(set(plain) | set(j5)):
+        if key in ("", "HH:MM", "HH:MM:SS") or _is_arg_key(key):
+            continue
+        if key in j5:  # py:455-456
+            with open(j5[key]) as fh:
+                raw[key] = json5_loads(fh.read())
+        else:          # py:457-459
+            with open(plain[key]) as fh:
+                raw[key] = fh.read().strip()
+    return raw
+
+
+def inserts_dir_snapshot(path):
+    """(version, {key: recursive_escape(value)}) for read_inserts_dir(path), the escape on the
+    device; re-read at most every _DIR_TTL seconds (the reference reads at every lookup)."""
+    now = time.monotonic()
+    hit = _dir_snap.get(path)
+    if hit is not None and now - hit[0] < _DIR_TTL:
+        return hit[1], hit[2]
+    raw = read_inserts_dir(path)
+    keys = list(raw)
+    snap = dict(zip(keys, recursive_escape([raw[k] for k in keys]))) if keys else {}
+    version = 0 if hit is None else hit[1] + (hit[2] != snap)
+    _dir_snap[path] = (now, version, snap)
+    return version, snap
 
 
 def table_for(inserts, dialect="py", device=0):
     """The device table for this dict: rebuilt only when the dict changed; a new clock second
     rewrites the two clock entries in place (ie_table_set_clock). At most _CACHE_SIZE tables stay
-    alive (the dict is held with its table, so its id cannot be reused while cached)."""
+    alive (the dict is held with its table, so its id cannot be reused while cached). With
+    `inserts_dir` set the table also holds the directory's snapshot, after the inserts."""
     now = _dt.datetime.now()
     clock = (now.hour, now.minute, now.second)
+    dir_key = None
+    if inserts_dir:
+        dver, dsnap = inserts_dir_snapshot(inserts_dir)
+        dir_key = (inserts_dir, dver)
     key = (id(inserts), dialect, device)
     hit = _cache.pop(key, None)
     t = hit[1] if hit is not None and hit[0] is inserts else None
-    if t is not None and not t.matches(inserts):
+    if t is not None and (t.dir_key != dir_key or not t.matches(inserts)):
         t.close()
         t = None
     if t is not None and t.clock != clock and not t.set_clock(clock):
         t.close()
         t = None
     if t is None:
-        t = InsertsTable(inserts, dialect=dialect, clock=clock, device=device, has_inserts_dir=bool(inserts_dir))
+        extra = {k: v for k, v in dsnap.items() if k not in inserts} if dir_key else None
+        t = InsertsTable(inserts, dialect=dialect, clock=clock, device=device, has_inserts_dir=dir_key is not None,
+                         extra=extra)
+        t.dir_key = dir_key
     _cache[key] = (inserts, t)
     while len(_cache) > _CACHE_SIZE:
         _, old = _cache.pop(next(iter(_cache)))
@@ -292,6 +360,9 @@ def interpolate_states(states, items, dialect="py", device=0):
     """Batch interpolate_inserts over many inserts dicts (forked interpreter states, config 5):
     `items` is a list of (state index, content); one device table set, one batch. Failures are
     returned as exception instances, results in item order."""
+    if inserts_dir:  # every state's dict over the directory's snapshot (its own keys win)
+        snap = inserts_dir_snapshot(inserts_dir)[1]
+        states = [{**snap, **st} for st in states]
     tset = InsertsTableSet(states, dialect=dialect, device=device, has_inserts_dir=bool(inserts_dir))
     try:
         return tset.results([c for _, c in items], [i for i, _ in items])
@@ -308,7 +379,7 @@ def get_interpdata(inserts, insertkey):
         return _dt.datetime.now().strftime("%H:%M")
     if insertkey == "HH:MM:SS":
         return _dt.datetime.now().strftime("%H:%M:%S")
-    if isinstance(insertkey, str) and insertkey.startswith("ARG") and insertkey[3:].isdigit():
+    if isinstance(insertkey, str) and _is_arg_key(insertkey):
         if insertkey not in inserts:
             raise InterpolationException(
                 "Argument interpolation key '%s' is used, but the user passed less than %s program arguments."
@@ -318,8 +389,20 @@ def get_interpdata(inserts, insertkey):
         raise InterpolationException("Tried to interpolate empty string ''.")
     if insertkey in inserts:
         return inserts[insertkey]
-    raise InterpolationException("Could not find variable '%s' in interpdata. Available interpolation data keys are %r."
-                                 % (insertkey, list(inserts.keys())))
+    if inserts_dir:  # py:452-461
+        try:
+            try:
+                with open(os.path.join(inserts_dir, f"{insertkey}.json5")) as f:
+                    from .program import loads as json5_loads
+                    return recursive_escape(json5_loads(f.read()))
+            except FileNotFoundError:
+                with open(os.path.join(inserts_dir, insertkey)) as f:
+                    return recursive_escape(f.read().strip())
+        except FileNotFoundError:
+            pass
+    detail = " in interpdata" + (" or inserts directory '%s'" % inserts_dir if inserts_dir else "")
+    raise InterpolationException("Could not find variable '%s'%s. Available interpolation data keys are %r."
+                                 % (insertkey, detail, list(inserts.keys())))
 
 
 def get_simple_insertkey(content):

@@ -266,8 +266,24 @@ static int get_interpdata(const ieo_ctx* c, const char* k, size_t kn, value* v) 
     return IE_OK_STR;
   }
   if (is_arg) return IE_E_INTERP; /* py:440-442 / interp.rs:113-115: no inserts-dir lookup */
-  if (c->has_dir) return IE_NEEDS_HOST; /* py:452-461 / interp.rs:122-134 */
-  return IE_E_INTERP;                   /* py:465-467 / interp.rs:136 */
+  /* py:452-461 / interp.rs:122-134: with an inserts directory the caller adds every key a file
+   * answers to the inserts (after them) before building the context, so a miss is a miss there
+   * too; a key that is not a canonical relative file name (absolute, an empty, '.' or '..'
+   * component, a NUL: os.path.join may leave the directory) is left to the host */
+  if (c->has_dir) {
+    int odd = 0;
+    size_t c0 = 0;
+    for (size_t j = 0; j <= kn && !odd; j++) {
+      if (j < kn && k[j] == 0) odd = 1;
+      if (j == kn || k[j] == '/') {
+        size_t cl = j - c0;
+        odd |= cl == 0 || (cl == 1 && k[c0] == '.') || (cl == 2 && k[c0] == '.' && k[c0 + 1] == '.');
+        c0 = j + 1;
+      }
+    }
+    return odd ? IE_NEEDS_HOST : IE_E_INTERP;
+  }
+  return IE_E_INTERP; /* py:465-467 / interp.rs:136 */
 }
 
 /* get_interpdata called with a RAW value as the key (py:512 after a typed simple result) */

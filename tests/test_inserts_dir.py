@@ -1,0 +1,92 @@
+"""get_interpdata's inserts-directory fallback (py:452-461) against vectors the reference produced
+with a real directory (tests/golden/gen_inserts_dir.py): the directory is recreated from the
+fixture, read into a snapshot that follows the inserts (the device's view of the lookup order),
+and the oracle (CPU) and the device mirror (-m gpu) must reproduce every case."""
+import json
+import os
+
+import pytest
+
+import __graft_entry__ as G
+from oracle import oracle as O
+from tests.conftest import ROOT
+
+FIX = json.load(open(os.path.join(ROOT, "tests", "golden", "inserts_dir_py.json"), encoding="utf-8"))
+
+
+def make_dir(base):
+    for rel, text in FIX["files"].items():
+        p = os.path.join(base, rel)
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        with open(p, "w") as f:
+            f.write(text)
+    return str(base)
+
+
+def _escape_tree(v):
+    """recursive_escape (py:1449-1460) on the oracle's string escape"""
+    if type(v) == str:
+        return O.escape(v)
+    if type(v) == list:
+        return [_escape_tree(x) for x in v]
+    if type(v) == dict:
+        return {_escape_tree(k): _escape_tree(x) for k, x in v.items()}
+    return v
+
+
+def test_oracle_with_directory_snapshot(tmp_path):
+    pkg = G.load_package()
+    from interpolation_engine_amd import interpolation_engine as M
+    raw = M.read_inserts_dir(make_dir(tmp_path))
+    merged = {**{k: _escape_tree(v) for k, v in raw.items()}, **FIX["inserts"]}
+    ref = O.Oracle(merged, "py", has_dir=True)
+    vals = list(merged.values())
+    for c in FIX["cases"]:
+        st, out, vid = ref.interpolate(c["s"])
+        assert st == c["st"], c
+        if st == "OK_STR":
+            assert out == c["out"], c
+        if st == "OK_VALUE":
+            assert vals[vid] == c["value"], c
+    del pkg
+
+
+def test_canonical_path_rule():
+    """Keys that are not canonical relative file names stay with the host (NEEDS_HOST)."""
+    ref = O.Oracle({"a": "A"}, "py", has_dir=True)
+    for k, want in [("x", "E_INTERP"), ("sub/x", "E_INTERP"), ("/etc/passwd", "NEEDS_HOST"), ("../x", "NEEDS_HOST"),
+                    ("a//b", "NEEDS_HOST"), ("./x", "NEEDS_HOST"), ("x/", "NEEDS_HOST"), ("..", "NEEDS_HOST"),
+                    ("ARG1", "E_INTERP")]:
+        assert ref.interpolate("{%s}" % k)[0] == want, k
+
+
+@pytest.mark.gpu
+def test_device_mirror_with_inserts_dir(tmp_path):
+    pkg = G.load_package()
+    from interpolation_engine_amd import interpolation_engine as M
+    d = make_dir(tmp_path)
+    old = M.inserts_dir
+    M.inserts_dir = d
+    try:
+        for c in FIX["cases"]:
+            try:
+                r = pkg.interpolate_inserts(dict(FIX["inserts"]), c["s"])
+                st = "OK_STR" if c["st"] == "OK_STR" else "OK_VALUE"
+                if st == "OK_STR":
+                    assert r == c["out"], c
+                else:
+                    assert c["st"] == "OK_VALUE" and r == c["value"], (c, r)
+            except pkg.InterpolationException:
+                assert c["st"] == "E_INTERP", c
+            except AssertionError as e:
+                if c["st"] not in ("E_ASSERT_TYPE", "E_ASSERT_BRACES"):
+                    raise AssertionError("%r: %r" % (c, e))
+            # the host helper follows the same order
+        assert M.get_interpdata(dict(FIX["inserts"]), "count") == 42
+        assert M.get_interpdata(dict(FIX["inserts"]), "over") == "from the inserts"
+        with pytest.raises(pkg.InterpolationException):
+            M.get_interpdata(dict(FIX["inserts"]), "missing")
+        with pytest.raises(NotImplementedError):
+            pkg.interpolate_inserts({}, "{../outside}")
+    finally:
+        M.inserts_dir = old
