@@ -165,6 +165,12 @@ int ie_table_build(const ie_kv* kv, uint64_t n, int32_t dialect, const ie_clock*
 int ie_table_set_build(const ie_kv* kv, const uint64_t* kv_start, uint32_t n_tables, int32_t dialect,
                        const ie_clock* now, uint32_t flags, int32_t device, ie_table** out);
 void ie_table_free(ie_table* t);
+/* Multi-GPU (the path shards, no data-path collective). ie_table_replicate copies a
+ * built table to another device (device-to-device, over xGMI between GPUs); ie_shard_bounds
+ * splits a packed batch into n_shards byte-balanced contiguous string ranges,
+ * first[k] .. first[k+1] (first has n_shards + 1 entries; binary search on offsets). */
+int ie_table_replicate(const ie_table* t, int32_t device, ie_table** out);
+int ie_shard_bounds(const uint64_t* offsets, uint64_t n, uint32_t n_shards, uint64_t* first);
 /* Re-read the clock (py:433-436) without a rebuild: rewrites the 'HH:MM' / 'HH:MM:SS' entries in
  * place. IE_ERR_INVALID when a brace-bearing value pre-resolved at build read the clock (rebuild). */
 int ie_table_set_clock(ie_table* t, const ie_clock* now);

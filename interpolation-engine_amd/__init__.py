@@ -19,6 +19,7 @@ from .interpolation_engine import (  # noqa: F401
     recursive_interpolate,
     recursive_unescape,
 )
+from .multi import MultiDevice, shard_bounds  # noqa: F401
 from .wildcard import Wildcards, get_wildcard_matches, is_wildcard_match  # noqa: F401
 
 __version__ = "0.1.0"

@@ -36,6 +36,7 @@ EXPORTS = [
     "ie_synth_create", "ie_synth_free", "ie_synth_kv", "ie_synth_strings_host",
     "ie_synth_strings_device", "ie_debug_probe",
     "ie_wildcards_build", "ie_wildcards_free", "ie_wildcard_match_device", "ie_wildcard_match_batch",
+    "ie_table_replicate", "ie_shard_bounds",
 ]
 WC_MAX_CAP = 16
 
@@ -121,6 +122,8 @@ def lib():
         "ie_escape_batch": (ctypes.c_int, [vp, vp, vp, u64, ctypes.POINTER(ctypes.POINTER(BatchRes))]),
         "ie_batch_free": (None, [ctypes.POINTER(BatchRes)]),
         "ie_simple_insertkey": (ctypes.c_int, [ctypes.c_char_p, u64, i32, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
+        "ie_table_replicate": (ctypes.c_int, [vp, i32, pvp]),
+        "ie_shard_bounds": (ctypes.c_int, [vp, u64, u32, vp]),
         "ie_wildcards_build": (ctypes.c_int, [vp, vp, u32, i32, pvp]),
         "ie_wildcards_free": (None, [vp]),
         "ie_wildcard_match_device": (ctypes.c_int, [vp, vp, vp, vp, u64, vp, vp, vp, vp]),

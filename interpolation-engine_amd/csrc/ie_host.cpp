@@ -761,6 +761,58 @@ int ie_table_build(const ie_kv* kv, uint64_t n, int32_t dialect, const ie_clock*
   return ie_table_set_build(kv, start, 1, dialect, now, flags, device, out);
 }
 
+// a copy of a built table on another device (or the same one): device-to-device copies of the
+// entries, pilots and arena (hipMemcpyPeer: over xGMI between MI355X GPUs), no host placement or
+// pre-resolution pass (the table is read-only and replicated per device)
+int ie_table_replicate(const ie_table* t, int32_t device, ie_table** out) {
+  if (!t || !out) return fail(IE_ERR_INVALID, "null argument");
+  *out = nullptr;
+  int rc = set_device(device);
+  if (rc) return rc;
+  ie_table* c = new ie_table();
+  c->device = device;
+  c->dialect = t->dialect;
+  c->flags = t->flags;
+  c->n_entries = t->n_entries;
+  c->n_tables = t->n_tables;
+  c->clock_entries = t->clock_entries;
+  c->clock_dependent = t->clock_dependent;
+  c->dev = t->dev;
+  auto copy = [&](DevBuf& dst, const DevBuf& src) -> hipError_t {
+    hipError_t e = dst.ensure(src.bytes);
+    if (e != hipSuccess || !src.bytes) return e;
+    return hipMemcpyPeer(dst.p, device, src.p, t->device, src.bytes);
+  };
+  hipError_t e = copy(c->entries, t->entries);
+  if (e == hipSuccess) e = copy(c->pilots, t->pilots);
+  if (e == hipSuccess) e = copy(c->arena, t->arena);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e != hipSuccess) {
+    delete c;
+    return fail(IE_ERR_HIP, std::string("table replicate: ") + hipGetErrorString(e));
+  }
+  c->dev.entries = (const Entry*)c->entries.p;
+  c->dev.pilots = (const uint16_t*)c->pilots.p;
+  c->dev.arena = (const uint8_t*)c->arena.p;
+  *out = c;
+  return IE_SUCCESS;
+}
+
+// byte-balanced shards of a packed batch: shard k = strings [first[k], first[k+1]),
+// first[k] = the first string whose offset reaches k/n_shards of the payload (binary search)
+int ie_shard_bounds(const uint64_t* offsets, uint64_t n, uint32_t n_shards, uint64_t* first) {
+  if (!offsets || !first || n_shards == 0) return fail(IE_ERR_INVALID, "null argument");
+  const uint64_t lo = offsets[0], total = offsets[n] - lo;
+  first[0] = 0;
+  for (uint32_t k = 1; k < n_shards; k++) {
+    const uint64_t target = lo + (uint64_t)((unsigned __int128)total * k / n_shards);
+    first[k] = (uint64_t)(std::lower_bound(offsets, offsets + n, target) - offsets);
+    if (first[k] < first[k - 1]) first[k] = first[k - 1];
+  }
+  first[n_shards] = n;
+  return IE_SUCCESS;
+}
+
 void ie_table_free(ie_table* t) {
   if (t) {
     (void)hipSetDevice(t->device);

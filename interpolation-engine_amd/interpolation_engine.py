@@ -153,11 +153,12 @@ class InsertsTableSet:
         return self.keys[self.starts[t]:self.starts[t + 1]]
 
     # --------------------------------------------------------------------------------------
-    def run(self, strings, table_ids=None):
+    def run(self, strings, table_ids=None, exec_=None):
         """Resolve a list of str on the device -> list of (status, payload); string i against dict
-        table_ids[i] (all against dict 0 when table_ids is None)."""
+        table_ids[i] (all against dict 0 when table_ids is None); exec_: the caller's ie_exec
+        (one per host thread), else this device's shared one."""
         blob, offs = N.pack(strings)
-        x = get_exec(self.device)
+        x = exec_ or get_exec(self.device)
         res = ctypes.POINTER(N.BatchRes)()
         bp = ctypes.c_char_p(blob)
         if table_ids is None:
