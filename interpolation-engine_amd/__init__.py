@@ -10,6 +10,11 @@ from .interpolation_engine import (  # noqa: F401
     InsertsTableSet,
     InterpolationException,
     VersionedInserts,
+    display_text,
+    display_texts,
+    ingest_args,
+    ingest_user_input,
+    ingest_user_inputs,
     get_interpdata,
     get_simple_insertkey,
     interpolate_batch,

@@ -494,6 +494,40 @@ def recursive_escape(x):
     return _map_strings(x, lambda ss: _escape_strings(ss, False))
 
 
+# ------------------------------------------------------------------------------------------
+# ingestion and display sites: the reference's own byte maps on caller text, on
+# the device escape / unescape kernels
+# ------------------------------------------------------------------------------------------
+def ingest_user_inputs(texts):
+    """The user_input command's escaping of what the user typed (py:1564-1568: '{' -> '\\{',
+    '}' -> '\\}'), for a batch of inputs in one device call."""
+    return _escape_strings(list(texts), False)
+
+
+def ingest_user_input(text):
+    return ingest_user_inputs([text])[0]
+
+
+def ingest_args(args):
+    """ARG1, ARG2, ... seeded from the program's command-line arguments, escaped
+    (py:2343-2349), one device call: {'ARG1': ..., ...}."""
+    return {"ARG%d" % i: v for i, v in enumerate(_escape_strings(list(args), False), start=1)}
+
+
+def display_texts(texts):
+    """The print command's text (py:1669-1673): escaped braces shown as braces, then str(). The
+    reference calls .replace before str(), so a non-str text raises AttributeError there and
+    here."""
+    for t in texts:
+        if not isinstance(t, str):
+            raise AttributeError("'%s' object has no attribute 'replace'" % type(t).__name__)
+    return _escape_strings(list(texts), True)
+
+
+def display_text(text):
+    return display_texts([text])[0]
+
+
 _LOOP_CMDS = ("for", "serial", "parallel_wait", "parallel_race")
 
 

@@ -312,16 +312,15 @@ class Runner:
         self.state = state
         self.resolve = resolve or IE.recursive_interpolate
         self.write = write or (lambda s: None)
-        for i, a in enumerate(args, start=1):  # py:2343-2349
-            state["inserts"]["ARG%d" % i] = a.replace("{", "\\{").replace("}", "\\}")
+        if args:  # py:2343-2349, escaped on the device
+            state["inserts"].update(IE.ingest_args(args))
 
     def step(self, task):
         inserts = self.state["inserts"]
         task = self.resolve(inserts, task)  # py:1501
         cmd = task.get("cmd")
-        if cmd == "print":  # py:1669-1675
-            text = task["text"].replace("\\{", "{").replace("\\}", "}") if isinstance(task["text"], str) else task["text"]
-            text = str(text)
+        if cmd == "print":  # py:1669-1675 (the display unescape on the device)
+            text = self.IE.display_text(task["text"])
             self.state["output"] += text
             self.write(text)
         elif cmd == "set":  # py:1657-1658

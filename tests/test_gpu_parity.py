@@ -803,3 +803,18 @@ def test_interpolate_states_batch():
             assert r is states[j]["L"]
         else:
             assert r == c.replace("{scenario}", states[j]["scenario"]).replace("{stage}", "first")
+
+
+def test_ingestion_and_display_sites():
+    """SURVEY §8f-3 on the device kernels: user_input escaping (py:1564-1568), ARGn seeding
+    (py:2343-2349) and the print command's unescape (py:1669-1673), against the oracle's byte
+    maps; a non-str print text raises AttributeError as the reference's .replace does."""
+    rng = random.Random(21)
+    texts = ["", "{", "}", "\\{x\\}", "a{b}c", "é{😀}", "{{}}", "\\\\{"]
+    texts += ["".join(rng.choice("ab{}\\\\ é") for _ in range(rng.randrange(0, 40))) for _ in range(300)]
+    assert PKG.ingest_user_inputs(texts) == [O.escape(t) for t in texts]
+    assert PKG.ingest_user_input("say {hi}") == "say \\{hi\\}"
+    assert PKG.ingest_args(["x{y}", "z"]) == {"ARG1": "x\\{y\\}", "ARG2": "z"}
+    assert PKG.display_texts(texts) == [O.escape(t, unescape=True) for t in texts]
+    with pytest.raises(AttributeError):
+        PKG.display_text(5)
