@@ -260,11 +260,13 @@ void ie_batch_free(ie_batch* b);
  * [range[2i], range[2i+1]) when range is given) that matches; match[i] = p or -1, ncap[i] the
  * number of captures and caps[i * 2 * IE_WC_MAX_CAP + 2c .. +1] = {byte start, byte length} of
  * capture c within string i (re.findall's groups; a wildcard without '*' captures its whole match,
- * as re.findall returns it). Wildcards with more than IE_WC_MAX_CAP groups are rejected. ---- */
+ * as re.findall returns it). Wildcards with more than IE_WC_MAX_CAP groups are rejected.
+ * IE_DIALECT_RS follows runtime.rs's regex-crate pattern instead: only '*' is a group, '$' matches
+ * at the end only, and a wildcard without '*' has no captures (parity unpinned: no toolchain). ---- */
 #define IE_WC_MAX_CAP 16
 typedef struct ie_wildcards ie_wildcards;
-int ie_wildcards_build(const uint8_t* bytes, const uint64_t* offsets, uint32_t n_patterns, int32_t device,
-                       ie_wildcards** out);
+int ie_wildcards_build(const uint8_t* bytes, const uint64_t* offsets, uint32_t n_patterns, int32_t dialect,
+                       int32_t device, ie_wildcards** out);
 void ie_wildcards_free(ie_wildcards* w);
 int ie_wildcard_match_device(ie_exec* x, const ie_wildcards* w, const uint8_t* d_bytes, const uint64_t* d_offsets,
                              uint64_t n, const uint32_t* d_range, int32_t* d_match, uint8_t* d_ncap, uint32_t* d_caps);

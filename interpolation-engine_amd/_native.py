@@ -124,7 +124,7 @@ def lib():
         "ie_simple_insertkey": (ctypes.c_int, [ctypes.c_char_p, u64, i32, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "ie_table_replicate": (ctypes.c_int, [vp, i32, pvp]),
         "ie_shard_bounds": (ctypes.c_int, [vp, u64, u32, vp]),
-        "ie_wildcards_build": (ctypes.c_int, [vp, vp, u32, i32, pvp]),
+        "ie_wildcards_build": (ctypes.c_int, [vp, vp, u32, i32, i32, pvp]),
         "ie_wildcards_free": (None, [vp]),
         "ie_wildcard_match_device": (ctypes.c_int, [vp, vp, vp, vp, u64, vp, vp, vp, vp]),
         "ie_wildcard_match_batch": (ctypes.c_int, [vp, vp, vp, vp, u64, vp, vp, vp, vp]),

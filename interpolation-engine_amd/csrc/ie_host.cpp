@@ -1108,8 +1108,9 @@ int ie_escape_batch(ie_exec* x, const uint8_t* bytes, const uint64_t* offsets, u
 // A wildcard compiles to its literals: the text between consecutive group markers, where a marker
 // is '*' or U+3020 (the reference's w.replace('*', '〠') then '〠' -> '(.*)', so a literal U+3020
 // is a group as well); re.escape makes every other byte literal.
-int ie_wildcards_build(const uint8_t* bytes, const uint64_t* offsets, uint32_t n_patterns, int32_t device,
-                       ie_wildcards** out) {
+int ie_wildcards_build(const uint8_t* bytes, const uint64_t* offsets, uint32_t n_patterns, int32_t dialect,
+                       int32_t device, ie_wildcards** out) {
+  const bool rs = dialect == IE_DIALECT_RS;  // runtime.rs:1633-1647: only '*' is a group
   if (!out || (n_patterns && (!offsets || (!bytes && offsets[n_patterns])))) return fail(IE_ERR_INVALID, "null argument");
   *out = nullptr;
   int rc = set_device(device);
@@ -1124,7 +1125,7 @@ int ie_wildcards_build(const uint8_t* bytes, const uint64_t* offsets, uint32_t n
     uint32_t groups = 0;
     for (uint64_t k = a; k < b;) {
       const uint8_t* c = bytes + base + k;
-      const uint32_t mk = c[0] == '*' ? 1u : (k + 2 < b && c[0] == 0xE3 && c[1] == 0x80 && c[2] == 0xA0) ? 3u : 0u;
+      const uint32_t mk = c[0] == '*' ? 1u : (!rs && k + 2 < b && c[0] == 0xE3 && c[1] == 0x80 && c[2] == 0xA0) ? 3u : 0u;
       if (!mk) {
         k++;
         continue;
@@ -1157,7 +1158,7 @@ int ie_wildcards_build(const uint8_t* bytes, const uint64_t* offsets, uint32_t n
     return fail(IE_ERR_HIP, std::string("wildcard upload: ") + hipGetErrorString(e));
   }
   w->dev = WcSet{(const uint8_t*)w->bytes.p, (const uint32_t*)w->lit_off.p, (const uint32_t*)w->lit_len.p,
-                 (const uint32_t*)w->pat_lit.p, n_patterns};
+                 (const uint32_t*)w->pat_lit.p, n_patterns, rs ? 1u : 0u};
   *out = w;
   return IE_SUCCESS;
 }

@@ -62,6 +62,7 @@ struct WcSet {
   const uint32_t* lit_len;
   const uint32_t* pat_lit;  // n_pat + 1
   uint32_t n_pat;
+  uint32_t rs;              // IE_DIALECT_RS: '$' at the end only, no capture without a group
 };
 hipError_t launch_wildcard(const WcSet& P, const uint8_t* bytes, const uint64_t* off, uint64_t n,
                            const uint32_t* range, int32_t* match, uint8_t* ncap, uint32_t* caps, hipStream_t st);

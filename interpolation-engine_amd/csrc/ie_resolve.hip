@@ -1478,10 +1478,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES
   }
   __syncthreads();
   const uint64_t base = s_red[kBlock / 64];
-  if (i < B.n) {
-    gst(B.out_off + i, base + local);
-    gst(B.status + i, st);
-    if (st == IE_OK_VALUE) gst(B.value_id + i, s_olen[tid]);
+  // the lane index, opaque to the compiler from here on: the tail recomputes its indices instead
+  // of keeping (and spilling) the staging loop's, which are equal expressions of threadIdx.x
+  uint32_t tid_t;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(tid_t) : "v"(tid));
+  const uint64_t i_t = first + tid_t;
+  if (i_t < B.n) {
+    gst(B.out_off + i_t, base + local);
+    gst(B.status + i_t, st);
+    if (st == IE_OK_VALUE) gst(B.value_id + i_t, s_olen[tid_t]);
   }
   if (last == B.n && tid == 0) {
     B.out_off[B.n] = base + tile_total;
@@ -1493,7 +1498,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES
   //      two stage blocks it straddles (the shift is uniform over the tile) ----
   uint8_t* const g = out + base;
   if (write_bytes && in_stage) {
-    stream_stage(g, s_u, (uint32_t)tile_total, tid);
+    stream_stage(g, s_u, (uint32_t)tile_total, tid_t);
   } else if (write_bytes) {
     // a tile whose output exceeds the stage (long strings, large expansions) or whose input was
     // not staged: its descriptors go to the defer list and k_emit_windows writes its bytes
@@ -1502,7 +1507,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES
     if (tid == 0) s_misc[2] = atomicAdd(W.defer_count, 1u);
     __syncthreads();
     const uint32_t slot = s_misc[2];
-    uint4* dd = W.defer_desc + ((uint64_t)slot * kBlock + tid) * 4;
+    uint4* dd = W.defer_desc + ((uint64_t)slot * kBlock + tid_t) * 4;
     const uint32_t nt = mine ? d.ntop : 0u;
     gst4(dd, make_uint4(nt, d.open[0], d.open[1], d.open[2]));
     gst4(dd + 1, make_uint4(d.close[0], d.close[1], d.close[2], n32));

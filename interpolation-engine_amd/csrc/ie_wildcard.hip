@@ -17,6 +17,9 @@
 // Byte positions equal the regex's code-point positions: a valid UTF-8 literal can only match at
 // code-point boundaries, and every other position is fixed by the literals and the end.
 //
+// IE_DIALECT_RS (runtime.rs:1633-1647, 1754-1775, the regex crate): only '*' is a group, '$'
+// matches at the end only, and a group-less wildcard captures nothing.
+//
 // One wave per string (wave-uniform control flow, byte comparisons spread over the 64 lanes);
 // strings up to kWcStage bytes are staged in LDS, longer ones are read from global memory.
 #include <hip/hip_runtime.h>
@@ -94,7 +97,7 @@ __global__ __launch_bounds__(64 * kWcWaves) void k_wildcard(WcSet P, const uint8
       const uint32_t l0 = P.pat_lit[p], nl = P.pat_lit[p + 1] - l0, k = nl - 1;
       const uint32_t len0 = P.lit_len[l0];
       if (len0 > len || !wc_eq(s, 0, P.bytes + P.lit_off[l0], len0)) continue;
-      const bool nl_end = len > 0 && s[len - 1] == '\n';
+      const bool nl_end = !P.rs && len > 0 && s[len - 1] == '\n';  // py '$'; the regex crate's is the end only
       if (k == 0) {
         if (len0 == len || (nl_end && len0 + 1 == len)) {
           found = (int32_t)p;
@@ -134,9 +137,9 @@ __global__ __launch_bounds__(64 * kWcWaves) void k_wildcard(WcSet P, const uint8
       continue;
     }
     const uint32_t l0 = P.pat_lit[found];
-    if (k_found == 0) {  // no group: the whole match
+    if (k_found == 0) {  // no group: re.findall returns the whole match (py); no capture (rs)
       if (lane == 0) {
-        ncap[i] = 1;
+        ncap[i] = P.rs ? 0 : 1;
         c[0] = 0;
         c[1] = P.lit_len[l0];
       }

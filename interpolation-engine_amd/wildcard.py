@@ -11,7 +11,9 @@ the matcher of goto_map, replace_map and delete_except (py:1688-1773; rust-proje
 Semantics are those of the reference's regex '^' + re.escape(w.replace('*', '〠')).replace('〠',
 '(.*)') + '$' under DOTALL (see csrc/ie_wildcard.hip): greedy groups, '$' also before a trailing
 newline, a literal U+3020 acting as '*', and a group-less wildcard "capturing" its whole match.
-Every match runs in the k_wildcard kernel; without libie_amd.so or a GPU these calls raise.
+dialect="rs" follows rust-project/src/runtime.rs's regex-crate construction instead ('$' at the
+end only, no U+3020 group, no capture without a group; parity unpinned). Every match runs in the
+k_wildcard kernel; without libie_amd.so or a GPU these calls raise.
 """
 import ctypes
 
@@ -23,15 +25,16 @@ from . import _native as N
 class Wildcards:
     """An ordered list of wildcards compiled onto one device (ie_wildcards_build)."""
 
-    def __init__(self, patterns, device=0):
+    def __init__(self, patterns, device=0, dialect="py"):
         self.patterns = list(patterns)
         self.device = device
+        self.dialect = dialect
         blob, offs = N.pack(self.patterns)
         self._blob = blob
         self.h = ctypes.c_void_p()
         bp = ctypes.c_char_p(blob)
         N.check(N.lib().ie_wildcards_build(ctypes.cast(bp, ctypes.c_void_p), offs.ctypes.data, len(self.patterns),
-                                           device, ctypes.byref(self.h)), "ie_wildcards_build")
+                                           N.IE_DIALECT[dialect], device, ctypes.byref(self.h)), "ie_wildcards_build")
 
     def close(self):
         if self.h:

@@ -221,3 +221,19 @@ def first_wildcard_match(patterns, s):
         if is_wildcard_match(w, s):
             return p, get_wildcard_matches(w, s)
     return -1, []
+
+
+def wildcard_regex_rs(wildcard_s):
+    """runtime.rs:1633-1647 / 1754-1775 restated on Python re: '*' -> '(.*)', every other char
+    escaped (no U+3020 rule), '$' of the regex crate = Python's \\Z (the end only). Unpinned."""
+    import re
+    return "^" + "".join("(.*)" if ch == "*" else re.escape(ch) for ch in wildcard_s) + r"\Z"
+
+
+def first_wildcard_match_rs(patterns, s):
+    import re
+    for p, w in enumerate(patterns):
+        m = re.match(wildcard_regex_rs(w), s, re.DOTALL)
+        if m:
+            return p, list(m.groups())
+    return -1, []

@@ -818,3 +818,19 @@ def test_ingestion_and_display_sites():
     assert PKG.display_texts(texts) == [O.escape(t, unescape=True) for t in texts]
     with pytest.raises(AttributeError):
         PKG.display_text(5)
+
+
+def test_rust_dialect_hand_derived_vectors():
+    """The hand-derived interp.rs vectors of test_oracle_golden.py on the device (rs dialect)."""
+    from tests.test_oracle_golden import test_oracle_rust_dialect_restated as T
+    cases = [m.args[1] for m in T.pytestmark if m.name == "parametrize"][0]
+    t = {"a": "A", "L": ["x", "y"], "f": 1.5, "k": "K", "open": "}{", "n": 5, "5": "five", "t": True,
+         "nested": ["p", [1, 2], {"z": 1}], "none": None, "obj": {"b": 2}, "q-5": "Q5", "i": 5, "neg": -3,
+         "two": 2.0, "bs": "q\\", "e": "", "big": 12345678901234567890}
+    got, _ = run_product(t, [s for s, _ in cases], "rs")
+    for (s, want), (st, payload) in zip(cases, got):
+        assert N.STATUS_NAMES[st] == want[0], (s, N.STATUS_NAMES[st], want)
+        if want[1] is not None and want[0] == "OK_STR":
+            assert payload == want[1], (s, payload)
+        if want[1] is not None and want[0] == "OK_VALUE":
+            assert list(t)[payload] == want[1], (s, payload)

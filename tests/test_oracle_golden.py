@@ -64,12 +64,43 @@ def test_oracle_simple_insertkey_golden():
     ("{{n}}", ("OK_VALUE", None)),          # D4: rs value_to_string(5) == "5" is a key here
     ("x{t}", ("E_ASSERT_TYPE", None)),      # bool is not splicable in rs either
     ("{}", ("E_INTERP", None)),             # D10
+    # derived line by line from interp.rs:31-89 (interpolate_inserts), 91-137 (get_interpdata),
+    # 314-322 (value_to_string)
+    ("x{nested}y", ("E_INTERP", None)),     # :74 join -> 'p12{"z":1}'; the loop (:55) re-reads '{"z":1}' as a key
+    ("x{none}y", ("E_ASSERT_TYPE", None)),  # :76-79 Null is unsupported
+    ("x{obj}y", ("E_ASSERT_TYPE", None)),   # :76-79 Object is unsupported
+    ("x{n}y", ("OK_STR", "x5y")),           # :73 Number::to_string
+    ("x{neg}y", ("OK_STR", "x-3y")),
+    ("x{two}", ("OK_STR", "x2.0")),         # serde_json prints f64 2.0 as "2.0"
+    ("{q-{i}}", ("OK_VALUE", "q-5")),       # :50-51 the key is interpolated first: "q-5"
+    ("a{e}b", ("OK_STR", "ab")),
+    ("\\{a\\}", ("OK_STR", "\\{a\\}")),    # :42-43 protected, :84-85 restored
+    ("{a", ("E_ASSERT_BRACES", None)),      # :56-61 uneven count
+    ("a}", ("OK_STR", "a}")),               # :54 no '{': the loop never runs
+    ("{bs}x", ("OK_STR", "q\\x")),
+    ("{bs}{a}", ("OK_STR", "q\\A")),        # rightmost first: {a}, then {bs}
+    ("{a}{bs}", ("OK_STR", "Aq\\")),
+    ("{t}", ("OK_VALUE", "t")),             # :44-52 simple path returns the Bool itself
+    ("{{a}}", ("E_INTERP", None)),          # :46-48 subkey a -> "A" is then the key: missing
+    ("{{f}}", ("E_INTERP", None)),          # value_to_string(1.5) = "1.5": missing
+    ("{5}", ("OK_VALUE", "5")),
+    ("x{}y", ("E_INTERP", None)),           # :103 '' key
+    ("{ARG1}", ("E_INTERP", None)),         # :109-115 ARGn not provided
+    ("}{", ("E_RS_PANIC", None)),           # :63-66 no '}' after the last '{': unwrap() on None
+    ("a}{b", ("E_RS_PANIC", None)),
+    ("x{L}{L}", ("OK_STR", "xxyxy")),
+    ("n={big}", ("OK_STR", "n=12345678901234567890")),
 ])
 def test_oracle_rust_dialect_restated(s, want):
-    """Rust dialect: hand-derived from rust-project/src/interp.rs (parity unpinned)."""
-    t = {"a": "A", "L": ["x", "y"], "f": 1.5, "k": "K", "open": "}{", "n": 5, "5": "five", "t": True}
+    """Rust dialect: hand-derived from rust-project/src/interp.rs (parity unpinned).
+    For OK_VALUE the second field names the key whose value is returned."""
+    t = {"a": "A", "L": ["x", "y"], "f": 1.5, "k": "K", "open": "}{", "n": 5, "5": "five", "t": True,
+         "nested": ["p", [1, 2], {"z": 1}], "none": None, "obj": {"b": 2}, "q-5": "Q5", "i": 5, "neg": -3,
+         "two": 2.0, "bs": "q\\", "e": "", "big": 12345678901234567890}
     o = O.Oracle(t, "rs")
     st, out, vid = o.interpolate(s)
     assert st == want[0]
-    if want[1] is not None:
+    if want[1] is not None and st == "OK_STR":
         assert out == want[1]
+    if want[1] is not None and st == "OK_VALUE":
+        assert list(t)[vid] == want[1]

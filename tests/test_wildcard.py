@@ -142,3 +142,19 @@ def test_device_long_strings_and_random_vs_oracle():
     for s, g in zip(strings, got):
         assert g == O.first_wildcard_match(pats, s), s[:80]
     W.close()
+
+
+@pytest.mark.gpu
+def test_device_rust_dialect_vs_restated_regex():
+    """IE_DIALECT_RS: the regex-crate construction of runtime.rs (parity unpinned: no toolchain),
+    against its restatement on Python re (\\Z for the crate's '$')."""
+    pkg = _pkg()
+    rng = random.Random(13)
+    pats = ["*", "a*", "*\n", "x〠y", "*|*", "", "ab\n", "*a*b*"] + \
+        ["".join(rng.choice("ab*\n 〠") for _ in range(rng.randrange(0, 6))) for _ in range(30)]
+    strings = ["", "\n", "ab\n", "x〠y", "a|b"] + \
+        ["".join(rng.choice(["a", "b", "\n", " ", "〠"]) for _ in range(rng.randrange(0, 14))) for _ in range(3000)]
+    W = pkg.Wildcards(pats, dialect="rs")
+    for s, g in zip(strings, W.first_match(strings)):
+        assert g == O.first_wildcard_match_rs(pats, s), s
+    W.close()
