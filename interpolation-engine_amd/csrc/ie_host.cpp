@@ -258,7 +258,7 @@ int set_device(int32_t dev) {
 // [2..3] pool bytes used (u64), [4..8] telemetry (literal strings, deferred tiles, look-back polls,
 // exact-path strings, chain failures), [9] deferred-tile count; zeroed on every call.
 int ensure_work(ie_exec* x, int op, uint64_t n) {
-  const uint64_t tiles = (n + kBlock - 1) / kBlock + 1;
+  const uint64_t tiles = (n + kBlock - 1) / kBlock + 1;  // (kRBlock >= kBlock: enough for k_resolve too)
   IE_HIP(x->counters.ensure(64));
   if (op == kOpInterp) {
     IE_HIP(x->tile_state.ensure(tiles * sizeof(uint64_t)));
@@ -266,7 +266,7 @@ int ensure_work(ie_exec* x, int op, uint64_t n) {
     // room for every tile to be deferred (64 B of descriptor per string; grow-only, never read
     // unless written, so only HBM capacity is spent)
     IE_HIP(x->defer_tiles.ensure(tiles * sizeof(uint32_t)));
-    IE_HIP(x->defer_desc.ensure(tiles * kBlock * 64));
+    IE_HIP(x->defer_desc.ensure(tiles * kBlock * 64));  // tiles * kBlock >= resolve tiles * kRBlock
   } else {
     IE_HIP(x->out_len.ensure((n + 1) * sizeof(uint32_t)));
     IE_HIP(x->tile_sum.ensure(tiles * sizeof(uint64_t)));
@@ -313,7 +313,7 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
   if (rc) return rc;
   x->stamp_tiles = 0;
   if (op == kOpInterp && !x->stamps_path.empty()) {  // diagnostic build hook, see DESIGN.md
-    const uint64_t tiles = (n + kBlock - 1) / kBlock;
+    const uint64_t tiles = (n + kRBlock - 1) / kRBlock;
     IE_HIP(x->stamps.ensure(tiles * 128));
     x->stamp_tiles = tiles;
   }
@@ -327,7 +327,7 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
     IE_HIP(hipMemsetAsync(out->offsets, 0, sizeof(uint64_t), st));
     IE_HIP(hipMemsetAsync(out->total, 0, sizeof(uint64_t), st));
   } else if (op == kOpInterp) {
-    const uint64_t tiles = (n + kBlock - 1) / kBlock;
+    const uint64_t tiles = (n + kRBlock - 1) / kRBlock;
     IE_HIP(hipMemsetAsync(x->tile_state.p, 0, tiles * sizeof(uint64_t), st));
     // fail commit: forced by the option (diagnostics, tests), else adaptive on the count of chain
     // failures (misses / unspliceable hits) an earlier batch saw, in either variant

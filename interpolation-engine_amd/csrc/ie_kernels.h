@@ -12,8 +12,16 @@ constexpr int kBlock = 256;          // lanes per workgroup = strings per tile
 constexpr int kMaxDepth = 6;         // fast-path nesting limit (deeper: literal path)
 constexpr int kKeyCap = 32;          // exact-evaluator key bytes per lane (longer keys: literal path)
 
-constexpr int kTileBytes = 17664;    // LDS input stage; larger tiles read global memory directly
-constexpr int kStageBytes = 20480;   // LDS output stage; a larger tile's lanes store their own bytes
+constexpr int kTileBytes = 17664;    // escape kernels: LDS input stage per 256-string tile
+constexpr int kStageBytes = 20480;   // escape kernels: LDS output stage
+
+// k_resolve's tile: IE_RBLOCK strings (one lane each); the stages scale with it
+#ifndef IE_RBLOCK
+#define IE_RBLOCK 256
+#endif
+constexpr int kRBlock = IE_RBLOCK;
+constexpr int kRTileBytes = 17664 * (IE_RBLOCK / 256);   // LDS input stage: the tile's first bytes
+constexpr int kRStageBytes = 20480 * (IE_RBLOCK / 256);  // LDS output stage; larger outputs: k_emit_windows
 
 enum { kOpInterp = 0, kOpUnescape = 1, kOpEscape = 2 };
 

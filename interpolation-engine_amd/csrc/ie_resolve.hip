@@ -299,7 +299,7 @@ __device__ __forceinline__ void put_words(lds_u8* dst, const uint32_t (&t)[8], u
 // Exact evaluator (any string; the reference semantics of SURVEY §3.3). Rounds: every lane scans
 // up to its next closing brace, then all lanes that reached one probe the table together.
 // Scratch is lane-private LDS: the key buffer (kKeyCap bytes, 4-aligned) and the stack
-// (kMaxDepth words, stride kBlock) reuse the lane's own chain-evaluator columns.
+// (kMaxDepth words, stride kRBlock) reuse the lane's own chain-evaluator columns.
 // ------------------------------------------------------------------------------------------
 template <bool STAGED>
 __device__ uint8_t eval_exact(const DevTable& T, uint32_t tid, const Src<STAGED> s, uint32_t n, bool active, lds_u8* kbuf,
@@ -381,7 +381,7 @@ __device__ uint8_t eval_exact(const DevTable& T, uint32_t tid, const Src<STAGED>
           status = kStatusPending;
           break;
         }
-        stack[depth * kBlock] = (klen << 24) | i;  // the enclosing key resumes at klen
+        stack[depth * kRBlock] = (klen << 24) | i;  // the enclosing key resumes at klen
         klen = ks;
         poison &= ~(1u << depth);
         depth++;
@@ -396,7 +396,7 @@ __device__ uint8_t eval_exact(const DevTable& T, uint32_t tid, const Src<STAGED>
           continue;
         }
         depth--;
-        const uint32_t st = stack[depth * kBlock];
+        const uint32_t st = stack[depth * kRBlock];
         const uint32_t open = st & 0xFFFFFFu, resume = st >> 24, ks = (resume + 3) & ~3u;
         c_kl = klen - ks;
         c_ks = ks;
@@ -584,11 +584,11 @@ struct ChainJobs {  // LDS views, tile-wide
   lds_u16* meta;    // kJobCap: string lane | depth << 12
   lds_u32* res_k;   // kJobCap: the job's result: value kind << 30 | text length; kResFail | status | open << 8; kResReject
   lds_u32* res_s;   // kJobCap: value source (entry index / arena offset)
-  lds_u16* p0;      // kBlock: each string's first byte in the stage
-  lds_u32* tbl;     // kBlock: each string's table in the set
-  lds_u64* ev;      // kBlock x 4 columns: the event masks of strings with chains deeper than 2
+  lds_u16* p0;      // kRBlock: each string's first byte in the stage
+  lds_u32* tbl;     // kRBlock: each string's table in the set
+  lds_u64* ev;      // kRBlock x 4 columns: the event masks of strings with chains deeper than 2
 };
-constexpr uint32_t kJobCap = kMaxTop * kBlock;
+constexpr uint32_t kJobCap = kMaxTop * kRBlock;
 constexpr uint32_t kResFail = 1u << 29, kResReject = 1u << 28;
 
 // the string's chains (<= kMaxTop, depth <= kChainDepth; records as in ChainJobs::crec). False:
@@ -714,12 +714,12 @@ __device__ bool parse_chains(const lds_u8* tile, uint32_t p0, uint32_t n, const 
   bad |= ev_first(ev_from(Ev{Om.lo | Cm.lo, Om.hi | Cm.hi}, pos)) < 128u;  // more than kMaxTop chains
   ok = !bad && !(nch == 1 && whole);  // a whole-string pair: typed result (py:510-514), exact evaluator
   if (__any(ok && maxd > 2u)) {  // middle levels are found from these masks in their round
-    ev[0] = Om.lo, ev[kBlock] = Om.hi, ev[2 * kBlock] = Cm.lo, ev[3 * kBlock] = Cm.hi;
+    ev[0] = Om.lo, ev[kRBlock] = Om.hi, ev[2 * kRBlock] = Cm.lo, ev[3 * kRBlock] = Cm.hi;
   }
   return ok;
 }
 
-// The jobs [j0, j0 + 2 * kBlock) of the tile: lane t takes jobs j0 + t and j0 + kBlock + t. Round r
+// The jobs [j0, j0 + 2 * kRBlock) of the tile: lane t takes jobs j0 + t and j0 + kRBlock + t. Round r
 // resolves level r of each job (the innermost pair in round 0); the key of a level is A | T | B
 // (template before the child, the child's splice text, template after it; a leaf: A only),
 // assembled in registers and looked up with one pilot and one 48-byte entry read. A job ends at
@@ -739,7 +739,7 @@ __device__ void resolve_jobs(const DevTable& T, const lds_u8* tile, const ChainJ
   uint32_t maxd = 0;
 #pragma unroll
   for (int q = 0; q < NJ; q++) {
-    job[q] = j0 + (uint32_t)q * kBlock + tid;
+    job[q] = j0 + (uint32_t)q * kRBlock + tid;
     const bool valid = job[q] < njobs;
     cr[q] = valid ? J.crec[job[q]] : 0u;
     const uint32_t mt = valid ? (uint32_t)J.meta[job[q]] : 0u;
@@ -771,8 +771,8 @@ __device__ void resolve_jobs(const DevTable& T, const lds_u8* tile, const ChainJ
       if (__any(mid)) {
         if (mid) {
           const lds_u64* e = J.ev + ls[q];
-          o = ev_last(ev_below(Ev{e[0], e[kBlock]}, co_[q]));
-          c = ev_first(ev_from(Ev{e[2 * kBlock], e[3 * kBlock]}, cl_[q] + 1u));
+          o = ev_last(ev_below(Ev{e[0], e[kRBlock]}, co_[q]));
+          c = ev_first(ev_from(Ev{e[2 * kRBlock], e[3 * kRBlock]}, cl_[q] + 1u));
         }
       }
       open[q] = on[q] ? o : 0u;
@@ -980,7 +980,7 @@ __device__ uint64_t block_scan(uint64_t v, uint64_t* lds_w, uint64_t* total) {
   __syncthreads();
   uint64_t base = 0, tot = 0;
 #pragma unroll
-  for (uint32_t w = 0; w < kBlock / 64; w++) {
+  for (uint32_t w = 0; w < kRBlock / 64; w++) {
     const uint64_t x = lds_w[w];
     if (w < wid) base += x;
     tot += x;
@@ -994,18 +994,18 @@ __device__ uint64_t block_scan(uint64_t v, uint64_t* lds_w, uint64_t* total) {
 //   classification + evaluation: key areas [0, kKbufLds) | exact-evaluator stacks
 //     [kKbufLds, kEvalLds) | chunk event masks [kCmOff, ..) | odd-chunk bits [kOddOff, ..)
 //     (the masks are read only while building a lane's event window)
-//   literal results: pool offsets at [0, 4 * kBlock)
+//   literal results: pool offsets at [0, 4 * kRBlock)
 //   output: the tile's output bytes (tile-relative), read back for the realigned stream-out
-constexpr uint32_t kKbufLds = kBlock * kKeyCap;
-constexpr uint32_t kStackLds = kBlock * 32;  // exact-evaluator stacks (kMaxDepth words) | chain event masks
+constexpr uint32_t kKbufLds = kRBlock * kKeyCap;
+constexpr uint32_t kStackLds = kRBlock * 32;  // exact-evaluator stacks (kMaxDepth words) | chain event masks
 constexpr uint32_t kEvalLds = kKbufLds + kStackLds;
-constexpr uint32_t kChunks = (kTileBytes + 32) / 16;
-constexpr uint32_t kOddWords = ((kChunks + kBlock - 1) / kBlock) * (kBlock / 32) + 2;
+constexpr uint32_t kChunks = (kRTileBytes + 32) / 16;
+constexpr uint32_t kOddWords = ((kChunks + kRBlock - 1) / kRBlock) * (kRBlock / 32) + 2;
 constexpr uint32_t kCmOff = kEvalLds;
 constexpr uint32_t kOddOff = kCmOff + 4 * (kChunks + 10);
 constexpr uint32_t kEscOff = kOddOff + 4 * kOddWords;
 constexpr uint32_t kClassEnd = kEscOff + 4 * kOddWords;
-constexpr uint32_t kUnionLds = kClassEnd > (uint32_t)kStageBytes + 32 ? kClassEnd : (uint32_t)kStageBytes + 32;
+constexpr uint32_t kUnionLds = kClassEnd > (uint32_t)kRStageBytes + 32 ? kClassEnd : (uint32_t)kRStageBytes + 32;
 static_assert(kKeyCap >= 32 && kMaxDepth <= 8, "evaluator scratch");
 
 // where a tile's strings lie: [lo, hi) for the tile, this lane's string at so (sn bytes)
@@ -1014,9 +1014,9 @@ struct TileGeo {
 };
 __device__ __forceinline__ TileGeo load_geo(const Batch& B, uint32_t tile, uint32_t tid) {
   TileGeo g{0, 0, 0, 0};
-  const uint64_t first = (uint64_t)tile * kBlock;
+  const uint64_t first = (uint64_t)tile * kRBlock;
   if (first >= B.n) return g;
-  const uint64_t last = min(first + (uint64_t)kBlock, B.n), i = first + tid;
+  const uint64_t last = min(first + (uint64_t)kRBlock, B.n), i = first + tid;
   g.lo = gld(B.in_off + first);
   g.hi = gld(B.in_off + last);
   if (i < B.n) {
@@ -1026,7 +1026,7 @@ __device__ __forceinline__ TileGeo load_geo(const Batch& B, uint32_t tile, uint3
   return g;
 }
 
-constexpr uint32_t kStageChunks = (kTileBytes + 31) / 16;  // the input stage: the tile's first chunks
+constexpr uint32_t kStageChunks = (kRTileBytes + 31) / 16;  // the input stage: the tile's first chunks
 
 // a tile's input chunks in flight into registers, written to the LDS stage later
 template <int MAXV>
@@ -1040,19 +1040,19 @@ struct TilePrefetch {
     nv = (uint32_t)min((uint64_t)((shift + (g.hi - g.lo) + 15) >> 4), (uint64_t)kStageChunks);
 #pragma unroll
     for (int k = 0; k < MAXV; k++) {
-      const uint32_t j = tid + (uint32_t)k * kBlock;
+      const uint32_t j = tid + (uint32_t)k * kRBlock;
       if (j < nv) v[k] = gld4(src + j);
     }
   }
   __device__ __forceinline__ void commit(uint4* dst, uint32_t tid) const {
 #pragma unroll
     for (int k = 0; k < MAXV; k++) {
-      const uint32_t j = tid + (uint32_t)k * kBlock;
+      const uint32_t j = tid + (uint32_t)k * kRBlock;
       if (j < nv) dst[j] = v[k];
     }
   }
 };
-constexpr int kStageV = (kStageChunks + kBlock - 1) / kBlock;
+constexpr int kStageV = (kStageChunks + kRBlock - 1) / kRBlock;
 
 // bytes r..r+15 (r wave-uniform, 0..15) of the 32 bytes x | y
 __device__ __forceinline__ uint4 bytes_at(u32x4 x, u32x4 y, uint32_t r) {
@@ -1074,7 +1074,7 @@ __device__ __forceinline__ void stream_stage(uint8_t* g, const uint8_t* stage, u
   const uintptr_t pg = (uintptr_t)g, pe = pg + len;
   const uintptr_t a_up = (pg + 15) & ~(uintptr_t)15, b_down = pe & ~(uintptr_t)15;
   if (a_up >= b_down) {
-    for (uint32_t k = tid; k < len; k += kBlock) gst(g + k, ((const lds_u8*)stage)[k]);
+    for (uint32_t k = tid; k < len; k += kRBlock) gst(g + k, ((const lds_u8*)stage)[k]);
     return;
   }
   const uint32_t head = (uint32_t)(a_up - pg), tail = (uint32_t)(pe - b_down);
@@ -1084,11 +1084,11 @@ __device__ __forceinline__ void stream_stage(uint8_t* g, const uint8_t* stage, u
     gst(g + k, ((const lds_u8*)stage)[k]);
   }
   const uint32_t nv = (uint32_t)((b_down - a_up) >> 4);
-  constexpr int kOutV = (kStageBytes + kBlock * 16 - 1) / (kBlock * 16);
+  constexpr int kOutV = (kRStageBytes + kRBlock * 16 - 1) / (kRBlock * 16);
   uint4 v[kOutV];
 #pragma unroll
   for (int k = 0; k < kOutV; k++) {
-    const uint32_t c = tid + (uint32_t)k * kBlock;
+    const uint32_t c = tid + (uint32_t)k * kRBlock;
     if (c < nv) {
       const lds_u128* blk = (const lds_u128*)(const lds_u8*)stage + c;
       const u32x4 x = blk[0], y = blk[1];
@@ -1098,7 +1098,7 @@ __device__ __forceinline__ void stream_stage(uint8_t* g, const uint8_t* stage, u
   uint4* dstv = (uint4*)a_up;
 #pragma unroll
   for (int k = 0; k < kOutV; k++) {
-    const uint32_t c = tid + (uint32_t)k * kBlock;
+    const uint32_t c = tid + (uint32_t)k * kRBlock;
     if (c < nv) gst4(dstv + c, v[k]);
   }
 }
@@ -1153,16 +1153,16 @@ __device__ __forceinline__ void window_piece(lds_u8* win, int64_t rel, const uin
 // The deferred tiles' bytes (see k_resolve): one workgroup per deferred tile at a time. Each
 // lane rebuilds its string's pieces from the stored descriptor (template runs from the input in
 // global memory, values from the table or the literal pool) and the tile's output goes through
-// the LDS stage in windows of kStageBytes (long pieces copied by a whole wave).
-__global__ __launch_bounds__(kBlock) void k_emit_windows(Batch B, Work W, DevTable T, uint8_t* out) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_win[kStageBytes + 48];
+// the LDS stage in windows of kRStageBytes (long pieces copied by a whole wave).
+__global__ __launch_bounds__(kRBlock) void k_emit_windows(Batch B, Work W, DevTable T, uint8_t* out) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_win[kRStageBytes + 48];
   const uint32_t count = __hip_atomic_load(W.defer_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t tid = threadIdx.x;
   for (uint32_t slot = blockIdx.x; slot < count; slot += gridDim.x) {
     const uint32_t tile = gld(W.defer_tiles + slot);
-    const uint64_t first = (uint64_t)tile * kBlock, last = min(first + (uint64_t)kBlock, B.n), i = first + tid;
+    const uint64_t first = (uint64_t)tile * kRBlock, last = min(first + (uint64_t)kRBlock, B.n), i = first + tid;
     const uint64_t base = gld(B.out_off + first), tile_total = gld(B.out_off + last) - base;
-    const uint4* dd = W.defer_desc + ((uint64_t)slot * kBlock + tid) * 4;
+    const uint4* dd = W.defer_desc + ((uint64_t)slot * kRBlock + tid) * 4;
     Desc d;
     uint32_t olen = 0, n32 = 0;
     uint64_t local = 0;
@@ -1184,8 +1184,8 @@ __global__ __launch_bounds__(kBlock) void k_emit_windows(Batch B, Work W, DevTab
     }
     const bool mine = olen != 0;
     lds_u8* const win = (lds_u8*)s_win;
-    for (uint64_t w0 = 0; w0 < tile_total; w0 += (uint64_t)kStageBytes) {
-      const uint32_t wl = (uint32_t)min((uint64_t)kStageBytes, tile_total - w0);
+    for (uint64_t w0 = 0; w0 < tile_total; w0 += (uint64_t)kRStageBytes) {
+      const uint32_t wl = (uint32_t)min((uint64_t)kRStageBytes, tile_total - w0);
       const int64_t rel0 = (int64_t)local - (int64_t)w0;  // this lane's output, window-relative
       const bool on = mine && rel0 < (int64_t)wl && rel0 + (int64_t)olen > 0;
       const uint32_t ntop = mine ? d.ntop : 0u;
@@ -1216,22 +1216,22 @@ __global__ __launch_bounds__(kBlock) void k_emit_windows(Batch B, Work W, DevTab
 // FAILC: chain failures commit in the chain evaluator (else they take the exact evaluator). Both
 // give the reference's results; the host picks per batch stream (ie_host.cpp, "fail commit").
 template <bool FAILC, bool MULTI>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES_PER_EU))) void k_resolve(Batch B, Work W, DevTable T, uint8_t* out,
+__global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES_PER_EU))) void k_resolve(Batch B, Work W, DevTable T, uint8_t* out,
                                                     uint64_t cap) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_in[kTileBytes + 48];
+  __shared__ __attribute__((aligned(16))) uint8_t s_in[kRTileBytes + 48];
   __shared__ __attribute__((aligned(16))) uint8_t s_u[kUnionLds];
-  __shared__ uint32_t s_olen[kBlock];  // output length; the value id for IE_OK_VALUE strings
-  __shared__ uint8_t s_st[kBlock];
-  __shared__ uint8_t s_pend[kBlock];
+  __shared__ uint32_t s_olen[kRBlock];  // output length; the value id for IE_OK_VALUE strings
+  __shared__ uint8_t s_st[kRBlock];
+  __shared__ uint16_t s_pend[kRBlock];
   __shared__ uint32_t s_misc[4];  // tile, pending count, defer slot
-  __shared__ uint64_t s_red[kBlock / 64 + 2];
+  __shared__ uint64_t s_red[kRBlock / 64 + 2];
   lds_u32* const s_cm = (lds_u32*)(lds_u8*)(s_u + kCmOff);    // event masks of the staged chunks (+ pad)
   lds_u32* const s_odd = (lds_u32*)(lds_u8*)(s_u + kOddOff);  // one bit per chunk: 0xE3 inside
   lds_u32* const s_esc = (lds_u32*)(lds_u8*)(s_u + kEscOff);  // one bit per chunk: '\' inside
   lds_u32* const s_lit = (lds_u32*)(lds_u8*)s_u;              // literal-path results: pool offset >> 4
 
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
-  const uint32_t ntiles = (uint32_t)((B.n + kBlock - 1) / kBlock);
+  const uint32_t ntiles = (uint32_t)((B.n + kRBlock - 1) / kRBlock);
   // Tile = workgroup index: workgroups are dispatched in index order, so every tile a look-back
   // waits on is already resident (no ticket: a single-address atomic serializes chip-wide).
   uint32_t tile = blockIdx.x;
@@ -1258,8 +1258,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     stamp_row[7] = ((uint64_t)xcc << 32) | hw;
   }
-  const uint64_t first = (uint64_t)tile * kBlock;
-  const uint64_t last = min(first + (uint64_t)kBlock, B.n);
+  const uint64_t first = (uint64_t)tile * kRBlock;
+  const uint64_t last = min(first + (uint64_t)kRBlock, B.n);
   const uint64_t i = first + tid;
   const uint64_t lo = geo.lo, hi = geo.hi, so = geo.so, sn = geo.sn;
   const uint32_t shift = (uint32_t)((uintptr_t)(B.bytes + lo) & 15);
@@ -1271,7 +1271,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES
   {
     pre.commit((uint4*)s_in, tid);
     __syncthreads();
-    for (uint32_t c0 = 0; c0 < nv; c0 += kBlock) {  // uniform trip count: ballots below
+    for (uint32_t c0 = 0; c0 < nv; c0 += kRBlock) {  // uniform trip count: ballots below
       const uint32_t c = c0 + tid;
       bool odd = false, esc = false;
       if (c < nv) s_cm[c] = chunk_classify((const lds_u32*)(lds_u8*)s_in + 4 * c, odd, esc);
@@ -1340,7 +1340,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES
       J.tbl[tid] = tid_s;
       __syncthreads();
       IE_STAMP(9);
-      for (uint32_t j0 = 0; j0 < njobs; j0 += 2 * kBlock) resolve_jobs<FAILC>(T, (const lds_u8*)s_in, J, j0, njobs, chain_fail, j0 == 0 ? stamp_row : nullptr);
+      for (uint32_t j0 = 0; j0 < njobs; j0 += 2 * kRBlock) resolve_jobs<FAILC>(T, (const lds_u8*)s_in, J, j0, njobs, chain_fail, j0 == 0 ? stamp_row : nullptr);
       IE_STAMP(10);
       __syncthreads();
       IE_STAMP(11);
@@ -1367,7 +1367,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES
     }
     if (active) st = r;
     pend = i < B.n && st == kStatusPending;
-    if (pend) s_pend[atomicAdd(&s_misc[1], 1u)] = (uint8_t)tid;
+    if (pend) s_pend[atomicAdd(&s_misc[1], 1u)] = (uint16_t)tid;
     s_st[tid] = st;
     s_olen[tid] = st == IE_OK_STR ? olen : (st == IE_OK_VALUE ? vid : 0u);
   }
@@ -1377,7 +1377,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES
   // ---- 3. literal path for the pending strings, one wave each; results in the union ----
   const uint32_t npend = s_misc[1];
   if (tid == 0 && npend) atomicAdd(W.stats, npend);
-  for (uint32_t k = wave; k < npend; k += kBlock / 64) {
+  for (uint32_t k = wave; k < npend; k += kRBlock / 64) {
     const uint32_t j = s_pend[k];
     const uint64_t gi = first + j;
     const uint64_t po = gld(B.in_off + gi), pn = gld(B.in_off + gi + 1) - po;
@@ -1427,7 +1427,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES
 
   // ---- 5. the tile's output bytes into the LDS stage (tile-relative offsets) while the
   //      look-back is pending; tiles whose output does not fit store straight to HBM later ----
-  const bool in_stage = tile_total <= (uint64_t)kStageBytes;
+  const bool in_stage = tile_total <= (uint64_t)kRStageBytes;
   const bool mine = i < B.n && st == IE_OK_STR && olen;
   if (in_stage) {
     // entry texts of the values (inline, <= kInlineText bytes): into registers first, all in flight
@@ -1474,10 +1474,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES
   IE_STAMP(4);
   if (wave == 0) {
     const uint64_t b = look_back(W.tile_state, tile, tile_total, W.err, W.stamps ? W.stats + 2 : nullptr, lb_early);
-    if (tid == 0) s_red[kBlock / 64] = b;
+    if (tid == 0) s_red[kRBlock / 64] = b;
   }
   __syncthreads();
-  const uint64_t base = s_red[kBlock / 64];
+  const uint64_t base = s_red[kRBlock / 64];
   // the lane index, opaque to the compiler from here on: the tail recomputes its indices instead
   // of keeping (and spilling) the staging loop's, which are equal expressions of threadIdx.x
   uint32_t tid_t;
@@ -1507,7 +1507,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES
     if (tid == 0) s_misc[2] = atomicAdd(W.defer_count, 1u);
     __syncthreads();
     const uint32_t slot = s_misc[2];
-    uint4* dd = W.defer_desc + ((uint64_t)slot * kBlock + tid_t) * 4;
+    uint4* dd = W.defer_desc + ((uint64_t)slot * kRBlock + tid_t) * 4;
     const uint32_t nt = mine ? d.ntop : 0u;
     gst4(dd, make_uint4(nt, d.open[0], d.open[1], d.open[2]));
     gst4(dd + 1, make_uint4(d.close[0], d.close[1], d.close[2], n32));
@@ -1556,17 +1556,17 @@ hipError_t launch_debug_probe(const DevTable& T, const uint8_t* key, uint32_t kl
 
 hipError_t launch_resolve(const Batch& B, const Work& W, const DevTable& T, uint8_t* out, uint64_t cap,
                           hipStream_t st) {
-  const uint64_t tiles = (B.n + kBlock - 1) / kBlock;
+  const uint64_t tiles = (B.n + kRBlock - 1) / kRBlock;
   if (!tiles) return hipSuccess;
   if (tiles > 0xFFFFFFFFull) return hipErrorInvalidValue;
   const uint32_t grid = (uint32_t)tiles;
   const bool multi = B.table_id != nullptr;
-  if (W.fail_commit && multi) hipLaunchKernelGGL((k_resolve<true, true>), dim3(grid), dim3(kBlock), 0, st, B, W, T, out, cap);
-  else if (W.fail_commit) hipLaunchKernelGGL((k_resolve<true, false>), dim3(grid), dim3(kBlock), 0, st, B, W, T, out, cap);
-  else if (multi) hipLaunchKernelGGL((k_resolve<false, true>), dim3(grid), dim3(kBlock), 0, st, B, W, T, out, cap);
-  else hipLaunchKernelGGL((k_resolve<false, false>), dim3(grid), dim3(kBlock), 0, st, B, W, T, out, cap);
+  if (W.fail_commit && multi) hipLaunchKernelGGL((k_resolve<true, true>), dim3(grid), dim3(kRBlock), 0, st, B, W, T, out, cap);
+  else if (W.fail_commit) hipLaunchKernelGGL((k_resolve<true, false>), dim3(grid), dim3(kRBlock), 0, st, B, W, T, out, cap);
+  else if (multi) hipLaunchKernelGGL((k_resolve<false, true>), dim3(grid), dim3(kRBlock), 0, st, B, W, T, out, cap);
+  else hipLaunchKernelGGL((k_resolve<false, false>), dim3(grid), dim3(kRBlock), 0, st, B, W, T, out, cap);
   // the deferred (oversized) tiles' bytes; exits at once when there are none
-  if (out) hipLaunchKernelGGL(k_emit_windows, dim3(grid < 512u ? grid : 512u), dim3(kBlock), 0, st, B, W, T, out);
+  if (out) hipLaunchKernelGGL(k_emit_windows, dim3(grid < 512u ? grid : 512u), dim3(kRBlock), 0, st, B, W, T, out);
   return hipGetLastError();
 }
 
