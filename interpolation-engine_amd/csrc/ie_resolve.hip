@@ -1006,6 +1006,9 @@ constexpr uint32_t kOddOff = kCmOff + 4 * (kChunks + 10);
 constexpr uint32_t kEscOff = kOddOff + 4 * kOddWords;
 constexpr uint32_t kClassEnd = kEscOff + 4 * kOddWords;
 constexpr uint32_t kUnionLds = kClassEnd > (uint32_t)kRStageBytes + 32 ? kClassEnd : (uint32_t)kRStageBytes + 32;
+// the output stage: all of the union the classification needs anyway (config 2's 256-string
+// tiles average 20.4 KB of output; a 20 KB stage sent a third of them to k_emit_windows)
+constexpr uint32_t kOutStage = (kUnionLds - 32) & ~15u;
 static_assert(kKeyCap >= 32 && kMaxDepth <= 8, "evaluator scratch");
 
 // where a tile's strings lie: [lo, hi) for the tile, this lane's string at so (sn bytes)
@@ -1041,7 +1044,7 @@ struct TilePrefetch {
 #pragma unroll
     for (int k = 0; k < MAXV; k++) {
       const uint32_t j = tid + (uint32_t)k * kRBlock;
-      if (j < nv) v[k] = gld4(src + j);
+      if (j < nv) v[k] = gld4s(src + j);
     }
   }
   __device__ __forceinline__ void commit(uint4* dst, uint32_t tid) const {
@@ -1084,7 +1087,7 @@ __device__ __forceinline__ void stream_stage(uint8_t* g, const uint8_t* stage, u
     gst(g + k, ((const lds_u8*)stage)[k]);
   }
   const uint32_t nv = (uint32_t)((b_down - a_up) >> 4);
-  constexpr int kOutV = (kRStageBytes + kRBlock * 16 - 1) / (kRBlock * 16);
+  constexpr int kOutV = (kOutStage + kRBlock * 16 - 1) / (kRBlock * 16);
   uint4 v[kOutV];
 #pragma unroll
   for (int k = 0; k < kOutV; k++) {
@@ -1099,7 +1102,7 @@ __device__ __forceinline__ void stream_stage(uint8_t* g, const uint8_t* stage, u
 #pragma unroll
   for (int k = 0; k < kOutV; k++) {
     const uint32_t c = tid + (uint32_t)k * kRBlock;
-    if (c < nv) gst4(dstv + c, v[k]);
+    if (c < nv) gst4s(dstv + c, v[k]);
   }
 }
 
@@ -1124,7 +1127,15 @@ __device__ void wave_copy(lds_u8* dst, const uint8_t* src, uint32_t len) {
   const uint32_t sh = (uint32_t)(sa & 3u);
   const uint32_t* s32 = (const uint32_t*)(sa - sh);
   lds_u32* d32 = (lds_u32*)(dst + h);
-  for (uint32_t q = lane; q < nw; q += 64) {
+  uint32_t q = lane;
+  for (; q + 192 < nw; q += 256) {  // 1 KB per step, every load of the step in flight together
+    uint32_t a[4], b[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) a[k] = rd32(s32 + q + 64 * k), b[k] = rd32(s32 + q + 64 * k + 1);
+#pragma unroll
+    for (int k = 0; k < 4; k++) d32[q + 64 * k] = sh ? __builtin_amdgcn_alignbyte(b[k], a[k], sh) : a[k];
+  }
+  for (; q < nw; q += 64) {
     const uint32_t w0 = rd32(s32 + q);
     d32[q] = sh ? __builtin_amdgcn_alignbyte(rd32(s32 + q + 1), w0, sh) : w0;
   }
@@ -1147,6 +1158,21 @@ __device__ __forceinline__ void window_piece(lds_u8* win, int64_t rel, const uin
     const uint32_t fl = __shfl((uint32_t)f, l, 64), fh = __shfl((uint32_t)(f >> 32), l, 64);
     const uint32_t aa = __shfl((uint32_t)a, l, 64), nn = __shfl(n, l, 64);
     wave_copy<SRC_LDS>(win + aa, (const uint8_t*)(uintptr_t)(((uint64_t)fh << 32) | fl), nn);
+  }
+}
+
+// len bytes at src (global memory) -> stage + off, by this lane; pieces over 96 bytes (multi-KB
+// values such as a state's history) by the whole wave instead, so that one lane's long copy does
+// not hold up its tile (and with it every later tile's look-back). Uniform control flow.
+__device__ __forceinline__ void stage_piece(lds_u8* stage, bool on, uint32_t off, const uint8_t* src, uint32_t len) {
+  const bool big = on && len > 96u;
+  if (on && !big && len) copy_bytes<true, false>((uint8_t*)(stage + off), src, len);
+  for (uint64_t m = __ballot(big); m; m &= m - 1) {
+    const int l = __builtin_ctzll(m);
+    const uint64_t f = (uint64_t)(uintptr_t)src;
+    const uint32_t fl = __shfl((uint32_t)f, l, 64), fh = __shfl((uint32_t)(f >> 32), l, 64);
+    const uint32_t oo = __shfl(off, l, 64), nn = __shfl(len, l, 64);
+    wave_copy<false>(stage + oo, (const uint8_t*)(uintptr_t)(((uint64_t)fh << 32) | fl), nn);
   }
 }
 
@@ -1427,7 +1453,7 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
 
   // ---- 5. the tile's output bytes into the LDS stage (tile-relative offsets) while the
   //      look-back is pending; tiles whose output does not fit store straight to HBM later ----
-  const bool in_stage = tile_total <= (uint64_t)kRStageBytes;
+  const bool in_stage = tile_total <= (uint64_t)kOutStage;
   const bool mine = i < B.n && st == IE_OK_STR && olen;
   if (in_stage) {
     // entry texts of the values (inline, <= kInlineText bytes): into registers first, all in flight
@@ -1464,10 +1490,10 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
       const uint32_t kind = d.vk[j] >> 30, len = von ? d.vk[j] & kLenMask : 0u;
       const bool ent = von && kind == kValEntry;
       if (__any(ent) && ent) put_words(dd + w, tt[j], len);
-      if (von && kind == kValArena)
-        copy_bytes<true, false>((uint8_t*)(dd + w), T.arena + d.vs[j], len);
-      else if (von && kind == kValPool)
-        copy_bytes<true, false>((uint8_t*)(dd + w), W.pool + ((uint64_t)d.vs[j] << 4), len);
+      const bool far = von && kind != kValEntry;  // an arena or literal-pool text
+      if (__any(far))
+        stage_piece((lds_u8*)s_u, far, (uint32_t)(mine ? local : 0) + w,
+                    kind == kValArena ? T.arena + d.vs[j] : W.pool + ((uint64_t)d.vs[j] << 4), len);
       w += len;
     }
   }
@@ -1484,8 +1510,8 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
   asm volatile("v_mov_b32 %0, %1" : "=v"(tid_t) : "v"(tid));
   const uint64_t i_t = first + tid_t;
   if (i_t < B.n) {
-    gst(B.out_off + i_t, base + local);
-    gst(B.status + i_t, st);
+    gsts(B.out_off + i_t, base + local);
+    gsts(B.status + i_t, st);
     if (st == IE_OK_VALUE) gst(B.value_id + i_t, s_olen[tid_t]);
   }
   if (last == B.n && tid == 0) {

@@ -24,3 +24,10 @@ if m.any():
     m2 = c[:, 15] > 0
     if m2.any():
         print("round 1 (keys+pilot+entry) %.2f us; after -> resolved %.2f us" % (((c[m2, 15] - c[m2, 14]) / 100).mean(), ((c[m2, 10] - c[m2, 15]) / 100).mean()))
+# the slowest tiles (a slow tile holds back every later tile's look-back)
+print("life p50 %.2f p99 %.2f p99.9 %.2f max %.2f us" % (*np.percentile(life, [50, 99, 99.9]), life.max()))
+idx = np.argsort(-life)[:8]
+for t in idx:
+    row = b[t]
+    print("  tile %6d life %8.2f us: " % (np.flatnonzero(ok)[t], life[t]) +
+          " ".join("%s %.1f" % (nm, (row[y] - row[x]) / 100.0) for x, y, nm in order))
