@@ -15,4 +15,4 @@ for v in "$@"; do
   fi
 done
 for v in "$@"; do for f in gpurun_out/ab_${v}_cfg*.log gpurun_out/ab_${v}_noeval.log; do
-  [ -f "$f" ] && echo "$f $(python3 -c "import json; d=json.loads(open('$f').read().strip().splitlines()[-1]); r=d['roofline']; print(d['ms_per_step'], r['launch_ms'], r['frac'], r.get('telemetry',{}).get('windowed_tiles'))")"; done; done
+  if [ -f "$f" ]; then echo "$f $(python3 -c "import json; d=json.loads(open('$f').read().strip().splitlines()[-1]); r=d['roofline']; print(d['ms_per_step'], r['launch_ms'], r['frac'], r.get('telemetry',{}).get('windowed_tiles'))")"; fi; done; done
