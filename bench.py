@@ -285,12 +285,13 @@ def main():
 
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic_cfg%d.json" % cfg)
-    if cfg == 3 and not os.path.exists(pmc_path):
-        pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_path):
         try:
             pm = json.load(open(pmc_path))
-            if pm.get("config") == cfg and pm.get("n") == n:
+            # only figures measured on this very build of the kernels count
+            bid = L.ie_build_id()
+            bid = bid.decode() if isinstance(bid, bytes) else str(bid)
+            if pm.get("config") == cfg and pm.get("n") == n and pm.get("build_id") == bid:
                 traffic = pm.get("hbm_bytes_per_step")
         except (OSError, ValueError):
             traffic = None

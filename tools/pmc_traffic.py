@@ -1,0 +1,58 @@
+"""HBM traffic per k_resolve launch from a FETCH_SIZE and a WRITE_SIZE rocprofv3 --pmc pass of
+`bench.py --config C` (tools/gpu_round.sh), written to profiles/pmc_traffic_cfgC.json, which
+bench.py reads for `roofline.traffic`.
+
+Which dispatches count: the k_resolve dispatches of the batch (the largest grid; the table
+build's small pre-resolution dispatch is left out). In config 4 every step launches k_resolve
+twice (the interpolation, then the unescape command's second resolve): the roofline kernel is the
+first, so every other batch-sized dispatch counts, starting with the first. FETCH_SIZE is doubled
+(MI355X_MICROARCH.md: gfx950 tallies 128-byte reads as 64 B); both counters are in KB.
+
+  python3 tools/pmc_traffic.py C N <fetch_dir> <write_dir> <build_id>
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def per_dispatch(d, counter, cfg):
+    rows = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if "k_resolve" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                k = int(r["Dispatch_Id"])
+                g = int(r["Grid_Size"])
+                rows.setdefault(k, [g, 0.0])[1] += float(r["Counter_Value"])
+    gmax = max(g for g, _ in rows.values())
+    vals = [v for k, (g, v) in sorted(rows.items()) if g == gmax]
+    if cfg == 4:
+        vals = vals[0::2]
+    return sum(vals) / len(vals), len(vals)
+
+
+def main():
+    cfg, n, fdir, wdir, bid = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], sys.argv[5]
+    fetch, nf = per_dispatch(fdir, "FETCH_SIZE", cfg)
+    write, nw = per_dispatch(wdir, "WRITE_SIZE", cfg)
+    out = {
+        "config": cfg,
+        "n": n,
+        "build_id": bid,
+        "k_resolve_launches": [nf, nw],
+        "fetch_size_kb": round(fetch),
+        "write_size_kb": round(write),
+        "hbm_bytes_per_step": int(round((2 * fetch + write) * 1024)),
+        "how": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes over bench.py --config %d "
+               "(tools/gpu_round.sh); per k_resolve launch of the batch (the roofline kernel; config 4: the "
+               "first resolve of each step); FETCH_SIZE doubled per MI355X_MICROARCH.md, WRITE_SIZE as is" % cfg,
+        "source": [os.path.relpath(fdir), os.path.relpath(wdir)],
+    }
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "pmc_traffic_cfg%d.json" % cfg)
+    json.dump(out, open(path, "w"), indent=1)
+    print(path, out["hbm_bytes_per_step"])
+
+
+if __name__ == "__main__":
+    main()
