@@ -34,6 +34,9 @@ FILES = {
     "sub/leaf": "leaf text",
     "x.json5": "'x as json5'",
     "ARG1": "never read",
+    "ARG\u00b2": "never read: str.isdigit() is true for a superscript two",
+    "ARG\u0663": "never read: an Arabic-Indic digit three",
+    "ARGx": "ARGx is not an argument key",
     "empty": "",
     "unicode": "héllo 😀 〠",
     "q-42": "forty-two",
@@ -46,7 +49,7 @@ INSERTS = {"name": "Tom", "adj": "tall", "over": "from the inserts", "k": "keyna
 CASES = [
     "{greet}", "x{greet}y", "{title}", "a {title} b", "{count}", "n={count}", "{list}", "L={list}",
     "{plain}", "[{plain}]", "{both}", "<{both}>", "{over}", "{sub/nested}", "{sub/leaf}", "({sub/leaf})",
-    "{x.json5}", "{x}", "{ARG1}", "{ARG2}", "{missing}", "{missing/x}", "{sub/missing}", "{empty}", "[{empty}]",
+    "{x.json5}", "{x}", "{ARG1}", "{ARG2}", "{ARG\u00b2}", "{ARG\u0663}", "{ARGx}", "a {ARG\u00b2} b", "{missing}", "{missing/x}", "{sub/missing}", "{empty}", "[{empty}]",
     "{unicode}", "u={unicode}", "{q-{count}}", "{q-{n}}", "{{k}}", "{{keyname}}", "{wrapped}", "w={wrapped}",
     "{dotted.name}", "{spaces key}", "{name} and {count} and {plain}", "\\{count\\} {count}", "{n}{count}{n}",
     "{HH:MM}", "{}", "no refs at all", "{name}",
