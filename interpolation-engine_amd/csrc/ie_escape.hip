@@ -72,6 +72,52 @@ __device__ uint32_t escape_len_lds(const uint8_t* s, uint32_t n) {
   return OP == kOpUnescape ? n - cnt : n + cnt;
 }
 
+// LDS views (ds_* accesses) and an LDS -> LDS copy at any alignments with aligned accesses only
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+// 16 bytes at any LDS address: five aligned dword reads and v_alignbyte (reads up to 19 bytes
+// past p)
+__device__ __forceinline__ u32x4 esc_ld16a(const lds_u8* p) {
+  const uint32_t sh = (uint32_t)(uintptr_t)p & 3u;
+  const lds_u32* q = (const lds_u32*)(p - sh);
+  const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4];
+  return u32x4{__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+               __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh)};
+}
+
+// len bytes LDS -> LDS: head bytes until dst is 4-aligned, 16-byte units as aligned dwords, then
+// the tail as dwords, a short and a byte. Wave-uniform call (lanes with len 0 copy nothing).
+__device__ __forceinline__ void lds_copy_any(lds_u8* dst, const lds_u8* src, uint32_t len) {
+  const uint32_t h0 = (0u - (uint32_t)(uintptr_t)dst) & 3u, h = h0 < len ? h0 : len;
+  if (h > 0) dst[0] = src[0];
+  if (h > 1) dst[1] = src[1];
+  if (h > 2) dst[2] = src[2];
+  const uint32_t body = (len - h) & ~15u;
+  for (uint32_t k = 0; __any(k < body); k += 16u) {
+    if (k < body) {
+      const u32x4 v = esc_ld16a(src + h + k);
+      lds_u32* q = (lds_u32*)(dst + h + k);
+      q[0] = v.x, q[1] = v.y, q[2] = v.z, q[3] = v.w;
+    }
+  }
+  const uint32_t kt = h + body;
+  if (kt < len) {
+    const u32x4 v = esc_ld16a(src + kt);
+    const uint32_t n = len - kt;
+    lds_u32* q = (lds_u32*)(dst + kt);
+    if (n >= 4) q[0] = v.x;
+    if (n >= 8) q[1] = v.y;
+    if (n >= 12) q[2] = v.z;
+    const uint32_t nw = n >> 2, r = n & 3u;
+    const uint32_t x = nw == 0 ? v.x : nw == 1 ? v.y : nw == 2 ? v.z : v.w;
+    lds_u8* b = dst + kt + (n & ~3u);
+    if (r & 2u) *(lds_u16*)b = (uint16_t)x;
+    if (r & 1u) b[r & 2u] = (uint8_t)(x >> (8u * (r & 2u)));
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // workgroup helpers
 // ------------------------------------------------------------------------------------------
@@ -93,29 +139,51 @@ __device__ uint64_t block_excl_scan(uint64_t v, uint64_t* lds_w /*kBlock/64*/, u
   return base + inc - v;
 }
 
-// Stage bytes [lo, hi) of the batch into LDS so that LDS position p holds byte (lo16 + p) where
-// lo16 = lo rounded down to 16 B. Body with 16-byte loads, ragged head/tail byte by byte (never
-// touches bytes outside [lo, hi)). Returns the LDS offset of byte `lo`.
-__device__ uint32_t stage_tile(const uint8_t* __restrict__ bytes, uint64_t lo, uint64_t hi,
-                               uint8_t* lds) {
-  const uintptr_t plo = (uintptr_t)(bytes + lo), phi = (uintptr_t)(bytes + hi);
-  const uintptr_t a_down = plo & ~(uintptr_t)15;
-  const uintptr_t a_up = (plo + 15) & ~(uintptr_t)15;
-  const uintptr_t b_down = phi & ~(uintptr_t)15;
-  const uint32_t shift = (uint32_t)(plo - a_down);
-  if (a_up >= b_down) {  // tiny tile: bytewise
-    for (uint32_t j = threadIdx.x; j < (uint32_t)(phi - plo); j += kBlock)
-      lds[shift + j] = ((const uint8_t*)plo)[j];
-  } else {
-    const uint32_t head = (uint32_t)(a_up - plo), tail = (uint32_t)(phi - b_down);
-    if (threadIdx.x < head) lds[shift + threadIdx.x] = ((const uint8_t*)plo)[threadIdx.x];
-    if (threadIdx.x < tail) lds[(uint32_t)(b_down - a_down) + threadIdx.x] = ((const uint8_t*)b_down)[threadIdx.x];
-    const uint4* src = (const uint4*)a_up;
-    uint4* dst = (uint4*)(lds + (a_up - a_down));
-    const uint32_t nv = (uint32_t)((b_down - a_up) >> 4);
-    for (uint32_t j = threadIdx.x; j < nv; j += kBlock) dst[j] = src[j];
+// Stage bytes [lo, hi) of the batch (hi - lo <= kTileBytes) into LDS so that LDS position p holds
+// byte (lo16 + p) where lo16 = lo rounded down to 16 B: whole aligned 16-byte chunks (one never
+// crosses a page; the bytes around [lo, hi) it carries are ignored), every load of the thread in
+// flight before the first LDS write, with the non-temporal policy (read once). Returns the LDS
+// offset of byte `lo`.
+__device__ uint32_t stage_tile(const uint8_t* __restrict__ bytes, uint64_t lo, uint64_t hi, uint8_t* lds) {
+  const uintptr_t plo = (uintptr_t)(bytes + lo);
+  const uint32_t shift = (uint32_t)(plo & 15);
+  const uint32_t nv = (uint32_t)((shift + (hi - lo) + 15) >> 4);
+  constexpr int MAXV = (kTileBytes + 30) / 16 / kBlock + 1;
+  const uint4* src = (const uint4*)(plo - shift);
+  uint4 v[MAXV];
+#pragma unroll
+  for (int k = 0; k < MAXV; k++) {
+    const uint32_t j = threadIdx.x + (uint32_t)k * kBlock;
+    if (j < nv) v[k] = gld4s(src + j);
+  }
+#pragma unroll
+  for (int k = 0; k < MAXV; k++) {
+    const uint32_t j = threadIdx.x + (uint32_t)k * kBlock;
+    if (j < nv) ((uint4*)lds)[j] = v[k];
   }
   return shift;
+}
+
+// ------------------------------------------------------------------------------------------
+// Sub-batches: a tile's strings go through the LDS stage in runs [start, end) whose bytes fit it
+// (a tile of resolve outputs averages 17.4 KB in config 4, so one tile in seven needs two runs);
+// a single string longer than the stage is handled from global memory by its own lane.
+// ------------------------------------------------------------------------------------------
+struct SubBatch {
+  uint64_t start, end, lo, hi;  // strings [start, end), bytes [lo, hi)
+  bool staged;
+};
+// the run that starts at string `start` of the tile [.., last); every lane calls it (barrier)
+__device__ __forceinline__ SubBatch next_run(const Batch& B, uint64_t start, uint64_t last, uint64_t i, uint64_t eo) {
+  SubBatch r;
+  r.start = start;
+  r.lo = B.in_off[start];
+  const bool fits = i >= start && i < last && eo - r.lo <= (uint64_t)kTileBytes;
+  const uint64_t cnt = (uint64_t)__syncthreads_count(fits);  // fits is monotone in i
+  r.staged = cnt > 0;
+  r.end = start + (cnt > 0 ? cnt : 1);
+  r.hi = B.in_off[r.end];
+  return r;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -123,33 +191,34 @@ __device__ uint32_t stage_tile(const uint8_t* __restrict__ bytes, uint64_t lo, u
 // ------------------------------------------------------------------------------------------
 template <int OP>
 __global__ __launch_bounds__(kBlock) void k_measure(Batch B, Work W) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_in[kTileBytes + 32];
+  __shared__ __attribute__((aligned(16))) uint8_t s_in[kTileBytes + 64];
   __shared__ uint64_t s_red[kBlock / 64];
 
   const uint64_t tile = blockIdx.x;
   const uint64_t first = tile * kBlock;
   const uint64_t i = first + threadIdx.x;
   const uint64_t last = min(first + kBlock, B.n);  // exclusive
-  const uint64_t lo = B.in_off[first], hi = B.in_off[last];
-  const bool staged = (hi - lo) <= kTileBytes;
-  uint32_t shift = 0;
-  if (staged) shift = stage_tile(B.bytes, lo, hi, s_in);
-  __syncthreads();
-
-  uint64_t my_len = 0;
+  const uint64_t so = i < B.n ? B.in_off[i] : 0, eo = i < B.n ? B.in_off[i + 1] : 0;
+  uint32_t olen = 0;
+  for (uint64_t start = first; start < last;) {  // uniform
+    const SubBatch r = next_run(B, start, last, i, eo);
+    const bool mine = i >= r.start && i < r.end;
+    if (r.staged) {
+      const uint32_t shift = stage_tile(B.bytes, r.lo, r.hi, s_in);
+      __syncthreads();
+      if (mine) olen = escape_len_lds<OP>(s_in + shift + (so - r.lo), (uint32_t)(eo - so));
+    } else if (mine) {
+      eval_escape<OP>(B.bytes + so, (uint32_t)(eo - so), nullptr, olen, false);
+    }
+    __syncthreads();  // the stage is free for the next run
+    start = r.end;
+  }
   if (i < B.n) {
-    const uint64_t so = B.in_off[i], eo = B.in_off[i + 1];
-    const uint8_t* s = staged ? s_in + shift + (so - lo) : B.bytes + so;
-    uint32_t olen = 0;
-    uint8_t st = IE_OK_STR;
-    if (staged) olen = escape_len_lds<OP>(s, (uint32_t)(eo - so));
-    else st = eval_escape<OP>(s, (uint32_t)(eo - so), nullptr, olen, false);
     W.out_len[i] = olen;
-    my_len = olen;
-    B.status[i] = st;
+    gsts(B.status + i, (uint8_t)IE_OK_STR);
   }
   uint64_t total;
-  block_excl_scan(my_len, s_red, &total);
+  block_excl_scan(olen, s_red, &total);
   if (threadIdx.x == 0) W.tile_sum[tile] = total;
 }
 
@@ -179,12 +248,34 @@ __global__ __launch_bounds__(kBlock) void k_scan_tiles(Work W, uint64_t n_tiles,
 // ------------------------------------------------------------------------------------------
 // k_emit
 // ------------------------------------------------------------------------------------------
+// the LDS stage [0, len) -> g (any alignment; stage position p holds output byte p - oshift is
+// NOT assumed: the stage is laid out tile-relative and realigned here), 16-byte aligned stores
+__device__ __forceinline__ void stream_out(uint8_t* g, const uint8_t* stage, uint32_t oshift, uint32_t len) {
+  const uintptr_t pg = (uintptr_t)g, pe = pg + len;
+  const uintptr_t a_up = (pg + 15) & ~(uintptr_t)15, b_down = pe & ~(uintptr_t)15;
+  if (a_up >= b_down) {
+    for (uint32_t k = threadIdx.x; k < len; k += kBlock) g[k] = stage[oshift + k];
+    return;
+  }
+  const uint32_t head = (uint32_t)(a_up - pg), tail = (uint32_t)(pe - b_down);
+  if (threadIdx.x < head) g[threadIdx.x] = stage[oshift + threadIdx.x];
+  if (threadIdx.x < tail) {
+    const uint32_t k = (uint32_t)(b_down - pg) + threadIdx.x;
+    g[k] = stage[oshift + k];
+  }
+  const uint32_t nv = (uint32_t)((b_down - a_up) >> 4);
+  const uint4* src = (const uint4*)(stage + oshift + head);  // 16-aligned: oshift = pg & 15
+  uint4* dstv = (uint4*)a_up;
+  for (uint32_t j = threadIdx.x; j < nv; j += kBlock) gst4s(dstv + j, src[j]);
+}
+
 template <int OP>
 __global__ __launch_bounds__(kBlock) void k_emit(Batch B, Work W, uint8_t* out_bytes, uint64_t out_cap,
                                                  const uint64_t* total) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_in[kTileBytes + 32];
+  __shared__ __attribute__((aligned(16))) uint8_t s_in[kTileBytes + 64];
   __shared__ __attribute__((aligned(16))) uint8_t s_out[kStageBytes + 32];
   __shared__ uint64_t s_red[kBlock / 64];
+  __shared__ uint32_t s_loc[kBlock + 1];  // tile-relative output offsets
 
   const uint64_t tile = blockIdx.x;
   const uint64_t first = tile * kBlock;
@@ -196,43 +287,37 @@ __global__ __launch_bounds__(kBlock) void k_emit(Batch B, Work W, uint8_t* out_b
   const uint32_t my_len = (i < B.n) ? W.out_len[i] : 0;
   uint64_t tile_out;
   const uint64_t local = block_excl_scan(my_len, s_red, &tile_out);
-  if (i < B.n) B.out_off[i] = base + local;
+  if (i < B.n) gsts(B.out_off + i, base + local);
   if (!write_bytes) return;  // uniform across the workgroup
+  s_loc[threadIdx.x] = (uint32_t)local;
+  if (threadIdx.x == 0) s_loc[kBlock] = (uint32_t)tile_out;
+  const uint64_t so = i < B.n ? B.in_off[i] : 0, eo = i < B.n ? B.in_off[i + 1] : 0, n = eo - so;
 
-  const uint64_t lo = B.in_off[first], hi = B.in_off[last];
-  const bool staged_in = (hi - lo) <= kTileBytes;
-  const uint32_t oshift = (uint32_t)(((uintptr_t)(out_bytes + base)) & 15);
-  const bool staged_out = tile_out + oshift <= kStageBytes;
-  uint32_t shift = 0;
-  if (staged_in) shift = stage_tile(B.bytes, lo, hi, s_in);
-  __syncthreads();
-
-  if (i < B.n && my_len) {
-    uint8_t* dst = staged_out ? s_out + oshift + local : out_bytes + base + local;
-    const uint64_t so = B.in_off[i], n = B.in_off[i + 1] - so;
-    const uint8_t* s = staged_in ? s_in + shift + (so - lo) : B.bytes + so;
-    uint32_t olen = 0;
-    eval_escape<OP>(s, (uint32_t)n, dst, olen, true);
-  }
-  if (!staged_out) return;
-  __syncthreads();
-  // stream the stage out: LDS position oshift + k holds output byte base + k
-  uint8_t* g = out_bytes + base;
-  const uintptr_t pg = (uintptr_t)g, pe = pg + tile_out;
-  const uintptr_t a_up = (pg + 15) & ~(uintptr_t)15, b_down = pe & ~(uintptr_t)15;
-  if (a_up >= b_down) {
-    for (uint32_t k = threadIdx.x; k < tile_out; k += kBlock) g[k] = s_out[oshift + k];
-  } else {
-    const uint32_t head = (uint32_t)(a_up - pg), tail = (uint32_t)(pe - b_down);
-    if (threadIdx.x < head) g[threadIdx.x] = s_out[oshift + threadIdx.x];
-    if (threadIdx.x < tail) {
-      const uint32_t k = (uint32_t)(b_down - pg) + threadIdx.x;
-      g[k] = s_out[oshift + k];
+  for (uint64_t start = first; start < last;) {  // uniform (next_run's barrier publishes s_loc)
+    const SubBatch r = next_run(B, start, last, i, eo);
+    const bool mine = i >= r.start && i < r.end && my_len;
+    const uint32_t o_lo = s_loc[r.start - first], o_hi = s_loc[r.end - first];
+    const uint64_t gb = base + o_lo;  // the run's first output byte
+    const uint32_t oshift = (uint32_t)(((uintptr_t)(out_bytes + gb)) & 15);
+    const bool staged_out = r.staged && o_hi - o_lo + oshift <= (uint32_t)kStageBytes;
+    uint32_t shift = 0;
+    if (r.staged) shift = stage_tile(B.bytes, r.lo, r.hi, s_in);
+    __syncthreads();
+    // a string the map leaves as it is (most of them): aligned LDS moves instead of the byte loop
+    const bool same = staged_out && mine && my_len == n;
+    if (__any(same))
+      lds_copy_any((lds_u8*)(s_out + oshift + (same ? (uint32_t)local - o_lo : 0)),
+                   (const lds_u8*)(s_in + shift + (same ? so - r.lo : 0)), same ? my_len : 0u);
+    if (mine && !same) {
+      uint8_t* dst = staged_out ? s_out + oshift + ((uint32_t)local - o_lo) : out_bytes + base + local;
+      const uint8_t* s = r.staged ? s_in + shift + (so - r.lo) : B.bytes + so;
+      uint32_t olen = 0;
+      eval_escape<OP>(s, (uint32_t)n, dst, olen, true);
     }
-    const uint32_t nv = (uint32_t)((b_down - a_up) >> 4);
-    const uint4* src = (const uint4*)(s_out + oshift + head);
-    uint4* dstv = (uint4*)a_up;
-    for (uint32_t j = threadIdx.x; j < nv; j += kBlock) dstv[j] = src[j];
+    __syncthreads();
+    if (staged_out) stream_out(out_bytes + gb, s_out, oshift, o_hi - o_lo);
+    __syncthreads();  // the stages are free for the next run
+    start = r.end;
   }
 }
 
