@@ -43,6 +43,36 @@ __device__ uint8_t eval_escape(const uint8_t* __restrict__ s, uint32_t n, uint8_
   return IE_OK_STR;
 }
 
+// The same map on one string by the whole wave (arguments uniform; generic pointers: LDS or
+// global): 64 bytes per step, each lane decides its byte and places it by a ballot prefix count.
+// Unescape drops position p iff s[p] == '\\' and s[p + 1] is a brace (a pair's second byte is a
+// brace, never a '\\', so the decisions are independent); escape puts a '\\' before each brace.
+template <int OP>
+__device__ void wave_escape(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint32_t n) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t lower = (1ull << lane) - 1ull;
+  uint32_t w = 0;
+  for (uint32_t p0 = 0; p0 < n; p0 += 64) {
+    const uint32_t p = p0 + lane;
+    const bool in = p < n;
+    const uint8_t c = in ? src[p] : 0;
+    if (OP == kOpUnescape) {
+      const uint8_t nx = p + 1 < n ? src[p + 1] : 0;
+      const bool keep = in && !(c == '\\' && (nx == '{' || nx == '}'));
+      const uint64_t km = __ballot(keep);
+      if (keep) dst[w + (uint32_t)__popcll(km & lower)] = c;
+      w += (uint32_t)__popcll(km);
+    } else {
+      const bool br = in && (c == '{' || c == '}');
+      const uint64_t bm = __ballot(br);
+      uint32_t pos = w + lane + (uint32_t)__popcll(bm & lower);
+      if (br) dst[pos++] = '\\';
+      if (in) dst[pos] = c;
+      w += (n - p0 < 64u ? n - p0 : 64u) + (uint32_t)__popcll(bm);
+    }
+  }
+}
+
 // Output length of one string staged in LDS, a dword at a time: unescape drops one byte per '\'
 // followed by a brace (such pairs never overlap: the second byte of one is never a '\'), escape
 // adds one per brace. Same result as eval_escape's byte loop (measure mode).
@@ -223,23 +253,37 @@ __global__ __launch_bounds__(kBlock) void k_measure(Batch B, Work W) {
 }
 
 // ------------------------------------------------------------------------------------------
-// k_scan_tiles: one workgroup, exclusive scan of tile sums (chunked), grand total.
+// k_scan_tiles: one 1024-lane workgroup, exclusive scan of the tile sums (a contiguous chunk per
+// lane, its loads in flight together), grand total.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_scan_tiles(Work W, uint64_t n_tiles, uint64_t* total,
-                                                       uint64_t* offsets_n) {
-  __shared__ uint64_t s_red[kBlock / 64];
-  const uint64_t per = (n_tiles + kBlock - 1) / kBlock;
-  const uint64_t b = threadIdx.x * per, e = min(b + per, n_tiles);
+constexpr int kScanLanes = 1024;
+__global__ __launch_bounds__(kScanLanes) void k_scan_tiles(Work W, uint64_t n_tiles, uint64_t* total,
+                                                           uint64_t* offsets_n) {
+  __shared__ uint64_t s_w[kScanLanes / 64];
+  const uint32_t t = threadIdx.x, lane = t & 63u, wid = t >> 6;
+  const uint64_t per = (n_tiles + kScanLanes - 1) / kScanLanes;
+  const uint64_t b = min((uint64_t)t * per, n_tiles), e = min(b + per, n_tiles);
   uint64_t sum = 0;
-  for (uint64_t t = b; t < e; t++) sum += W.tile_sum[t];
-  uint64_t tot;
-  uint64_t run = block_excl_scan(sum, s_red, &tot);
-  for (uint64_t t = b; t < e; t++) {
-    const uint64_t v = W.tile_sum[t];
-    W.tile_base[t] = run;
+#pragma unroll 8
+  for (uint64_t k = b; k < e; k++) sum += W.tile_sum[k];
+  const uint64_t inc = wave_incl_scan(sum);
+  if (lane == 63) s_w[wid] = inc;
+  __syncthreads();
+  uint64_t run = 0, tot = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < kScanLanes / 64; w++) {
+    const uint64_t x = s_w[w];
+    if (w < wid) run += x;
+    tot += x;
+  }
+  run += inc - sum;
+#pragma unroll 8
+  for (uint64_t k = b; k < e; k++) {
+    const uint64_t v = W.tile_sum[k];
+    W.tile_base[k] = run;
     run += v;
   }
-  if (threadIdx.x == 0) {
+  if (t == 0) {
     *total = tot;
     *offsets_n = tot;
   }
@@ -308,11 +352,18 @@ __global__ __launch_bounds__(kBlock) void k_emit(Batch B, Work W, uint8_t* out_b
     if (__any(same))
       lds_copy_any((lds_u8*)(s_out + oshift + (same ? (uint32_t)local - o_lo : 0)),
                    (const lds_u8*)(s_in + shift + (same ? so - r.lo : 0)), same ? my_len : 0u);
-    if (mine && !same) {
-      uint8_t* dst = staged_out ? s_out + oshift + ((uint32_t)local - o_lo) : out_bytes + base + local;
-      const uint8_t* s = r.staged ? s_in + shift + (so - r.lo) : B.bytes + so;
-      uint32_t olen = 0;
-      eval_escape<OP>(s, (uint32_t)n, dst, olen, true);
+    // the others (a brace pair to drop or a brace to escape) one at a time by the whole wave
+    const bool slow = mine && !same;
+    uint8_t* const dst = staged_out ? s_out + oshift + ((uint32_t)local - o_lo) : out_bytes + base + local;
+    const uint8_t* const src = r.staged ? s_in + shift + (so - r.lo) : B.bytes + so;
+    for (uint64_t m = __ballot(slow); m; m &= m - 1) {
+      const int l = __builtin_ctzll(m);
+      const uint64_t d64 = (uint64_t)(uintptr_t)dst, s64 = (uint64_t)(uintptr_t)src;
+      uint8_t* const d = (uint8_t*)(uintptr_t)(((uint64_t)__shfl((uint32_t)(d64 >> 32), l, 64) << 32) |
+                                                __shfl((uint32_t)d64, l, 64));
+      const uint8_t* const q = (const uint8_t*)(uintptr_t)(((uint64_t)__shfl((uint32_t)(s64 >> 32), l, 64) << 32) |
+                                                           __shfl((uint32_t)s64, l, 64));
+      wave_escape<OP>(d, q, (uint32_t)__shfl((uint32_t)n, l, 64));
     }
     __syncthreads();
     if (staged_out) stream_out(out_bytes + gb, s_out, oshift, o_hi - o_lo);
@@ -414,7 +465,7 @@ hipError_t launch_escape(int op, const Batch& B, const Work& W, uint8_t* out, ui
   if (!tiles) return hipSuccess;
   if (op == kOpUnescape) hipLaunchKernelGGL(k_measure<kOpUnescape>, dim3((uint32_t)tiles), dim3(kBlock), 0, st, B, W);
   else hipLaunchKernelGGL(k_measure<kOpEscape>, dim3((uint32_t)tiles), dim3(kBlock), 0, st, B, W);
-  hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kBlock), 0, st, W, tiles, W.total, B.out_off + B.n);
+  hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kScanLanes), 0, st, W, tiles, W.total, B.out_off + B.n);
   if (op == kOpUnescape) hipLaunchKernelGGL(k_emit<kOpUnescape>, dim3((uint32_t)tiles), dim3(kBlock), 0, st, B, W, out, cap, W.total);
   else hipLaunchKernelGGL(k_emit<kOpEscape>, dim3((uint32_t)tiles), dim3(kBlock), 0, st, B, W, out, cap, W.total);
   return hipGetLastError();
