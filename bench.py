@@ -268,7 +268,10 @@ def main():
     wall_max = max_over_ranks(wall, dist)
 
     x.set_timing(True)  # one more call with the library's own events for the telemetry
-    N.check(L.ie_interpolate_device_ids(x.h, W.table, ids, W.d_in.ptr, W.d_off.ptr, n, ctypes.byref(o)), "timing")
+    if cmd and os.environ.get("IE_DIAG_CMD_RESOLVE"):  # diagnostic: the command's second resolve instead
+        N.check(L.ie_interpolate_device(x.h, W.table, d_u.ptr, d_uoff.ptr, n, ctypes.byref(o2)), "timing")
+    else:
+        N.check(L.ie_interpolate_device_ids(x.h, W.table, ids, W.d_in.ptr, W.d_off.ptr, n, ctypes.byref(o)), "timing")
     tm = x.timing()
     x.set_timing(False)
 

@@ -151,11 +151,26 @@ __device__ __forceinline__ void copy_bytes(uint8_t* __restrict__ dst, const uint
     const uint32_t* s32 = (const uint32_t*)(a - sh);
     uint32_t* d32 = (uint32_t*)(dst + k);
     const uint32_t nw = (len - k) >> 2;
+    // four dwords per step with their loads in flight together (a global source costs one
+    // memory round trip per step, not per dword)
+    uint32_t q = 0;
     if (sh == 0) {
-      for (uint32_t q = 0; q < nw; q++) wr32(d32, q, rd32(s32, q));
+      for (; q + 4 <= nw; q += 4) {
+        const uint32_t a0 = rd32(s32, q), a1 = rd32(s32, q + 1), a2 = rd32(s32, q + 2), a3 = rd32(s32, q + 3);
+        wr32(d32, q, a0), wr32(d32, q + 1, a1), wr32(d32, q + 2, a2), wr32(d32, q + 3, a3);
+      }
+      for (; q < nw; q++) wr32(d32, q, rd32(s32, q));
     } else {
       uint32_t w0 = rd32(s32, 0);
-      for (uint32_t q = 0; q < nw; q++) {
+      for (; q + 4 <= nw; q += 4) {
+        const uint32_t a1 = rd32(s32, q + 1), a2 = rd32(s32, q + 2), a3 = rd32(s32, q + 3), a4 = rd32(s32, q + 4);
+        wr32(d32, q, __builtin_amdgcn_alignbyte(a1, w0, sh));
+        wr32(d32, q + 1, __builtin_amdgcn_alignbyte(a2, a1, sh));
+        wr32(d32, q + 2, __builtin_amdgcn_alignbyte(a3, a2, sh));
+        wr32(d32, q + 3, __builtin_amdgcn_alignbyte(a4, a3, sh));
+        w0 = a4;
+      }
+      for (; q < nw; q++) {
         const uint32_t w1 = rd32(s32, q + 1);
         wr32(d32, q, __builtin_amdgcn_alignbyte(w1, w0, sh));
         w0 = w1;
@@ -1271,7 +1286,7 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
   const uint32_t ntiles = (uint32_t)((B.n + kRBlock - 1) / kRBlock);
   // Tile = workgroup index: workgroups are dispatched in index order, so every tile a look-back
   // waits on is already resident (no ticket: a single-address atomic serializes chip-wide).
-  uint32_t tile = blockIdx.x;
+  const uint32_t tile = blockIdx.x;
   const TileGeo geo = load_geo(B, tile, tid);
   TilePrefetch<kStageV> pre;
   pre.nv = 0;
