@@ -186,11 +186,14 @@ int ie_exec_sync(ie_exec* x);
 int ie_exec_set_timing(ie_exec* x, int32_t enabled);
 int ie_exec_timing(ie_exec* x, ie_timing* out); /* syncs */
 /* Exec options (defaults from the environment at ie_exec_create: IE_FAIL_COMMIT, IE_FAST,
- * IE_DEBUG_NOEVAL). IE_OPT_FAIL_COMMIT: -1 adaptive (default), 0 / 1 forces the k_resolve variant
- * (both give the reference's results; tests run under both). */
+ * IE_DEBUG_NOEVAL, IE_TILE). IE_OPT_FAIL_COMMIT: -1 adaptive (default), 0 / 1 forces the k_resolve
+ * variant (both give the reference's results; tests run under both). IE_OPT_TILE: 0 (default)
+ * 512-string tiles for the unescape command's second resolve and 256 elsewhere; 256 / 512 force one
+ * size (same results; a performance choice). */
 #define IE_OPT_FAIL_COMMIT 1
 #define IE_OPT_FAST 2
 #define IE_OPT_DEBUG_NOEVAL 3
+#define IE_OPT_TILE 4
 int ie_exec_set_option(ie_exec* x, int32_t option, int64_t value);
 /* Literal-path scratch pool size. Setting it makes ie_interpolate_device fully asynchronous: it no
  * longer waits to check the pool's demand, and strings that ran out of it report IE_E_OVERFLOW. */

@@ -18,7 +18,7 @@ STATUS_NAMES = ["OK_STR", "OK_VALUE", "E_INTERP", "E_ASSERT_BRACES", "E_ASSERT_T
                 "E_UNHASHABLE", "E_RS_PANIC", "NEEDS_HOST", "DIVERGED", "E_OVERFLOW"]
 VID_NONE, VID_HHMM, VID_HHMMSS = 0xFFFFFFFF, 0xFFFFFFFE, 0xFFFFFFFD
 TABLE_HAS_INSERTS_DIR = 1
-OPT_FAIL_COMMIT, OPT_FAST, OPT_DEBUG_NOEVAL = 1, 2, 3
+OPT_FAIL_COMMIT, OPT_FAST, OPT_DEBUG_NOEVAL, OPT_TILE = 1, 2, 3, 4
 
 # every symbol include/ie_amd.h declares (tests check the .so exports exactly these)
 EXPORTS = [

@@ -102,6 +102,8 @@ struct ie_exec {
   // options (ie_exec_set_option); defaults read once from the environment at ie_exec_create
   int32_t opt_fail_commit = -1;   // -1 adaptive, 0 / 1 forced (IE_FAIL_COMMIT)
   uint32_t opt_fast = 1;          // 0: exact evaluator only (IE_FAST)
+  int32_t opt_tile = 0;           // k_resolve tile: 0 by call site, 256 or 512 forced (IE_TILE)
+  bool in_cmd = false;            // inside the unescape command's second resolve
   uint32_t opt_noeval = 0;        // diagnostic verbatim copy (IE_DEBUG_NOEVAL)
   std::string stamps_path;        // diagnostic phase stamps (IE_DEBUG_STAMPS)
   // fail commit (k_resolve<true>): chosen from the chain-failure count of an earlier batch, read
@@ -340,7 +342,11 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
     }
     W.fail_commit = forced ? (uint32_t)x->opt_fail_commit : (uint32_t)x->fail_commit;
     if (x->timing) IE_HIP(hipEventRecord(x->ev[1], st));
-    IE_HIP(launch_resolve(B, W, t->dev, out->bytes, cap, st));
+    // 512-string tiles halve the look-back hops: the unescape command's second resolve (its input
+    // is interpolation output, so its evaluation is light and the look-back bounds it) takes them
+    // by default; everything else the 256-string tiles (ie_resolve512.hip has the numbers)
+    const bool wide = x->opt_tile == 512 || (x->opt_tile == 0 && x->in_cmd);
+    IE_HIP(wide ? launch_resolve512(B, W, t->dev, out->bytes, cap, st) : launch_resolve(B, W, t->dev, out->bytes, cap, st));
     if (!forced && !x->stat_pending) {
       if (!x->stat_host) {
         IE_HIP(hipHostMalloc((void**)&x->stat_host, 4, hipHostMallocDefault));
@@ -851,6 +857,7 @@ int ie_exec_create(int32_t device, void* hip_stream, ie_exec** out) {
   if (const char* e = getenv("IE_FAIL_COMMIT")) x->opt_fail_commit = atoi(e) != 0 ? 1 : 0;
   if (const char* e = getenv("IE_FAST")) x->opt_fast = (uint32_t)atoi(e);
   if (getenv("IE_DEBUG_NOEVAL")) x->opt_noeval = 1;
+  if (const char* e = getenv("IE_TILE")) x->opt_tile = atoi(e) == 512 ? 512 : atoi(e) == 256 ? 256 : 0;
   if (const char* e = getenv("IE_DEBUG_STAMPS")) x->stamps_path = e;
   if (hip_stream) {
     x->stream = (hipStream_t)hip_stream;
@@ -969,6 +976,10 @@ int ie_exec_set_option(ie_exec* x, int32_t option, int64_t value) {
     case IE_OPT_DEBUG_NOEVAL:
       x->opt_noeval = value ? 1u : 0u;
       return IE_SUCCESS;
+    case IE_OPT_TILE:
+      if (value != 0 && value != 256 && value != 512) return fail(IE_ERR_INVALID, "tile must be 0, 256 or 512");
+      x->opt_tile = (int32_t)value;
+      return IE_SUCCESS;
     default:
       return fail(IE_ERR_INVALID, "unknown exec option");
   }
@@ -1080,7 +1091,9 @@ int ie_unescape_cmd_device(ie_exec* x, const ie_table* t, const uint32_t* d_tabl
   // the unescaped bytes feed the interpolation (py:1666). Unescaping never lengthens a string, so
   // a tmp as large as the input always fits; a smaller one that overflowed is flagged on the
   // device (no wait here) and reported by ie_exec_sync as IE_ERR_CAPACITY
+  x->in_cmd = true;
   rc = ie_interpolate_device_ids(x, t, d_table_id, tmp->bytes, tmp->offsets, n, out);
+  x->in_cmd = false;
   if (rc) return rc;
   IE_HIP(launch_cap_check(tmp->total, tmp->bytes_cap, (uint32_t*)x->counters.p + 1, x->stream));
   if (d_status_in) IE_HIP(launch_status_carry(d_status_in, out->status, n, x->stream));

@@ -77,6 +77,9 @@ hipError_t launch_wildcard(const WcSet& P, const uint8_t* bytes, const uint64_t*
 
 hipError_t launch_resolve(const Batch& B, const Work& W, const DevTable& T, uint8_t* out,
                           uint64_t cap, hipStream_t st);
+// the same with 512-string tiles (ie_resolve512.hip)
+hipError_t launch_resolve512(const Batch& B, const Work& W, const DevTable& T, uint8_t* out,
+                             uint64_t cap, hipStream_t st);
 hipError_t launch_escape(int op, const Batch& B, const Work& W, uint8_t* out, uint64_t cap,
                          hipStream_t st);
 hipError_t launch_cap_check(const uint64_t* total, uint64_t cap, uint32_t* err, hipStream_t st);

@@ -37,7 +37,14 @@
 #define IE_WAVES_PER_EU 4
 #endif
 
+#ifndef IE_RNS
+#define IE_RNS r256
+#endif
+
 namespace ie {
+// everything of one tile size lives in its own namespace: ie_resolve512.hip compiles this file
+// again with 512-string tiles (IE_RBLOCK=512, IE_RNS=r512, IE_RESOLVE_WIDE)
+namespace IE_RNS {
 
 // value kinds of a descriptor: arena text, literal-path pool result (16-byte units), an entry's
 // inline text (entry index; texts <= kInlineText)
@@ -1601,13 +1608,13 @@ __global__ void k_debug_probe(DevTable T, const uint8_t* key, uint32_t klen, uin
   out[13] = agree;
 }
 
-hipError_t launch_debug_probe(const DevTable& T, const uint8_t* key, uint32_t klen, uint64_t* out, hipStream_t st) {
+hipError_t launch_debug_probe_impl(const DevTable& T, const uint8_t* key, uint32_t klen, uint64_t* out, hipStream_t st) {
   hipLaunchKernelGGL(k_debug_probe, dim3(1), dim3(64), 0, st, T, key, klen, out);
   return hipGetLastError();
 }
 
-hipError_t launch_resolve(const Batch& B, const Work& W, const DevTable& T, uint8_t* out, uint64_t cap,
-                          hipStream_t st) {
+hipError_t launch_resolve_impl(const Batch& B, const Work& W, const DevTable& T, uint8_t* out, uint64_t cap,
+                               hipStream_t st) {
   const uint64_t tiles = (B.n + kRBlock - 1) / kRBlock;
   if (!tiles) return hipSuccess;
   if (tiles > 0xFFFFFFFFull) return hipErrorInvalidValue;
@@ -1621,5 +1628,22 @@ hipError_t launch_resolve(const Batch& B, const Work& W, const DevTable& T, uint
   if (out) hipLaunchKernelGGL(k_emit_windows, dim3(grid < 512u ? grid : 512u), dim3(kRBlock), 0, st, B, W, T, out);
   return hipGetLastError();
 }
+
+}  // namespace IE_RNS
+
+#if defined(IE_RESOLVE_WIDE)
+hipError_t launch_resolve512(const Batch& B, const Work& W, const DevTable& T, uint8_t* out, uint64_t cap,
+                             hipStream_t st) {
+  return IE_RNS::launch_resolve_impl(B, W, T, out, cap, st);
+}
+#else
+hipError_t launch_resolve(const Batch& B, const Work& W, const DevTable& T, uint8_t* out, uint64_t cap,
+                          hipStream_t st) {
+  return IE_RNS::launch_resolve_impl(B, W, T, out, cap, st);
+}
+hipError_t launch_debug_probe(const DevTable& T, const uint8_t* key, uint32_t klen, uint64_t* out, hipStream_t st) {
+  return IE_RNS::launch_debug_probe_impl(T, key, klen, out, st);
+}
+#endif
 
 }  // namespace ie

@@ -30,15 +30,21 @@ def run_product(table_dict, strings, dialect="py", has_dir=False):
     return t.run(strings), t
 
 
-@pytest.fixture(params=["0", "1"], ids=["chain-fail-exact", "chain-fail-commit"])
+@pytest.fixture(params=["0", "1", "1w"], ids=["chain-fail-exact", "chain-fail-commit", "chain-fail-commit-512"])
 def fail_commit(request, monkeypatch):
     """Both k_resolve variants: chain failures sent to the exact evaluator, or committed in the
-    chain evaluator (the library picks one adaptively; IE_FAIL_COMMIT / IE_OPT_FAIL_COMMIT force it).
-    Execs read the environment when they are created; the mirror's cached exec is set directly."""
-    monkeypatch.setenv("IE_FAIL_COMMIT", request.param)
-    PKG.interpolation_engine.get_exec(0).set_option(N.OPT_FAIL_COMMIT, int(request.param))
-    yield request.param
-    PKG.interpolation_engine.get_exec(0).set_option(N.OPT_FAIL_COMMIT, -1)
+    chain evaluator (the library picks one adaptively; IE_FAIL_COMMIT / IE_OPT_FAIL_COMMIT force it);
+    the last also with 512-string tiles (ie_resolve512.hip, IE_OPT_TILE). Execs read the environment
+    when they are created; the mirror's cached exec is set directly."""
+    fc, tile = request.param[0], 512 if request.param.endswith("w") else 0
+    monkeypatch.setenv("IE_FAIL_COMMIT", fc)
+    monkeypatch.setenv("IE_TILE", str(tile))
+    x = PKG.interpolation_engine.get_exec(0)
+    x.set_option(N.OPT_FAIL_COMMIT, int(fc))
+    x.set_option(N.OPT_TILE, tile)
+    yield fc
+    x.set_option(N.OPT_FAIL_COMMIT, -1)
+    x.set_option(N.OPT_TILE, 0)
 
 
 def compare_with_oracle(table_dict, strings, dialect="py", has_dir=False):
