@@ -37,6 +37,15 @@ def test_library_exports_every_declared_symbol():
         assert getattr(L, f) is not None
 
 
+def test_header_constants_match_the_binding():
+    """The option and status numbers the Python binding uses are the header's."""
+    src = open(os.path.join(ROOT, "include", "ie_amd.h")).read()
+    defs = dict(re.findall(r"#define (IE_OPT_[A-Z_]+) (-?\d+)", src))
+    assert {k: int(v) for k, v in defs.items()} == {
+        "IE_OPT_FAIL_COMMIT": N.OPT_FAIL_COMMIT, "IE_OPT_FAST": N.OPT_FAST,
+        "IE_OPT_DEBUG_NOEVAL": N.OPT_DEBUG_NOEVAL, "IE_OPT_TILE": N.OPT_TILE}
+
+
 def test_abi_version():
     assert N.lib().ie_abi_version() == 1
 

@@ -840,3 +840,21 @@ def test_rust_dialect_hand_derived_vectors():
             assert payload == want[1], (s, payload)
         if want[1] is not None and want[0] == "OK_VALUE":
             assert list(t)[payload] == want[1], (s, payload)
+
+
+@pytest.mark.gpu
+def test_tile_option_is_validated_and_keeps_results():
+    """IE_OPT_TILE takes 0, 256 or 512 and nothing else; every size gives the same bytes."""
+    x = N.Exec(0)
+    with pytest.raises(RuntimeError):
+        x.set_option(N.OPT_TILE, 384)
+    table = {"k%d" % i: "v%d" % i for i in range(50)}
+    strings = ["a{k%d}b{k%d}" % (i % 50, (7 * i) % 50) for i in range(3000)] + ["plain %d" % i for i in range(3000)]
+    ie = PKG.interpolation_engine
+    got = []
+    for tile in (256, 512, 0):
+        ie.get_exec(0).set_option(N.OPT_TILE, tile)
+        got.append(run_product(table, strings)[0])
+    ie.get_exec(0).set_option(N.OPT_TILE, 0)
+    assert got[0] == got[1] == got[2]
+
