@@ -114,7 +114,7 @@ struct ie_exec {
   uint32_t* stat_host = nullptr;  // pinned
   hipEvent_t stat_ev = nullptr;
   // workspace
-  DevBuf counters, tile_state, pool, out_len, tile_sum, tile_base, defer_tiles, defer_desc;
+  DevBuf counters, pool, out_len, tile_sum, tile_base, defer_tiles, defer_desc;
   // host-API staging
   DevBuf in_bytes, in_off, in_tid, o_bytes, o_off, o_status, o_vid, o_total, wc_range, wc_match, wc_ncap, wc_caps;
   // synth scratch
@@ -122,7 +122,7 @@ struct ie_exec {
   DevBuf stamps;        // diagnostic phase stamps (env IE_DEBUG_STAMPS=<file>)
   uint64_t stamp_tiles = 0;
   ~ie_exec() {
-    for (DevBuf* b : {&counters, &tile_state, &pool, &out_len, &tile_sum, &tile_base, &defer_tiles, &defer_desc, &in_bytes,
+    for (DevBuf* b : {&counters, &pool, &out_len, &tile_sum, &tile_base, &defer_tiles, &defer_desc, &in_bytes,
                       &in_off, &in_tid, &o_bytes, &o_off, &o_status, &o_vid, &o_total, &wc_range, &wc_match, &wc_ncap, &wc_caps,
                       &s_lens, &s_part, &stamps})
       b->release();
@@ -261,9 +261,9 @@ int set_device(int32_t dev) {
 // exact-path strings, chain failures), [9] deferred-tile count; zeroed on every call.
 int ensure_work(ie_exec* x, int op, uint64_t n) {
   const uint64_t tiles = (n + kBlock - 1) / kBlock + 1;  // (kRBlock >= kBlock: enough for k_resolve too)
-  IE_HIP(x->counters.ensure(64));
+  // counters, then (interpolation) the look-back words: one buffer, zeroed by one memset per call
+  IE_HIP(x->counters.ensure(64 + (op == kOpInterp ? tiles * sizeof(uint64_t) : 0)));
   if (op == kOpInterp) {
-    IE_HIP(x->tile_state.ensure(tiles * sizeof(uint64_t)));
     IE_HIP(x->pool.ensure(x->pool_request));
     // room for every tile to be deferred (64 B of descriptor per string; grow-only, never read
     // unless written, so only HBM capacity is spent)
@@ -290,7 +290,7 @@ Work make_work(ie_exec* x, uint64_t* total) {
   W.defer_count = (uint32_t*)x->counters.p + 9;
   W.defer_tiles = (uint32_t*)x->defer_tiles.p;
   W.defer_desc = (uint4*)x->defer_desc.p;
-  W.tile_state = (uint64_t*)x->tile_state.p;
+  W.tile_state = (uint64_t*)((uint8_t*)x->counters.p + 64);
   W.pool = (uint8_t*)x->pool.p;
   W.pool_bytes = x->pool.bytes;
   W.lit_cap_max = x->lit_cap_max;
@@ -324,13 +324,13 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
   hipStream_t st = x->stream;
   const uint64_t cap = out->bytes ? out->bytes_cap : 0;
   if (x->timing) IE_HIP(hipEventRecord(x->ev[0], st));
-  IE_HIP(hipMemsetAsync(x->counters.p, 0, 64, st));
+  // the counters and, for an interpolation, the look-back words (one fill instead of two)
+  const uint64_t zero_tiles = (op == kOpInterp && n) ? (n + kRBlock - 1) / kRBlock : 0;
+  IE_HIP(hipMemsetAsync(x->counters.p, 0, 64 + zero_tiles * sizeof(uint64_t), st));
   if (n == 0) {
     IE_HIP(hipMemsetAsync(out->offsets, 0, sizeof(uint64_t), st));
     IE_HIP(hipMemsetAsync(out->total, 0, sizeof(uint64_t), st));
   } else if (op == kOpInterp) {
-    const uint64_t tiles = (n + kRBlock - 1) / kRBlock;
-    IE_HIP(hipMemsetAsync(x->tile_state.p, 0, tiles * sizeof(uint64_t), st));
     // fail commit: forced by the option (diagnostics, tests), else adaptive on the count of chain
     // failures (misses / unspliceable hits) an earlier batch saw, in either variant
     const bool forced = x->opt_fail_commit >= 0;
