@@ -73,6 +73,9 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (wall seconds)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--layout", choices=["views", "packed"], default="",
+                    help="output layout (default: views, config 4 packed): views = each tile claims its "
+                         "output range with one atomic (no look-back), packed = input order (look-back)")
     return ap.parse_args(argv)
 
 
@@ -213,10 +216,21 @@ def main():
     d_st = N.DeviceBuffer(x, n + 1)
     d_vid = N.DeviceBuffer(x, 4 * n + 4)
     d_tot = N.DeviceBuffer(x, 8)
-    o = N.DevOut(d_out.ptr, out_cap, d_ooff.ptr, d_st.ptr, d_vid.ptr, d_tot.ptr)
     ids = W.d_ids.ptr if W.d_ids is not None else None
-
     cmd = cfg == 4  # the unescape command on the results (py:1660-1667): unescape, interpolate again
+    layout = args.layout or ("packed" if cmd else "views")
+    views = layout == "views"
+    assert not (views and cmd), "the unescape command takes a packed batch"
+    d_olen = N.DeviceBuffer(x, 4 * n + 4) if views else None
+    if views:
+        o = N.DevViews(d_out.ptr, out_cap, d_ooff.ptr, d_olen.ptr, d_st.ptr, d_vid.ptr, d_tot.ptr)
+    else:
+        o = N.DevOut(d_out.ptr, out_cap, d_ooff.ptr, d_st.ptr, d_vid.ptr, d_tot.ptr)
+
+    def resolve():
+        if views:
+            return L.ie_interpolate_device_views(x.h, W.table, ids, W.d_in.ptr, W.d_off.ptr, None, n, ctypes.byref(o))
+        return L.ie_interpolate_device_ids(x.h, W.table, ids, W.d_in.ptr, W.d_off.ptr, n, ctypes.byref(o))
     if cmd:
         d_u = N.DeviceBuffer(x, out_cap)
         d_uoff = N.DeviceBuffer(x, (n + 1) * 8)
@@ -232,8 +246,7 @@ def main():
     def step(k=None):
         if k is not None:
             x.mark(3 * k)
-        N.check(L.ie_interpolate_device_ids(x.h, W.table, ids, W.d_in.ptr, W.d_off.ptr, n, ctypes.byref(o)),
-                "ie_interpolate_device_ids")
+        N.check(resolve(), "resolve")
         if k is not None:
             x.mark(3 * k + 1)
         if cmd:
@@ -271,7 +284,7 @@ def main():
     if cmd and os.environ.get("IE_DIAG_CMD_RESOLVE"):  # diagnostic: the command's second resolve instead
         N.check(L.ie_interpolate_device(x.h, W.table, d_u.ptr, d_uoff.ptr, n, ctypes.byref(o2)), "timing")
     else:
-        N.check(L.ie_interpolate_device_ids(x.h, W.table, ids, W.d_in.ptr, W.d_off.ptr, n, ctypes.byref(o)), "timing")
+        N.check(resolve(), "timing")
     tm = x.timing()
     x.set_timing(False)
 
@@ -284,7 +297,9 @@ def main():
 
     cpu = None
     if rank == 0 and not args.no_cpu:
-        cpu = cpu_baseline(args, W, N, d_ooff2 if cmd else d_ooff, d_out2 if cmd else d_out, d_st2 if cmd else d_st)
+        res = Result(N, n, d_out2 if cmd else d_out, d_ooff2 if cmd else d_ooff, d_st2 if cmd else d_st,
+                     d_olen, d_tot2 if cmd else d_tot)
+        cpu = cpu_baseline(args, W, N, res)
 
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic_cfg%d.json" % cfg)
@@ -314,13 +329,14 @@ def main():
             "dtype": "u8",
             "data": "synthetic (SURVEY §8d generators; configs 2-4 splitmix64 seed 0x1E5EED00+config generated in "
                     "HBM; config 5 seeded states + the reference-recorded call stream)",
-            "config": {"workload": WORKLOADS[cfg], "strings_per_gpu": n, "input_bytes_per_gpu": in_bytes,
+            "config": {"workload": WORKLOADS[cfg], "layout": layout, "strings_per_gpu": n, "input_bytes_per_gpu": in_bytes,
                        "output_bytes_per_gpu": out_bytes, "inserts": W.inserts, "parallelism": "shard%d" % world,
                        "statuses": status_counts, "table_build_s": round(W.build_s, 3)},
             "strings_per_s": round(strings_per_s, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "k_resolve (single pass: stage, evaluate, look-back, emit) + k_emit_windows",
+                         "kernel": "k_resolve (single pass: stage, evaluate, %s, emit) + k_emit_windows"
+                                   % ("claim the tile's output range" if views else "look-back"),
                          "launch_ms": round(gpu_ms, 4), "alg_bytes_per_launch": alg_bytes,
                          "telemetry": {"kernel_ms": round(tm.resolve_ms, 4), "literal_strings": int(tm.n_complex),
                                        "windowed_tiles": int(tm.n_direct), "exact_strings": int(tm.n_exact),
@@ -342,7 +358,32 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(args, W, N, d_ooff, d_out, d_st):
+class Result:
+    """The device results of a step in either layout, read back for the checks."""
+
+    def __init__(self, N, n, d_out, d_off, d_st, d_len, d_tot):
+        self.N, self.n, self.d_out, self.d_off, self.d_st, self.d_len, self.d_tot = N, n, d_out, d_off, d_st, d_len, d_tot
+
+    def spans(self, m):
+        """(starts, lengths) of strings [0, m), uint64"""
+        if self.d_len is not None:
+            return self.d_off.to_numpy(np.uint64, m), self.d_len.to_numpy(np.uint32, m).astype(np.uint64)
+        oo = self.d_off.to_numpy(np.uint64, m + 1)
+        return oo[:-1], np.diff(oo)
+
+    def compare(self, m, st, ln, hs, threads):
+        """strings [0, m) against the oracle's statuses, lengths and FNV-1a hashes"""
+        from oracle import oracle as O
+        gst = self.d_st.to_numpy(np.uint8, m)
+        starts, lens = self.spans(m)
+        if not np.array_equal(gst, st) or not np.array_equal(lens[gst == 0], ln[gst == 0]):
+            return False
+        total = int(self.d_tot.to_numpy(np.uint64, 1)[0])
+        blob = self.d_out.to_numpy(np.uint8, total)
+        return bool(np.array_equal(O.hash_spans(blob, starts, lens, gst, threads), hs))
+
+
+def cpu_baseline(args, W, N, res):
     """The oracle (a literal C restatement of interpolate_inserts, kind "port") timed on this host
     over a bounded sample of the same workload, single-thread and on every core of this rank's
     share; the GPU's results on the sample are checked against it string by string."""
@@ -352,7 +393,7 @@ def cpu_baseline(args, W, N, d_ooff, d_out, d_st):
         threads = args.cpu_threads
     budget = args.cpu_seconds
     if args.config == 5:
-        return cpu_baseline_states(args, W, N, d_ooff, d_out, d_st, model, budget)
+        return cpu_baseline_states(args, W, N, res, model, budget, threads)
     ref = O.Oracle.from_kv(ctypes.cast(W.kvp, ctypes.c_void_p), W.nkv, "py", clock=CLOCK)
     cmd = args.config == 4
     buf, offs = W.host_sample(20000)
@@ -366,7 +407,7 @@ def cpu_baseline(args, W, N, d_ooff, d_out, d_st):
     ln = np.zeros(m, np.uint64)
     hs = np.zeros(m, np.uint64)
     wall = ref.run_batch(buf, offs, m, threads, st, ln, hs, None, unescape_cmd=cmd)
-    same = compare_sample(N, d_ooff, d_out, d_st, 0, m, st, ln, hs)
+    same = res.compare(m, st, ln, hs, threads)
     return {"value": round(int(offs[m]) / wall / 1e6, 2), "unit": "MB/s", "cores": threads, "kind": "port",
             "value_1t": round(int(offs[m1]) / wall1 / 1e6, 2), "threads_all": threads, "cpu_model": model,
             "nproc_visible": os.cpu_count(), "strings_per_s": round(m / wall, 1),
@@ -376,49 +417,24 @@ def cpu_baseline(args, W, N, d_ooff, d_out, d_st):
                          "; each OK result then through the unescape command" if cmd else "", m, same)}
 
 
-def compare_sample(N, d_ooff, d_out, d_st, lo, m, st, ln, hs):
-    """GPU strings [lo, lo+m) against the oracle's statuses, lengths and FNV-1a hashes."""
+def cpu_baseline_states(args, W, N, res, model, budget, threads):
+    """Config 5: every state of this rank's batch, each string against its own state's inserts
+    (one oracle context per state, built untimed), on all threads of this rank's share and
+    single-thread; the GPU's results are compared on the whole batch."""
     from oracle import oracle as O
-    gst = d_st.to_numpy(np.uint8, lo + m)[lo:]
-    goff = d_ooff.to_numpy(np.uint64, lo + m + 1)[lo:]
-    if not (np.array_equal(gst, st) and np.array_equal(np.diff(goff.astype(np.int64)), ln.astype(np.int64))):
-        return False
-    base = int(goff[0])
-    gout = d_out.to_numpy(np.uint8, int(goff[m]) - base, offset_bytes=base).tobytes()
-    for i in range(m):  # the oracle hashes OK_STR outputs only (0 for status rows)
-        h = O.fnv1a(gout[int(goff[i]) - base:int(goff[i + 1]) - base]) if gst[i] == 0 else 0
-        if h != int(hs[i]):
-            return False
-    return True
-
-
-def cpu_baseline_states(args, W, N, d_ooff, d_out, d_st, model, budget):
-    """Config 5: per state, the oracle over that state's inserts and strings (states in order,
-    single-thread: one oracle table per state is built on the host each time, as the reference
-    interpreter resolves one state at a time)."""
-    from oracle import oracle as O
-    t_start = time.perf_counter()
-    k, nbytes, wall, j = 0, 0, 0.0, 0
-    st_all = np.zeros(W.n, np.uint8)
-    ln_all = np.zeros(W.n, np.uint64)
-    hs_all = np.zeros(W.n, np.uint64)
-    buf = np.frombuffer(W.blob, np.uint8)
-    while j < len(W.states) and time.perf_counter() - t_start < budget:
-        ref = O.Oracle(W.states[j], "py", clock=CLOCK)
-        cnt = int(np.count_nonzero(W.ids == j))
-        offs = np.ascontiguousarray(W.offs[k:k + cnt + 1])
-        s_, l_, h_ = np.zeros(cnt, np.uint8), np.zeros(cnt, np.uint64), np.zeros(cnt, np.uint64)
-        wall += ref.run_batch(buf, offs, cnt, 1, s_, l_, h_)
-        st_all[k:k + cnt], ln_all[k:k + cnt], hs_all[k:k + cnt] = s_, l_, h_
-        nbytes += int(offs[-1] - offs[0])
-        k += cnt
-        j += 1
-    same = compare_sample(N, d_ooff, d_out, d_st, 0, k, st_all[:k], ln_all[:k], hs_all[:k])
-    return {"value": round(nbytes / max(wall, 1e-9) / 1e6, 2), "unit": "MB/s", "cores": 1, "kind": "port",
-            "value_1t": round(nbytes / max(wall, 1e-9) / 1e6, 2), "threads_all": 1, "cpu_model": model,
-            "nproc_visible": os.cpu_count(), "strings_per_s": round(k / max(wall, 1e-9), 1),
-            "sample": "the first %d states (%d strings, %d B), one oracle table per state, single-thread "
-                      "(%.2f s of interpolation); GPU results identical on all: %s" % (j, k, nbytes, wall, same)}
+    oracles = [O.Oracle(ins, "py", clock=CLOCK) for ins in W.states]
+    buf = np.frombuffer(W.blob + bytes(1), np.uint8)
+    n = W.n
+    st, ln, hs = np.zeros(n, np.uint8), np.zeros(n, np.uint64), np.zeros(n, np.uint64)
+    wall = O.run_batch_sets(oracles, W.ids, buf, W.offs, threads, st, ln, hs)
+    wall1 = O.run_batch_sets(oracles, W.ids, buf, W.offs, 1)
+    same = res.compare(n, st, ln, hs, threads)
+    return {"value": round(W.in_bytes / max(wall, 1e-9) / 1e6, 2), "unit": "MB/s", "cores": threads, "kind": "port",
+            "value_1t": round(W.in_bytes / max(wall1, 1e-9) / 1e6, 2), "threads_all": threads, "cpu_model": model,
+            "nproc_visible": os.cpu_count(), "strings_per_s": round(n / max(wall, 1e-9), 1),
+            "sample": "all %d states (%d strings, %d B), each string against its own state's dict, "
+                      "oracle/ie_oracle.c on %d threads (%.3f s) and single-thread (%.3f s); GPU results "
+                      "identical on all: %s" % (len(W.states), n, W.in_bytes, threads, wall, wall1, same)}
 
 
 if __name__ == "__main__":

@@ -63,7 +63,12 @@ enum ie_status {
   IE_E_RS_PANIC = 6,      /* Rust dialect: unwrap() panic on a '}{' leftover (interp.rs:63-66) */
   IE_NEEDS_HOST = 7,      /* key missing and an --inserts-dir is configured (py:452-461)   */
   IE_DIVERGED = 8,        /* iteration cap hit: the reference would loop forever           */
-  IE_E_OVERFLOW = 9       /* string over its single-pass scratch budget (host APIs retry)  */
+  IE_E_OVERFLOW = 9,      /* string over its single-pass scratch budget (host APIs retry)  */
+  IE_RECURSE = 10         /* ie_unescape_cmd_device, py dialect: the unescaped item is a whole-string
+                             '{key}' as written, so recursive_interpolate walks its result again
+                             (py:1463-1464); the result (a str, list or dict; value_id = the insert
+                             when the result was one) is not final: the caller resolves the item
+                             with recursive_interpolate itself, as the mirror does                */
 };
 
 /* ---- API return codes ---- */
@@ -186,7 +191,7 @@ int ie_exec_sync(ie_exec* x);
 int ie_exec_set_timing(ie_exec* x, int32_t enabled);
 int ie_exec_timing(ie_exec* x, ie_timing* out); /* syncs */
 /* Exec options (defaults from the environment at ie_exec_create: IE_FAIL_COMMIT, IE_FAST,
- * IE_DEBUG_NOEVAL, IE_TILE). IE_OPT_FAIL_COMMIT: -1 adaptive (default), 0 / 1 forces the k_resolve
+ * IE_DEBUG_NOEVAL, IE_TILE, IE_VIEWS). IE_OPT_FAIL_COMMIT: -1 adaptive (default), 0 / 1 forces the k_resolve
  * variant (both give the reference's results; tests run under both). IE_OPT_TILE: 0 (default)
  * 512-string tiles for the unescape command's second resolve and 256 elsewhere; 256 / 512 force one
  * size (same results; a performance choice). */
@@ -194,6 +199,8 @@ int ie_exec_timing(ie_exec* x, ie_timing* out); /* syncs */
 #define IE_OPT_FAST 2
 #define IE_OPT_DEBUG_NOEVAL 3
 #define IE_OPT_TILE 4
+#define IE_OPT_VIEWS 5 /* 1: the host batch APIs resolve into a views layout (no look-back) and pack
+                          the results in input order on the host; 0 (default): packed on the device */
 int ie_exec_set_option(ie_exec* x, int32_t option, int64_t value);
 /* Literal-path scratch pool size. Setting it makes ie_interpolate_device fully asynchronous: it no
  * longer waits to check the pool's demand, and strings that ran out of it report IE_E_OVERFLOW. */
@@ -231,6 +238,28 @@ int ie_interpolate_device_ids(ie_exec* x, const ie_table* t, const uint32_t* d_t
                               const uint64_t* d_offsets, uint64_t n, const ie_dev_out* out);
 int ie_interpolate_batch_ids(ie_exec* x, const ie_table* t, const uint32_t* table_id, const uint8_t* bytes,
                              const uint64_t* offsets, uint64_t n, ie_batch** out);
+/* Views layout (no global order). The reference returns one object per string (py:497-541,
+ * interp.rs:31-89); the order in which results are stored is not part of that contract. A views
+ * output holds string i's result at bytes[offsets[i] .. offsets[i] + lengths[i]) (offsets has n
+ * entries, no offsets[n]); tiles of consecutive strings claim their byte ranges in completion
+ * order with one atomic each, so the device never waits for an earlier tile (no look-back), and
+ * the bytes of the whole batch are packed without gaps: *total = sum of lengths. A string that
+ * failed has length 0. d_lengths (nullable) makes the INPUT a views layout too (string i =
+ * d_bytes[d_offsets[i] .. + d_lengths[i]), e.g. an earlier views output); null means packed input
+ * (d_offsets[n + 1]). When *total exceeds bytes_cap, the tiles that did not fit wrote no bytes:
+ * re-run with a larger buffer (offsets, lengths and statuses are valid either way). */
+typedef struct ie_dev_views {
+  uint8_t* bytes;
+  uint64_t bytes_cap;
+  uint64_t* offsets;  /* n */
+  uint32_t* lengths;  /* n */
+  uint8_t* status;    /* n */
+  uint32_t* value_id; /* n */
+  uint64_t* total;    /* 1 */
+} ie_dev_views;
+int ie_interpolate_device_views(ie_exec* x, const ie_table* t, const uint32_t* d_table_id, const uint8_t* d_bytes,
+                                const uint64_t* d_offsets, const uint32_t* d_lengths, uint64_t n,
+                                const ie_dev_views* out);
 /* scalar drop-in: one string (a batch of one on the device) */
 int ie_interpolate(ie_exec* x, const ie_table* t, const char* s, uint64_t len, ie_batch** out);
 
@@ -245,7 +274,10 @@ int ie_unescape_batch(ie_exec* x, const uint8_t* bytes, const uint64_t* offsets,
  * 1044-1050): recursive_unescape, then recursive_interpolate, on a batch of strings (table ids
  * nullable). tmp receives the unescaped strings (caller-sized; IE_ERR_CAPACITY when too small).
  * d_status_in (nullable): the statuses of the step that produced the input; a string that failed
- * there keeps that status (a failed item never reaches the command). Synchronous once (capacity). */
+ * there keeps that status (a failed item never reaches the command). A tmp too small for the
+ * unescaped strings: nothing past tmp->bytes_cap is read, the outputs are void and ie_exec_sync
+ * reports IE_ERR_CAPACITY. Waits once for the literal path's scratch demand, as
+ * ie_interpolate_device (not with ie_exec_set_scratch). */
 int ie_unescape_cmd_device(ie_exec* x, const ie_table* t, const uint32_t* d_table_id, const uint8_t* d_bytes,
                            const uint64_t* d_offsets, uint64_t n, const uint8_t* d_status_in, const ie_dev_out* tmp,
                            const ie_dev_out* out);

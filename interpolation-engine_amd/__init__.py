@@ -23,6 +23,7 @@ from .interpolation_engine import (  # noqa: F401
     recursive_escape,
     recursive_interpolate,
     recursive_unescape,
+    unescape_command,
 )
 from .multi import MultiDevice, shard_bounds  # noqa: F401
 from .wildcard import Wildcards, get_wildcard_matches, is_wildcard_match  # noqa: F401

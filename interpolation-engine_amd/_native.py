@@ -13,12 +13,12 @@ LIB_PATH = os.environ.get("IE_LIB_PATH") or os.path.join(PKG_DIR, "libie_amd.so"
 IE_DIALECT = {"py": 0, "rs": 1}
 KIND_STR, KIND_INT, KIND_LIST, KIND_FLOAT, KIND_BOOL, KIND_NULL, KIND_DICT = range(7)
 (OK_STR, OK_VALUE, E_INTERP, E_ASSERT_BRACES, E_ASSERT_TYPE, E_UNHASHABLE, E_RS_PANIC, NEEDS_HOST,
- DIVERGED, E_OVERFLOW) = range(10)
+ DIVERGED, E_OVERFLOW, RECURSE) = range(11)
 STATUS_NAMES = ["OK_STR", "OK_VALUE", "E_INTERP", "E_ASSERT_BRACES", "E_ASSERT_TYPE",
-                "E_UNHASHABLE", "E_RS_PANIC", "NEEDS_HOST", "DIVERGED", "E_OVERFLOW"]
+                "E_UNHASHABLE", "E_RS_PANIC", "NEEDS_HOST", "DIVERGED", "E_OVERFLOW", "RECURSE"]
 VID_NONE, VID_HHMM, VID_HHMMSS = 0xFFFFFFFF, 0xFFFFFFFE, 0xFFFFFFFD
 TABLE_HAS_INSERTS_DIR = 1
-OPT_FAIL_COMMIT, OPT_FAST, OPT_DEBUG_NOEVAL, OPT_TILE = 1, 2, 3, 4
+OPT_FAIL_COMMIT, OPT_FAST, OPT_DEBUG_NOEVAL, OPT_TILE, OPT_VIEWS = 1, 2, 3, 4, 5
 
 # every symbol include/ie_amd.h declares (tests check the .so exports exactly these)
 EXPORTS = [
@@ -30,7 +30,7 @@ EXPORTS = [
     "ie_dev_alloc", "ie_dev_free", "ie_copy_h2d", "ie_copy_d2h", "ie_memset_d", "ie_exec_mark",
     "ie_exec_elapsed",
     "ie_interpolate_device", "ie_interpolate_batch", "ie_interpolate", "ie_interpolate_device_ids",
-    "ie_interpolate_batch_ids",
+    "ie_interpolate_batch_ids", "ie_interpolate_device_views",
     "ie_unescape_device", "ie_escape_device", "ie_unescape_batch", "ie_escape_batch", "ie_unescape_cmd_device",
     "ie_batch_free", "ie_simple_insertkey",
     "ie_synth_create", "ie_synth_free", "ie_synth_kv", "ie_synth_strings_host",
@@ -57,6 +57,12 @@ class DevOut(ctypes.Structure):
                 ("value_id", ctypes.c_void_p), ("total", ctypes.c_void_p)]
 
 
+class DevViews(ctypes.Structure):
+    _fields_ = [("bytes", ctypes.c_void_p), ("bytes_cap", ctypes.c_uint64),
+                ("offsets", ctypes.c_void_p), ("lengths", ctypes.c_void_p), ("status", ctypes.c_void_p),
+                ("value_id", ctypes.c_void_p), ("total", ctypes.c_void_p)]
+
+
 class BatchRes(ctypes.Structure):
     _fields_ = [("bytes", ctypes.POINTER(ctypes.c_uint8)), ("bytes_len", ctypes.c_uint64),
                 ("offsets", ctypes.POINTER(ctypes.c_uint64)), ("status", ctypes.POINTER(ctypes.c_uint8)),
@@ -72,18 +78,12 @@ class Timing(ctypes.Structure):
 _lib = None
 
 
-def lib():
-    """Load libie_amd.so (raises if it was not built: there is no fallback)."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
-        raise ImportError("libie_amd.so is not built (%s); run `python -c \"import __graft_entry__ as g; "
-                          "g.build()\"`" % LIB_PATH)
-    L = ctypes.CDLL(LIB_PATH)
+def signatures():
+    """{symbol: (restype, argtypes)} for every entry point of include/ie_amd.h (tests/test_abi.py
+    checks this table against the header's prototypes)."""
     vp, u64, i32, u32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int32, ctypes.c_uint32
     pvp = ctypes.POINTER(ctypes.c_void_p)
-    sig = {
+    return {
         "ie_abi_version": (i32, []),
         "ie_build_id": (ctypes.c_char_p, []),
         "ie_last_error": (ctypes.c_char_p, []),
@@ -114,6 +114,7 @@ def lib():
         "ie_interpolate": (ctypes.c_int, [vp, vp, ctypes.c_char_p, u64, ctypes.POINTER(ctypes.POINTER(BatchRes))]),
         "ie_interpolate_device_ids": (ctypes.c_int, [vp, vp, vp, vp, vp, u64, ctypes.POINTER(DevOut)]),
         "ie_interpolate_batch_ids": (ctypes.c_int, [vp, vp, vp, vp, vp, u64, ctypes.POINTER(ctypes.POINTER(BatchRes))]),
+        "ie_interpolate_device_views": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, u64, ctypes.POINTER(DevViews)]),
         "ie_unescape_device": (ctypes.c_int, [vp, vp, vp, u64, ctypes.POINTER(DevOut)]),
         "ie_escape_device": (ctypes.c_int, [vp, vp, vp, u64, ctypes.POINTER(DevOut)]),
         "ie_unescape_batch": (ctypes.c_int, [vp, vp, vp, u64, ctypes.POINTER(ctypes.POINTER(BatchRes))]),
@@ -123,6 +124,7 @@ def lib():
         "ie_batch_free": (None, [ctypes.POINTER(BatchRes)]),
         "ie_simple_insertkey": (ctypes.c_int, [ctypes.c_char_p, u64, i32, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "ie_table_replicate": (ctypes.c_int, [vp, i32, pvp]),
+        "ie_debug_probe": (ctypes.c_int, [vp, ctypes.c_char_p, u64, vp]),
         "ie_shard_bounds": (ctypes.c_int, [vp, u64, u32, vp]),
         "ie_wildcards_build": (ctypes.c_int, [vp, vp, u32, i32, i32, pvp]),
         "ie_wildcards_free": (None, [vp]),
@@ -134,7 +136,18 @@ def lib():
         "ie_synth_strings_host": (ctypes.c_int, [vp, u64, u64, vp, u64, vp, ctypes.POINTER(u64)]),
         "ie_synth_strings_device": (ctypes.c_int, [vp, vp, u64, u64, vp, u64, vp, ctypes.POINTER(u64)]),
     }
-    for name, (res, args) in sig.items():
+
+
+def lib():
+    """Load libie_amd.so (raises if it was not built: there is no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libie_amd.so is not built (%s); run `python -c \"import __graft_entry__ as g; "
+                          "g.build()\"`" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in signatures().items():
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args

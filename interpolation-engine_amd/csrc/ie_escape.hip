@@ -331,7 +331,11 @@ __global__ __launch_bounds__(kBlock) void k_emit(Batch B, Work W, uint8_t* out_b
   const uint32_t my_len = (i < B.n) ? W.out_len[i] : 0;
   uint64_t tile_out;
   const uint64_t local = block_excl_scan(my_len, s_red, &tile_out);
-  if (i < B.n) gsts(B.out_off + i, base + local);
+  // over capacity inside a multi-step command: offsets all 0 (empty strings), so that the next
+  // step reads nothing past the caller's buffer; the error is reported at the exec's sync
+  const bool zero = !write_bytes && W.zero_on_overflow;
+  if (i < B.n) gsts(B.out_off + i, zero ? (uint64_t)0 : base + local);
+  if (zero && i + 1 == B.n) gsts(B.out_off + B.n, (uint64_t)0);
   if (!write_bytes) return;  // uniform across the workgroup
   s_loc[threadIdx.x] = (uint32_t)local;
   if (threadIdx.x == 0) s_loc[kBlock] = (uint32_t)tile_out;

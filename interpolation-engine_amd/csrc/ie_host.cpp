@@ -103,7 +103,9 @@ struct ie_exec {
   int32_t opt_fail_commit = -1;   // -1 adaptive, 0 / 1 forced (IE_FAIL_COMMIT)
   uint32_t opt_fast = 1;          // 0: exact evaluator only (IE_FAST)
   int32_t opt_tile = 0;           // k_resolve tile: 0 by call site, 256 or 512 forced (IE_TILE)
+  int32_t opt_views = 0;          // host batch APIs resolve into a views layout (IE_VIEWS)
   bool in_cmd = false;            // inside the unescape command's second resolve
+  bool cmd_first = false;         // the unescape command's unescape step (offsets zeroed on overflow)
   uint32_t opt_noeval = 0;        // diagnostic verbatim copy (IE_DEBUG_NOEVAL)
   std::string stamps_path;        // diagnostic phase stamps (IE_DEBUG_STAMPS)
   // fail commit (k_resolve<true>): chosen from the chain-failure count of an earlier batch, read
@@ -116,14 +118,14 @@ struct ie_exec {
   // workspace
   DevBuf counters, pool, out_len, tile_sum, tile_base, defer_tiles, defer_desc;
   // host-API staging
-  DevBuf in_bytes, in_off, in_tid, o_bytes, o_off, o_status, o_vid, o_total, wc_range, wc_match, wc_ncap, wc_caps;
+  DevBuf in_bytes, in_off, in_tid, o_bytes, o_off, o_len, o_status, o_vid, o_total, wc_range, wc_match, wc_ncap, wc_caps;
   // synth scratch
   DevBuf s_lens, s_part;
   DevBuf stamps;        // diagnostic phase stamps (env IE_DEBUG_STAMPS=<file>)
   uint64_t stamp_tiles = 0;
   ~ie_exec() {
     for (DevBuf* b : {&counters, &pool, &out_len, &tile_sum, &tile_base, &defer_tiles, &defer_desc, &in_bytes,
-                      &in_off, &in_tid, &o_bytes, &o_off, &o_status, &o_vid, &o_total, &wc_range, &wc_match, &wc_ncap, &wc_caps,
+                      &in_off, &in_tid, &o_bytes, &o_off, &o_len, &o_status, &o_vid, &o_total, &wc_range, &wc_match, &wc_ncap, &wc_caps,
                       &s_lens, &s_part, &stamps})
       b->release();
     for (auto& e : ev)
@@ -258,7 +260,8 @@ int set_device(int32_t dev) {
 
 // workspace for a batch of n strings. counters (u32 words): [0] tile ticket, [1] look-back error,
 // [2..3] pool bytes used (u64), [4..8] telemetry (literal strings, deferred tiles, look-back polls,
-// exact-path strings, chain failures), [9] deferred-tile count; zeroed on every call.
+// exact-path strings, chain failures), [9] deferred-tile count, [10..11] views output cursor (u64);
+// zeroed on every call.
 int ensure_work(ie_exec* x, int op, uint64_t n) {
   const uint64_t tiles = (n + kBlock - 1) / kBlock + 1;  // (kRBlock >= kBlock: enough for k_resolve too)
   // counters, then (interpolation) the look-back words: one buffer, zeroed by one memset per call
@@ -291,6 +294,8 @@ Work make_work(ie_exec* x, uint64_t* total) {
   W.defer_tiles = (uint32_t*)x->defer_tiles.p;
   W.defer_desc = (uint4*)x->defer_desc.p;
   W.tile_state = (uint64_t*)((uint8_t*)x->counters.p + 64);
+  W.cursor = (uint64_t*)x->counters.p + 5;  // words 10-11
+  W.zero_on_overflow = x->cmd_first ? 1u : 0u;
   W.pool = (uint8_t*)x->pool.p;
   W.pool_bytes = x->pool.bytes;
   W.lit_cap_max = x->lit_cap_max;
@@ -300,8 +305,10 @@ Work make_work(ie_exec* x, uint64_t* total) {
   return W;
 }
 
+// d_out_len / d_in_len (k_resolve only): views output / views input (ie_interpolate_device_views)
 int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, const uint64_t* d_off,
-               uint64_t n, const ie_dev_out* out, const uint32_t* d_tid = nullptr) {
+               uint64_t n, const ie_dev_out* out, const uint32_t* d_tid = nullptr, uint32_t* d_out_len = nullptr,
+               const uint32_t* d_in_len = nullptr) {
   if (!x || !d_off || !out || !out->offsets || !out->status || !out->total || (op == kOpInterp && !t))
     return fail(IE_ERR_INVALID, "null argument");
   if (n && !d_bytes) return fail(IE_ERR_INVALID, "null input bytes");
@@ -319,16 +326,19 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
     IE_HIP(x->stamps.ensure(tiles * 128));
     x->stamp_tiles = tiles;
   }
-  Batch B{d_bytes, d_off, n, out->offsets, out->status, out->value_id, d_tid};
+  if (op != kOpInterp && (d_out_len || d_in_len)) return fail(IE_ERR_INVALID, "views are an interpolation layout");
+  if (n && d_out_len == nullptr && out->offsets == nullptr) return fail(IE_ERR_INVALID, "null offsets");
+  Batch B{d_bytes, d_off, n, out->offsets, out->status, out->value_id, d_tid, d_in_len, d_out_len};
   Work W = make_work(x, out->total);
+  W.recurse = op == kOpInterp && x->in_cmd && t->dialect == IE_DIALECT_PY ? 1u : 0u;
   hipStream_t st = x->stream;
   const uint64_t cap = out->bytes ? out->bytes_cap : 0;
   if (x->timing) IE_HIP(hipEventRecord(x->ev[0], st));
-  // the counters and, for an interpolation, the look-back words (one fill instead of two)
-  const uint64_t zero_tiles = (op == kOpInterp && n) ? (n + kRBlock - 1) / kRBlock : 0;
+  // the counters and, for a packed interpolation, the look-back words (one fill instead of two)
+  const uint64_t zero_tiles = (op == kOpInterp && n && !d_out_len) ? (n + kRBlock - 1) / kRBlock : 0;
   IE_HIP(hipMemsetAsync(x->counters.p, 0, 64 + zero_tiles * sizeof(uint64_t), st));
   if (n == 0) {
-    IE_HIP(hipMemsetAsync(out->offsets, 0, sizeof(uint64_t), st));
+    if (!d_out_len) IE_HIP(hipMemsetAsync(out->offsets, 0, sizeof(uint64_t), st));
     IE_HIP(hipMemsetAsync(out->total, 0, sizeof(uint64_t), st));
   } else if (op == kOpInterp) {
     // fail commit: forced by the option (diagnostics, tests), else adaptive on the count of chain
@@ -345,7 +355,7 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
     // 512-string tiles halve the look-back hops: the unescape command's second resolve (its input
     // is interpolation output, so its evaluation is light and the look-back bounds it) takes them
     // by default; everything else the 256-string tiles (ie_resolve512.hip has the numbers)
-    const bool wide = x->opt_tile == 512 || (x->opt_tile == 0 && x->in_cmd);
+    const bool wide = x->opt_tile == 512 || (x->opt_tile == 0 && x->in_cmd && !d_out_len && !d_in_len);
     IE_HIP(wide ? launch_resolve512(B, W, t->dev, out->bytes, cap, st) : launch_resolve(B, W, t->dev, out->bytes, cap, st));
     if (!forced && !x->stat_pending) {
       if (!x->stat_host) {
@@ -411,7 +421,13 @@ int run_host(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, const 
   cap = x->o_bytes.bytes;
   ie_dev_out o{(uint8_t*)x->o_bytes.p, cap, (uint64_t*)x->o_off.p, (uint8_t*)x->o_status.p,
                (uint32_t*)x->o_vid.p, (uint64_t*)x->o_total.p};
-  rc = run_device(x, op, t, (const uint8_t*)x->in_bytes.p, (const uint64_t*)x->in_off.p, n, &o, d_tid);
+  // views: the device writes each string where its tile claimed room; packed on the host below
+  uint32_t* d_len = nullptr;
+  if (op == kOpInterp && x->opt_views && n) {
+    IE_HIP(x->o_len.ensure(n * 4));
+    d_len = (uint32_t*)x->o_len.p;
+  }
+  rc = run_device(x, op, t, (const uint8_t*)x->in_bytes.p, (const uint64_t*)x->in_off.p, n, &o, d_tid, d_len);
   if (rc) return rc;
   uint64_t total = 0;
   IE_HIP(hipMemcpyAsync(&total, o.total, 8, hipMemcpyDeviceToHost, x->stream));
@@ -421,7 +437,7 @@ int run_host(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, const 
     IE_HIP(x->o_bytes.ensure(total + 4096));
     o.bytes = (uint8_t*)x->o_bytes.p;
     o.bytes_cap = x->o_bytes.bytes;
-    rc = run_device(x, op, t, (const uint8_t*)x->in_bytes.p, (const uint64_t*)x->in_off.p, n, &o, d_tid);
+    rc = run_device(x, op, t, (const uint8_t*)x->in_bytes.p, (const uint64_t*)x->in_off.p, n, &o, d_tid, d_len);
     if (rc) return rc;
     IE_HIP(hipMemcpyAsync(&total, o.total, 8, hipMemcpyDeviceToHost, x->stream));
     IE_HIP(hipStreamSynchronize(x->stream));
@@ -436,12 +452,40 @@ int run_host(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, const 
   b->status = new uint8_t[n + 1];
   b->value_id = new uint32_t[n + 1];
   if (total) IE_HIP(hipMemcpyAsync(b->bytes, o.bytes, total, hipMemcpyDeviceToHost, x->stream));
-  IE_HIP(hipMemcpyAsync(b->offsets, o.offsets, (n + 1) * 8, hipMemcpyDeviceToHost, x->stream));
+  std::vector<uint32_t> lens;
+  if (d_len) {
+    lens.resize(n);
+    IE_HIP(hipMemcpyAsync(b->offsets, o.offsets, n * 8, hipMemcpyDeviceToHost, x->stream));
+    IE_HIP(hipMemcpyAsync(lens.data(), d_len, n * 4, hipMemcpyDeviceToHost, x->stream));
+  } else {
+    IE_HIP(hipMemcpyAsync(b->offsets, o.offsets, (n + 1) * 8, hipMemcpyDeviceToHost, x->stream));
+  }
   if (n) IE_HIP(hipMemcpyAsync(b->status, o.status, n, hipMemcpyDeviceToHost, x->stream));
   if (n) IE_HIP(hipMemcpyAsync(b->value_id, o.value_id, n * 4, hipMemcpyDeviceToHost, x->stream));
   IE_HIP(hipStreamSynchronize(x->stream));
+  if (d_len) {  // views -> packed in input order
+    uint8_t* packed = new uint8_t[total + 1];
+    uint64_t w = 0;
+    for (uint64_t i = 0; i < n; i++) {
+      if (b->offsets[i] + lens[i] > total) {
+        delete[] packed;
+        ie_batch_free(b);
+        return fail(IE_ERR_HIP, "views output outside the batch's bytes");
+      }
+      if (lens[i]) memcpy(packed + w, b->bytes + b->offsets[i], lens[i]);
+      b->offsets[i] = w;
+      w += lens[i];
+    }
+    b->offsets[n] = w;
+    delete[] b->bytes;
+    b->bytes = packed;
+    if (w != total) {
+      ie_batch_free(b);
+      return fail(IE_ERR_HIP, "views output lengths do not add up to its total");
+    }
+  }
   for (uint64_t i = 0; i < n; i++)
-    if (b->status[i] != IE_OK_VALUE) b->value_id[i] = IE_VID_NONE;
+    if (b->status[i] != IE_OK_VALUE && b->status[i] != IE_RECURSE) b->value_id[i] = IE_VID_NONE;
 
   // literal-path strings that ran out of scratch: re-run them alone with the full working space
   if (op == kOpInterp) {
@@ -858,6 +902,7 @@ int ie_exec_create(int32_t device, void* hip_stream, ie_exec** out) {
   if (const char* e = getenv("IE_FAST")) x->opt_fast = (uint32_t)atoi(e);
   if (getenv("IE_DEBUG_NOEVAL")) x->opt_noeval = 1;
   if (const char* e = getenv("IE_TILE")) x->opt_tile = atoi(e) == 512 ? 512 : atoi(e) == 256 ? 256 : 0;
+  if (const char* e = getenv("IE_VIEWS")) x->opt_views = atoi(e) != 0;
   if (const char* e = getenv("IE_DEBUG_STAMPS")) x->stamps_path = e;
   if (hip_stream) {
     x->stream = (hipStream_t)hip_stream;
@@ -980,6 +1025,9 @@ int ie_exec_set_option(ie_exec* x, int32_t option, int64_t value) {
       if (value != 0 && value != 256 && value != 512) return fail(IE_ERR_INVALID, "tile must be 0, 256 or 512");
       x->opt_tile = (int32_t)value;
       return IE_SUCCESS;
+    case IE_OPT_VIEWS:
+      x->opt_views = value ? 1 : 0;
+      return IE_SUCCESS;
     default:
       return fail(IE_ERR_INVALID, "unknown exec option");
   }
@@ -1064,6 +1112,22 @@ int ie_interpolate_device(ie_exec* x, const ie_table* t, const uint8_t* d_bytes,
   return ie_interpolate_device_ids(x, t, nullptr, d_bytes, d_offsets, n, out);
 }
 
+int ie_interpolate_device_views(ie_exec* x, const ie_table* t, const uint32_t* d_table_id, const uint8_t* d_bytes,
+                                const uint64_t* d_offsets, const uint32_t* d_lengths, uint64_t n,
+                                const ie_dev_views* out) {
+  if (!out || (n && (!out->offsets || !out->lengths))) return fail(IE_ERR_INVALID, "null argument");
+  const ie_dev_out o{out->bytes, out->bytes_cap, out->offsets, out->status, out->value_id, out->total};
+  int rc = run_device(x, kOpInterp, t, d_bytes, d_offsets, n, &o, d_table_id, out->lengths, d_lengths);
+  if (rc || !n || x->pool_fixed) return rc;
+  // the literal path's scratch demand, as ie_interpolate_device_ids
+  uint64_t used = 0;
+  IE_HIP(hipMemcpyAsync(&used, (uint64_t*)x->counters.p + 1, 8, hipMemcpyDeviceToHost, x->stream));
+  IE_HIP(hipStreamSynchronize(x->stream));
+  if (used <= x->pool.bytes) return IE_SUCCESS;
+  x->pool_request = std::max<uint64_t>(x->pool_request, used + used / 8 + (1ull << 20));
+  return run_device(x, kOpInterp, t, d_bytes, d_offsets, n, &o, d_table_id, out->lengths, d_lengths);
+}
+
 int ie_interpolate_batch_ids(ie_exec* x, const ie_table* t, const uint32_t* table_id, const uint8_t* bytes,
                              const uint64_t* offsets, uint64_t n, ie_batch** out) {
   if (!t) return fail(IE_ERR_INVALID, "null table");
@@ -1086,11 +1150,14 @@ int ie_unescape_cmd_device(ie_exec* x, const ie_table* t, const uint32_t* d_tabl
                            const uint64_t* d_offsets, uint64_t n, const uint8_t* d_status_in, const ie_dev_out* tmp,
                            const ie_dev_out* out) {
   if (!tmp || !out || !tmp->bytes || !out->status) return fail(IE_ERR_INVALID, "null argument");
+  x->cmd_first = true;
   int rc = run_device(x, kOpUnescape, nullptr, d_bytes, d_offsets, n, tmp);  // py:1665
+  x->cmd_first = false;
   if (rc) return rc;
   // the unescaped bytes feed the interpolation (py:1666). Unescaping never lengthens a string, so
   // a tmp as large as the input always fits; a smaller one that overflowed is flagged on the
-  // device (no wait here) and reported by ie_exec_sync as IE_ERR_CAPACITY
+  // device (no wait here) and reported by ie_exec_sync as IE_ERR_CAPACITY. Its offsets are then
+  // all 0 (k_emit, zero_on_overflow), so the interpolation below reads nothing past tmp->bytes.
   x->in_cmd = true;
   rc = ie_interpolate_device_ids(x, t, d_table_id, tmp->bytes, tmp->offsets, n, out);
   x->in_cmd = false;

@@ -27,12 +27,18 @@ enum { kOpInterp = 0, kOpUnescape = 1, kOpEscape = 2 };
 
 struct Batch {
   const uint8_t* bytes;     // input payload
-  const uint64_t* in_off;   // n + 1 input offsets
+  const uint64_t* in_off;   // n + 1 input offsets (packed), or n starts (views input: in_len set)
   uint64_t n;
-  uint64_t* out_off;        // n + 1 output offsets
+  uint64_t* out_off;        // n + 1 output offsets (packed), or n starts (views output: out_len set)
   uint8_t* status;          // n
   uint32_t* value_id;       // n
   const uint32_t* table_id; // n: the table of the set each string is resolved against, or null (0)
+  // views (k_resolve only): string i is bytes[in_off[i], + in_len[i]); any placement is accepted,
+  // strings of one tile that lie together in order are staged together (what a views output is)
+  const uint32_t* in_len;   // n or null
+  // views output: no global order, so no look-back: each tile claims its output range with one
+  // atomic on the exec's cursor; string i's result is out[out_off[i], + out_len[i])
+  uint32_t* out_len;        // n or null
 };
 
 struct Work {
@@ -55,6 +61,11 @@ struct Work {
   uint32_t* defer_count; // 1
   uint32_t* defer_tiles; // tiles
   uint4* defer_desc;     // tiles * kBlock * 4: each string's descriptor
+  uint64_t* cursor;      // 1   views output: bytes claimed so far (zeroed per call)
+  uint32_t recurse;      // k_resolve in the unescape command (py dialect): whole-string items whose
+                         // result recursive_interpolate walks again report IE_RECURSE
+  uint32_t zero_on_overflow; // escape kernels: when the output exceeds its capacity, write every
+                             // offset as 0 (a step that reads these strings next then reads nothing)
   // escape pipeline
   uint32_t* out_len;     // n
   uint64_t* tile_sum;    // tiles

@@ -153,6 +153,7 @@ struct LitOut {
   uint64_t res_off;  // pool offset of the result bytes
   uint64_t res_len;
   uint32_t vid;
+  uint32_t flags;    // the entry flags of an IE_OK_VALUE result
 };
 
 // One complex string, executed by all 64 lanes of a wave with uniform control flow.
@@ -246,6 +247,7 @@ __device__ LitOut w_literal(const DevTable& T, uint32_t tid, const uint8_t* s, u
   }
   r.status = IE_OK_VALUE;
   r.vid = cur_hit.vid;
+  r.flags = cur_hit.flags;
   return r;
 }
 

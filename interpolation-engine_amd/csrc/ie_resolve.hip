@@ -336,7 +336,7 @@ __device__ __forceinline__ void put_words(lds_u8* dst, const uint32_t (&t)[8], u
 // ------------------------------------------------------------------------------------------
 template <bool STAGED>
 __device__ uint8_t eval_exact(const DevTable& T, uint32_t tid, const Src<STAGED> s, uint32_t n, bool active, lds_u8* kbuf,
-                              lds_u32* stack, Desc& d, uint32_t& out_len, uint32_t& vid) {
+                              lds_u32* stack, Desc& d, uint32_t& out_len, uint32_t& vid, uint32_t& vflags) {
   constexpr uint8_t kRunning = 0xFF;
   uint8_t status = active ? kRunning : (uint8_t)IE_OK_STR;
   uint32_t depth = 0, klen = 0, vsum = 0, span = 0, ntop = 0;
@@ -364,6 +364,7 @@ __device__ uint8_t eval_exact(const DevTable& T, uint32_t tid, const Src<STAGED>
     if (err_off >= 0) return err_cls;
     if (wrapped) {
       vid = wrap_h.vid;
+      vflags = wrap_h.flags;
       return IE_OK_VALUE;
     }
     return IE_OK_STR;
@@ -647,7 +648,6 @@ __device__ bool parse_chains(const lds_u8* tile, uint32_t p0, uint32_t n, const 
     return clean;
   }
   bool ok = active && n <= kChainMax;
-  const lds_u8* s = tile + p0;
   // ---- 1. the string's open / close events as 128-bit windows ----
   uint32_t O[4], C[4];
   {
@@ -1054,12 +1054,23 @@ __device__ __forceinline__ TileGeo load_geo(const Batch& B, uint32_t tile, uint3
   if (first >= B.n) return g;
   const uint64_t last = min(first + (uint64_t)kRBlock, B.n), i = first + tid;
   g.lo = gld(B.in_off + first);
-  g.hi = gld(B.in_off + last);
+  if (B.in_len) {  // views input: the tile's span ends with its last string (nothing staged if it
+                   // lies before the first: such strings are read where they are)
+    const uint64_t e = gld(B.in_off + last - 1) + gld(B.in_len + last - 1);
+    g.hi = e > g.lo ? e : g.lo;
+  } else {
+    g.hi = gld(B.in_off + last);
+  }
   if (i < B.n) {
     g.so = gld(B.in_off + i);
-    g.sn = gld(B.in_off + i + 1) - g.so;
+    g.sn = B.in_len ? (uint64_t)gld(B.in_len + i) : gld(B.in_off + i + 1) - g.so;
   }
   return g;
+}
+
+// byte length of input string i (packed or views input)
+__device__ __forceinline__ uint64_t in_length(const Batch& B, uint64_t i) {
+  return B.in_len ? (uint64_t)gld(B.in_len + i) : gld(B.in_off + i + 1) - gld(B.in_off + i);
 }
 
 constexpr uint32_t kStageChunks = (kRTileBytes + 31) / 16;  // the input stage: the tile's first chunks
@@ -1209,6 +1220,28 @@ __device__ __forceinline__ void stage_piece(lds_u8* stage, bool on, uint32_t off
   }
 }
 
+// The unescape command's recursive_interpolate (py:1463-1464): an item that is a whole-string
+// '{key}' as written (raw_simple) is interpolated again through its result, unless that result is
+// an int / float / bool / None value; such items report IE_RECURSE (W.recurse) and the caller
+// walks them. Status and entry flags of a final result -> does recursive_interpolate re-enter it?
+__device__ __forceinline__ bool recurses(uint8_t st, uint32_t flags) {
+  const uint32_t k = flags & EF_KIND_MASK;
+  return st == IE_OK_STR || (st == IE_OK_VALUE && (k == IE_KIND_STR || k == IE_KIND_LIST || k == IE_KIND_DICT));
+}
+
+// get_simple_insertkey truthy on the string as written (py:477-495: at least 3 characters, a '{'
+// first and a '}' last that close each other: depth > 0 everywhere in between). Any address space.
+__device__ bool raw_simple(const uint8_t* s, uint32_t n) {
+  if (n < 3 || s[0] != '{' || s[n - 1] != '}') return false;
+  int32_t depth = 1;
+  for (uint32_t k = 1; k + 1 < n; k++) {
+    const uint8_t c = s[k];
+    depth += c == '{' ? 1 : c == '}' ? -1 : 0;
+    if (depth <= 0) return false;
+  }
+  return depth == 1;
+}
+
 // The deferred tiles' bytes (see k_resolve): one workgroup per deferred tile at a time. Each
 // lane rebuilds its string's pieces from the stored descriptor (template runs from the input in
 // global memory, values from the table or the literal pool) and the tile's output goes through
@@ -1217,10 +1250,14 @@ __global__ __launch_bounds__(kRBlock) void k_emit_windows(Batch B, Work W, DevTa
   __shared__ __attribute__((aligned(16))) uint8_t s_win[kRStageBytes + 48];
   const uint32_t count = __hip_atomic_load(W.defer_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t tid = threadIdx.x;
+  // views output: the bytes every tile claimed are the batch's total (k_resolve has finished)
+  if (B.out_len && blockIdx.x == 0 && tid == 0) *W.total = *W.cursor;
   for (uint32_t slot = blockIdx.x; slot < count; slot += gridDim.x) {
     const uint32_t tile = gld(W.defer_tiles + slot);
     const uint64_t first = (uint64_t)tile * kRBlock, last = min(first + (uint64_t)kRBlock, B.n), i = first + tid;
-    const uint64_t base = gld(B.out_off + first), tile_total = gld(B.out_off + last) - base;
+    const uint64_t base = gld(B.out_off + first);
+    const uint64_t tile_total =
+        (B.out_len ? gld(B.out_off + last - 1) + gld(B.out_len + last - 1) : gld(B.out_off + last)) - base;
     const uint4* dd = W.defer_desc + ((uint64_t)slot * kRBlock + tid) * 4;
     Desc d;
     uint32_t olen = 0, n32 = 0;
@@ -1234,7 +1271,7 @@ __global__ __launch_bounds__(kRBlock) void k_emit_windows(Batch B, Work W, DevTa
       d.vs[0] = e.x, d.vs[1] = e.y, d.vs[2] = e.z;
       const uint64_t o = gld(B.out_off + i);
       local = o - base;
-      olen = gld(B.status + i) == IE_OK_STR ? (uint32_t)(gld(B.out_off + i + 1) - o) : 0u;
+      olen = gld(B.status + i) != IE_OK_STR ? 0u : B.out_len ? gld(B.out_len + i) : (uint32_t)(gld(B.out_off + i + 1) - o);
       s = B.bytes + gld(B.in_off + i);
     } else {
       d.ntop = 0;
@@ -1274,7 +1311,9 @@ __global__ __launch_bounds__(kRBlock) void k_emit_windows(Batch B, Work W, DevTa
 
 // FAILC: chain failures commit in the chain evaluator (else they take the exact evaluator). Both
 // give the reference's results; the host picks per batch stream (ie_host.cpp, "fail commit").
-template <bool FAILC, bool MULTI>
+// VIEWS: B.out_len set; each tile claims its output range with one atomic on W.cursor (no
+// global order, no look-back) and writes each string's start and length.
+template <bool FAILC, bool MULTI, bool VIEWS>
 __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES_PER_EU))) void k_resolve(Batch B, Work W, DevTable T, uint8_t* out,
                                                     uint64_t cap) {
   __shared__ __attribute__((aligned(16))) uint8_t s_in[kRTileBytes + 48];
@@ -1320,13 +1359,14 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
   const uint64_t first = (uint64_t)tile * kRBlock;
   const uint64_t last = min(first + (uint64_t)kRBlock, B.n);
   const uint64_t i = first + tid;
-  const uint64_t lo = geo.lo, hi = geo.hi, so = geo.so, sn = geo.sn;
+  const uint64_t lo = geo.lo, so = geo.so, sn = geo.sn;
   const uint32_t shift = (uint32_t)((uintptr_t)(B.bytes + lo) & 15);
   // the stage holds the tile's first kStageChunks 16-byte chunks: strings that end inside it are
-  // evaluated from LDS, the rest (a tile of long strings) from global memory
+  // evaluated from LDS, the rest (a tile of long strings; a views input string placed apart from
+  // its tile) from global memory
   const uint32_t nv = pre.nv;
-  const uint32_t p0 = shift + (uint32_t)(so - lo);
-  const bool lane_staged = p0 + sn <= 16ull * nv;
+  const bool lane_staged = so >= lo && shift + (so - lo) + sn <= 16ull * nv;
+  const uint32_t p0 = lane_staged ? shift + (uint32_t)(so - lo) : 0u;
   {
     pre.commit((uint4*)s_in, tid);
     __syncthreads();
@@ -1358,7 +1398,7 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
   const uint32_t tid_s = (MULTI && i < B.n) ? gld(B.table_id + i) : 0u;
   {
     uint8_t st = IE_OK_STR;
-    uint32_t olen = 0, vid = IE_VID_NONE;
+    uint32_t olen = 0, vid = IE_VID_NONE, vflags = 0;
     bool active = false;
     if (i < B.n) {
       s = lane_staged ? s_in + p0 : B.bytes + so;
@@ -1420,15 +1460,19 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
       uint8_t r2 = kStatusPending;
 #ifndef IE_EXP_NOEXACT
       // staged strings through a generic pointer into the stage, the rest in global memory
-      r2 = eval_exact<false>(T, tid_s, Src<false>{s}, (uint32_t)sn, slow, kb, stk, d, o2, vid);
+      r2 = eval_exact<false>(T, tid_s, Src<false>{s}, (uint32_t)sn, slow, kb, stk, d, o2, vid, vflags);
 #endif
       if (slow) r = r2, olen = o2;
     }
     if (active) st = r;
     pend = i < B.n && st == kStatusPending;
     if (pend) s_pend[atomicAdd(&s_misc[1], 1u)] = (uint16_t)tid;
+    if (W.recurse && active && recurses(st, vflags) && raw_simple(s, (uint32_t)sn)) {
+      if (st == IE_OK_STR) vid = IE_VID_NONE;
+      st = IE_RECURSE;
+    }
     s_st[tid] = st;
-    s_olen[tid] = st == IE_OK_STR ? olen : (st == IE_OK_VALUE ? vid : 0u);
+    s_olen[tid] = st == IE_OK_STR ? olen : (st == IE_OK_VALUE || st == IE_RECURSE ? vid : 0u);
   }
   __syncthreads();
   IE_STAMP(2);
@@ -1439,7 +1483,7 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
   for (uint32_t k = wave; k < npend; k += kRBlock / 64) {
     const uint32_t j = s_pend[k];
     const uint64_t gi = first + j;
-    const uint64_t po = gld(B.in_off + gi), pn = gld(B.in_off + gi + 1) - po;
+    const uint64_t po = gld(B.in_off + gi), pn = in_length(B, gi);
     uint64_t rcap = W.lit_cap_max ? IE_SIZE_CAP(pn, T.maxtext) + 4 * T.maxtext + 64
                                   : 4 * pn + 4 * T.maxtext + 256;
     rcap = (rcap + 15) & ~15ull;
@@ -1457,8 +1501,12 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
     if (r.status == IE_OK_STR && (r.res_len > kLenMask || (r.res_off >> 4) > 0xFFFFFFFFull))
       r.status = IE_E_OVERFLOW;
     if (lane == 0) {
+      if (W.recurse && recurses(r.status, r.flags) && raw_simple(B.bytes + po, (uint32_t)pn)) {
+        if (r.status == IE_OK_STR) r.vid = IE_VID_NONE;
+        r.status = IE_RECURSE;
+      }
       s_st[j] = r.status;
-      s_olen[j] = r.status == IE_OK_STR ? (uint32_t)r.res_len : (r.status == IE_OK_VALUE ? r.vid : 0u);
+      s_olen[j] = r.status == IE_OK_STR ? (uint32_t)r.res_len : (r.status == IE_OK_VALUE || r.status == IE_RECURSE ? r.vid : 0u);
       s_lit[j] = (uint32_t)(r.res_off >> 4);
     }
   }
@@ -1479,7 +1527,10 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
   uint64_t tile_total;
   const uint64_t local = block_scan(olen, s_red, &tile_total);  // (its barriers also retire s_lit)
   uint64_t lb_early = 0;
-  if (wave == 0) {
+  if (VIEWS) {
+    // the tile's output range: one atomic, its answer consumed after the build
+    if (tid == 0) lb_early = atomicAdd((unsigned long long*)W.cursor, (unsigned long long)tile_total);
+  } else if (wave == 0) {
     publish_aggregate(W.tile_state, tile, tile_total);
     if (tile != 0) lb_early = lb_poll(W.tile_state, (int64_t)tile - 1);  // consumed after the build
   }
@@ -1531,7 +1582,9 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
     }
   }
   IE_STAMP(4);
-  if (wave == 0) {
+  if (VIEWS) {
+    if (tid == 0) s_red[kRBlock / 64] = lb_early;
+  } else if (wave == 0) {
     const uint64_t b = look_back(W.tile_state, tile, tile_total, W.err, W.stamps ? W.stats + 2 : nullptr, lb_early);
     if (tid == 0) s_red[kRBlock / 64] = b;
   }
@@ -1544,10 +1597,11 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
   const uint64_t i_t = first + tid_t;
   if (i_t < B.n) {
     gsts(B.out_off + i_t, base + local);
+    if (VIEWS) gsts(B.out_len + i_t, s_st[tid_t] == IE_OK_STR ? s_olen[tid_t] : 0u);
     gsts(B.status + i_t, st);
-    if (st == IE_OK_VALUE) gst(B.value_id + i_t, s_olen[tid_t]);
+    if (st == IE_OK_VALUE || st == IE_RECURSE) gst(B.value_id + i_t, s_olen[tid_t]);
   }
-  if (last == B.n && tid == 0) {
+  if (!VIEWS && last == B.n && tid == 0) {
     B.out_off[B.n] = base + tile_total;
     *W.total = base + tile_total;
   }
@@ -1620,12 +1674,22 @@ hipError_t launch_resolve_impl(const Batch& B, const Work& W, const DevTable& T,
   if (tiles > 0xFFFFFFFFull) return hipErrorInvalidValue;
   const uint32_t grid = (uint32_t)tiles;
   const bool multi = B.table_id != nullptr;
-  if (W.fail_commit && multi) hipLaunchKernelGGL((k_resolve<true, true>), dim3(grid), dim3(kRBlock), 0, st, B, W, T, out, cap);
-  else if (W.fail_commit) hipLaunchKernelGGL((k_resolve<true, false>), dim3(grid), dim3(kRBlock), 0, st, B, W, T, out, cap);
-  else if (multi) hipLaunchKernelGGL((k_resolve<false, true>), dim3(grid), dim3(kRBlock), 0, st, B, W, T, out, cap);
-  else hipLaunchKernelGGL((k_resolve<false, false>), dim3(grid), dim3(kRBlock), 0, st, B, W, T, out, cap);
-  // the deferred (oversized) tiles' bytes; exits at once when there are none
-  if (out) hipLaunchKernelGGL(k_emit_windows, dim3(grid < 512u ? grid : 512u), dim3(kRBlock), 0, st, B, W, T, out);
+  const int variant = (W.fail_commit ? 4 : 0) | (multi ? 2 : 0) | (B.out_len ? 1 : 0);
+  switch (variant) {
+#define IE_LAUNCH(V, F, M, S) \
+  case V: hipLaunchKernelGGL((k_resolve<F, M, S>), dim3(grid), dim3(kRBlock), 0, st, B, W, T, out, cap); break;
+    IE_LAUNCH(0, false, false, false)
+    IE_LAUNCH(1, false, false, true)
+    IE_LAUNCH(2, false, true, false)
+    IE_LAUNCH(3, false, true, true)
+    IE_LAUNCH(4, true, false, false)
+    IE_LAUNCH(5, true, false, true)
+    IE_LAUNCH(6, true, true, false)
+    IE_LAUNCH(7, true, true, true)
+#undef IE_LAUNCH
+  }
+  // the deferred (oversized) tiles' bytes (exits at once when there are none); views: the total
+  if (out || B.out_len) hipLaunchKernelGGL(k_emit_windows, dim3(grid < 512u ? grid : 512u), dim3(kRBlock), 0, st, B, W, T, out);
   return hipGetLastError();
 }
 

@@ -528,6 +528,14 @@ def display_text(text):
     return display_texts([text])[0]
 
 
+def unescape_command(inserts, item):
+    """The `unescape` command's transform of its item (py:1660-1667): recursive_unescape, then
+    recursive_interpolate, which re-enters the result of a whole-string item (py:1463-1464). The
+    C ABI's batch form, ie_unescape_cmd_device, reports such items as IE_RECURSE; this is the walk
+    its callers do for them."""
+    return recursive_interpolate(inserts, recursive_unescape(item))
+
+
 _LOOP_CMDS = ("for", "serial", "parallel_wait", "parallel_race")
 
 

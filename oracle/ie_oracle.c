@@ -523,38 +523,70 @@ typedef struct {
   uint64_t* out_len;
   uint64_t* out_hash; /* FNV-1a of each output (0 if not OK_STR) */
   uint32_t* vid;
-  int32_t mode; /* 0: interpolate_inserts; 1: then the `unescape` command on the result (py:1660-1667) */
+  int32_t mode; /* 0: interpolate_inserts; 1: then the `unescape` command on the result (py:1660-1667);
+                  2: the `unescape` command alone */
+  const ieo_ctx* const* ctxs; /* table sets: string i against ctxs[table_id[i]] (else c) */
+  const uint32_t* table_id;
 } job;
+
+/* recursive_unescape of one string (py:1436-1440): two plain str.replace passes */
+static void unescape_str(sb* out, const char* s, size_t n) {
+  sb a = {0};
+  str_replace(&a, s, n, ESC_START, 2, "{", 1);
+  str_replace(out, a.p ? a.p : "", a.n, ESC_STOP, 2, "}", 1);
+  sb_free(&a);
+}
+
+/* the unescape command's transform of a string item (py:1665-1666): recursive_unescape, then
+ * recursive_interpolate. recursive_interpolate re-enters the result of an item that is a
+ * whole-string '{key}' as written (py:1463-1464) unless that result is an int/float/bool/None
+ * value; such items report IE_RECURSE (the device does the same; callers walk them). */
+static void unescape_command(const ieo_ctx* c, const char* s, size_t n, result* r) {
+  sb b = {0};
+  unescape_str(&b, s, n);
+  interpolate(c, b.p ? b.p : "", b.n, r, 0);
+  size_t ko, kl;
+  if (c->dialect == IE_DIALECT_PY && (r->status == IE_OK_STR || r->status == IE_OK_VALUE) &&
+      simple_key(IE_DIALECT_PY, b.p ? b.p : "", b.n, &ko, &kl) &&
+      (r->status == IE_OK_STR || r->v.kind == IE_KIND_STR || r->v.kind == IE_KIND_LIST || r->v.kind == IE_KIND_DICT)) {
+    if (r->status == IE_OK_STR) r->v.vid = IE_VID_NONE;
+    r->status = IE_RECURSE;
+    sb_free(&r->str);
+  }
+  sb_free(&b);
+}
 
 static void* run_job(void* p) {
   job* j = (job*)p;
   for (uint64_t i = j->lo; i < j->hi; i++) {
     result r = {0};
-    interpolate(j->c, (const char*)j->bytes + j->offsets[i], j->offsets[i + 1] - j->offsets[i], &r, 0);
-    if (j->mode == 1 && r.status == IE_OK_STR) {
-      /* recursive_unescape (py:1665) then recursive_interpolate of the string (py:1666) */
-      sb a = {0}, b = {0};
-      str_replace(&a, r.str.p ? r.str.p : "", r.str.n, ESC_START, 2, "{", 1);
-      str_replace(&b, a.p ? a.p : "", a.n, ESC_STOP, 2, "}", 1);
-      sb_free(&a);
-      sb_free(&r.str);
-      memset(&r, 0, sizeof r);
-      interpolate(j->c, b.p ? b.p : "", b.n, &r, 0);
-      sb_free(&b);
+    const ieo_ctx* c = j->ctxs ? j->ctxs[j->table_id[i]] : j->c;
+    const char* s = (const char*)j->bytes + j->offsets[i];
+    const size_t n = j->offsets[i + 1] - j->offsets[i];
+    if (j->mode == 2) {
+      unescape_command(c, s, n, &r); /* the command alone on the item */
+    } else {
+      interpolate(c, s, n, &r, 0);
+      if (j->mode == 1 && r.status == IE_OK_STR) { /* config 4's step: then the command on the result */
+        result r2 = {0};
+        unescape_command(c, r.str.p ? r.str.p : "", r.str.n, &r2);
+        sb_free(&r.str);
+        r = r2;
+      }
     }
     if (j->status) j->status[i] = (uint8_t)r.status;
     if (j->out_len) j->out_len[i] = r.status == IE_OK_STR ? r.str.n : 0;
     if (j->out_hash) j->out_hash[i] = r.status == IE_OK_STR ? fnv(r.str.p ? r.str.p : "", r.str.n) : 0;
-    if (j->vid) j->vid[i] = r.status == IE_OK_VALUE ? r.v.vid : IE_VID_NONE;
+    if (j->vid) j->vid[i] = (r.status == IE_OK_VALUE || r.status == IE_RECURSE) ? r.v.vid : IE_VID_NONE;
     sb_free(&r.str);
   }
   return NULL;
 }
 
 /* returns wall seconds; threads split the batch into contiguous, byte-balanced shards */
-double ieo_run_batch_mode(const ieo_ctx* c, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
-                          int32_t nthreads, uint8_t* status, uint64_t* out_len, uint64_t* out_hash,
-                          uint32_t* vid, int32_t mode) {
+static double run_batch(const ieo_ctx* c, const ieo_ctx* const* ctxs, const uint32_t* table_id,
+                        const uint8_t* bytes, const uint64_t* offsets, uint64_t n, int32_t nthreads,
+                        uint8_t* status, uint64_t* out_len, uint64_t* out_hash, uint32_t* vid, int32_t mode) {
   if (nthreads < 1) nthreads = 1;
   if (nthreads > 256) nthreads = 256;
   job jobs[256];
@@ -574,7 +606,7 @@ double ieo_run_batch_mode(const ieo_ctx* c, const uint8_t* bytes, const uint64_t
       }
       hi = a;
     }
-    jobs[t] = (job){c, bytes, offsets, lo, hi, status, out_len, out_hash, vid, mode};
+    jobs[t] = (job){c, bytes, offsets, lo, hi, status, out_len, out_hash, vid, mode, ctxs, table_id};
     lo = hi;
   }
   struct timespec t0, t1;
@@ -585,6 +617,19 @@ double ieo_run_batch_mode(const ieo_ctx* c, const uint8_t* bytes, const uint64_t
   return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
 
+double ieo_run_batch_mode(const ieo_ctx* c, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                          int32_t nthreads, uint8_t* status, uint64_t* out_len, uint64_t* out_hash,
+                          uint32_t* vid, int32_t mode) {
+  return run_batch(c, NULL, NULL, bytes, offsets, n, nthreads, status, out_len, out_hash, vid, mode);
+}
+
+/* a table-set batch (config 5's forked states): string i against ctxs[table_id[i]] */
+double ieo_run_batch_sets(const ieo_ctx* const* ctxs, const uint32_t* table_id, const uint8_t* bytes,
+                          const uint64_t* offsets, uint64_t n, int32_t nthreads, uint8_t* status,
+                          uint64_t* out_len, uint64_t* out_hash, uint32_t* vid) {
+  return run_batch(NULL, ctxs, table_id, bytes, offsets, n, nthreads, status, out_len, out_hash, vid, 0);
+}
+
 double ieo_run_batch(const ieo_ctx* c, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
                      int32_t nthreads, uint8_t* status, uint64_t* out_len, uint64_t* out_hash,
                      uint32_t* vid) {
@@ -592,3 +637,35 @@ double ieo_run_batch(const ieo_ctx* c, const uint8_t* bytes, const uint64_t* off
 }
 
 uint64_t ieo_fnv1a(const uint8_t* p, uint64_t n) { return fnv((const char*)p, n); }
+
+/* ---- bulk checker: FNV-1a of every result of a device batch (packed or views), so a test can
+ * compare a whole BASELINE-size batch with ieo_run_batch's hashes. starts[i], lens[i] locate
+ * string i in bytes; strings whose status is not IE_OK_STR hash to 0 (as ieo_run_batch). ---- */
+typedef struct {
+  const uint8_t* bytes;
+  const uint64_t* starts;
+  const uint64_t* lens;
+  const uint8_t* status;
+  uint64_t lo, hi;
+  uint64_t* out_hash;
+} hjob;
+
+static void* run_hash(void* p) {
+  hjob* j = (hjob*)p;
+  for (uint64_t i = j->lo; i < j->hi; i++)
+    j->out_hash[i] = j->status[i] == IE_OK_STR ? fnv((const char*)j->bytes + j->starts[i], j->lens[i]) : 0;
+  return NULL;
+}
+
+void ieo_hash_spans(const uint8_t* bytes, const uint64_t* starts, const uint64_t* lens, const uint8_t* status,
+                    uint64_t n, int32_t nthreads, uint64_t* out_hash) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  hjob jobs[256];
+  pthread_t th[256];
+  for (int t = 0; t < nthreads; t++)
+    jobs[t] = (hjob){bytes, starts, lens, status, n * (uint64_t)t / (uint64_t)nthreads,
+                     n * (uint64_t)(t + 1) / (uint64_t)nthreads, out_hash};
+  for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, run_hash, &jobs[t]);
+  for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+}

@@ -18,7 +18,7 @@ SO = os.path.join(HERE, "libie_oracle.so")
 DIALECT = {"py": 0, "rs": 1}
 KIND_STR, KIND_INT, KIND_LIST, KIND_FLOAT, KIND_BOOL, KIND_NULL, KIND_DICT = range(7)
 STATUS_NAMES = ["OK_STR", "OK_VALUE", "E_INTERP", "E_ASSERT_BRACES", "E_ASSERT_TYPE",
-                "E_UNHASHABLE", "E_RS_PANIC", "NEEDS_HOST", "DIVERGED", "E_OVERFLOW"]
+                "E_UNHASHABLE", "E_RS_PANIC", "NEEDS_HOST", "DIVERGED", "E_OVERFLOW", "RECURSE"]
 VID_NONE, VID_HHMM, VID_HHMMSS = 0xFFFFFFFF, 0xFFFFFFFE, 0xFFFFFFFD
 
 
@@ -73,6 +73,13 @@ def lib():
         L.ieo_run_batch_mode.argtypes = L.ieo_run_batch.argtypes + [ctypes.c_int32]
         L.ieo_fnv1a.restype = ctypes.c_uint64
         L.ieo_fnv1a.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+        L.ieo_run_batch_sets.restype = ctypes.c_double
+        L.ieo_run_batch_sets.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_uint64, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_void_p]
+        L.ieo_hash_spans.restype = None
+        L.ieo_hash_spans.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_uint64, ctypes.c_int32, ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -158,13 +165,28 @@ class Oracle:
         return st, out, vid
 
     def run_batch(self, bytes_arr, offsets_arr, n, nthreads=1, status=None, out_len=None, out_hash=None, vid=None,
-                  unescape_cmd=False):
+                  unescape_cmd=False, command_only=False):
         """numpy arrays in/out; returns wall seconds. unescape_cmd: each OK result then goes through
-        the `unescape` command (unescape, interpolate again: py:1660-1667), as config 4's step."""
+        the `unescape` command (unescape, interpolate again: py:1660-1667), as config 4's step;
+        command_only: the `unescape` command alone on each string (item)."""
         def p(a):
             return None if a is None else a.ctypes.data
+        mode = 2 if command_only else 1 if unescape_cmd else 0
         return lib().ieo_run_batch_mode(self.h, p(bytes_arr), p(offsets_arr), n, nthreads,
-                                        p(status), p(out_len), p(out_hash), p(vid), 1 if unescape_cmd else 0)
+                                        p(status), p(out_len), p(out_hash), p(vid), mode)
+
+
+def run_batch_sets(oracles, table_id, bytes_arr, offsets_arr, nthreads=1, status=None, out_len=None,
+                   out_hash=None, vid=None):
+    """A table-set batch: string i against oracles[table_id[i]] (one C call over every string, on
+    nthreads threads); returns wall seconds."""
+    import numpy as np
+    hs = (ctypes.c_void_p * max(1, len(oracles)))(*[o.h for o in oracles])
+    tid = np.ascontiguousarray(table_id, dtype=np.uint32)
+    def p(a):
+        return None if a is None else a.ctypes.data
+    return lib().ieo_run_batch_sets(hs, tid.ctypes.data, p(bytes_arr), p(offsets_arr), len(tid), nthreads,
+                                    p(status), p(out_len), p(out_hash), p(vid))
 
 
 def escape(s, unescape=False):
@@ -185,6 +207,22 @@ def simple_insertkey(s, dialect="py"):
 
 def fnv1a(b):
     return lib().ieo_fnv1a(b, len(b))
+
+
+def hash_spans(blob, starts, lens, status, nthreads=16):
+    """FNV-1a of every OK_STR result of a device batch (0 for status rows): numpy uint8 blob,
+    uint64 starts / lengths, uint8 statuses -> uint64 hashes (what run_batch's out_hash holds)."""
+    import numpy as np
+    blob = np.ascontiguousarray(blob, dtype=np.uint8)
+    starts = np.ascontiguousarray(starts, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint64)
+    status = np.ascontiguousarray(status, dtype=np.uint8)
+    n = len(status)
+    out = np.zeros(n, np.uint64)
+    if n:
+        lib().ieo_hash_spans(blob.ctypes.data, starts.ctypes.data, lens.ctypes.data, status.ctypes.data, n,
+                             nthreads, out.ctypes.data)
+    return out
 
 
 # ---------------------------------------------------------------------------------------------

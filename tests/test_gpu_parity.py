@@ -30,21 +30,34 @@ def run_product(table_dict, strings, dialect="py", has_dir=False):
     return t.run(strings), t
 
 
-@pytest.fixture(params=["0", "1", "1w"], ids=["chain-fail-exact", "chain-fail-commit", "chain-fail-commit-512"])
+@pytest.fixture(params=["0", "1", "1w", "0v", "1v"],
+                ids=["chain-fail-exact", "chain-fail-commit", "chain-fail-commit-512", "chain-fail-exact-views",
+                     "chain-fail-commit-views"])
 def fail_commit(request, monkeypatch):
     """Both k_resolve variants: chain failures sent to the exact evaluator, or committed in the
     chain evaluator (the library picks one adaptively; IE_FAIL_COMMIT / IE_OPT_FAIL_COMMIT force it);
-    the last also with 512-string tiles (ie_resolve512.hip, IE_OPT_TILE). Execs read the environment
-    when they are created; the mirror's cached exec is set directly."""
+    also with 512-string tiles (ie_resolve512.hip, IE_OPT_TILE) and with the views output layout
+    (no look-back; IE_OPT_VIEWS, packed on the host by the batch API; _device_run uses
+    ie_interpolate_device_views). Execs read the environment when they are created; the mirror's
+    cached exec is set directly. Yields the fail-commit digit; VIEWS[0] tells _device_run."""
     fc, tile = request.param[0], 512 if request.param.endswith("w") else 0
+    views = 1 if request.param.endswith("v") else 0
     monkeypatch.setenv("IE_FAIL_COMMIT", fc)
     monkeypatch.setenv("IE_TILE", str(tile))
+    monkeypatch.setenv("IE_VIEWS", str(views))
     x = PKG.interpolation_engine.get_exec(0)
     x.set_option(N.OPT_FAIL_COMMIT, int(fc))
     x.set_option(N.OPT_TILE, tile)
+    x.set_option(N.OPT_VIEWS, views)
+    VIEWS[0] = bool(views)
     yield fc
+    VIEWS[0] = False
     x.set_option(N.OPT_FAIL_COMMIT, -1)
     x.set_option(N.OPT_TILE, 0)
+    x.set_option(N.OPT_VIEWS, 0)
+
+
+VIEWS = [False]  # set by the fail_commit fixture: device runs use the views layout
 
 
 def compare_with_oracle(table_dict, strings, dialect="py", has_dir=False):
@@ -370,10 +383,29 @@ class DevResult:
 
 
 def _device_run(x, table, d_bytes, d_off, n, cap=None):
+    """A packed result; with the views fixture the device writes views, packed here on the host in
+    input order (the check then runs on the same packed form)."""
     r = DevResult(x, n, cap if cap is not None else int(d_bytes.nbytes * 2 + 4096))
-    N.check(N.lib().ie_interpolate_device(x.h, table, d_bytes.ptr, d_off.ptr, n, ctypes.byref(r.out)),
-            "ie_interpolate_device")
+    if not VIEWS[0]:
+        N.check(N.lib().ie_interpolate_device(x.h, table, d_bytes.ptr, d_off.ptr, n, ctypes.byref(r.out)),
+                "ie_interpolate_device")
+        x.sync()
+        return r
+    lens = N.DeviceBuffer(x, 4 * n + 4)
+    v = N.DevViews(r.bytes.ptr, r.out.bytes_cap, r.off.ptr, lens.ptr, r.status.ptr, r.vid.ptr, r.total_d.ptr)
+    N.check(N.lib().ie_interpolate_device_views(x.h, table, None, d_bytes.ptr, d_off.ptr, None, n, ctypes.byref(v)),
+            "ie_interpolate_device_views")
     x.sync()
+    tot = r.total()
+    starts = r.off.to_numpy(np.uint64, n)
+    ln = lens.to_numpy(np.uint32, n).astype(np.uint64)
+    blob = r.bytes.to_numpy(np.uint8, tot)
+    assert int(ln.sum()) == tot
+    packed = np.concatenate([blob[int(starts[i]):int(starts[i] + ln[i])] for i in range(n)]) if n else blob
+    offs = np.zeros(n + 1, np.uint64)
+    offs[1:] = np.cumsum(ln)
+    r.bytes = N.DeviceBuffer.from_numpy(x, np.concatenate([packed, np.zeros(16, np.uint8)]))
+    r.off = N.DeviceBuffer.from_numpy(x, offs)
     return r
 
 
@@ -477,6 +509,33 @@ def test_config4_step_vs_oracle(fail_commit):
     assert np.array_equal(hashes, rhash)
     # the escaped {lit} of ~10 % of the strings is live after the unescape and resolves to LIT
     assert 0.08 < ob.count(b"LIT") / n < 0.12
+    N.lib().ie_table_free(table)
+
+
+def test_unescape_command_tmp_too_small_reports_capacity():
+    """a tmp buffer smaller than the unescaped strings. The command must read
+    nothing past it (the unescape step writes all offsets as 0 on overflow) and ie_exec_sync must
+    report IE_ERR_CAPACITY; a tmp of the right size then gives the oracle's results."""
+    h, kvp, nkv = _synth(4)
+    table = _table_from_kv(kvp, nkv)
+    x = N.Exec(0)
+    n = 50_000
+    buf, offs = _host_strings(h, 0, n)
+    d_bytes = N.DeviceBuffer.from_numpy(x, buf)
+    d_off = N.DeviceBuffer.from_numpy(x, offs)
+    r = _device_run(x, table, d_bytes, d_off, n)
+    tmp = DevResult(x, n, 4096)  # far too small
+    out = DevResult(x, n, 2 * r.total() + 4096)
+    N.check(N.lib().ie_unescape_cmd_device(x.h, table, None, r.bytes.ptr, r.off.ptr, n, r.status.ptr,
+                                           ctypes.byref(tmp.out), ctypes.byref(out.out)), "ie_unescape_cmd_device")
+    assert N.lib().ie_exec_sync(x.h) == -6  # IE_ERR_CAPACITY
+    assert tmp.total() > 4096
+    assert int(np.count_nonzero(tmp.off.to_numpy(np.uint64, n + 1))) == 0
+    _, u = _unescape_cmd(x, table, r, n, r.total() + 4096)
+    ref = O.Oracle.from_kv(ctypes.cast(kvp, ctypes.c_void_p), nkv, "py", clock=CLOCK)
+    rst = np.zeros(n, np.uint8)
+    ref.run_batch(buf, offs, n, 8, rst, None, None, None, unescape_cmd=True)
+    assert np.array_equal(u.status.to_numpy(np.uint8, n), rst)
     N.lib().ie_table_free(table)
 
 
@@ -858,3 +917,63 @@ def test_tile_option_is_validated_and_keeps_results():
     ie.get_exec(0).set_option(N.OPT_TILE, 0)
     assert got[0] == got[1] == got[2]
 
+
+
+# ------------------------------------------------------------------------------------------
+# the `unescape` command's recursion into whole-string results (py:1463-1464)
+# ------------------------------------------------------------------------------------------
+def test_unescape_command_device_statuses_match_oracle():
+    """ie_unescape_cmd_device on the reference-generated items: statuses (including IE_RECURSE for
+    whole-string items whose result recursive_interpolate re-enters), bytes and value ids equal the
+    oracle's command (ieo_run_batch mode 2)."""
+    g = load_golden("unescape_cmd_py.json")
+    table, rows = g["table"], g["rows"]
+    strings = [r["s"] for r in rows]
+    t = PKG.InsertsTable(table, clock=CLOCK)
+    x = N.Exec(0)
+    blob, offs = N.pack(strings)
+    n = len(strings)
+    d_bytes = N.DeviceBuffer.from_numpy(x, np.frombuffer(blob + bytes(16), np.uint8))
+    d_off = N.DeviceBuffer.from_numpy(x, offs)
+    tmp, out = DevResult(x, n, len(blob) + 4096), DevResult(x, n, 64 * len(blob) + (1 << 20))
+    N.check(N.lib().ie_unescape_cmd_device(x.h, t.h, None, d_bytes.ptr, d_off.ptr, n, None, ctypes.byref(tmp.out),
+                                           ctypes.byref(out.out)), "ie_unescape_cmd_device")
+    x.sync()
+    st = out.status.to_numpy(np.uint8, n)
+    oo = out.off.to_numpy(np.uint64, n + 1)
+    ob = out.bytes.to_numpy(np.uint8, out.total()).tobytes()
+    vid = out.vid.to_numpy(np.uint32, n)
+    ref = O.Oracle(table, "py", clock=CLOCK)
+    buf = np.frombuffer(blob + b"\0", np.uint8)
+    rst, rlen, rhash, rvid = np.zeros(n, np.uint8), np.zeros(n, np.uint64), np.zeros(n, np.uint64), np.zeros(n, np.uint32)
+    ref.run_batch(buf, offs, n, 4, rst, rlen, rhash, rvid, command_only=True)
+    assert np.array_equal(st, rst), [(strings[i], st[i], rst[i]) for i in np.flatnonzero(st != rst)[:8]]
+    ok = st == N.OK_STR
+    assert np.array_equal(np.diff(oo.astype(np.int64))[ok], rlen.astype(np.int64)[ok])
+    for i in np.flatnonzero(ok):
+        assert O.fnv1a(ob[int(oo[i]):int(oo[i + 1])]) == int(rhash[i]), strings[i]
+    typed = (st == N.OK_VALUE) | (st == N.RECURSE)
+    assert np.array_equal(vid[typed], rvid[typed])
+    assert int(np.count_nonzero(st == N.RECURSE)) > 20
+    t.close()
+
+
+def test_unescape_command_mirror_matches_reference():
+    """The mirror's unescape_command (recursive_unescape, then recursive_interpolate, both on the
+    device) reproduces the reference's result for every item, including the recursion."""
+    g = load_golden("unescape_cmd_py.json")
+    table, rows = g["table"], g["rows"]
+    exc = {"E_INTERP": PKG.InterpolationException, "E_ASSERT_BRACES": AssertionError,
+           "E_ASSERT_TYPE": AssertionError, "E_UNHASHABLE": TypeError, "DIVERGED": RecursionError}
+    bad = []
+    for r in rows:
+        try:
+            got = PKG.unescape_command(table, r["s"])
+        except Exception as e:  # noqa: BLE001 — the class is what is compared
+            if r["st"] not in exc or not isinstance(e, exc[r["st"]]):
+                bad.append((r, repr(e)))
+            continue
+        want = r.get("out", r.get("value"))
+        if r["st"] not in ("OK_STR", "OK_VALUE") or got != want or type(got) != type(want):
+            bad.append((r, got))
+    assert not bad, (len(bad), bad[:5])

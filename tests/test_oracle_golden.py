@@ -104,3 +104,49 @@ def test_oracle_rust_dialect_restated(s, want):
         assert out == want[1]
     if want[1] is not None and st == "OK_VALUE":
         assert list(t)[vid] == want[1]
+
+
+def _unescape_cmd_oracle(table, strings):
+    """The oracle's unescape command (ieo_run_batch mode 1) over strings -> (statuses, hashes, vids)."""
+    import numpy as np
+    o = O.Oracle(table, "py")
+    bs = [O.enc(s) for s in strings]
+    offs = np.zeros(len(bs) + 1, np.uint64)
+    offs[1:] = np.cumsum([len(b) for b in bs])
+    blob = np.frombuffer(b"".join(bs) + b"\0", np.uint8)
+    n = len(bs)
+    st, ln, hs, vid = np.zeros(n, np.uint8), np.zeros(n, np.uint64), np.zeros(n, np.uint64), np.zeros(n, np.uint32)
+    o.run_batch(blob, offs, n, 4, st, ln, hs, vid, command_only=True)
+    return o, [O.STATUS_NAMES[k] for k in st], hs, vid
+
+
+def test_oracle_unescape_command_matches_reference():
+    """The `unescape` command (py:1660-1667) on the reference-generated vectors: the oracle gives
+    the reference's result wherever recursive_interpolate does not re-enter a whole-string result;
+    where it does (py:1463-1464), it reports RECURSE, which must be exactly the items that are a
+    whole-string '{key}' after the unescape and whose interpolation is a str, list or dict."""
+    g = load_golden("unescape_cmd_py.json")
+    table, rows = g["table"], g["rows"]
+    o, st, hs, vid = _unescape_cmd_oracle(table, [r["s"] for r in rows])
+    keys = list(table.keys())
+    bad, n_rec = [], 0
+    for k, r in enumerate(rows):
+        u = r["s"].replace("\\{", "{").replace("\\}", "}")
+        simple = bool(O.simple_insertkey(u)) and len(u) >= 3
+        if st[k] == "RECURSE":
+            n_rec += 1
+            if not simple:
+                bad.append(("recurse on a non-simple item", r, st[k]))
+            continue
+        if st[k] != r["st"]:
+            bad.append((r, st[k]))
+        elif st[k] == "OK_STR" and int(hs[k]) != O.fnv1a(O.enc(r["out"])):
+            bad.append((r, "bytes"))
+        elif st[k] == "OK_VALUE":
+            v = table[keys[vid[k]]] if vid[k] < len(keys) else None
+            if simple and isinstance(v, (str, list, dict)):
+                bad.append(("typed container result not re-entered", r))
+            elif v != r["value"] and vid[k] < len(keys):
+                bad.append((r, "value", v))
+    assert not bad, (len(bad), bad[:5])
+    assert n_rec > 20  # the fixture exercises the recursion
