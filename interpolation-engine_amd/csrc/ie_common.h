@@ -73,6 +73,39 @@ IE_HD uint32_t ph_slot(uint64_t h, uint32_t pilot, uint32_t m) {
 }
 
 
+// get_simple_insertkey (py:477-495 / interp.rs:11-29) on n bytes of UTF-8 (any address space via
+// the byte reader): true when the reference returns a truthy key (py) / Some (rs); koff / klen
+// locate the key, content[1:-1] in characters. The py loop runs over characters with NO test that
+// the edges are braces: 'a}b{c' is simple (key '}b{', the depth dips below 0 and comes back at the
+// last character), so the edge test is "first or last character", not "first or last byte". The
+// rs version requires a '{' first and a '}' last (interp.rs:14-16) and gives Some("") for "{}".
+template <class ByteAt>
+IE_HD bool simple_insertkey(ByteAt at, uint64_t n, uint32_t dialect, uint64_t& koff, uint64_t& klen) {
+  koff = klen = 0;
+  uint64_t nch = 0, l0 = n, last = 0;  // characters, bytes of the first, start of the last
+  for (uint64_t k = 0; k < n; k++) {
+    if ((at(k) & 0xC0u) == 0x80u) continue;  // a continuation byte: the same character
+    if (nch == 1) l0 = k;
+    last = k;
+    nch++;
+  }
+  if (dialect == 1u && (nch < 2 || at(0) != '{' || at(n - 1) != '}')) return false;
+  int64_t depth = 0;
+  uint64_t ci = 0;
+  for (uint64_t k = 0; k < n; k++) {
+    const uint8_t c = at(k);
+    if ((c & 0xC0u) == 0x80u) continue;
+    if (c == '}') depth--;
+    if ((depth == 0) != (ci == 0 || ci == nch - 1)) return false;
+    if (c == '{') depth++;
+    ci++;
+  }
+  if (nch <= 2) return dialect == 1u && nch == 2;  // py: '' is falsy; rs: Some("") for "{}"
+  koff = l0;
+  klen = last - l0;
+  return true;
+}
+
 // Entry.flags
 enum : uint32_t {
   EF_KIND_MASK = 7u,

@@ -1305,19 +1305,10 @@ int ie_simple_insertkey(const char* s, uint64_t len, int32_t dialect, uint64_t* 
   if (key_len) *key_len = 0;
   if (!s && len) return 0;
   const uint8_t* p = (const uint8_t*)s;
-  if (dialect == IE_DIALECT_RS) {
-    if (len < 2 || p[0] != '{' || p[len - 1] != '}') return 0;
-  } else if (len < 3 || p[0] != '{' || p[len - 1] != '}') {
-    return 0;
-  }
-  int64_t depth = 0;
-  for (uint64_t k = 0; k < len; k++) {
-    if (p[k] == '}') depth--;
-    if ((depth == 0) != (k == 0 || k == len - 1)) return 0;
-    if (p[k] == '{') depth++;
-  }
-  if (key_off) *key_off = 1;
-  if (key_len) *key_len = len - 2;
+  uint64_t ko = 0, kl = 0;
+  if (!simple_insertkey([&](uint64_t k) { return p[k]; }, len, dialect == IE_DIALECT_RS ? 1u : 0u, ko, kl)) return 0;
+  if (key_off) *key_off = ko;
+  if (key_len) *key_len = kl;
   return 1;
 }
 

@@ -120,31 +120,41 @@ __device__ int64_t w_find(const uint8_t* p, uint64_t from, uint64_t n, uint8_t c
   return -1;
 }
 
-// get_simple_insertkey on protected bytes (py:477-495 / interp.rs:11-29): truthy / Some.
-// Byte-level equals the code-point loop: only ASCII '{' / '}' positions matter.
-__device__ bool w_simple(uint32_t dialect, const uint8_t* p, uint64_t n) {
-  if (dialect == IE_DIALECT_RS) {
-    if (n < 2 || p[0] != '{' || p[n - 1] != '}') return false;
-    if (n == 2) return true;  // Some("")
-  } else if (n < 3 || p[0] != '{' || p[n - 1] != '}') {
-    return false;
-  }
+// get_simple_insertkey on protected bytes (py:477-495 / interp.rs:11-29): truthy / Some, with
+// l0 / ll the byte lengths of the first and the last character (content[1:-1] drops them). The
+// py rule has no brace test at the edges ('a}b{c' is simple: ie_common.h simple_insertkey), so
+// the depth test skips continuation bytes and treats the first and last CHARACTER as the edges.
+// Wave-uniform; every lane returns the same.
+__device__ bool w_simple(uint32_t dialect, const uint8_t* p, uint64_t n, uint64_t& l0, uint64_t& ll) {
+  l0 = ll = 0;
+  if (n == 0) return false;
+  if (dialect == IE_DIALECT_RS && (n < 2 || p[0] != '{' || p[n - 1] != '}')) return false;
+  // the first character's bytes and the last character's first byte (at most 3 bytes back)
+  const uint8_t c0 = p[0];
+  const uint64_t f = c0 < 0x80u ? 1u : (c0 & 0xE0u) == 0xC0u ? 2u : (c0 & 0xF0u) == 0xE0u ? 3u : 4u;
+  uint64_t last = n - 1;
+  while (last > 0 && last + 3 >= n && (p[last] & 0xC0u) == 0x80u) last--;
+  // py: content[1:-1] must be non-empty (3+ characters); rs: Some("") for "{}"
+  if (dialect != IE_DIALECT_RS && last <= f) return false;
   uint64_t carry = 0;  // signed sums in two's complement
   for (uint64_t base = 0; base < n; base += 64) {
     const uint64_t k = base + lane_id();
     uint64_t e = 0;
-    bool close = false;
+    bool close = false, lead = false;
     if (k < n) {
       const uint8_t c = p[k];
+      lead = (c & 0xC0u) != 0x80u;
       e = c == '{' ? 1ull : (c == '}' ? ~0ull : 0ull);
       close = c == '}';
     }
     const uint64_t incl = wave_incl_scan(e);
     const uint64_t depth = carry + incl - e - (close ? 1ull : 0ull);  // after the decrement at k
-    const bool edge = (k == 0 || k == n - 1);
-    if (__ballot(k < n && ((depth == 0) != edge))) return false;
+    const bool edge = (k == 0 || k == last);
+    if (__ballot(k < n && lead && ((depth == 0) != edge))) return false;
     carry += __shfl(incl, 63, 64);
   }
+  l0 = f < n ? f : n;
+  ll = n - last;
   return true;
 }
 
@@ -158,9 +168,9 @@ struct LitOut {
 
 // One complex string, executed by all 64 lanes of a wave with uniform control flow.
 // Scratch: four regions of `cap` bytes at R[0..3] (pool offset `pool_off` of R[0]).
-__device__ LitOut w_literal(const DevTable& T, uint32_t tid, const uint8_t* s, uint64_t n, uint8_t* R0,
+__device__ LitOut w_literal(const DevTable T, uint32_t tid, const uint8_t* s, uint64_t n, uint8_t* R0,
                             uint64_t cap, uint64_t pool_off, bool max_mode) {
-  LitOut r{0, 0, 0, IE_VID_NONE};
+  LitOut r{0, 0, 0, IE_VID_NONE, 0};
   uint8_t* R[4] = {R0, R0 + cap, R0 + 2 * cap, R0 + 3 * cap};
   uint8_t* K = R[2];
   uint8_t* K2 = R[3];
@@ -171,9 +181,10 @@ __device__ LitOut w_literal(const DevTable& T, uint32_t tid, const uint8_t* s, u
   uint32_t W = 0;
   for (;;) {
     if (W > 900) { r.status = IE_DIVERGED; return r; }  // CPython's recursion limit (oracle twin)
-    if (!w_simple(T.dialect, R[0] + cur, clen)) break;
-    cur += 1;
-    clen -= 2;
+    uint64_t l0, ll;
+    if (!w_simple(T.dialect, R[0] + cur, clen, l0, ll)) break;
+    cur += l0;
+    clen -= l0 + ll;
     W++;
   }
   const uint64_t n0 = W ? clen : n;

@@ -1042,6 +1042,7 @@ constexpr uint32_t kUnionLds = kClassEnd > (uint32_t)kRStageBytes + 32 ? kClassE
 // the output stage: all of the union the classification needs anyway (config 2's 256-string
 // tiles average 20.4 KB of output; a 20 KB stage sent a third of them to k_emit_windows)
 constexpr uint32_t kOutStage = (kUnionLds - 32) & ~15u;
+static_assert(4 * kRBlock + 13 * 4 * kRBlock <= kUnionLds, "parked descriptors fit the union");
 static_assert(kKeyCap >= 32 && kMaxDepth <= 8, "evaluator scratch");
 
 // where a tile's strings lie: [lo, hi) for the tile, this lane's string at so (sn bytes)
@@ -1229,17 +1230,15 @@ __device__ __forceinline__ bool recurses(uint8_t st, uint32_t flags) {
   return st == IE_OK_STR || (st == IE_OK_VALUE && (k == IE_KIND_STR || k == IE_KIND_LIST || k == IE_KIND_DICT));
 }
 
-// get_simple_insertkey truthy on the string as written (py:477-495: at least 3 characters, a '{'
-// first and a '}' last that close each other: depth > 0 everywhere in between). Any address space.
-__device__ bool raw_simple(const uint8_t* s, uint32_t n) {
-  if (n < 3 || s[0] != '{' || s[n - 1] != '}') return false;
-  int32_t depth = 1;
-  for (uint32_t k = 1; k + 1 < n; k++) {
-    const uint8_t c = s[k];
-    depth += c == '{' ? 1 : c == '}' ? -1 : 0;
-    if (depth <= 0) return false;
-  }
-  return depth == 1;
+// may the string (as written) be get_simple_insertkey-truthy (py:477-495)? Necessary conditions
+// only: at least 3 bytes, and a '{' first or a '}' right after the first character (the depth must
+// leave 0 at the second character). Any address space.
+__device__ __forceinline__ bool maybe_simple(const uint8_t* s, uint32_t n) {
+  if (n < 3) return false;
+  const uint8_t c0 = s[0];
+  if (c0 == '{') return true;
+  const uint32_t l = c0 < 0x80u ? 1u : (c0 & 0xE0u) == 0xC0u ? 2u : (c0 & 0xF0u) == 0xE0u ? 3u : 4u;
+  return l < n && s[l] == '}';
 }
 
 // The deferred tiles' bytes (see k_resolve): one workgroup per deferred tile at a time. Each
@@ -1365,8 +1364,8 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
   // evaluated from LDS, the rest (a tile of long strings; a views input string placed apart from
   // its tile) from global memory
   const uint32_t nv = pre.nv;
-  const bool lane_staged = so >= lo && shift + (so - lo) + sn <= 16ull * nv;
-  const uint32_t p0 = lane_staged ? shift + (uint32_t)(so - lo) : 0u;
+  const uint32_t p0 = shift + (uint32_t)(so - lo);
+  const bool lane_staged = p0 + sn <= 16ull * nv;
   {
     pre.commit((uint4*)s_in, tid);
     __syncthreads();
@@ -1402,7 +1401,10 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
     bool active = false;
     if (i < B.n) {
       s = lane_staged ? s_in + p0 : B.bytes + so;
-      active = sn < 0xFFFF0000ull;
+      // the unescape command (W.recurse): an item that may be a whole-string '{key}' as written
+      // goes to the literal path, which decides IE_RECURSE with the whole wave (rare: a '{' first,
+      // or a '}' right after the first character)
+      active = sn < 0xFFFF0000ull && !(W.recurse && maybe_simple(s, (uint32_t)sn));
       if (!active) st = kStatusPending;
     }
     uint8_t r = IE_OK_STR;
@@ -1467,10 +1469,6 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
     if (active) st = r;
     pend = i < B.n && st == kStatusPending;
     if (pend) s_pend[atomicAdd(&s_misc[1], 1u)] = (uint16_t)tid;
-    if (W.recurse && active && recurses(st, vflags) && raw_simple(s, (uint32_t)sn)) {
-      if (st == IE_OK_STR) vid = IE_VID_NONE;
-      st = IE_RECURSE;
-    }
     s_st[tid] = st;
     s_olen[tid] = st == IE_OK_STR ? olen : (st == IE_OK_VALUE || st == IE_RECURSE ? vid : 0u);
   }
@@ -1479,7 +1477,19 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
 
   // ---- 3. literal path for the pending strings, one wave each; results in the union ----
   const uint32_t npend = s_misc[1];
-  if (tid == 0 && npend) atomicAdd(W.stats, npend);
+  if (npend) {  // uniform
+  if (tid == 0) atomicAdd(W.stats, npend);
+  // the descriptors wait in the free part of the union while the waves run the literal path (its
+  // registers are what the wave then needs; s_lit uses the union's first 4 * kRBlock bytes)
+  lds_u32* const park = (lds_u32*)(lds_u8*)(s_u + 4 * kRBlock) + tid;
+  park[0] = d.ntop;
+#pragma unroll
+  for (int q = 0; q < kMaxTop; q++) {
+    park[(1 + q) * kRBlock] = d.open[q];
+    park[(4 + q) * kRBlock] = d.close[q];
+    park[(7 + q) * kRBlock] = d.vk[q];
+    park[(10 + q) * kRBlock] = d.vs[q];
+  }
   for (uint32_t k = wave; k < npend; k += kRBlock / 64) {
     const uint32_t j = s_pend[k];
     const uint64_t gi = first + j;
@@ -1500,8 +1510,12 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
                     W.lit_cap_max != 0);
     if (r.status == IE_OK_STR && (r.res_len > kLenMask || (r.res_off >> 4) > 0xFFFFFFFFull))
       r.status = IE_E_OVERFLOW;
+
     if (lane == 0) {
-      if (W.recurse && recurses(r.status, r.flags) && raw_simple(B.bytes + po, (uint32_t)pn)) {
+      uint64_t ko, kl;  // W.recurse: get_simple_insertkey on the item as written (py:1463)
+      const uint8_t* const item = B.bytes + po;
+      if (W.recurse && recurses(r.status, r.flags) &&
+          simple_insertkey([item](uint64_t k) { return item[k]; }, pn, 0u, ko, kl)) {
         if (r.status == IE_OK_STR) r.vid = IE_VID_NONE;
         r.status = IE_RECURSE;
       }
@@ -1509,6 +1523,15 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
       s_olen[j] = r.status == IE_OK_STR ? (uint32_t)r.res_len : (r.status == IE_OK_VALUE || r.status == IE_RECURSE ? r.vid : 0u);
       s_lit[j] = (uint32_t)(r.res_off >> 4);
     }
+  }
+  d.ntop = park[0];
+#pragma unroll
+  for (int q = 0; q < kMaxTop; q++) {
+    d.open[q] = park[(1 + q) * kRBlock];
+    d.close[q] = park[(4 + q) * kRBlock];
+    d.vk[q] = park[(7 + q) * kRBlock];
+    d.vs[q] = park[(10 + q) * kRBlock];
+  }
   }
   __syncthreads();
   IE_STAMP(3);
@@ -1540,18 +1563,19 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
   const bool in_stage = tile_total <= (uint64_t)kOutStage;
   const bool mine = i < B.n && st == IE_OK_STR && olen;
   if (in_stage) {
-    // entry texts of the values (inline, <= kInlineText bytes): into registers first, all in flight
-    uint32_t tt[kMaxTop][8];
-#pragma unroll
-    for (int j = 0; j < kMaxTop; j++) {
+    // entry texts of the values (inline, <= kInlineText bytes): into registers, value j's loads
+    // issued one value ahead of its use
+    uint32_t tt[2][8];
+    auto load_text = [&](int j, uint32_t (&t)[8]) {
       const bool need = mine && (uint32_t)j < d.ntop && (d.vk[j] >> 30) == kValEntry;
       if (__any(need)) {
         const uint4* tp = (const uint4*)(T.entries + (need ? d.vs[j] : 0u)) + 2;
         const uint4 t2 = gld4(tp), t3 = gld4(tp + 1);
-        tt[j][0] = t2.x, tt[j][1] = t2.y, tt[j][2] = t2.z, tt[j][3] = t2.w;
-        tt[j][4] = t3.x, tt[j][5] = t3.y, tt[j][6] = t3.z, tt[j][7] = 0;
+        t[0] = t2.x, t[1] = t2.y, t[2] = t2.z, t[3] = t2.w;
+        t[4] = t3.x, t[5] = t3.y, t[6] = t3.z, t[7] = 0;
       }
-    }
+    };
+    load_text(0, tt[0]);
     lds_u8* const dd = (lds_u8*)(s_u + (mine ? local : 0));
     const lds_u8* const ls = (const lds_u8*)s;
     const uint32_t ntop = mine ? d.ntop : 0u;
@@ -1570,10 +1594,11 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
       w += tl;
       if (j == kMaxTop) break;
       // value j
+      if (j + 1 < kMaxTop) load_text(j + 1, tt[(j + 1) & 1]);
       const bool von = mine && (uint32_t)j < ntop;
       const uint32_t kind = d.vk[j] >> 30, len = von ? d.vk[j] & kLenMask : 0u;
       const bool ent = von && kind == kValEntry;
-      if (__any(ent) && ent) put_words(dd + w, tt[j], len);
+      if (__any(ent) && ent) put_words(dd + w, tt[j & 1], len);
       const bool far = von && kind != kValEntry;  // an arena or literal-pool text
       if (__any(far))
         stage_piece((lds_u8*)s_u, far, (uint32_t)(mine ? local : 0) + w,

@@ -124,6 +124,7 @@ def named_table():
         "{b}": "braced-key", "5": "five", "B": "bee", "K": "kay", "Why?": "because",
         "tom": "{name}", "loop": "{loop}", "grow": "{grow}{grow}", "aa": "{b}{b}",
         "nest": "{a}", "self": "x{self}", "\\{x\\}": "escaped-key", "x\\{": "xesc",
+        "}n{": "NEGKEY", "}{": "braces-key",
     }
 
 
@@ -151,6 +152,10 @@ def named_cases():
         "x\\\\{k}", "x\\\\\\{k}", "\\\\\\\\", "é{k}é", "😀{u}😀", "{k}\n{k}", "〠", ".〠",
         "〠.", "{k}.〠", "〠.{k}", "x{k}〠y", "a.\\{b", "a\\}.b", "\\{.\\}", "\\}.\\{",
         "x{dot}{cl}", "{dot}{cl}", "x{k}\\}\\}", "x\\}{k}", "{k}{bsb}", "{bsb}",
+        # get_simple_insertkey has no brace test at the edges (py:485-495): the depth may dip below
+        # 0 and come back at the last character, so these are whole-string forms too
+        "a}n{b", "a}b{c", "k}{\\", "é}n{é", "😀}n{😀", "a}{b", "x}{y}{z", "a}n{", "}n{b", "a}}n{{b",
+        "a}{k}{b", "é}{é", "a}n{{k}", "a}\\{n{b",
     ]
     return c
 
