@@ -22,9 +22,11 @@ from .interpolation_engine import (  # noqa: F401
     interpolate_states,
     recursive_escape,
     recursive_interpolate,
+    recursive_interpolate_states,
     recursive_unescape,
     unescape_command,
 )
+from .maps import goto_map, goto_map_states, replace_map, replace_map_states  # noqa: F401
 from .multi import MultiDevice, shard_bounds  # noqa: F401
 from .wildcard import Wildcards, get_wildcard_matches, is_wildcard_match  # noqa: F401
 

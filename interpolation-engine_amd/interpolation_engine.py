@@ -543,48 +543,111 @@ def recursive_interpolate(inserts, x, _depth=0):
     """py:1462-1494 with every string leaf of `x` resolved in one device batch."""
     if _depth > 900:
         raise RecursionError("maximum recursion depth exceeded in recursive_interpolate")
-    tbl = table_for(inserts)
-    leaves = []
+    r = recursive_interpolate_states([inserts], [x], tables=_OneTable(inserts), _depth=_depth)[0]
+    if isinstance(r, BaseException):
+        raise r
+    return r
 
-    def collect(v):
-        if type(v) == str:
-            leaves.append(v)
-        elif type(v) == list:
-            for xx in v:
-                collect(xx)
-        elif type(v) == dict:
-            if v.get("cmd") in ("goto_map", "replace_map") or v.get("cmd") in _LOOP_CMDS:
-                return
-            for k, vv in v.items():
-                collect(k)
-                collect(vv)
 
-    collect(x)
-    res = iter(tbl.results(leaves) if leaves else [])
+class _OneTable:
+    """table_for(inserts) in the shape recursive_interpolate_states uses (one dict, cached)."""
 
-    def rebuild(v):
-        if type(v) == str:
-            r = next(res)
-            if isinstance(r, BaseException):
-                raise r
-            if get_simple_insertkey(v):  # py:1463-1464: re-interpolate the typed result
-                return recursive_interpolate(inserts, r, _depth + 1)
-            return r
-        if type(v) == list:
-            return [rebuild(xx) for xx in v]
-        if type(v) == dict:
-            cmd = v.get("cmd")
-            if cmd in ("goto_map", "replace_map"):  # py:1471-1477
-                return v
-            if cmd in _LOOP_CMDS:  # py:1479-1489
-                v = copy.deepcopy(v)
-                if (k := get_simple_insertkey(v["tasks"])):
-                    v["tasks"] = get_interpdata(inserts, k)
-                for i in range(len(v["tasks"])):
-                    if (k := get_simple_insertkey(v["tasks"][i])):
-                        v["tasks"][i] = get_interpdata(inserts, k)
-                return v
-            return {rebuild(k): rebuild(vv) for k, vv in v.items()}
-        return v
+    def __init__(self, inserts):
+        self.t = table_for(inserts)
 
-    return rebuild(x)
+    def results(self, strings, ids):
+        return self.t.results(strings)
+
+
+def recursive_interpolate_states(states, xs, dialect="py", device=0, tables=None, clock=None, _depth=0):
+    """recursive_interpolate (py:1462-1494) of many (state, value) pairs at once: xs[i] is walked
+    against states[i] (forked interpreter states, each with its own inserts dict: config 5, the
+    per-task pre-pass py:1501 of every state in ONE device batch over a table set; the Rust
+    runtime clones the whole map per task instead, rust-project/src/runtime.rs:700-701). Every
+    string leaf of every tree goes into the batch; whole-string leaves whose typed result the
+    reference walks again (py:1463-1464) go into the next batch. Returns one result per pair, or
+    the exception the reference would raise first in that tree's traversal order."""
+    n = len(states)
+    if len(xs) != n:
+        raise ValueError("one value per state")
+    own = tables is None
+    if own:
+        tables = InsertsTableSet(states, dialect=dialect, clock=clock, device=device)
+    try:
+        leaves, ids = [], []
+        skels = [None] * n
+        fails = [None] * n
+        for i in range(n):
+            try:
+                skels[i] = _tree_leaves(states[i], xs[i], leaves, ids, i)
+            except (InterpolationException, AssertionError, TypeError, KeyError) as e:
+                fails[i] = e  # the loop-command branch's get_interpdata (py:1483-1488)
+        res = tables.results(leaves, ids) if leaves else []
+    finally:
+        if own:
+            tables.close()
+    # leaves whose result the reference walks again (py:1463-1464): the next batch
+    again = [k for k, leaf in enumerate(leaves) if not isinstance(res[k], BaseException) and get_simple_insertkey(leaf)]
+    if again:
+        if _depth > 900:
+            for k in again:
+                res[k] = RecursionError("maximum recursion depth exceeded in recursive_interpolate")
+        else:
+            sub = recursive_interpolate_states([states[ids[k]] for k in again], [res[k] for k in again], dialect,
+                                               device, None, clock, _depth + 1)
+            for k, r in zip(again, sub):
+                res[k] = r
+    out = []
+    for i in range(n):
+        if fails[i] is not None:
+            out.append(fails[i])
+            continue
+        try:
+            out.append(_tree_rebuild(skels[i], res))
+        except BaseException as e:  # noqa: BLE001 — the first failing leaf in traversal order
+            out.append(e)
+    return out
+
+
+_LEAF = "__ie_leaf__"
+
+
+def _tree_leaves(inserts, v, leaves, ids, i):
+    """The walk of py:1462-1494 without the string work: a skeleton whose str leaves point into
+    `leaves` (goto_map / replace_map dicts are kept as they are, py:1471-1477; loop commands get
+    their simple `tasks` entries from get_interpdata, py:1479-1489, on the host)."""
+    if type(v) == str:
+        leaves.append(v)
+        ids.append(i)
+        return (_LEAF, len(leaves) - 1)
+    if type(v) == list:
+        return [_tree_leaves(inserts, xx, leaves, ids, i) for xx in v]
+    if type(v) == dict:
+        cmd = v.get("cmd")
+        if cmd in ("goto_map", "replace_map"):  # py:1471-1477
+            return (_LEAF + "const", v)
+        if cmd in _LOOP_CMDS:  # py:1479-1489
+            v = copy.deepcopy(v)
+            if (k := get_simple_insertkey(v["tasks"])):
+                v["tasks"] = get_interpdata(inserts, k)
+            for j in range(len(v["tasks"])):
+                if (k := get_simple_insertkey(v["tasks"][j])):
+                    v["tasks"][j] = get_interpdata(inserts, k)
+            return (_LEAF + "const", v)
+        return (_LEAF + "dict", [(_tree_leaves(inserts, k, leaves, ids, i), _tree_leaves(inserts, vv, leaves, ids, i))
+                                 for k, vv in v.items()])
+    return (_LEAF + "const", v)
+
+
+def _tree_rebuild(skel, res):
+    if type(skel) == list:
+        return [_tree_rebuild(x, res) for x in skel]
+    tag, val = skel
+    if tag == _LEAF:
+        r = res[val]
+        if isinstance(r, BaseException):
+            raise r
+        return r
+    if tag == _LEAF + "dict":
+        return {_tree_rebuild(k, res): _tree_rebuild(vv, res) for k, vv in val}
+    return val

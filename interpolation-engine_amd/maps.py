@@ -1,0 +1,310 @@
+"""goto_map and replace_map over batches of interpreter states, on the device.
+
+The reference runs these two commands one string at a time (py:1689-1773): every interpolation
+is an interpolate_inserts call, every wildcard test a Python regex. Here one state or many
+forked states are advanced together: each step of the reference's loop is ONE device batch over
+every state still running it (interpolations on a table set with one inserts dict per state,
+k_resolve; wildcard first-match with captures, k_wildcard), so a task costs a handful of launches
+whatever the number of states.
+
+  goto_map(inserts, task)              py:1689-1711 for one state (returns what execute_task
+                                       returns: {'goto_target': t} or None)
+  replace_map(inserts, task)           py:1713-1773 for one state (sets inserts[output_name])
+  goto_map_states(states, task)        the same over many states: a list of results, an
+  replace_map_states(states, task)     exception instance where the reference would raise
+
+Semantics kept from the reference, step by step:
+  goto_map    the text is interpolated first and only InterpolationException is caught
+              (py:1692-1696); then every key and every value is interpolated and str()-ed
+              (py:1698-1699, errors propagate); on an interpolation error the 'NULL' key's value
+              is the target (py:1702-1705), else the first key that wildcard-matches the text.
+  replace_map output_name is interpolated (py:1715); recursive_replace walks the item, resolving
+              whole-string keys with get_interpdata (py:1749-1754); each string runs replace_str:
+              interpolate, then the first map whose interpolated key matches (keys in order: a
+              key that fails to interpolate before any match raises), captures bound as '1', '2',
+              ... in `inserts | extra_inserts` to interpolate the value, repeated until nothing
+              changes when repeat_until_done (py:1720-1745); an InterpolationException anywhere
+              sets the raw 'NULL' value instead (py:1761-1771), or fails the task's assertion.
+Known difference: the reference re-interpolates the map keys on every pass of its loop; the
+inserts cannot change inside the command, so the keys are interpolated once per state (only a
+clock key read in a key could differ between passes).
+"""
+import copy
+
+from . import interpolation_engine as IE
+from .wildcard import Wildcards
+
+# a loop that never reaches a fixed point (the reference spins forever): stop and raise
+MAX_PASSES = 100000
+
+
+def _first_key(d):
+    return next(iter(d.keys()))
+
+
+def _first_value(d):
+    return next(iter(d.values()))
+
+
+def _str_results(tset, strings, ids):
+    """interpolate_inserts on the device, then str() (py:1692, 1698-1699, 1722, 1738)."""
+    if not strings:
+        return []
+    return [r if isinstance(r, BaseException) else str(r) for r in tset.results(strings, ids)]
+
+
+# ------------------------------------------------------------------------------------------
+# goto_map (py:1689-1711)
+# ------------------------------------------------------------------------------------------
+def goto_map_states(states, task, dialect="py", device=0):
+    """goto_map for each state: [{'goto_target': t} | None | exception instance]."""
+    maps = task["target_maps"]
+    n, m = len(states), len(maps)
+    out = [None] * n
+    if n == 0:
+        return out
+    tset = IE.InsertsTableSet(states, dialect=dialect, device=device)
+    try:
+        # value text, then all keys, then all values, for every state in one batch
+        strings, ids = [], []
+        for s in range(n):
+            strings.append(task["text"])
+            strings.extend(_first_key(d) for d in maps)
+            strings.extend(_first_value(d) for d in maps)
+            ids.extend([s] * (1 + 2 * m))
+        res = _str_results(tset, strings, ids)
+    finally:
+        tset.close()
+    texts, keys, vals = [], [], []
+    for s in range(n):
+        r = res[s * (1 + 2 * m):(s + 1) * (1 + 2 * m)]
+        texts.append(r[0])
+        keys.append(r[1:1 + m])
+        vals.append(r[1 + m:])
+    # every matching test of every state in one launch: state s tries keys [s*m, (s+1)*m)
+    pending, pats, ranges = [], [], []
+    for s in range(n):
+        t = texts[s]
+        if isinstance(t, BaseException) and not isinstance(t, IE.InterpolationException):
+            out[s] = t  # py:1693 catches InterpolationException only
+            continue
+        bad = next((x for x in keys[s] + vals[s] if isinstance(x, BaseException)), None)
+        if bad is not None:  # py:1698-1699 propagate
+            out[s] = bad
+            continue
+        if isinstance(t, IE.InterpolationException):  # py:1702-1705
+            if "NULL" not in keys[s]:
+                out[s] = AssertionError("Order Index %s: value text '%s' could not be resolved but 'NULL' is not "
+                                        "a key in target_maps." % (task.get("traceback_label"), task["text"]))
+                continue
+            target = vals[s][keys[s].index("NULL")]
+            out[s] = {"goto_target": target} if target != "CONTINUE" else None
+            continue
+        pending.append(s)
+        ranges.append((len(pats), len(pats) + m))
+        pats.extend(keys[s])
+    if pending:
+        w = Wildcards(pats, device=device, dialect=dialect)
+        try:
+            found = w.first_match([texts[s] for s in pending], ranges)
+        finally:
+            w.close()
+        for s, (r, (p, _)) in zip(pending, zip(ranges, found)):
+            if p < 0:  # py:1708
+                out[s] = AssertionError("Order Index %s: goto_map has no matches for '%s'."
+                                        % (task.get("traceback_label"), texts[s]))
+                continue
+            target = vals[s][p - r[0]]
+            out[s] = {"goto_target": target} if target != "CONTINUE" else None
+    return out
+
+
+def goto_map(inserts, task):
+    """py:1689-1711 for one state: {'goto_target': t} or None; raises where the reference raises."""
+    r = goto_map_states([inserts], task)[0]
+    if isinstance(r, BaseException):
+        raise r
+    return r
+
+
+# ------------------------------------------------------------------------------------------
+# replace_map (py:1713-1773)
+# ------------------------------------------------------------------------------------------
+class _Fail(Exception):
+    def __init__(self, exc):
+        super().__init__(repr(exc))
+        self.exc = exc
+
+
+def _leaves(inserts, x, out):
+    """recursive_replace's walk (py:1748-1759) without the string work: whole-string keys are
+    resolved with get_interpdata on the host (py:1749-1754); returns a skeleton whose str leaves
+    are indices into `out` (the strings replace_str must run on)."""
+    k = IE.get_simple_insertkey(x)
+    if k:
+        sub = IE.get_simple_insertkey(k)
+        if sub:
+            return _leaves(inserts, IE.insert_start + IE.get_interpdata(inserts, sub) + IE.insert_stop, out)
+        return _leaves(inserts, IE.get_interpdata(inserts, k), out)
+    if type(x) == str:
+        out.append(x)
+        return ("__leaf__", len(out) - 1)
+    if type(x) == list:
+        return [_leaves(inserts, xx, out) for xx in x]
+    if type(x) == dict:
+        return {("__key__", _leaves(inserts, xk, out)): _leaves(inserts, xv, out) for xk, xv in x.items()}
+    return x
+
+
+def _rebuild(skel, done):
+    if type(skel) == tuple and len(skel) == 2 and skel[0] == "__leaf__":
+        return done[skel[1]]
+    if type(skel) == list:
+        return [_rebuild(x, done) for x in skel]
+    if type(skel) == dict:
+        return {_rebuild(k[1], done): _rebuild(v, done) for k, v in skel.items()}
+    return skel
+
+
+def replace_map_states(states, task, dialect="py", device=0):
+    """replace_map for each state: [(output_name, value) | exception instance]. The caller
+    stores value under output_name (set_interpdata, py:1771-1773); nothing is mutated here."""
+    maps = task["wildcard_maps"]
+    n, m = len(states), len(maps)
+    repeat = task.get("repeat_until_done", False)
+    out = [None] * n
+    if n == 0:
+        return out
+    no_value = object()
+    value_if_error = ([_first_value(d) for d in maps if _first_key(d) == "NULL"] + [no_value])[0]  # py:1761
+    tset = IE.InsertsTableSet(states, dialect=dialect, device=device)
+    try:
+        names = tset.results([task["output_name"]] * n, list(range(n)))  # py:1715 (no str(): as the reference)
+        keys = _str_results(tset, [_first_key(d) for d in maps] * n, [s for s in range(n) for _ in range(m)])
+        # the leaves of every state's item (host walk; a get_interpdata error fails that state)
+        skels, leaves, owner = [None] * n, [], []
+        for s in range(n):
+            if isinstance(names[s], BaseException):
+                out[s] = names[s]
+                continue
+            mine = []
+            try:
+                skels[s] = _leaves(states[s], task["item"], mine)
+            except (IE.InterpolationException, AssertionError, TypeError) as e:
+                out[s] = e
+                continue
+            skels[s] = (skels[s], len(leaves))
+            leaves.extend(mine)
+            owner.extend([s] * len(mine))
+        done, err = _replace_strings(tset, states, leaves, owner, keys, maps, m, repeat, dialect, device)
+    finally:
+        tset.close()
+    # per state: the first failing leaf in the reference's traversal order decides (py:1763-1771)
+    for s in range(n):
+        if out[s] is not None:
+            e = out[s]
+        else:
+            skel, base = skels[s]
+            cnt = sum(1 for o in owner if o == s)
+            e = next((err[base + k] for k in range(cnt) if err[base + k] is not None), None)
+        if e is None:
+            out[s] = (names[s], _rebuild(skels[s][0], done[skels[s][1]:]))
+        elif isinstance(e, IE.InterpolationException):
+            if value_if_error is no_value:  # py:1765-1766
+                out[s] = AssertionError("%s: replace_map encountered an interpolation error without 'NULL' key: %r"
+                                        % (task.get("traceback_label"), e))
+            elif isinstance(names[s], BaseException):
+                out[s] = names[s]
+            else:
+                out[s] = (names[s], copy.deepcopy(value_if_error))
+        else:
+            out[s] = e
+    return out
+
+
+def _replace_strings(tset, states, leaves, owner, keys, maps, m, repeat, dialect, device):
+    """replace_str (py:1720-1745) on every leaf at once: (results, first error per leaf)."""
+    L = len(leaves)
+    cur = list(leaves)
+    last = list(leaves)
+    err = [None] * L
+    active = list(range(L))
+    vals_raw = [_first_value(d) for d in maps]
+    # per state: the keys before the first key that failed to interpolate (later keys are never
+    # tried once one fails: the failure propagates) and that failure
+    key_ok, key_err = {}, {}
+    for s in set(owner):
+        ks = keys[s * m:(s + 1) * m]
+        f = next((j for j, k in enumerate(ks) if isinstance(k, BaseException)), m)
+        key_ok[s] = f
+        key_err[s] = ks[f] if f < m else None
+    passes = 0
+    while active:
+        passes += 1
+        if passes > MAX_PASSES:
+            for i in active:
+                err[i] = RecursionError("replace_map does not reach a fixed point")
+            break
+        # 1. interpolate (py:1722)
+        res = _str_results(tset, [cur[i] for i in active], [owner[i] for i in active])
+        alive = []
+        for i, r in zip(active, res):
+            if isinstance(r, BaseException):
+                err[i] = r
+            else:
+                cur[i] = r
+                alive.append(i)
+        # 2. the first map whose key matches (py:1725-1735), all leaves in one launch
+        pats, ranges, tried = [], [], []
+        for i in alive:
+            s = owner[i]
+            ranges.append((len(pats), len(pats) + key_ok[s]))
+            pats.extend(keys[s * m:s * m + key_ok[s]])
+            tried.append(i)
+        hits = []
+        if pats:
+            w = Wildcards(pats, device=device, dialect=dialect)
+            try:
+                found = w.first_match([cur[i] for i in tried], ranges)
+            finally:
+                w.close()
+        else:
+            found = [(-1, [])] * len(tried)
+        for i, r, (p, caps) in zip(tried, ranges, found):
+            if p >= 0:
+                hits.append((i, p - r[0], caps))
+            elif key_err[owner[i]] is not None:  # a key failed before anything matched
+                err[i] = key_err[owner[i]]
+        # 3. the matched maps' values against inserts | captures (py:1736-1738), one table per leaf
+        if hits:
+            dicts = [dict(states[owner[i]], **{str(k + 1): c for k, c in enumerate(caps)}) for i, _, caps in hits]
+            xs = IE.InsertsTableSet(dicts, dialect=dialect, device=device)
+            try:
+                vres = _str_results(xs, [vals_raw[p] for _, p, _ in hits], list(range(len(hits))))
+            finally:
+                xs.close()
+            for (i, _, _), v in zip(hits, vres):
+                if isinstance(v, BaseException):
+                    err[i] = v
+                else:
+                    cur[i] = v
+        # 4. a fixed point, or one pass without repeat_until_done (py:1742-1745)
+        nxt = []
+        for i in alive:
+            if err[i] is not None:
+                continue
+            if last[i] == cur[i] or not repeat:
+                continue
+            last[i] = cur[i]
+            nxt.append(i)
+        active = nxt
+    return cur, err
+
+
+def replace_map(inserts, task):
+    """py:1713-1773 for one state: stores the result under the interpolated output_name."""
+    r = replace_map_states([inserts], task)[0]
+    if isinstance(r, BaseException):
+        raise r
+    name, value = r
+    inserts[name] = value  # set_interpdata (py:470-471)

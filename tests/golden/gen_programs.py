@@ -15,6 +15,9 @@ Writes (JSON data only, no reference source):
                        add_line_numbers on edge-case texts
   config1_py.json      examples/hello_world.json5 run to the end: every top-level
                        interpolate_inserts call (content -> result), final state, printed text
+  config5_trees.json   the same replay's per-task pre-pass (recursive_interpolate py:1501, and
+                       the unescape command's py:1666) of the first 12 states: task tree in,
+                       inserts version, tree out (or the error class)
   config5_stream.json  examples/text_adventure.json5 replayed from label '@loop' to the first
                        `chat` for STATES synthetic states: every top-level interpolate_inserts
                        call with the caller (the per-task pre-pass py:1501, or replace_map /
@@ -150,6 +153,37 @@ class Recorder:
         return rec["out"]
 
 
+class TreeRecorder:
+    """Wraps the module-global recursive_interpolate: records the depth-0 calls (the per-task
+    pre-pass py:1501 and the unescape command's py:1666) with the task tree passed in, the inserts
+    version the call saw (shared with the Recorder) and the tree the reference returned."""
+
+    def __init__(self, ie, orig, rec):
+        self.ie, self.orig, self.rec = ie, orig, rec
+        self.depth = 0
+        self.trees = []
+
+    def __call__(self, inserts, x):
+        if self.depth:
+            return self.orig(inserts, x)
+        caller = sys._getframe(1).f_code.co_name
+        v = self.rec.version_of(inserts)
+        tree = json.loads(json.dumps(x, ensure_ascii=False))
+        self.depth += 1
+        try:
+            r = self.orig(inserts, x)
+        except self.ie.InterpolationException:
+            self.trees.append({"v": v, "by": caller, "x": tree, "st": "E_INTERP"})
+            raise
+        except AssertionError:
+            self.trees.append({"v": v, "by": caller, "x": tree, "st": "E_ASSERT"})
+            raise
+        finally:
+            self.depth -= 1
+        self.trees.append({"v": v, "by": caller, "x": tree, "st": "OK", "out": json.loads(json.dumps(r, ensure_ascii=False))})
+        return r
+
+
 async def drive(ie, program, state, stop_at_chat=True, max_tasks=400):
     completion_args = program.get("completion_args", {})
     named = program.get("named_tasks", {})
@@ -213,6 +247,8 @@ def main():
     defaults = copy.deepcopy(state0["inserts"])
     loop_at = 1 + next(i for i, t in enumerate(program0["order"]) if t["cmd"] == "label" and t["name"] == "@loop")
     out = {"defaults": defaults, "clock": CLOCK, "states": []}
+    trees = {"clock": CLOCK, "states": []}
+    orig_ri = ie.recursive_interpolate
     total = 0
     for j in range(args.states):
         syn = W.state_inserts(defaults, j, max_entries=8 if j < args.states - 4 else 36)  # 4 long-history states
@@ -222,17 +258,25 @@ def main():
         program = copy.deepcopy(program0)
         rec = Recorder(ie, orig)
         ie.interpolate_inserts = rec
+        tr = TreeRecorder(ie, orig_ri, rec)
+        ie.recursive_interpolate = tr
         install_fakes(ie, [syn["new_user_input"], "look around"])
         try:
             asyncio.run(drive(ie, program, state))
             raise RuntimeError("no chat reached")
         except StopReplay:
             pass
+        ie.recursive_interpolate = orig_ri
         out["states"].append({"stage": syn["stage"], "deltas": rec.deltas, "calls": rec.calls})
+        if j < 12:  # the per-task pre-pass trees of the first 12 states (file size)
+            trees["states"].append({"stage": syn["stage"], "deltas": rec.deltas, "trees": tr.trees})
         total += len(rec.calls)
     ie.interpolate_inserts = orig
     with open(os.path.join(HERE, "config5_stream.json"), "w", encoding="utf-8") as fh:
         json.dump(out, fh, ensure_ascii=False, separators=(",", ":"))
+    with open(os.path.join(HERE, "config5_trees.json"), "w", encoding="utf-8") as fh:
+        json.dump(trees, fh, ensure_ascii=False, separators=(",", ":"))
+    print("config 5 trees: %d bytes" % os.path.getsize(os.path.join(HERE, "config5_trees.json")))
     print("config 5: %d states, %d calls, %d bytes" % (args.states, total,
                                                       os.path.getsize(os.path.join(HERE, "config5_stream.json"))))
 

@@ -1,0 +1,95 @@
+"""goto_map / replace_map (py:1689-1773) over batches of forked states on the device, against the
+reference's own execute_task run on the same states (tests/golden/gen_maps.py -> maps_py.json):
+every goto_map and replace_map task of examples/text_adventure.json5, applied in program order to
+240 synthetic states (both history replace_maps with repeat_until_done, the suggestion maps with
+captures and 'NULL', every goto_map). One device batch per task over all states."""
+import pytest
+
+import __graft_entry__ as G
+from tests.conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+G.build()
+PKG = G.load_package()
+from interpolation_engine_amd import maps as M  # noqa: E402
+from interpolation_engine_amd import workloads as W  # noqa: E402
+
+INPUTS = ["1", "2", "3", "/undo", "/restart", "look around", "", "go {north}", None]
+OUTPUTS = ["(unset)", "You see a door.", None]
+
+
+def make_state(defaults, j):
+    """tests/golden/gen_maps.py make_state (the same deterministic states)."""
+    ins = W.state_inserts(defaults, j, max_entries=12)
+    v = {"new_user_input": INPUTS[j % len(INPUTS)], "output": OUTPUTS[(j // 3) % len(OUTPUTS)],
+         "enable_suggestions": "true" if (j // 2) % 2 else "false", "suggestions": (j // 5) % 2 == 0}
+    for k in ("new_user_input", "output"):
+        if v[k] is None:
+            ins.pop(k, None)
+        else:
+            ins[k] = v[k]
+    ins.pop("maybe_input", None)
+    ins["enable_suggestions"] = v["enable_suggestions"]
+    if v["suggestions"]:
+        ins.update({"suggestion_1": "open the gate", "suggestion_2": "ask the {guard}", "suggestion_3": "wait"})
+    n = len(ins["history_list"])
+    ins.update({"isodd": n % 2, "length_history": n if j % 7 else 0, "should_summarize": (j % 3) - 1,
+                "summarize_ok": (j % 5 > 1) - (j % 5 == 0)})
+    return ins
+
+
+def fnv(s):
+    h = 0xCBF29CE484222325
+    for b in s.encode("utf-8", "surrogatepass"):
+        h = ((h ^ b) * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def _check(want, got):
+    if "err" in want:
+        return isinstance(got, BaseException) and type(got).__name__ == want["err"]
+    if isinstance(got, BaseException):
+        return False
+    if "goto" in want:
+        return (got["goto_target"] if got else None) == want["goto"]
+    name, value = got
+    if want["set"][0] != name:
+        return False
+    if "fnv" in want:
+        return isinstance(value, str) and len(value) == want["len"] and fnv(value) == want["fnv"]
+    return value == want["set"][1] and type(value) == type(want["set"][1])
+
+
+def test_text_adventure_maps_match_reference():
+    g = load_golden("maps_py.json")
+    states = [make_state(g["defaults"], j) for j in range(g["states"])]
+    bad = []
+    for k, task in enumerate(g["tasks"]):
+        fn = M.goto_map_states if task["cmd"] == "goto_map" else M.replace_map_states
+        got = fn(states, task)
+        for j, r in enumerate(got):
+            if not _check(g["results"][j][k], r):
+                bad.append((k, task["cmd"], task.get("text", task.get("item")), j, g["results"][j][k],
+                            repr(r)[:200]))
+            if task["cmd"] == "replace_map" and not isinstance(r, BaseException):
+                states[j][r[0]] = r[1]  # set_interpdata: the later tasks see it
+    assert not bad, (len(bad), bad[:6])
+
+
+def test_single_state_entry_points():
+    """goto_map / replace_map for one state (the reference's call regime) agree with the batch."""
+    g = load_golden("maps_py.json")
+    ins = make_state(g["defaults"], 1)
+    for k, task in enumerate(g["tasks"][:8]):
+        want = g["results"][1][k]
+        if task["cmd"] == "goto_map":
+            if "err" in want:
+                with pytest.raises(AssertionError):
+                    M.goto_map(ins, task)
+            else:
+                r = M.goto_map(ins, task)
+                assert (r["goto_target"] if r else None) == want["goto"]
+        elif "err" not in want:
+            M.replace_map(ins, task)
+            assert _check(want, (want["set"][0], ins[want["set"][0]]))

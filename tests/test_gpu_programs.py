@@ -87,3 +87,30 @@ def fail_commit(request, monkeypatch):
     PKG.interpolation_engine.get_exec(0).set_option(N.OPT_FAIL_COMMIT, int(request.param))
     yield request.param
     PKG.interpolation_engine.get_exec(0).set_option(N.OPT_FAIL_COMMIT, -1)
+
+
+def test_config5_prepass_trees_of_all_states_in_one_batch():
+    """The per-task pre-pass (recursive_interpolate, py:1501) of every recorded state of the
+    text_adventure loop, tree for tree against what the reference returned (gen_programs.py ->
+    config5_trees.json), all states' trees in ONE device batch (recursive_interpolate_states)."""
+    g = load_golden("config5_trees.json")
+    states, xs, want = [], [], []
+    for st in g["states"]:
+        vs = rebuild_versions(st["deltas"])
+        for t in st["trees"]:
+            states.append(vs[t["v"]])
+            xs.append(t["x"])
+            want.append(t)
+    got = PKG.recursive_interpolate_states(states, xs, clock=tuple(g["clock"]))
+    bad = []
+    for w, r in zip(want, got):
+        if w["st"] == "OK":
+            ok = not isinstance(r, BaseException) and r == w["out"]
+        elif w["st"] == "E_INTERP":
+            ok = isinstance(r, PKG.InterpolationException)
+        else:
+            ok = isinstance(r, AssertionError)
+        if not ok:
+            bad.append((w["x"], w["st"], repr(r)[:200]))
+    assert not bad, (len(bad), bad[:3])
+    assert len(want) >= 200
