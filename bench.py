@@ -7,9 +7,11 @@ One step = one pass of the hot path over one batch of synthetic strings already 
   config 4: 12.5M strings per GPU (the 100M batch over 8), mixed-depth chains, escapes,
             brace-bearing values, misses; step = interpolate, then the `unescape` command
             (recursive_unescape + recursive_interpolate, py:1660-1667) on the results
-  config 5: text_adventure.json5 forked states (10k per GPU): the per-iteration pre-pass stream
-            recorded from the reference (tests/golden/config5_stream.json) against one inserts
-            dict per state, all states in one table set, a table id per string
+  config 5: text_adventure.json5 forked states (10k per GPU): per state every string one loop
+            iteration interpolates (the pre-pass of every executed task tree and the goto_map /
+            replace_map first-round strings, from the reference-recorded trees in
+            tests/golden/config5_trees.json) against one inserts dict per state, all states in
+            one table set, a table id per string
 Multi-GPU: one process per GPU, each resolving its own shard (weak scaling; the table is built
 per rank, no data-path collective — only the barrier and the max-over-ranks time go over
 torch.distributed, gloo on the host).
@@ -41,8 +43,9 @@ WORKLOADS = {
     4: "cfg4: 12.5M strings/GPU (100M over 8), 48-80 B, 1-2 chain refs of depth 1-4 (40/30/20/10 %), "
        "10 % \\{lit\\} escapes, 2 % brace-bearing values, 1 % missing keys, 100k-entry inserts; "
        "step = interpolate + the unescape command (unescape, interpolate again)",
-    5: "cfg5: text_adventure.json5 agent-loop states (10k/GPU), the recorded per-iteration pre-pass "
-       "stream per state, one inserts dict per state in one table set",
+    5: "cfg5: text_adventure.json5 agent-loop states (10k/GPU), per state every string one loop iteration "
+       "interpolates against its dict (the pre-pass of every executed task tree + the goto_map/replace_map "
+       "first-round strings, ~180), one inserts dict per state in one table set",
 }
 DEFAULT_N = {2: 1_000_000, 3: 10_000_000, 4: 12_500_000, 5: 10_000}  # strings (configs 2-4) / states (5)
 
@@ -140,19 +143,39 @@ class Synth:
         self.L.ie_synth_free(self.synth)
 
 
+def iteration_strings(trees):
+    """Every string one text_adventure loop iteration interpolates against the state's dict: the
+    per-task pre-pass of every executed task tree (recursive_interpolate, py:1501: every str leaf,
+    goto_map / replace_map kept whole, py:1471-1477) and the first-round strings of the executed
+    goto_map (text, keys, values: py:1692-1699) and replace_map tasks (output_name, item, keys:
+    py:1715-1735). The trees are the reference's own (tests/golden/config5_trees.json)."""
+    from interpolation_engine_amd import interpolation_engine as IE
+    leaves, ids = [], []
+    for x in trees:
+        IE._tree_leaves({}, x, leaves, ids, 0)
+        if x.get("cmd") == "goto_map":
+            maps = x["target_maps"]
+            leaves += [x["text"]] + [next(iter(d)) for d in maps] + [next(iter(d.values())) for d in maps]
+        elif x.get("cmd") == "replace_map":
+            leaves += [x["output_name"], x["item"]] + [next(iter(d)) for d in x["wildcard_maps"]]
+    return leaves
+
+
 class States:
     """Config 5: one inserts dict per agent-loop state (interpolation-engine_amd/workloads.py) in
-    one table set, and per state the pre-pass strings the reference resolved in one loop
-    iteration with that stage (recorded, tests/golden/config5_stream.json)."""
+    one table set, and per state every string one loop iteration with that stage interpolates
+    (iteration_strings over the reference-recorded task trees, ~180 per state)."""
 
     def __init__(self, N, L, x, pkg, first, n, dev):
         from interpolation_engine_amd import workloads as Wk
-        c5 = json.load(open(os.path.join(ROOT, "tests", "golden", "config5_stream.json"), encoding="utf-8"))
+        c5 = json.load(open(os.path.join(ROOT, "tests", "golden", "config5_trees.json"), encoding="utf-8"))
+        defaults = json.load(open(os.path.join(ROOT, "tests", "golden", "config5_stream.json"),
+                                  encoding="utf-8"))["defaults"]
         self.stream = {}
-        for st in c5["states"]:  # the pre-pass templates of the first recorded state of each stage
+        for st in c5["states"]:  # the executed tasks of the first recorded state of each stage
             if st["stage"] not in self.stream:
-                self.stream[st["stage"]] = [c["s"] for c in st["calls"] if c["by"] == "recursive_interpolate"]
-        self.states = [Wk.state_inserts(c5["defaults"], first + j) for j in range(n)]
+                self.stream[st["stage"]] = iteration_strings([t["x"] for t in st["trees"]])
+        self.states = [Wk.state_inserts(defaults, first + j) for j in range(n)]
         strings, ids = [], []
         for j, ins in enumerate(self.states):
             tpl = self.stream[ins["stage"]]

@@ -565,8 +565,9 @@ def recursive_interpolate_states(states, xs, dialect="py", device=0, tables=None
     per-task pre-pass py:1501 of every state in ONE device batch over a table set; the Rust
     runtime clones the whole map per task instead, rust-project/src/runtime.rs:700-701). Every
     string leaf of every tree goes into the batch; whole-string leaves whose typed result the
-    reference walks again (py:1463-1464) go into the next batch. Returns one result per pair, or
-    the exception the reference would raise first in that tree's traversal order."""
+    reference walks again (py:1463-1464) go into the next batch, on the same table set. Returns
+    one result per pair, or the exception the reference would raise first in that tree's
+    traversal order."""
     n = len(states)
     if len(xs) != n:
         raise ValueError("one value per state")
@@ -574,27 +575,32 @@ def recursive_interpolate_states(states, xs, dialect="py", device=0, tables=None
     if own:
         tables = InsertsTableSet(states, dialect=dialect, clock=clock, device=device)
     try:
-        leaves, ids = [], []
-        skels = [None] * n
-        fails = [None] * n
-        for i in range(n):
-            try:
-                skels[i] = _tree_leaves(states[i], xs[i], leaves, ids, i)
-            except (InterpolationException, AssertionError, TypeError, KeyError) as e:
-                fails[i] = e  # the loop-command branch's get_interpdata (py:1483-1488)
-        res = tables.results(leaves, ids) if leaves else []
+        return _walk_states(states, xs, list(range(n)), tables, _depth)
     finally:
         if own:
             tables.close()
+
+
+def _walk_states(states, xs, owner, tables, depth):
+    """recursive_interpolate of xs[i] against states[owner[i]] (table owner[i] of `tables`)."""
+    n = len(xs)
+    leaves, ids = [], []
+    skels = [None] * n
+    fails = [None] * n
+    for i in range(n):
+        try:
+            skels[i] = _tree_leaves(states[owner[i]], xs[i], leaves, ids, owner[i])
+        except (InterpolationException, AssertionError, TypeError, KeyError) as e:
+            fails[i] = e  # the loop-command branch's get_interpdata (py:1483-1488)
+    res = tables.results(leaves, ids) if leaves else []
     # leaves whose result the reference walks again (py:1463-1464): the next batch
     again = [k for k, leaf in enumerate(leaves) if not isinstance(res[k], BaseException) and get_simple_insertkey(leaf)]
     if again:
-        if _depth > 900:
+        if depth >= 900:  # CPython's recursion limit stops the reference
             for k in again:
                 res[k] = RecursionError("maximum recursion depth exceeded in recursive_interpolate")
         else:
-            sub = recursive_interpolate_states([states[ids[k]] for k in again], [res[k] for k in again], dialect,
-                                               device, None, clock, _depth + 1)
+            sub = _walk_states(states, [res[k] for k in again], [ids[k] for k in again], tables, depth + 1)
             for k, r in zip(again, sub):
                 res[k] = r
     out = []

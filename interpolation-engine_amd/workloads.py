@@ -79,4 +79,11 @@ def state_inserts(defaults, index, seed=0x1E5EED05, max_entries=36):
     ins["output"] = "(unset)"
     ins["new_user_input"] = rng.words(2, 8)
     ins["maybe_input"] = ins["new_user_input"]
+    # what the loop's math commands compute from the history (text_adventure.json5:264-302)
+    lo, hi = int(ins.get("min_history_turns", 4)), int(ins.get("max_history_turns", 18))
+    ins["isodd"] = n % 2
+    ins["length_history"] = n
+    ins["n_summarize"] = n - 2 * lo
+    ins["should_summarize"] = (n > 2 * hi) - (n < 2 * hi)
+    ins["summarize_ok"] = (n > 2 * lo) - (n < 2 * lo)
     return ins

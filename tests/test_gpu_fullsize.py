@@ -9,7 +9,8 @@ output layout, so a failure names its config.
   config 3  10M strings, nested {q-{iM}}, 100k inserts                 packed and views output
   config 4  12.5M strings (the 100M batch's per-GPU shard): interpolate, then the `unescape`
             command (recursive_unescape + recursive_interpolate, py:1660-1667)
-  config 5  10k text_adventure.json5 states, one inserts dict per state in one table set
+  config 5  10k text_adventure.json5 states, one inserts dict per state in one table set, per
+            state every string one loop iteration interpolates (bench.iteration_strings)
 
 Reference: interpolate_inserts, /root/reference/src/interpolation_engine/interpolation_engine.py:
 497-541 (restated by the oracle).
@@ -185,14 +186,16 @@ def test_config4_full_step_vs_oracle():
 
 def test_config5_10k_states_vs_oracle():
     """Config 5's batch: 10k synthetic text_adventure.json5 states (one inserts dict each, one table
-    set), each state's recorded pre-pass stream for its stage; every string against the oracle
-    resolving it with that state's own dict."""
+    set), per state every string one loop iteration of its stage interpolates (the benchmark's
+    batch); every string against the oracle resolving it with that state's own dict."""
     from interpolation_engine_amd import workloads as Wk
+    from bench import iteration_strings  # the benchmark's own batch
     c5 = json.load(open(os.path.join(ROOT, "tests", "golden", "config5_stream.json"), encoding="utf-8"))
+    trees = json.load(open(os.path.join(ROOT, "tests", "golden", "config5_trees.json"), encoding="utf-8"))
     stream = {}
-    for st in c5["states"]:
+    for st in trees["states"]:
         if st["stage"] not in stream:
-            stream[st["stage"]] = [c["s"] for c in st["calls"] if c["by"] == "recursive_interpolate"]
+            stream[st["stage"]] = iteration_strings([t["x"] for t in st["trees"]])
     states = [Wk.state_inserts(c5["defaults"], j) for j in range(10_000)]
     strings, ids = [], []
     for j, ins in enumerate(states):
