@@ -77,7 +77,7 @@ def parse(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--layout", choices=["views", "packed"], default="",
-                    help="output layout (default: views, config 4 packed): views = each tile claims its "
+                    help="output layout (default views; config 4 views runs the fused unescape command): views = each tile claims its "
                          "output range with one atomic (no look-back), packed = input order (look-back)")
     return ap.parse_args(argv)
 
@@ -241,9 +241,8 @@ def main():
     d_tot = N.DeviceBuffer(x, 8)
     ids = W.d_ids.ptr if W.d_ids is not None else None
     cmd = cfg == 4  # the unescape command on the results (py:1660-1667): unescape, interpolate again
-    layout = args.layout or ("packed" if cmd else "views")
+    layout = args.layout or "views"
     views = layout == "views"
-    assert not (views and cmd), "the unescape command takes a packed batch"
     d_olen = N.DeviceBuffer(x, 4 * n + 4) if views else None
     if views:
         o = N.DevViews(d_out.ptr, out_cap, d_ooff.ptr, d_olen.ptr, d_st.ptr, d_vid.ptr, d_tot.ptr)
@@ -255,16 +254,20 @@ def main():
             return L.ie_interpolate_device_views(x.h, W.table, ids, W.d_in.ptr, W.d_off.ptr, None, n, ctypes.byref(o))
         return L.ie_interpolate_device_ids(x.h, W.table, ids, W.d_in.ptr, W.d_off.ptr, n, ctypes.byref(o))
     if cmd:
-        d_u = N.DeviceBuffer(x, out_cap)
-        d_uoff = N.DeviceBuffer(x, (n + 1) * 8)
-        d_ust = N.DeviceBuffer(x, n + 1)
-        d_utot = N.DeviceBuffer(x, 8)
-        tmp = N.DevOut(d_u.ptr, out_cap, d_uoff.ptr, d_ust.ptr, d_vid.ptr, d_utot.ptr)
         d_out2 = N.DeviceBuffer(x, out_cap)
         d_ooff2 = N.DeviceBuffer(x, (n + 1) * 8)
         d_st2 = N.DeviceBuffer(x, n + 1)
         d_tot2 = N.DeviceBuffer(x, 8)
-        o2 = N.DevOut(d_out2.ptr, out_cap, d_ooff2.ptr, d_st2.ptr, d_vid.ptr, d_tot2.ptr)
+        d_olen2 = N.DeviceBuffer(x, 4 * n + 4) if views else None
+        if views:  # fused: each tile unescaped in LDS and resolved (no unescaped copy in HBM)
+            o2 = N.DevViews(d_out2.ptr, out_cap, d_ooff2.ptr, d_olen2.ptr, d_st2.ptr, d_vid.ptr, d_tot2.ptr)
+        else:
+            d_u = N.DeviceBuffer(x, out_cap)
+            d_uoff = N.DeviceBuffer(x, (n + 1) * 8)
+            d_ust = N.DeviceBuffer(x, n + 1)
+            d_utot = N.DeviceBuffer(x, 8)
+            tmp = N.DevOut(d_u.ptr, out_cap, d_uoff.ptr, d_ust.ptr, d_vid.ptr, d_utot.ptr)
+            o2 = N.DevOut(d_out2.ptr, out_cap, d_ooff2.ptr, d_st2.ptr, d_vid.ptr, d_tot2.ptr)
 
     def step(k=None):
         if k is not None:
@@ -272,7 +275,10 @@ def main():
         N.check(resolve(), "resolve")
         if k is not None:
             x.mark(3 * k + 1)
-        if cmd:
+        if cmd and views:
+            N.check(L.ie_unescape_cmd_device_views(x.h, W.table, None, d_out.ptr, d_ooff.ptr, d_olen.ptr, n, d_st.ptr,
+                                                   ctypes.byref(o2)), "ie_unescape_cmd_device_views")
+        elif cmd:
             N.check(L.ie_unescape_cmd_device(x.h, W.table, None, d_out.ptr, d_ooff.ptr, n, d_st.ptr,
                                              ctypes.byref(tmp), ctypes.byref(o2)), "ie_unescape_cmd_device")
         if k is not None:
@@ -304,7 +310,7 @@ def main():
     wall_max = max_over_ranks(wall, dist)
 
     x.set_timing(True)  # one more call with the library's own events for the telemetry
-    if cmd and os.environ.get("IE_DIAG_CMD_RESOLVE"):  # diagnostic: the command's second resolve instead
+    if cmd and not views and os.environ.get("IE_DIAG_CMD_RESOLVE"):  # diagnostic: the command's second resolve instead
         N.check(L.ie_interpolate_device(x.h, W.table, d_u.ptr, d_uoff.ptr, n, ctypes.byref(o2)), "timing")
     else:
         N.check(resolve(), "timing")
@@ -321,7 +327,7 @@ def main():
     cpu = None
     if rank == 0 and not args.no_cpu:
         res = Result(N, n, d_out2 if cmd else d_out, d_ooff2 if cmd else d_ooff, d_st2 if cmd else d_st,
-                     d_olen, d_tot2 if cmd else d_tot)
+                     d_olen2 if cmd else d_olen, d_tot2 if cmd else d_tot)
         cpu = cpu_baseline(args, W, N, res)
 
     traffic = None
@@ -369,12 +375,16 @@ def main():
         if cfg == 5:
             line["config"]["states_per_gpu"] = n_units
         if cmd:
-            ub = int(d_utot.to_numpy(np.uint64, 1)[0])
             ob2 = int(d_tot2.to_numpy(np.uint64, 1)[0])
             ums = float(np.mean(cmd_ms))
-            ualg = out_bytes + ub + ub + ob2 + 2 * 17 * n  # unescape: read out1, write tmp; interpolate: read tmp, write out2
+            if views:  # fused: read out1 + its views and statuses, write out2 + views + statuses
+                ub = None
+                ualg = out_bytes + ob2 + 2 * 13 * n
+            else:  # unescape: read out1, write tmp; interpolate: read tmp, write out2
+                ub = int(d_utot.to_numpy(np.uint64, 1)[0])
+                ualg = out_bytes + ub + ub + ob2 + 2 * 17 * n
             line["unescape_cmd"] = {"ms": round(ums, 4), "unescaped_bytes": ub, "output_bytes": ob2,
-                                    "achieved_gbs": round(ualg / (ums * 1e-3) / 1e9, 1)}
+                                    "fused": views, "achieved_gbs": round(ualg / (ums * 1e-3) / 1e9, 1)}
         print(json.dumps(line), flush=True)
     W.close()
     if dist:

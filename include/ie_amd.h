@@ -177,7 +177,8 @@ void ie_table_free(ie_table* t);
 int ie_table_replicate(const ie_table* t, int32_t device, ie_table** out);
 int ie_shard_bounds(const uint64_t* offsets, uint64_t n, uint32_t n_shards, uint64_t* first);
 /* Re-read the clock (py:433-436) without a rebuild: rewrites the 'HH:MM' / 'HH:MM:SS' entries in
- * place. IE_ERR_INVALID when a brace-bearing value pre-resolved at build read the clock (rebuild). */
+ * place (values that read the clock, also through nested keys, are never pre-resolved at build,
+ * so every lookup sees the new time). Waits for the device first: no batch may be in flight. */
 int ie_table_set_clock(ie_table* t, const ie_clock* now);
 uint64_t ie_table_entries(const ie_table* t);
 uint32_t ie_table_tables(const ie_table* t);
@@ -281,6 +282,14 @@ int ie_unescape_batch(ie_exec* x, const uint8_t* bytes, const uint64_t* offsets,
 int ie_unescape_cmd_device(ie_exec* x, const ie_table* t, const uint32_t* d_table_id, const uint8_t* d_bytes,
                            const uint64_t* d_offsets, uint64_t n, const uint8_t* d_status_in, const ie_dev_out* tmp,
                            const ie_dev_out* out);
+/* The same command on a views batch (d_lengths nullable: packed input, d_offsets[n + 1]) into a views
+ * output, fused: each tile is unescaped in the LDS stage and resolved there, without an unescaped
+ * copy in HBM and without a look-back; the strings a tile cannot finish (not staged, or needing
+ * the literal path) are unescaped into the exec's scratch pool and resolved in a second pass.
+ * Statuses, bytes and IE_RECURSE as ie_unescape_cmd_device. */
+int ie_unescape_cmd_device_views(ie_exec* x, const ie_table* t, const uint32_t* d_table_id, const uint8_t* d_bytes,
+                                 const uint64_t* d_offsets, const uint32_t* d_lengths, uint64_t n,
+                                 const uint8_t* d_status_in, const ie_dev_views* out);
 int ie_escape_batch(ie_exec* x, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
                     ie_batch** out);
 

@@ -32,6 +32,7 @@ EXPORTS = [
     "ie_interpolate_device", "ie_interpolate_batch", "ie_interpolate", "ie_interpolate_device_ids",
     "ie_interpolate_batch_ids", "ie_interpolate_device_views",
     "ie_unescape_device", "ie_escape_device", "ie_unescape_batch", "ie_escape_batch", "ie_unescape_cmd_device",
+    "ie_unescape_cmd_device_views",
     "ie_batch_free", "ie_simple_insertkey",
     "ie_synth_create", "ie_synth_free", "ie_synth_kv", "ie_synth_strings_host",
     "ie_synth_strings_device", "ie_debug_probe",
@@ -121,6 +122,7 @@ def signatures():
         "ie_unescape_cmd_device": (ctypes.c_int, [vp, vp, vp, vp, vp, u64, vp, ctypes.POINTER(DevOut),
                                                   ctypes.POINTER(DevOut)]),
         "ie_escape_batch": (ctypes.c_int, [vp, vp, vp, u64, ctypes.POINTER(ctypes.POINTER(BatchRes))]),
+        "ie_unescape_cmd_device_views": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, u64, vp, ctypes.POINTER(DevViews)]),
         "ie_batch_free": (None, [ctypes.POINTER(BatchRes)]),
         "ie_simple_insertkey": (ctypes.c_int, [ctypes.c_char_p, u64, i32, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "ie_table_replicate": (ctypes.c_int, [vp, i32, pvp]),

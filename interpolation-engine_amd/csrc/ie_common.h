@@ -154,6 +154,8 @@ struct DevTable {
 
 // internal status: routed to the literal (complex) kernel
 constexpr uint8_t kStatusPending = 0xFE;
+// internal status: left to the fused unescape command's deferred pass (rewritten by it)
+constexpr uint8_t kStatusDeferred = 0xFD;
 
 // ------------------------------------------------------------------------------------------
 // Synthetic workloads: counter-based splitmix64, identical on host and device.

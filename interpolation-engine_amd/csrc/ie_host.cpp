@@ -79,7 +79,6 @@ struct ie_table {
   DevTable dev{};
   // the clock entries ('HH:MM', 'HH:MM:SS' of every table): slot, host copy (ie_table_set_clock)
   std::vector<std::pair<uint32_t, Entry>> clock_entries;
-  bool clock_dependent = false;  // a pre-resolved value read the clock: a new clock needs a rebuild
   DevBuf entries, pilots, arena;
   ~ie_table() {
     entries.release();
@@ -106,6 +105,7 @@ struct ie_exec {
   int32_t opt_views = 0;          // host batch APIs resolve into a views layout (IE_VIEWS)
   bool in_cmd = false;            // inside the unescape command's second resolve
   bool cmd_first = false;         // the unescape command's unescape step (offsets zeroed on overflow)
+  bool cmd_fused = false;         // the fused unescape command (views): launch_unescape_cmd
   uint32_t opt_noeval = 0;        // diagnostic verbatim copy (IE_DEBUG_NOEVAL)
   std::string stamps_path;        // diagnostic phase stamps (IE_DEBUG_STAMPS)
   // fail commit (k_resolve<true>): chosen from the chain-failure count of an earlier batch, read
@@ -117,6 +117,8 @@ struct ie_exec {
   hipEvent_t stat_ev = nullptr;
   // workspace
   DevBuf counters, pool, out_len, tile_sum, tile_base, defer_tiles, defer_desc;
+  // the fused unescape command's deferred pass: list, views into the pool, table ids
+  DevBuf u_list, u_off, u_len, u_tid;
   // host-API staging
   DevBuf in_bytes, in_off, in_tid, o_bytes, o_off, o_len, o_status, o_vid, o_total, wc_range, wc_match, wc_ncap, wc_caps;
   // synth scratch
@@ -124,6 +126,7 @@ struct ie_exec {
   DevBuf stamps;        // diagnostic phase stamps (env IE_DEBUG_STAMPS=<file>)
   uint64_t stamp_tiles = 0;
   ~ie_exec() {
+    for (DevBuf* b : {&u_list, &u_off, &u_len, &u_tid}) b->release();
     for (DevBuf* b : {&counters, &pool, &out_len, &tile_sum, &tile_base, &defer_tiles, &defer_desc, &in_bytes,
                       &in_off, &in_tid, &o_bytes, &o_off, &o_len, &o_status, &o_vid, &o_total, &wc_range, &wc_match, &wc_ncap, &wc_caps,
                       &s_lens, &s_part, &stamps})
@@ -260,8 +263,8 @@ int set_device(int32_t dev) {
 
 // workspace for a batch of n strings. counters (u32 words): [0] tile ticket, [1] look-back error,
 // [2..3] pool bytes used (u64), [4..8] telemetry (literal strings, deferred tiles, look-back polls,
-// exact-path strings, chain failures), [9] deferred-tile count, [10..11] views output cursor (u64);
-// zeroed on every call.
+// exact-path strings, chain failures), [9] deferred-tile count, [10..11] views output cursor (u64),
+// [12] the fused unescape command's deferred-string count; zeroed on every call.
 int ensure_work(ie_exec* x, int op, uint64_t n) {
   const uint64_t tiles = (n + kBlock - 1) / kBlock + 1;  // (kRBlock >= kBlock: enough for k_resolve too)
   // counters, then (interpolation) the look-back words: one buffer, zeroed by one memset per call
@@ -295,6 +298,7 @@ Work make_work(ie_exec* x, uint64_t* total) {
   W.defer_desc = (uint4*)x->defer_desc.p;
   W.tile_state = (uint64_t*)((uint8_t*)x->counters.p + 64);
   W.cursor = (uint64_t*)x->counters.p + 5;  // words 10-11
+  W.udefer_count = (uint32_t*)x->counters.p + 12;
   W.zero_on_overflow = x->cmd_first ? 1u : 0u;
   W.pool = (uint8_t*)x->pool.p;
   W.pool_bytes = x->pool.bytes;
@@ -356,7 +360,17 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
     // is interpolation output, so its evaluation is light and the look-back bounds it) takes them
     // by default; everything else the 256-string tiles (ie_resolve512.hip has the numbers)
     const bool wide = x->opt_tile == 512 || (x->opt_tile == 0 && x->in_cmd && !d_out_len && !d_in_len);
-    IE_HIP(wide ? launch_resolve512(B, W, t->dev, out->bytes, cap, st) : launch_resolve(B, W, t->dev, out->bytes, cap, st));
+    if (x->cmd_fused) {
+      IE_HIP(x->u_list.ensure(n * 4));
+      IE_HIP(x->u_off.ensure(n * 8));
+      IE_HIP(x->u_len.ensure(n * 4));
+      if (d_tid) IE_HIP(x->u_tid.ensure(n * 4));
+      W.udefer_list = (uint32_t*)x->u_list.p;
+      IE_HIP(launch_unescape_cmd(B, W, t->dev, out->bytes, cap, (uint64_t*)x->u_off.p, (uint32_t*)x->u_len.p,
+                                 d_tid ? (uint32_t*)x->u_tid.p : nullptr, st));
+    } else {
+      IE_HIP(wide ? launch_resolve512(B, W, t->dev, out->bytes, cap, st) : launch_resolve(B, W, t->dev, out->bytes, cap, st));
+    }
     if (!forced && !x->stat_pending) {
       if (!x->stat_host) {
         IE_HIP(hipHostMalloc((void**)&x->stat_host, 4, hipHostMallocDefault));
@@ -623,12 +637,9 @@ int upload_table(const std::vector<Ent>& ents, uint32_t n_tables, int32_t dialec
   std::vector<Entry> entries(m);
   for (size_t i = 0; i < items.size(); i++) entries[slot_of[i]] = items[i];
   std::vector<std::pair<uint32_t, Entry>> clock_entries;
-  bool clock_dependent = false;
-  for (size_t i = 0; i < items.size(); i++) {
+  for (size_t i = 0; i < items.size(); i++)
     if (items[i].vid == IE_VID_CLOCK_HHMM || items[i].vid == IE_VID_CLOCK_HHMMSS)
       clock_entries.emplace_back(slot_of[i], items[i]);
-    if ((ents[i].flags & EF_RAWALT) && ents[i].raw.find("HH:MM") != std::string_view::npos) clock_dependent = true;
-  }
   for (int pad = 0; pad < 16; pad++) arena.push_back(0);  // dword reads past the last text
   ie_table* t = new ie_table();
   t->device = device;
@@ -637,7 +648,6 @@ int upload_table(const std::vector<Ent>& ents, uint32_t n_tables, int32_t dialec
   t->n_entries = ents.size();
   t->n_tables = n_tables;
   t->clock_entries = std::move(clock_entries);
-  t->clock_dependent = clock_dependent;
   auto up = [&](DevBuf& b, const void* src, uint64_t bytes) -> hipError_t {
     hipError_t e = b.ensure(bytes + 16);
     if (e != hipSuccess) return e;
@@ -675,9 +685,12 @@ int upload_table(const std::vector<Ent>& ents, uint32_t n_tables, int32_t dialec
 // (never the whole-string simple form), and a result that is inert (no '{', '}', '\', U+3020)
 // replaces the splice text; lookups that need the raw value (py:512 / interp.rs:48) read it
 // from the arena (EF_RAWALT). Values whose resolution fails or stays structural keep the
-// literal path.
+// literal path, and so do values whose resolution reads the clock (py:433-436 reads it on every
+// lookup, also through a nested key: '{{a}}' with a = 'HH:MM', '{HH:{m}}'): they are resolved
+// under the build clock and under a second clock that differs in every field, and a value whose
+// status or text differs stays raw, so ie_table_set_clock never leaves a stale time behind.
 int preresolve(ie_table* t0, std::vector<Ent>& ents, uint32_t n_tables, int32_t dialect, uint32_t flags,
-               int32_t device, ie_table** out) {
+               int32_t device, const ie_clock& clock, ie_table** out) {
   auto clean_value = [](std::string_view v, bool need_brace) {
     size_t opens = 0;
     int64_t depth = 0;
@@ -710,13 +723,27 @@ int preresolve(ie_table* t0, std::vector<Ent>& ents, uint32_t n_tables, int32_t 
   int rc = ie_exec_create(device, nullptr, &x);
   if (rc) return rc;
   ie_batch* b = nullptr;
+  ie_batch* b2 = nullptr;
+  const ie_clock other{(clock.hour + 12) % 24, (clock.minute + 30) % 60, (clock.second + 30) % 60};
   rc = run_host(x, kOpInterp, t0, bytes.data(), offs.data(), cand.size(), &b, tids.data());
+  if (!rc) rc = ie_table_set_clock(t0, &other);
+  if (!rc) rc = run_host(x, kOpInterp, t0, bytes.data(), offs.data(), cand.size(), &b2, tids.data());
+  if (!rc) rc = ie_table_set_clock(t0, &clock);
   ie_exec_destroy(x);
-  if (rc) return rc;
+  if (rc) {
+    ie_batch_free(b);
+    ie_batch_free(b2);
+    return rc;
+  }
+  auto same = [&](uint64_t k) {
+    const uint64_t l1 = b->offsets[k + 1] - b->offsets[k], l2 = b2->offsets[k + 1] - b2->offsets[k];
+    return b->status[k] == b2->status[k] && l1 == l2 &&
+           memcmp(b->bytes + b->offsets[k], b2->bytes + b2->offsets[k], l1) == 0;
+  };
   std::vector<std::string> resolved(cand.size());
   size_t changed = 0;
   for (size_t k = 0; k < cand.size(); k++) {
-    if (b->status[k] != IE_OK_STR) continue;
+    if (b->status[k] != IE_OK_STR || !same(k)) continue;
     const uint64_t o = b->offsets[k], len = b->offsets[k + 1] - o;
     if (len < 1 || b->bytes[o] != 'a') continue;
     std::string_view r((const char*)b->bytes + o + 1, len - 1);
@@ -735,6 +762,7 @@ int preresolve(ie_table* t0, std::vector<Ent>& ents, uint32_t n_tables, int32_t 
     changed++;
   }
   ie_batch_free(b);
+  ie_batch_free(b2);
   if (!changed) return IE_SUCCESS;
   ie_table* t1 = nullptr;
   rc = upload_table(ents, n_tables, dialect, flags, device, &t1);
@@ -796,7 +824,8 @@ int ie_table_set_build(const ie_kv* kv, const uint64_t* kv_start, uint32_t n_tab
     return rc;
   }
   *out = t0;
-  rc = preresolve(t0, ents, n_tables, dialect, flags, device, out);
+  const ie_clock clk{h, mi, se};
+  rc = preresolve(t0, ents, n_tables, dialect, flags, device, clk, out);
   if (rc) {
     ie_table_free(*out);
     *out = nullptr;
@@ -826,7 +855,6 @@ int ie_table_replicate(const ie_table* t, int32_t device, ie_table** out) {
   c->n_entries = t->n_entries;
   c->n_tables = t->n_tables;
   c->clock_entries = t->clock_entries;
-  c->clock_dependent = t->clock_dependent;
   c->dev = t->dev;
   auto copy = [&](DevBuf& dst, const DevBuf& src) -> hipError_t {
     hipError_t e = dst.ensure(src.bytes);
@@ -871,9 +899,10 @@ void ie_table_free(ie_table* t) {
 }
 int ie_table_set_clock(ie_table* t, const ie_clock* now) {
   if (!t || !now) return fail(IE_ERR_INVALID, "null argument");
-  if (t->clock_dependent) return fail(IE_ERR_INVALID, "a pre-resolved value depends on the clock: rebuild the table");
   int rc = set_device(t->device);
   if (rc) return rc;
+  // no batch may still read the table (exec streams are non-blocking: not ordered with these copies)
+  IE_HIP(hipDeviceSynchronize());
   char hhmm[16], hhmmss[16];
   snprintf(hhmm, sizeof hhmm, "%02d:%02d", now->hour, now->minute);
   snprintf(hhmmss, sizeof hhmmss, "%02d:%02d:%02d", now->hour, now->minute, now->second);
@@ -1164,6 +1193,34 @@ int ie_unescape_cmd_device(ie_exec* x, const ie_table* t, const uint32_t* d_tabl
   if (rc) return rc;
   IE_HIP(launch_cap_check(tmp->total, tmp->bytes_cap, (uint32_t*)x->counters.p + 1, x->stream));
   if (d_status_in) IE_HIP(launch_status_carry(d_status_in, out->status, n, x->stream));
+  return IE_SUCCESS;
+}
+
+int ie_unescape_cmd_device_views(ie_exec* x, const ie_table* t, const uint32_t* d_table_id, const uint8_t* d_bytes,
+                                 const uint64_t* d_offsets, const uint32_t* d_lengths, uint64_t n,
+                                 const uint8_t* d_status_in, const ie_dev_views* out) {
+  if (!x || !out || !out->status || (n && (!out->offsets || !out->lengths))) return fail(IE_ERR_INVALID, "null argument");
+  const ie_dev_out o{out->bytes, out->bytes_cap, out->offsets, out->status, out->value_id, out->total};
+  auto run = [&]() -> int {
+    x->in_cmd = true;
+    x->cmd_fused = true;
+    const int r = run_device(x, kOpInterp, t, d_bytes, d_offsets, n, &o, d_table_id, out->lengths, d_lengths);
+    x->in_cmd = false;
+    x->cmd_fused = false;
+    return r;
+  };
+  int rc = run();
+  if (rc) return rc;
+  if (n && !x->pool_fixed) {  // the pool's demand (deferred strings + literal path), as ie_interpolate_device
+    uint64_t used = 0;
+    IE_HIP(hipMemcpyAsync(&used, (uint64_t*)x->counters.p + 1, 8, hipMemcpyDeviceToHost, x->stream));
+    IE_HIP(hipStreamSynchronize(x->stream));
+    if (used > x->pool.bytes) {
+      x->pool_request = std::max<uint64_t>(x->pool_request, used + used / 8 + (1ull << 20));
+      if ((rc = run())) return rc;
+    }
+  }
+  if (d_status_in && n) IE_HIP(launch_status_carry(d_status_in, out->status, n, x->stream));
   return IE_SUCCESS;
 }
 

@@ -39,6 +39,11 @@ struct Batch {
   // views output: no global order, so no look-back: each tile claims its output range with one
   // atomic on the exec's cursor; string i's result is out[out_off[i], + out_len[i])
   uint32_t* out_len;        // n or null
+  // a deferred subset (the unescape command's second pass): string i's results go to position
+  // out_index[i] of the output arrays, and only the first *n_dev strings exist (a device count;
+  // the grid is sized for n)
+  const uint32_t* out_index;  // n or null
+  const uint32_t* n_dev;      // 1 or null
 };
 
 struct Work {
@@ -62,6 +67,10 @@ struct Work {
   uint32_t* defer_tiles; // tiles
   uint4* defer_desc;     // tiles * kBlock * 4: each string's descriptor
   uint64_t* cursor;      // 1   views output: bytes claimed so far (zeroed per call)
+  // the fused unescape command (k_resolve<.., UNESC>): strings it cannot finish in the stage (not
+  // staged, or needing the literal path) are listed here for the deferred pass
+  uint32_t* udefer_list;  // n
+  uint32_t* udefer_count; // 1
   uint32_t recurse;      // k_resolve in the unescape command (py dialect): whole-string items whose
                          // result recursive_interpolate walks again report IE_RECURSE
   uint32_t zero_on_overflow; // escape kernels: when the output exceeds its capacity, write every
@@ -94,6 +103,10 @@ hipError_t launch_resolve512(const Batch& B, const Work& W, const DevTable& T, u
 hipError_t launch_escape(int op, const Batch& B, const Work& W, uint8_t* out, uint64_t cap,
                          hipStream_t st);
 hipError_t launch_cap_check(const uint64_t* total, uint64_t cap, uint32_t* err, hipStream_t st);
+// the unescape command, views in and out (ie_resolve.hip): the fused resolve (unescape while
+// staging), then the deferred strings: unescaped into the pool (k_unesc_deferred), resolved again
+hipError_t launch_unescape_cmd(const Batch& B, const Work& W, const DevTable& T, uint8_t* out, uint64_t cap,
+                               uint64_t* sub_off, uint32_t* sub_len, uint32_t* sub_tid, hipStream_t st);
 hipError_t launch_status_carry(const uint8_t* before, uint8_t* after, uint64_t n, hipStream_t st);
 hipError_t launch_debug_probe(const DevTable& T, const uint8_t* key, uint32_t klen, uint64_t* out,
                               hipStream_t st);

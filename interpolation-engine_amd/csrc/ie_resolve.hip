@@ -761,7 +761,7 @@ __device__ bool parse_chains(const lds_u8* tile, uint32_t p0, uint32_t n, const 
 // exact evaluator must decide (kResReject: a long key or text, a non-inert value, a failure when
 // !FAILC, a miss an inserts-dir might resolve).
 template <bool FAILC>
-__device__ void resolve_jobs(const DevTable& T, const lds_u8* tile, const ChainJobs& J, uint32_t j0, uint32_t njobs,
+__device__ void resolve_jobs(const DevTable& T, const lds_u8* tile, const ChainJobs J, uint32_t j0, uint32_t njobs,
                              bool& chain_fail, uint64_t* stamp) {
   constexpr int NJ = 2;
   const uint32_t tid = threadIdx.x;
@@ -911,7 +911,7 @@ __device__ void resolve_jobs(const DevTable& T, const lds_u8* tile, const ChainJ
 // a string's descriptor from its jobs [jb, jb + nch): false when any job needs the exact evaluator;
 // a failed job (FAILC) makes the string fail with the status of the failing pair with the largest
 // opening offset (the reference resolves the rightmost chain first and stops at its first failure)
-__device__ bool combine_chains(const ChainJobs& J, uint32_t jb, uint32_t nch, const uint32_t (&crec)[kMaxTop],
+__device__ bool combine_chains(const ChainJobs J, uint32_t jb, uint32_t nch, const uint32_t (&crec)[kMaxTop],
                                uint32_t n, Desc& d, uint32_t& out_len, uint8_t& status) {
   bool ok = true;
   uint32_t fw = 0, vsum = 0, span = 0;
@@ -1241,12 +1241,113 @@ __device__ __forceinline__ bool maybe_simple(const uint8_t* s, uint32_t n) {
   return l < n && s[l] == '}';
 }
 
+// The unescape command's recursive_unescape (py:1665 / rust-project/src/runtime.rs:1046), done on
+// the staged tile before it is resolved. recursive_unescape is two str.replace passes ('\\{' -> '{',
+// then '\\}' -> '}'); neither can create a pair for the other (a removed '\\' leaves a brace
+// behind the byte before it), so together they drop exactly the '\\' bytes followed by a brace
+// within the same string. The drops are marked per 16-byte chunk (bit k: byte k is dropped), a
+// '\\' that ends its string is restored (the brace after it is the next string's), an exclusive scan
+// gives every chunk's shift, and the chunks, still in the prefetch registers, are written back to
+// the stage compacted. Each lane then moves its string's start and length to the compacted stage
+// (only staged strings: the others are the deferred pass's). Every lane calls it (barriers).
+template <int MAXV>
+__device__ __attribute__((always_inline)) void unescape_stage(const uint4 (&v)[MAXV], lds_u8* stage, uint8_t* s_u,
+                                                             uint64_t* s_red, uint32_t nv, bool staged, uint32_t& p0,
+                                                             uint64_t& sn, uint32_t tid) {
+  lds_u32* const drop = (lds_u32*)(lds_u8*)s_u;                 // kChunks + 1 words
+  lds_u32* const dpre = (lds_u32*)(lds_u8*)s_u + kChunks + 8;   // kChunks + 1 words
+  auto mask_of = [](uint32_t x, uint32_t c) {  // top bit of each byte set where the byte is c
+    const uint32_t y = x ^ (c * 0x01010101u);
+    return ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u;
+  };
+  // 1. drop masks
+#pragma unroll
+  for (int k = 0; k < MAXV; k++) {
+    const uint32_t c = tid + (uint32_t)k * kRBlock;
+    if (c < nv) {
+      const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+      uint32_t bs = 0, br = 0;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        bs |= nib(mask_of(w[q], '\\')) << (4 * q);
+        br |= nib(mask_of(w[q], '{') | mask_of(w[q], '}')) << (4 * q);
+      }
+      const uint8_t nx = c + 1 < nv ? stage[16 * (c + 1)] : (uint8_t)0;
+      br |= (nx == '{' || nx == '}') ? 0x10000u : 0u;
+      // the whole stage: a views batch stages strings past the tile's span too (the bytes of no
+      // string move with the rest, harmlessly)
+      drop[c] = bs & (br >> 1) & 0xFFFFu;
+    }
+  }
+  if (tid == 0) drop[nv] = 0;
+  __syncthreads();
+  // 2. a '\\' that ends its string precedes the next string's brace: kept
+  if (staged && sn) {
+    const uint32_t x = p0 + (uint32_t)sn - 1u;
+    if ((drop[x >> 4] >> (x & 15u)) & 1u) atomicAnd((uint32_t*)(drop + (x >> 4)), ~(1u << (x & 15u)));
+  }
+  __syncthreads();
+  // 3. drops before each chunk (each lane a contiguous run of chunks)
+  const uint32_t R = (nv + kRBlock - 1) / kRBlock, c_lo = min(tid * R, nv), c_hi = min(c_lo + R, nv);
+  uint32_t cnt = 0;
+  for (uint32_t c = c_lo; c < c_hi; c++) cnt += (uint32_t)__popc(drop[c]);
+  uint64_t total;
+  uint32_t run = (uint32_t)block_scan(cnt, s_red, &total);
+  for (uint32_t c = c_lo; c < c_hi; c++) {
+    dpre[c] = run;
+    run += (uint32_t)__popc(drop[c]);
+  }
+  if (tid == 0) dpre[nv] = (uint32_t)total;
+  __syncthreads();
+  // 4. the chunks back to the stage, compacted (sources in registers: in place is safe)
+  if (total) {
+#pragma unroll
+    for (int k = 0; k < MAXV; k++) {
+      const uint32_t c = tid + (uint32_t)k * kRBlock;
+      const uint32_t dm = c < nv ? drop[c] : 0u;
+      const uint32_t sh = c < nv ? dpre[c] : 0u;
+      if (c < nv && sh) {
+        const uint32_t w[8] = {v[k].x, v[k].y, v[k].z, v[k].w, 0u, 0u, 0u, 0u};
+        if (dm == 0) {
+          put_words(stage + 16 * c - sh, w, 16);
+        } else {
+          uint32_t o = 16 * c - sh;
+          for (uint32_t b = 0; b < 16; b++)
+            if (!((dm >> b) & 1u)) stage[o++] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+        }
+      } else if (c < nv && dm) {  // no shift yet, but drops inside this chunk
+        const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+        uint32_t o = 16 * c;
+        for (uint32_t b = 0; b < 16; b++)
+          if (!((dm >> b) & 1u)) stage[o++] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+      }
+    }
+  }
+  __syncthreads();
+  // 5. this string in the compacted stage
+  if (staged && total) {
+    auto D = [&](uint32_t x) {
+      const uint32_t c = x >> 4;
+      return dpre[c] + (uint32_t)__popc(drop[c] & ((1u << (x & 15u)) - 1u));
+    };
+    const uint32_t e = p0 + (uint32_t)sn;
+    const uint32_t a = p0 - D(p0);
+    sn = (uint64_t)(e - D(e) - a);
+    p0 = a;
+  }
+}
+
 // The deferred tiles' bytes (see k_resolve): one workgroup per deferred tile at a time. Each
 // lane rebuilds its string's pieces from the stored descriptor (template runs from the input in
 // global memory, values from the table or the literal pool) and the tile's output goes through
 // the LDS stage in windows of kRStageBytes (long pieces copied by a whole wave).
-__global__ __launch_bounds__(kRBlock) void k_emit_windows(Batch B, Work W, DevTable T, uint8_t* out) {
+__global__ __launch_bounds__(kRBlock) void k_emit_windows(Batch B0, Work W, DevTable T, uint8_t* out) {
   __shared__ __attribute__((aligned(16))) uint8_t s_win[kRStageBytes + 48];
+  Batch B = B0;
+  if (B0.n_dev) {
+    const uint64_t nd = gld(B0.n_dev);
+    B.n = nd < B0.n ? nd : B0.n;
+  }
   const uint32_t count = __hip_atomic_load(W.defer_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t tid = threadIdx.x;
   // views output: the bytes every tile claimed are the batch's total (k_resolve has finished)
@@ -1254,9 +1355,12 @@ __global__ __launch_bounds__(kRBlock) void k_emit_windows(Batch B, Work W, DevTa
   for (uint32_t slot = blockIdx.x; slot < count; slot += gridDim.x) {
     const uint32_t tile = gld(W.defer_tiles + slot);
     const uint64_t first = (uint64_t)tile * kRBlock, last = min(first + (uint64_t)kRBlock, B.n), i = first + tid;
-    const uint64_t base = gld(B.out_off + first);
+    // (a deferred subset's results sit at out_index[] of the batch)
+    const uint64_t of = B.out_index ? gld(B.out_index + first) : first;
+    const uint64_t ol = B.out_index ? gld(B.out_index + last - 1) : last - 1;
+    const uint64_t base = gld(B.out_off + of);
     const uint64_t tile_total =
-        (B.out_len ? gld(B.out_off + last - 1) + gld(B.out_len + last - 1) : gld(B.out_off + last)) - base;
+        (B.out_len ? gld(B.out_off + ol) + gld(B.out_len + ol) : gld(B.out_off + last)) - base;
     const uint4* dd = W.defer_desc + ((uint64_t)slot * kRBlock + tid) * 4;
     Desc d;
     uint32_t olen = 0, n32 = 0;
@@ -1268,9 +1372,10 @@ __global__ __launch_bounds__(kRBlock) void k_emit_windows(Batch B, Work W, DevTa
       d.close[0] = b.x, d.close[1] = b.y, d.close[2] = b.z, n32 = b.w;
       d.vk[0] = c.x, d.vk[1] = c.y, d.vk[2] = c.z;
       d.vs[0] = e.x, d.vs[1] = e.y, d.vs[2] = e.z;
-      const uint64_t o = gld(B.out_off + i);
+      const uint64_t oi = B.out_index ? gld(B.out_index + i) : i;
+      const uint64_t o = gld(B.out_off + oi);
       local = o - base;
-      olen = gld(B.status + i) != IE_OK_STR ? 0u : B.out_len ? gld(B.out_len + i) : (uint32_t)(gld(B.out_off + i + 1) - o);
+      olen = gld(B.status + oi) != IE_OK_STR ? 0u : B.out_len ? gld(B.out_len + oi) : (uint32_t)(gld(B.out_off + i + 1) - o);
       s = B.bytes + gld(B.in_off + i);
     } else {
       d.ntop = 0;
@@ -1312,9 +1417,18 @@ __global__ __launch_bounds__(kRBlock) void k_emit_windows(Batch B, Work W, DevTa
 // give the reference's results; the host picks per batch stream (ie_host.cpp, "fail commit").
 // VIEWS: B.out_len set; each tile claims its output range with one atomic on W.cursor (no
 // global order, no look-back) and writes each string's start and length.
-template <bool FAILC, bool MULTI, bool VIEWS>
-__global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES_PER_EU))) void k_resolve(Batch B, Work W, DevTable T, uint8_t* out,
+// UNESC (with VIEWS): the unescape command's resolve, fused with its recursive_unescape: the tile
+// is unescaped in the LDS stage (unescape_stage) and then resolved; strings that cannot be finished
+// there (not staged, or needing the literal path) go to W.udefer_list for the deferred pass.
+template <bool FAILC, bool MULTI, bool VIEWS, bool UNESC = false>
+__global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES_PER_EU))) void k_resolve(Batch B0, Work W, DevTable T, uint8_t* out,
                                                     uint64_t cap) {
+  // a deferred subset counts its strings on the device (the grid is sized for B0.n)
+  Batch B = B0;
+  if (B0.n_dev) {
+    const uint64_t nd = gld(B0.n_dev);
+    B.n = nd < B0.n ? nd : B0.n;
+  }
   __shared__ __attribute__((aligned(16))) uint8_t s_in[kRTileBytes + 48];
   __shared__ __attribute__((aligned(16))) uint8_t s_u[kUnionLds];
   __shared__ uint32_t s_olen[kRBlock];  // output length; the value id for IE_OK_VALUE strings
@@ -1358,17 +1472,19 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
   const uint64_t first = (uint64_t)tile * kRBlock;
   const uint64_t last = min(first + (uint64_t)kRBlock, B.n);
   const uint64_t i = first + tid;
-  const uint64_t lo = geo.lo, so = geo.so, sn = geo.sn;
+  const uint64_t lo = geo.lo, so = geo.so;
+  uint64_t sn = geo.sn;
   const uint32_t shift = (uint32_t)((uintptr_t)(B.bytes + lo) & 15);
   // the stage holds the tile's first kStageChunks 16-byte chunks: strings that end inside it are
   // evaluated from LDS, the rest (a tile of long strings; a views input string placed apart from
   // its tile) from global memory
   const uint32_t nv = pre.nv;
-  const uint32_t p0 = shift + (uint32_t)(so - lo);
+  uint32_t p0 = shift + (uint32_t)(so - lo);
   const bool lane_staged = p0 + sn <= 16ull * nv;
   {
     pre.commit((uint4*)s_in, tid);
     __syncthreads();
+    if (UNESC) unescape_stage<kStageV>(pre.v, (lds_u8*)s_in, s_u, s_red, nv, lane_staged, p0, sn, tid);
     for (uint32_t c0 = 0; c0 < nv; c0 += kRBlock) {  // uniform trip count: ballots below
       const uint32_t c = c0 + tid;
       bool odd = false, esc = false;
@@ -1404,7 +1520,7 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
       // the unescape command (W.recurse): an item that may be a whole-string '{key}' as written
       // goes to the literal path, which decides IE_RECURSE with the whole wave (rare: a '{' first,
       // or a '}' right after the first character)
-      active = sn < 0xFFFF0000ull && !(W.recurse && maybe_simple(s, (uint32_t)sn));
+      active = sn < 0xFFFF0000ull && !(W.recurse && maybe_simple(s, (uint32_t)sn)) && (!UNESC || lane_staged);
       if (!active) st = kStatusPending;
     }
     uint8_t r = IE_OK_STR;
@@ -1467,6 +1583,20 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
       if (slow) r = r2, olen = o2;
     }
     if (active) st = r;
+    if (UNESC && i < B.n && st == kStatusPending) {
+      // the fused unescape command finishes in the stage only: the rest goes to the deferred pass
+      st = kStatusDeferred;
+    }
+    if (UNESC) {
+      const bool dfr = i < B.n && st == kStatusDeferred;
+      const uint64_t m = __ballot(dfr);
+      if (m) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(W.udefer_count, (uint32_t)__popcll(m));
+        base = __shfl(base, 0, 64);
+        if (dfr) W.udefer_list[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)i;
+      }
+    }
     pend = i < B.n && st == kStatusPending;
     if (pend) s_pend[atomicAdd(&s_misc[1], 1u)] = (uint16_t)tid;
     s_st[tid] = st;
@@ -1496,13 +1626,13 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
     const uint64_t po = gld(B.in_off + gi), pn = in_length(B, gi);
     uint64_t rcap = W.lit_cap_max ? IE_SIZE_CAP(pn, T.maxtext) + 4 * T.maxtext + 64
                                   : 4 * pn + 4 * T.maxtext + 256;
-    rcap = (rcap + 15) & ~15ull;
+    rcap = pn >= 0xFFFF0000ull ? 0ull : (rcap + 15) & ~15ull;  // (a string the pool never took: overflow)
     uint64_t pbase = 0;
     if (lane == 0) pbase = atomicAdd((unsigned long long*)W.pool_used, (unsigned long long)(4 * rcap));
     pbase = __shfl(pbase, 0, 64);
     LitOut r{IE_E_OVERFLOW, 0, 0, IE_VID_NONE};
 #ifndef IE_EXP_NOLIT
-    if (pbase + 4 * rcap <= W.pool_bytes)
+    if (rcap && pbase + 4 * rcap <= W.pool_bytes)
 #else
     if (false)
 #endif
@@ -1621,10 +1751,13 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
   asm volatile("v_mov_b32 %0, %1" : "=v"(tid_t) : "v"(tid));
   const uint64_t i_t = first + tid_t;
   if (i_t < B.n) {
-    gsts(B.out_off + i_t, base + local);
-    if (VIEWS) gsts(B.out_len + i_t, s_st[tid_t] == IE_OK_STR ? s_olen[tid_t] : 0u);
-    gsts(B.status + i_t, st);
-    if (st == IE_OK_VALUE || st == IE_RECURSE) gst(B.value_id + i_t, s_olen[tid_t]);
+    // (a deferred subset writes at its strings' places in the batch; a string the fused unescape
+    // command deferred is written again by the deferred pass)
+    const uint64_t o_i = B.out_index ? (uint64_t)gld(B.out_index + i_t) : i_t;
+    gsts(B.out_off + o_i, base + local);
+    if (VIEWS) gsts(B.out_len + o_i, s_st[tid_t] == IE_OK_STR ? s_olen[tid_t] : 0u);
+    gsts(B.status + o_i, st);
+    if (st == IE_OK_VALUE || st == IE_RECURSE) gst(B.value_id + o_i, s_olen[tid_t]);
   }
   if (!VIEWS && last == B.n && tid == 0) {
     B.out_off[B.n] = base + tile_total;
@@ -1692,13 +1825,69 @@ hipError_t launch_debug_probe_impl(const DevTable& T, const uint8_t* key, uint32
   return hipGetLastError();
 }
 
+// the unescape command's deferred strings (see k_resolve<.., UNESC>): each block takes 256 entries
+// of the deferred list, unescapes them (recursive_unescape, py:1665) into the literal pool with one
+// claim per block (so the strings of a block lie together, in list order) and writes the views the
+// deferred resolve reads; a string the pool cannot take gets the length that resolves to
+// IE_E_OVERFLOW
+__global__ __launch_bounds__(kRBlock) void k_unesc_deferred(Batch B, Work W, uint64_t* sub_off, uint32_t* sub_len,
+                                                           uint32_t* sub_tid) {
+  __shared__ uint64_t s_red[kRBlock / 64 + 2];
+  const uint32_t count = __hip_atomic_load(W.udefer_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (uint64_t blk = blockIdx.x; blk * kRBlock < count; blk += gridDim.x) {
+    const uint64_t j = blk * kRBlock + threadIdx.x;
+    const bool on = j < count;
+    uint32_t idx = 0;
+    uint64_t so = 0, n = 0, un = 0;
+    if (on) {
+      idx = W.udefer_list[j];
+      so = gld(B.in_off + idx);
+      n = in_length(B, idx);
+    }
+    const uint8_t* const src = B.bytes + so;
+    auto dropped = [&](uint64_t k) {  // '\\' before a brace of the same string
+      return src[k] == '\\' && k + 1 < n && (src[k + 1] == '{' || src[k + 1] == '}');
+    };
+    for (uint64_t k = 0; k < n; k++) un += dropped(k) ? 0u : 1u;
+    uint64_t tot;
+    const uint64_t local = block_scan(un, s_red, &tot);
+    if (threadIdx.x == 0)
+      s_red[kRBlock / 64] = atomicAdd((unsigned long long*)W.pool_used, (unsigned long long)((tot + 15) & ~15ull));
+    __syncthreads();
+    const uint64_t base = s_red[kRBlock / 64];
+    const bool fits = base + tot <= W.pool_bytes && un < 0xFFFF0000ull;
+    if (on) {
+      if (fits) {
+        uint8_t* const dst = W.pool + base + local;
+        uint64_t w = 0;
+        for (uint64_t k = 0; k < n; k++)
+          if (!dropped(k)) dst[w++] = src[k];
+      }
+      sub_off[j] = fits ? base + local : 0;
+      sub_len[j] = fits ? (uint32_t)un : 0xFFFFFFFFu;
+      if (sub_tid) sub_tid[j] = B.table_id ? gld(B.table_id + idx) : 0u;
+    }
+    __syncthreads();
+  }
+}
+
 hipError_t launch_resolve_impl(const Batch& B, const Work& W, const DevTable& T, uint8_t* out, uint64_t cap,
-                               hipStream_t st) {
+                               hipStream_t st, bool unesc = false) {
   const uint64_t tiles = (B.n + kRBlock - 1) / kRBlock;
   if (!tiles) return hipSuccess;
   if (tiles > 0xFFFFFFFFull) return hipErrorInvalidValue;
   const uint32_t grid = (uint32_t)tiles;
   const bool multi = B.table_id != nullptr;
+  if (unesc) {  // the fused unescape command (views only)
+    if (!B.out_len) return hipErrorInvalidValue;
+    const int v = (W.fail_commit ? 2 : 0) | (multi ? 1 : 0);
+    if (v == 0) hipLaunchKernelGGL((k_resolve<false, false, true, true>), dim3(grid), dim3(kRBlock), 0, st, B, W, T, out, cap);
+    if (v == 1) hipLaunchKernelGGL((k_resolve<false, true, true, true>), dim3(grid), dim3(kRBlock), 0, st, B, W, T, out, cap);
+    if (v == 2) hipLaunchKernelGGL((k_resolve<true, false, true, true>), dim3(grid), dim3(kRBlock), 0, st, B, W, T, out, cap);
+    if (v == 3) hipLaunchKernelGGL((k_resolve<true, true, true, true>), dim3(grid), dim3(kRBlock), 0, st, B, W, T, out, cap);
+    hipLaunchKernelGGL(k_emit_windows, dim3(grid < 512u ? grid : 512u), dim3(kRBlock), 0, st, B, W, T, out);
+    return hipGetLastError();
+  }
   const int variant = (W.fail_commit ? 4 : 0) | (multi ? 2 : 0) | (B.out_len ? 1 : 0);
   switch (variant) {
 #define IE_LAUNCH(V, F, M, S) \
@@ -1719,6 +1908,25 @@ hipError_t launch_resolve_impl(const Batch& B, const Work& W, const DevTable& T,
 }
 
 }  // namespace IE_RNS
+
+#if !defined(IE_RESOLVE_WIDE)
+// The unescape command on a views batch (py:1660-1667): the fused resolve on the tiles, then the
+// strings it deferred: unescaped into the pool and resolved as a deferred subset (results written
+// at their places in the batch, bytes claimed from the same cursor). Asynchronous.
+hipError_t launch_unescape_cmd(const Batch& B, const Work& W, const DevTable& T, uint8_t* out, uint64_t cap,
+                               uint64_t* sub_off, uint32_t* sub_len, uint32_t* sub_tid, hipStream_t st) {
+  hipError_t e = IE_RNS::launch_resolve_impl(B, W, T, out, cap, st, true);
+  if (e != hipSuccess) return e;
+  // the windowed-tile list is the deferred resolve's again
+  e = hipMemsetAsync(W.defer_count, 0, sizeof(uint32_t), st);
+  if (e != hipSuccess) return e;
+  const uint64_t blocks = (B.n + kRBlock - 1) / kRBlock;
+  hipLaunchKernelGGL(IE_RNS::k_unesc_deferred, dim3((uint32_t)(blocks < 1024 ? blocks : 1024)), dim3(kRBlock), 0, st, B,
+                     W, sub_off, sub_len, sub_tid);
+  Batch D{W.pool, sub_off, B.n, B.out_off, B.status, B.value_id, sub_tid, sub_len, B.out_len, W.udefer_list, W.udefer_count};
+  return IE_RNS::launch_resolve_impl(D, W, T, out, cap, st, false);
+}
+#endif
 
 #if defined(IE_RESOLVE_WIDE)
 hipError_t launch_resolve512(const Batch& B, const Work& W, const DevTable& T, uint8_t* out, uint64_t cap,

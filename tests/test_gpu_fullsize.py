@@ -156,10 +156,12 @@ def test_full_batch_vs_oracle(config, n, layout):
     N.lib().ie_synth_free(h)
 
 
-def test_config4_full_step_vs_oracle():
+@pytest.mark.parametrize("layout", ["packed", "views"])
+def test_config4_full_step_vs_oracle(layout):
     """Config 4's whole step on its per-GPU batch (12.5M strings, rank 3's shard of the 100M):
     interpolate, then the unescape command on the results; every string against the oracle doing
-    the same (ieo_run_batch mode 1)."""
+    the same (ieo_run_batch mode 1). Views: both steps in the views layout, the command fused
+    (ie_unescape_cmd_device_views reads the first step's views)."""
     h, kvp, nkv = _synth(4)
     table = _table(kvp, nkv)
     x = N.Exec(0)
@@ -167,17 +169,28 @@ def test_config4_full_step_vs_oracle():
     first = 3 * n
     d_off, d_bytes, in_total = _device_strings(x, h, first, n)
     cap = 2 * in_total + (1 << 20)
-    r = interpolate(x, table, d_bytes, d_off, n, cap, False)
-    tmp, u = Out(x, n, cap, False), Out(x, n, cap, False)
-    N.check(N.lib().ie_unescape_cmd_device(x.h, table, None, r.bytes.ptr, r.off.ptr, n, r.status.ptr,
-                                           ctypes.byref(tmp.desc), ctypes.byref(u.desc)), "ie_unescape_cmd_device")
+    views = layout == "views"
+    r = interpolate(x, table, d_bytes, d_off, n, cap, views)
+    u = Out(x, n, cap, views)
+    if views:
+        N.check(N.lib().ie_unescape_cmd_device_views(x.h, table, None, r.bytes.ptr, r.off.ptr, r.len.ptr, n,
+                                                     r.status.ptr, ctypes.byref(u.desc)),
+                "ie_unescape_cmd_device_views")
+    else:
+        tmp = Out(x, n, cap, False)
+        N.check(N.lib().ie_unescape_cmd_device(x.h, table, None, r.bytes.ptr, r.off.ptr, n, r.status.ptr,
+                                               ctypes.byref(tmp.desc), ctypes.byref(u.desc)), "ie_unescape_cmd_device")
     x.sync()
     buf = d_bytes.to_numpy(np.uint8, in_total + 1)
     offs = d_off.to_numpy(np.uint64, n + 1)
     ref = O.Oracle.from_kv(ctypes.cast(kvp, ctypes.c_void_p), nkv, "py", clock=CLOCK)
     rst, rlen, rhash = np.zeros(n, np.uint8), np.zeros(n, np.uint64), np.zeros(n, np.uint64)
     ref.run_batch(buf, offs, n, THREADS, rst, rlen, rhash, None, unescape_cmd=True)
-    st, _, _ = assert_matches_oracle(u, rst, rlen, rhash)
+    st, starts, lens = assert_matches_oracle(u, rst, rlen, rhash)
+    if views:  # the deferred strings' bytes follow the tiles': gap-free, not in input order
+        order = np.argsort(starts[st == 0], kind="stable")
+        s_, l_ = starts[st == 0][order].astype(np.int64), lens[st == 0][order].astype(np.int64)
+        assert s_[0] == 0 and np.all(s_[1:] == s_[:-1] + l_[:-1])
     names = N.STATUS_NAMES
     assert set(np.unique(st).tolist()) == {names.index("OK_STR"), names.index("E_INTERP")}
     N.lib().ie_table_free(table)
