@@ -369,7 +369,7 @@ def main():
                          "launch_ms": round(gpu_ms, 4), "alg_bytes_per_launch": alg_bytes,
                          "telemetry": {"kernel_ms": round(tm.resolve_ms, 4), "literal_strings": int(tm.n_complex),
                                        "windowed_tiles": int(tm.n_direct), "exact_strings": int(tm.n_exact),
-                                       "chain_failures": int(tm.n_chain_fail)}},
+                                       "chain_failures": int(tm.n_chain_fail), "deferred": int(tm.n_deferred)}},
             "cpu_baseline": cpu,
         }
         if cfg == 5:

@@ -151,6 +151,8 @@ typedef struct ie_timing {
   uint64_t n_polls;      /* look-back poll rounds that found a predecessor not yet published */
   uint64_t n_exact;      /* strings the level evaluator handed to the exact event evaluator */
   uint64_t n_chain_fail; /* strings whose chain evaluation met a miss or an unspliceable hit */
+  uint64_t n_deferred;   /* views batches: strings k_lean left to k_resolve (the fused unescape
+                            command: strings left to its deferred pass) */
 } ie_timing;
 
 /* ---- library ---- */
@@ -202,6 +204,9 @@ int ie_exec_timing(ie_exec* x, ie_timing* out); /* syncs */
 #define IE_OPT_TILE 4
 #define IE_OPT_VIEWS 5 /* 1: the host batch APIs resolve into a views layout (no look-back) and pack
                           the results in input order on the host; 0 (default): packed on the device */
+#define IE_OPT_LEAN 6  /* 1: a views batch runs k_lean (one wave per 64 strings, the common string shape,
+                          output claimed in striped shards: *total is then the extent used, gaps
+                          included) and then k_resolve on the strings it left; 0 (default): k_resolve */
 int ie_exec_set_option(ie_exec* x, int32_t option, int64_t value);
 /* Literal-path scratch pool size. Setting it makes ie_interpolate_device fully asynchronous: it no
  * longer waits to check the pool's demand, and strings that ran out of it report IE_E_OVERFLOW. */

@@ -18,7 +18,7 @@ STATUS_NAMES = ["OK_STR", "OK_VALUE", "E_INTERP", "E_ASSERT_BRACES", "E_ASSERT_T
                 "E_UNHASHABLE", "E_RS_PANIC", "NEEDS_HOST", "DIVERGED", "E_OVERFLOW", "RECURSE"]
 VID_NONE, VID_HHMM, VID_HHMMSS = 0xFFFFFFFF, 0xFFFFFFFE, 0xFFFFFFFD
 TABLE_HAS_INSERTS_DIR = 1
-OPT_FAIL_COMMIT, OPT_FAST, OPT_DEBUG_NOEVAL, OPT_TILE, OPT_VIEWS = 1, 2, 3, 4, 5
+OPT_FAIL_COMMIT, OPT_FAST, OPT_DEBUG_NOEVAL, OPT_TILE, OPT_VIEWS, OPT_LEAN = 1, 2, 3, 4, 5, 6
 
 # every symbol include/ie_amd.h declares (tests check the .so exports exactly these)
 EXPORTS = [
@@ -73,7 +73,8 @@ class BatchRes(ctypes.Structure):
 class Timing(ctypes.Structure):
     _fields_ = [("resolve_ms", ctypes.c_float), ("complex_ms", ctypes.c_float),
                 ("total_ms", ctypes.c_float), ("n_complex", ctypes.c_uint64), ("n_direct", ctypes.c_uint64),
-                ("n_polls", ctypes.c_uint64), ("n_exact", ctypes.c_uint64), ("n_chain_fail", ctypes.c_uint64)]
+                ("n_polls", ctypes.c_uint64), ("n_exact", ctypes.c_uint64), ("n_chain_fail", ctypes.c_uint64),
+                ("n_deferred", ctypes.c_uint64)]
 
 
 _lib = None

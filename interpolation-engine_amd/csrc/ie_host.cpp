@@ -103,6 +103,9 @@ struct ie_exec {
   uint32_t opt_fast = 1;          // 0: exact evaluator only (IE_FAST)
   int32_t opt_tile = 0;           // k_resolve tile: 0 by call site, 256 or 512 forced (IE_TILE)
   int32_t opt_views = 0;          // host batch APIs resolve into a views layout (IE_VIEWS)
+  int32_t opt_lean = 0;           // views batches: k_lean first, k_resolve on what it lists (IE_LEAN; measured
+                                  // slower than k_resolve alone: DESIGN.md, k_lean)
+  int32_t lean_grid = 0;          // resident k_lean workgroups on the device (0: not known yet)
   bool in_cmd = false;            // inside the unescape command's second resolve
   bool cmd_first = false;         // the unescape command's unescape step (offsets zeroed on overflow)
   bool cmd_fused = false;         // the fused unescape command (views): launch_unescape_cmd
@@ -265,10 +268,12 @@ int set_device(int32_t dev) {
 // [2..3] pool bytes used (u64), [4..8] telemetry (literal strings, deferred tiles, look-back polls,
 // exact-path strings, chain failures), [9] deferred-tile count, [10..11] views output cursor (u64),
 // [12] the fused unescape command's deferred-string count; zeroed on every call.
+constexpr uint32_t kLeanShards = 16;  // k_lean's cursor shards, 128 B apart after the counters
+constexpr uint64_t kCounterBytes = 64 + kLeanShards * 128;
 int ensure_work(ie_exec* x, int op, uint64_t n) {
   const uint64_t tiles = (n + kBlock - 1) / kBlock + 1;  // (kRBlock >= kBlock: enough for k_resolve too)
   // counters, then (interpolation) the look-back words: one buffer, zeroed by one memset per call
-  IE_HIP(x->counters.ensure(64 + (op == kOpInterp ? tiles * sizeof(uint64_t) : 0)));
+  IE_HIP(x->counters.ensure(kCounterBytes + (op == kOpInterp ? tiles * sizeof(uint64_t) : 0)));
   if (op == kOpInterp) {
     IE_HIP(x->pool.ensure(x->pool_request));
     // room for every tile to be deferred (64 B of descriptor per string; grow-only, never read
@@ -296,7 +301,10 @@ Work make_work(ie_exec* x, uint64_t* total) {
   W.defer_count = (uint32_t*)x->counters.p + 9;
   W.defer_tiles = (uint32_t*)x->defer_tiles.p;
   W.defer_desc = (uint4*)x->defer_desc.p;
-  W.tile_state = (uint64_t*)((uint8_t*)x->counters.p + 64);
+  W.tile_state = (uint64_t*)((uint8_t*)x->counters.p + kCounterBytes);
+  W.shards = (uint64_t*)((uint8_t*)x->counters.p + 64);
+  W.n_shards = kLeanShards;
+  W.stripe_log2 = 18;
   W.cursor = (uint64_t*)x->counters.p + 5;  // words 10-11
   W.udefer_count = (uint32_t*)x->counters.p + 12;
   W.zero_on_overflow = x->cmd_first ? 1u : 0u;
@@ -340,7 +348,7 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
   if (x->timing) IE_HIP(hipEventRecord(x->ev[0], st));
   // the counters and, for a packed interpolation, the look-back words (one fill instead of two)
   const uint64_t zero_tiles = (op == kOpInterp && n && !d_out_len) ? (n + kRBlock - 1) / kRBlock : 0;
-  IE_HIP(hipMemsetAsync(x->counters.p, 0, 64 + zero_tiles * sizeof(uint64_t), st));
+  IE_HIP(hipMemsetAsync(x->counters.p, 0, kCounterBytes + zero_tiles * sizeof(uint64_t), st));
   if (n == 0) {
     if (!d_out_len) IE_HIP(hipMemsetAsync(out->offsets, 0, sizeof(uint64_t), st));
     IE_HIP(hipMemsetAsync(out->total, 0, sizeof(uint64_t), st));
@@ -368,6 +376,32 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
       W.udefer_list = (uint32_t*)x->u_list.p;
       IE_HIP(launch_unescape_cmd(B, W, t->dev, out->bytes, cap, (uint64_t*)x->u_off.p, (uint32_t*)x->u_len.p,
                                  d_tid ? (uint32_t*)x->u_tid.p : nullptr, st));
+    } else if (d_out_len && x->opt_lean && !x->in_cmd && !x->opt_noeval) {
+      // a views batch: k_lean, then k_resolve on the strings it listed. Stripes of 2^18 bytes (at
+      // most 16 x 256 KB of the output left unused at the shards' ends), fewer for small batches
+      // (sized from the string count, ~64 B a string: no wait for the input's byte count)
+      uint32_t slog = 14;
+      while (slog < 18 && (1ull << slog) * kLeanShards < n * 64) slog++;
+      W.stripe_log2 = slog;
+      if (!x->lean_grid) {
+        int ncu = 0;
+        IE_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, x->device));
+        const int nb = lean_blocks_per_cu(0);  // (both variants: the same registers and LDS)
+        x->lean_grid = (nb > 0 ? nb : 8) * (ncu > 0 ? ncu : 256);
+      }
+      IE_HIP(x->u_list.ensure(n * 4 + 4));
+      IE_HIP(x->u_off.ensure(n * 8 + 8));
+      IE_HIP(x->u_len.ensure(n * 4 + 4));
+      if (d_tid) IE_HIP(x->u_tid.ensure(n * 4 + 4));
+      W.udefer_list = (uint32_t*)x->u_list.p;
+      const hipError_t le = launch_lean(B, W, t->dev, out->bytes, cap, (uint64_t*)x->u_off.p, (uint32_t*)x->u_len.p,
+                                        d_tid ? (uint32_t*)x->u_tid.p : nullptr, (uint32_t)x->lean_grid, st);
+      if (le != hipSuccess) {
+        char msg[160];
+        snprintf(msg, sizeof msg, "launch_lean (step %d, grid %d): %s", lean_failed_stage(), x->lean_grid,
+                 hipGetErrorString(le));
+        return fail(IE_ERR_HIP, msg);
+      }
     } else {
       IE_HIP(wide ? launch_resolve512(B, W, t->dev, out->bytes, cap, st) : launch_resolve(B, W, t->dev, out->bytes, cap, st));
     }
@@ -493,9 +527,10 @@ int run_host(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, const 
     b->offsets[n] = w;
     delete[] b->bytes;
     b->bytes = packed;
-    if (w != total) {
+    b->bytes_len = w;  // (a views total is the extent the device used: k_lean's stripes leave gaps)
+    if (w > total) {
       ie_batch_free(b);
-      return fail(IE_ERR_HIP, "views output lengths do not add up to its total");
+      return fail(IE_ERR_HIP, "views output lengths exceed its total");
     }
   }
   for (uint64_t i = 0; i < n; i++)
@@ -929,9 +964,10 @@ int ie_exec_create(int32_t device, void* hip_stream, ie_exec** out) {
   x->device = device;
   if (const char* e = getenv("IE_FAIL_COMMIT")) x->opt_fail_commit = atoi(e) != 0 ? 1 : 0;
   if (const char* e = getenv("IE_FAST")) x->opt_fast = (uint32_t)atoi(e);
-  if (getenv("IE_DEBUG_NOEVAL")) x->opt_noeval = 1;
+  if (const char* e = getenv("IE_DEBUG_NOEVAL")) x->opt_noeval = (uint32_t)atoi(e);
   if (const char* e = getenv("IE_TILE")) x->opt_tile = atoi(e) == 512 ? 512 : atoi(e) == 256 ? 256 : 0;
   if (const char* e = getenv("IE_VIEWS")) x->opt_views = atoi(e) != 0;
+  if (const char* e = getenv("IE_LEAN")) x->opt_lean = atoi(e) != 0;
   if (const char* e = getenv("IE_DEBUG_STAMPS")) x->stamps_path = e;
   if (hip_stream) {
     x->stream = (hipStream_t)hip_stream;
@@ -1001,6 +1037,9 @@ int ie_exec_timing(ie_exec* x, ie_timing* out) {
   out->n_direct = st[5];  // tiles deferred to the windowed emit (counter word 9)
   out->n_polls = st[2];
   out->n_exact = st[3];
+  uint32_t nd = 0;
+  if (x->counters.p) IE_HIP(hipMemcpy(&nd, (uint32_t*)x->counters.p + 12, 4, hipMemcpyDeviceToHost));
+  out->n_deferred = nd;
   out->n_chain_fail = st[4];
   return check_device_error(x);
 }
@@ -1056,6 +1095,9 @@ int ie_exec_set_option(ie_exec* x, int32_t option, int64_t value) {
       return IE_SUCCESS;
     case IE_OPT_VIEWS:
       x->opt_views = value ? 1 : 0;
+      return IE_SUCCESS;
+    case IE_OPT_LEAN:
+      x->opt_lean = value ? 1 : 0;
       return IE_SUCCESS;
     default:
       return fail(IE_ERR_INVALID, "unknown exec option");

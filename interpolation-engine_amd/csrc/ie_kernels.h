@@ -55,7 +55,8 @@ struct Work {
   uint32_t* stats;       // 5   telemetry: literal strings, direct tiles, look-back polls, exact-path
                          //     strings, chain failures (the adaptive variant choice)
   uint64_t* stamps;      // diagnostic (IE_DEBUG_STAMPS): 8 words per tile, or null
-  uint32_t debug_noeval; // diagnostic (IE_DEBUG_NOEVAL): copy strings verbatim (pipeline floor)
+  uint32_t debug_noeval; // diagnostic (IE_DEBUG_NOEVAL): bit 0 copy strings verbatim (pipeline floor),
+                         // bit 1 views tiles claim no output range (the range at twice the input offset)
   uint32_t fast_mode;    // level evaluator: 1 on (default), 0 off; diagnostics 2 = parse only, 3 = no probes
   uint8_t* pool;         // literal-path scratch
   uint64_t* pool_used;   // 1
@@ -71,6 +72,11 @@ struct Work {
   // staged, or needing the literal path) are listed here for the deferred pass
   uint32_t* udefer_list;  // n
   uint32_t* udefer_count; // 1
+  // k_lean (views output): R cursor shards (u64 words 16 apart; shard r owns the output stripes
+  // r, r + R, ... of 2^stripe_log2 bytes), zeroed per call
+  uint64_t* shards;
+  uint32_t n_shards;     // a power of two
+  uint32_t stripe_log2;
   uint32_t recurse;      // k_resolve in the unescape command (py dialect): whole-string items whose
                          // result recursive_interpolate walks again report IE_RECURSE
   uint32_t zero_on_overflow; // escape kernels: when the output exceeds its capacity, write every
@@ -107,6 +113,12 @@ hipError_t launch_cap_check(const uint64_t* total, uint64_t cap, uint32_t* err, 
 // staging), then the deferred strings: unescaped into the pool (k_unesc_deferred), resolved again
 hipError_t launch_unescape_cmd(const Batch& B, const Work& W, const DevTable& T, uint8_t* out, uint64_t cap,
                                uint64_t* sub_off, uint32_t* sub_len, uint32_t* sub_tid, hipStream_t st);
+// k_lean on a views batch (ie_lean.hip), then k_resolve on the strings it listed (their views in
+// sub_off / sub_len / sub_tid); grid_cap: resident 64-lane workgroups of the device
+hipError_t launch_lean(const Batch& B, const Work& W, const DevTable& T, uint8_t* out, uint64_t cap, uint64_t* sub_off,
+                       uint32_t* sub_len, uint32_t* sub_tid, uint32_t grid_cap, hipStream_t st);
+int lean_blocks_per_cu(int multi);
+int lean_failed_stage();
 hipError_t launch_status_carry(const uint8_t* before, uint8_t* after, uint64_t n, hipStream_t st);
 hipError_t launch_debug_probe(const DevTable& T, const uint8_t* key, uint32_t klen, uint64_t* out,
                               hipStream_t st);

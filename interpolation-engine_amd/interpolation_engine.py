@@ -271,6 +271,7 @@ _CACHE_SIZE = 8
 _cache = {}  # (id(inserts), dialect, device) -> (inserts, InsertsTable), least recently used first
 _DIR_TTL = 1.0  # seconds a directory snapshot is reused before the directory is read again
 _dir_snap = {}  # path -> (time read, version, {key: value})
+_dir_bad = {}   # file path -> the error reading it raised (left out of the snapshot)
 
 
 def _is_arg_key(k):
@@ -301,12 +302,18 @@ def read_inserts_dir(path):
     for key in sorted(set(plain) | set(j5)):
         if key in ("", "HH:MM", "HH:MM:SS") or _is_arg_key(key):
             continue
-        if key in j5:  # py:455-456
-            with open(j5[key]) as fh:
-                raw[key] = json5_loads(fh.read())
-        else:          # py:457-459
-            with open(plain[key]) as fh:
-                raw[key] = fh.read().strip()
+        try:
+            if key in j5:  # py:455-456
+                with open(j5[key]) as fh:
+                    raw[key] = json5_loads(fh.read())
+            else:          # py:457-459
+                with open(plain[key]) as fh:
+                    raw[key] = fh.read().strip()
+        except (OSError, UnicodeDecodeError, ValueError) as e:
+            # a file the reference could not read either: it raises only when that key is looked
+            # up (py:452-461), so one bad file must not break every other lookup; the key stays out
+            # of the snapshot (inserts directory: a lookup of it reports a miss here)
+            _dir_bad[os.path.join(path, key)] = e
     return raw
 
 

@@ -43,7 +43,8 @@ def test_header_constants_match_the_binding():
     defs = dict(re.findall(r"#define (IE_OPT_[A-Z_]+) (-?\d+)", src))
     assert {k: int(v) for k, v in defs.items()} == {
         "IE_OPT_FAIL_COMMIT": N.OPT_FAIL_COMMIT, "IE_OPT_FAST": N.OPT_FAST,
-        "IE_OPT_DEBUG_NOEVAL": N.OPT_DEBUG_NOEVAL, "IE_OPT_TILE": N.OPT_TILE, "IE_OPT_VIEWS": N.OPT_VIEWS}
+        "IE_OPT_DEBUG_NOEVAL": N.OPT_DEBUG_NOEVAL, "IE_OPT_TILE": N.OPT_TILE, "IE_OPT_VIEWS": N.OPT_VIEWS,
+        "IE_OPT_LEAN": N.OPT_LEAN}
 
 
 def test_abi_version():

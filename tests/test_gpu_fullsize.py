@@ -115,33 +115,48 @@ def assert_matches_oracle(o, ref_st, ref_len, ref_hash):
     ok = st == 0
     bad = np.flatnonzero(ok & (lens != ref_len))
     assert bad.size == 0, ("length", bad.size, bad[:8])
-    assert int(lens.sum()) == o.total()  # nothing but the results in the payload
+    if o.views:  # a views payload: disjoint results inside the extent used (k_lean leaves gaps)
+        assert_views_disjoint(starts, lens, o.total())
+    else:
+        assert int(lens.sum()) == o.total()  # nothing but the results in the payload
     hs = O.hash_spans(blob, starts, lens, st, THREADS)
     bad = np.flatnonzero(hs != ref_hash)
     assert bad.size == 0, ("bytes", bad.size, bad[:8])
     return st, starts, lens
 
 
+def assert_views_disjoint(starts, lens, total):
+    """Every result inside [0, total), no two overlapping (total: the extent the device used)."""
+    starts, lens = np.asarray(starts, np.int64), np.asarray(lens, np.int64)
+    nz = lens > 0
+    s, l = starts[nz], lens[nz]
+    assert np.all(s + l <= total) and int(l.sum()) <= total
+    o = np.argsort(s, kind="stable")
+    assert np.all(s[o][1:] >= (s[o] + l[o])[:-1])
+
+
 def assert_views_packing(starts, lens, total, n, tile=256):
-    """A views output is gap-free, and each tile's strings lie together in input order."""
-    order = np.argsort(starts, kind="stable")
-    s, l = starts[order].astype(np.int64), lens[order].astype(np.int64)
-    assert s[0] == 0 and int(s[-1] + l[-1]) == total
-    assert np.all(s[1:] == s[:-1] + l[:-1])
+    """A views output's 256-string tiles: each tile's strings lie together in input order, except
+    the rare string k_lean moved off a stripe boundary; the gaps (stripe ends) stay small."""
+    starts, lens = starts.astype(np.int64), lens.astype(np.int64)
+    assert total - int(lens.sum()) <= max(int(lens.sum()) // 50, 8 << 20)
     idx = np.arange(n)
     same_tile = (idx[1:] // tile) == (idx[:-1] // tile)
-    assert np.all((starts[1:].astype(np.int64) == starts[:-1].astype(np.int64) + lens[:-1].astype(np.int64))[same_tile])
+    follows = starts[1:] == starts[:-1] + lens[:-1]
+    assert np.count_nonzero(~follows[same_tile]) <= 2 * (total >> 14) + 16
 
 
-@pytest.mark.parametrize("layout", ["packed", "views"])
+@pytest.mark.parametrize("layout", ["packed", "views", "views-lean"])
 @pytest.mark.parametrize("config,n", [(2, 1_000_000), (3, 10_000_000)], ids=["cfg2-1M", "cfg3-10M"])
-def test_full_batch_vs_oracle(config, n, layout):
-    """Every string of the BASELINE-size batch against the oracle (status, length, bytes)."""
+def test_full_batch_vs_oracle(config, n, layout, monkeypatch):
+    """Every string of the BASELINE-size batch against the oracle (status, length, bytes); views-lean:
+    k_lean first (IE_LEAN), k_resolve on what it leaves."""
+    monkeypatch.setenv("IE_LEAN", "1" if layout == "views-lean" else "0")
     h, kvp, nkv = _synth(config)
     table = _table(kvp, nkv)
     x = N.Exec(0)
     d_off, d_bytes, in_total = _device_strings(x, h, 0, n)
-    views = layout == "views"
+    views = layout.startswith("views")
     o = interpolate(x, table, d_bytes, d_off, n, 2 * in_total + (1 << 20), views)
     buf = d_bytes.to_numpy(np.uint8, in_total + 1)
     offs = d_off.to_numpy(np.uint64, n + 1)

@@ -30,9 +30,9 @@ def run_product(table_dict, strings, dialect="py", has_dir=False):
     return t.run(strings), t
 
 
-@pytest.fixture(params=["0", "1", "1w", "0v", "1v"],
+@pytest.fixture(params=["0", "1", "1w", "0v", "1v", "0lv"],
                 ids=["chain-fail-exact", "chain-fail-commit", "chain-fail-commit-512", "chain-fail-exact-views",
-                     "chain-fail-commit-views"])
+                     "chain-fail-commit-views", "chain-fail-exact-views-lean"])
 def fail_commit(request, monkeypatch):
     """Both k_resolve variants: chain failures sent to the exact evaluator, or committed in the
     chain evaluator (the library picks one adaptively; IE_FAIL_COMMIT / IE_OPT_FAIL_COMMIT force it);
@@ -42,6 +42,8 @@ def fail_commit(request, monkeypatch):
     cached exec is set directly. Yields the fail-commit digit; VIEWS[0] tells _device_run."""
     fc, tile = request.param[0], 512 if request.param.endswith("w") else 0
     views = 1 if request.param.endswith("v") else 0
+    lean = 1 if "l" in request.param else 0  # k_lean first (ie_lean.hip), k_resolve on what it leaves
+    monkeypatch.setenv("IE_LEAN", str(lean))
     monkeypatch.setenv("IE_FAIL_COMMIT", fc)
     monkeypatch.setenv("IE_TILE", str(tile))
     monkeypatch.setenv("IE_VIEWS", str(views))
@@ -49,9 +51,11 @@ def fail_commit(request, monkeypatch):
     x.set_option(N.OPT_FAIL_COMMIT, int(fc))
     x.set_option(N.OPT_TILE, tile)
     x.set_option(N.OPT_VIEWS, views)
+    x.set_option(N.OPT_LEAN, lean)
     VIEWS[0] = bool(views)
     yield fc
     VIEWS[0] = False
+    x.set_option(N.OPT_LEAN, 0)
     x.set_option(N.OPT_FAIL_COMMIT, -1)
     x.set_option(N.OPT_TILE, 0)
     x.set_option(N.OPT_VIEWS, 0)
@@ -382,6 +386,17 @@ class DevResult:
         return int(self.total_d.to_numpy(np.uint64, 1)[0])
 
 
+def assert_views_disjoint(starts, lens, total):
+    """A views output: every result inside [0, total) and no two overlapping (k_lean's stripes may
+    leave gaps, so total is the extent used, at least the sum of the lengths)."""
+    starts, lens = np.asarray(starts, np.int64), np.asarray(lens, np.int64)
+    nz = lens > 0
+    s, l = starts[nz], lens[nz]
+    assert np.all(s + l <= total) and int(l.sum()) <= total
+    o = np.argsort(s, kind="stable")
+    assert np.all(s[o][1:] >= (s[o] + l[o])[:-1])
+
+
 def _device_run(x, table, d_bytes, d_off, n, cap=None):
     """A packed result; with the views fixture the device writes views, packed here on the host in
     input order (the check then runs on the same packed form)."""
@@ -400,12 +415,13 @@ def _device_run(x, table, d_bytes, d_off, n, cap=None):
     starts = r.off.to_numpy(np.uint64, n)
     ln = lens.to_numpy(np.uint32, n).astype(np.uint64)
     blob = r.bytes.to_numpy(np.uint8, tot)
-    assert int(ln.sum()) == tot
+    assert_views_disjoint(starts, ln, tot)
     packed = np.concatenate([blob[int(starts[i]):int(starts[i] + ln[i])] for i in range(n)]) if n else blob
     offs = np.zeros(n + 1, np.uint64)
     offs[1:] = np.cumsum(ln)
     r.bytes = N.DeviceBuffer.from_numpy(x, np.concatenate([packed, np.zeros(16, np.uint8)]))
     r.off = N.DeviceBuffer.from_numpy(x, offs)
+    r.total_d = N.DeviceBuffer.from_numpy(x, offs[-1:].copy())  # the packed form's total
     return r
 
 

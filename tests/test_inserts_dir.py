@@ -90,3 +90,19 @@ def test_device_mirror_with_inserts_dir(tmp_path):
             pkg.interpolate_inserts({}, "{../outside}")
     finally:
         M.inserts_dir = old
+
+
+def test_bad_file_stays_out_of_the_snapshot(tmp_path):
+    """One unreadable file (not UTF-8, a broken .json5) must not break the other lookups: the
+    reference raises only when that key is looked up (py:452-461); the snapshot leaves it out."""
+    G.load_package()
+    from interpolation_engine_amd import interpolation_engine as M
+    d = make_dir(tmp_path)
+    with open(os.path.join(d, "binary"), "wb") as f:
+        f.write(b"\xff\xfe\x00 not utf-8")
+    with open(os.path.join(d, "broken.json5"), "w") as f:
+        f.write("{unterminated: ")
+    raw = M.read_inserts_dir(d)
+    assert "binary" not in raw and "broken" not in raw
+    assert raw["count"] == 42
+    assert os.path.join(d, "binary") in M._dir_bad and os.path.join(d, "broken") in M._dir_bad
