@@ -238,7 +238,8 @@ constexpr uint32_t kChainMax = 112;
 __device__ __forceinline__ bool parse_chains(const lds_u8* tile, uint32_t p0, uint32_t n, const lds_u32* cm,
                                              const lds_u32* oddbits, const lds_u32* escbits, bool active,
                                              uint32_t (&crec)[kMaxTop], uint32_t (&cdep)[kMaxTop], uint32_t& nch,
-                                             Ev& Om_out, Ev& Cm_out, uint32_t& maxd_out) {
+                                             Ev& Om_out, Ev& Cm_out, uint32_t& maxd_out, bool& whole_out) {
+  whole_out = false;
   if (active && n > kChainMax) {
     // a long string is copied verbatim when none of its bytes is a brace and its chunks hold no
     // U+3020 lead byte (no pair to resolve, no placeholder to collide with: py:505-540 leave it
@@ -261,6 +262,7 @@ __device__ __forceinline__ bool parse_chains(const lds_u8* tile, uint32_t p0, ui
   bool ok = active && n <= kChainMax;
   // ---- 1. the string's open / close events as 128-bit windows ----
   uint32_t O[4], C[4];
+  bool any_esc = false;
   {
     const uint32_t c0 = ok ? p0 >> 4 : 0u, o = p0 & 15u;
     const uint32_t cl = ok && n ? (p0 + n - 1) >> 4 : c0;
@@ -270,6 +272,7 @@ __device__ __forceinline__ bool parse_chains(const lds_u8* tile, uint32_t p0, ui
     if ((ob >> (c0 & 31)) & span_m) ok = false;
     const uint64_t eb = ((uint64_t)escbits[(c0 >> 5) + 1] << 32) | escbits[c0 >> 5];
     const bool esc = ok && ((eb >> (c0 & 31)) & span_m) != 0;
+    any_esc = esc;
     uint32_t Wo[5], Wc[5];
 #pragma unroll
     for (int j = 0; j < 5; j++) {
@@ -356,7 +359,13 @@ __device__ __forceinline__ bool parse_chains(const lds_u8* tile, uint32_t p0, ui
     pos = take ? end + 1u : pos;
   }
   bad |= ev_first(ev_from(Ev{Om.lo | Cm.lo, Om.hi | Cm.hi}, pos)) < 128u;  // more than kMaxTop chains
-  ok = !bad && !(nch == 1 && whole);  // a whole-string pair: typed result (py:510-514), exact evaluator
+  // A whole-string pair is get_simple_insertkey-truthy (py:477-495, typed result py:510-514). The
+  // plain form -- one pair, no nesting, a non-empty key, no '\\' anywhere near (an escaped brace
+  // inside would break py's depth walk) -- is one lookup whose raw value is the result: the jobs
+  // take it (whole_out); every other whole-string pair goes to the exact evaluator.
+  const bool whole1 = !bad && nch == 1 && whole && cdep[0] == 1u && !any_esc && ((crec[0] >> 8) & 0xFFu) > 1u;
+  ok = !bad && (!(nch == 1 && whole) || whole1);
+  whole_out = ok && whole1;
   Om_out = Om, Cm_out = Cm;  // middle levels (depth > 2) are found from these masks in their round
   maxd_out = ok ? maxd : 0u;
   return ok;

@@ -326,8 +326,11 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(IE_LEAN_W
     const uint32_t tb = (MULTI && valid) ? gld(B.table_id + i) : 0u;
     uint32_t crec[kMaxTop], cdep[kMaxTop], nch = 0, maxd = 0;
     Ev Om, Cm;
+    bool whole1;  // (a whole-string '{key}': k_resolve's chain jobs take it, here the fallback)
     bool ok = parse_chains((const lds_u8*)s_stage, staged ? p0 : 0u, staged ? n32 : 0u, (const lds_u32*)s_cm,
-                           (const lds_u32*)s_odd, (const lds_u32*)s_esc, staged, crec, cdep, nch, Om, Cm, maxd);
+                           (const lds_u32*)s_odd, (const lds_u32*)s_esc, staged, crec, cdep, nch, Om, Cm, maxd,
+                           whole1);
+    ok = ok && !whole1;
     const lds_u8* const s = (const lds_u8*)s_stage + (staged ? p0 : 0u);
     uint32_t rk[kMaxTop], rs[kMaxTop];  // per chain: value kind << 30 | text length; entry / arena offset
     bool rej = false;

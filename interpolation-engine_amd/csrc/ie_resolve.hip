@@ -406,6 +406,7 @@ struct ChainJobs {  // LDS views, tile-wide
 };
 constexpr uint32_t kJobCap = kMaxTop * kRBlock;
 constexpr uint32_t kResFail = 1u << 29, kResReject = 1u << 28;
+constexpr uint32_t kResWhole = 1u << 27;  // a whole-string '{key}' (res_s: the value id; kind bits 0-2)
 
 // The jobs [j0, j0 + 2 * kRBlock) of the tile: lane t takes jobs j0 + t and j0 + kRBlock + t. Round r
 // resolves level r of each job (the innermost pair in round 0); the key of a level is A | T | B
@@ -420,7 +421,7 @@ __device__ void resolve_jobs(const DevTable& T, const lds_u8* tile, const ChainJ
                              bool& chain_fail, uint64_t* stamp) {
   constexpr int NJ = 2;
   const uint32_t tid = threadIdx.x;
-  bool on[NJ], done[NJ];
+  bool on[NJ], done[NJ], wh[NJ];
   uint32_t job[NJ], cr[NJ], dep[NJ], ls[NJ], tb[NJ], res_k[NJ], res_s[NJ];
   const lds_u8* s[NJ];
   uint32_t ct[NJ][4], ctl[NJ], co_[NJ], cl_[NJ];
@@ -432,7 +433,8 @@ __device__ void resolve_jobs(const DevTable& T, const lds_u8* tile, const ChainJ
     cr[q] = valid ? J.crec[job[q]] : 0u;
     const uint32_t mt = valid ? (uint32_t)J.meta[job[q]] : 0u;
     ls[q] = mt & 0xFFFu;
-    dep[q] = valid ? mt >> 12 : 0u;
+    dep[q] = valid ? (mt >> 12) & 7u : 0u;
+    wh[q] = valid && (mt >> 15) != 0u;  // a whole-string '{key}': the raw value, any type
     s[q] = tile + (valid ? (uint32_t)J.p0[ls[q]] : 0u);
     tb[q] = valid ? J.tbl[ls[q]] : 0u;
     done[q] = !valid;
@@ -506,13 +508,16 @@ __device__ void resolve_jobs(const DevTable& T, const lds_u8* tile, const ChainJ
       stamp[13] = __builtin_amdgcn_s_memrealtime();
     }
     Probe P[NJ];
+    uint32_t wvid[NJ];
 #pragma unroll
     for (int q = 0; q < NJ; q++) {
+      wvid[q] = IE_VID_NONE;
       if (__any(on[q])) {
         const uint4* e = (const uint4*)(T.entries + slot[q]);
         P[q].q0 = gld4(e);
         P[q].q1 = gld4(e + 1);
         P[q].q2 = gld4(e + 2);
+        if (__any(on[q] && wh[q])) wvid[q] = on[q] && wh[q] ? gld(&T.entries[slot[q]].vid) : IE_VID_NONE;
       }
     }
     if (stamp && threadIdx.x == 0 && r < 2) {  // diagnostic: entries arrived
@@ -526,11 +531,13 @@ __device__ void resolve_jobs(const DevTable& T, const lds_u8* tile, const ChainJ
       const bool hit = on[q] && (entry_head_ok(E.q0, klen[q], tb[q]) & (E.q1.x == kw[q].x) & (E.q1.y == kw[q].y) &
                                  (E.q1.z == kw[q].z) & (E.q1.w == kw[q].w));
       const uint32_t flags = E.q0.z, tlen = E.q0.y;
-      const bool good = hit && (flags & EF_SPLICE_OK) && (flags & EF_INERT);
+      // (a whole-string '{key}' takes any hit: its result is the raw value, nothing is spliced)
+      const bool good = hit && (wh[q] || ((flags & EF_SPLICE_OK) && (flags & EF_INERT)));
       // a miss (no inserts-dir: py:465 / interp.rs:136) or a hit that cannot be spliced
       // (py:530 / interp.rs:76-79) fails this pair; a hit on a value needing care, or a miss that
       // the inserts-dir might resolve, goes to the exact evaluator
-      const bool would_fail = on[q] && ((!hit && !(T.flags & TF_HAS_DIR)) || (hit && !(flags & EF_SPLICE_OK)));
+      const bool would_fail =
+          on[q] && ((!hit && !(T.flags & TF_HAS_DIR)) || (hit && !wh[q] && !(flags & EF_SPLICE_OK)));
       chain_fail |= would_fail;  // the adaptive variant choice counts these (either variant)
       const bool fail = FAILC && would_fail;
       const bool top = r + 1 == dep[q];
@@ -548,8 +555,8 @@ __device__ void resolve_jobs(const DevTable& T, const lds_u8* tile, const ChainJ
       }
       if (on[q] && good && top) {
         uint32_t src;
-        res_k[q] = value_kl(tlen, E.q0.w, slot[q], src);
-        res_s[q] = src;
+        res_k[q] = wh[q] ? (kResWhole | (flags & EF_KIND_MASK)) : value_kl(tlen, E.q0.w, slot[q], src);
+        res_s[q] = wh[q] ? wvid[q] : src;
         done[q] = true;
       }
     }
@@ -567,7 +574,19 @@ __device__ void resolve_jobs(const DevTable& T, const lds_u8* tile, const ChainJ
 // a failed job (FAILC) makes the string fail with the status of the failing pair with the largest
 // opening offset (the reference resolves the rightmost chain first and stops at its first failure)
 __device__ bool combine_chains(const ChainJobs J, uint32_t jb, uint32_t nch, const uint32_t (&crec)[kMaxTop],
-                               uint32_t n, Desc& d, uint32_t& out_len, uint8_t& status) {
+                               uint32_t n, Desc& d, uint32_t& out_len, uint8_t& status, uint32_t& vid,
+                               uint32_t& vflags) {
+  if (nch == 1u) {  // a whole-string '{key}' job: its raw value is the typed result (py:510-514)
+    const uint32_t rk = J.res_k[jb];
+    if ((rk & kResWhole) && !(rk & (kResFail | kResReject)) && (rk >> 30) == 0u) {
+      d.ntop = 0;
+      out_len = 0;
+      status = IE_OK_VALUE;
+      vid = J.res_s[jb];
+      vflags = rk & EF_KIND_MASK;
+      return true;
+    }
+  }
   bool ok = true;
   uint32_t fw = 0, vsum = 0, span = 0;
 #pragma unroll
@@ -1191,8 +1210,9 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
       uint32_t crec[kMaxTop], cdep[kMaxTop], nch = 0;
       Ev Om, Cm;
       uint32_t maxd;
+      bool whole1;
       const bool pok = parse_chains((const lds_u8*)s_in, p0, (uint32_t)sn, s_cm, s_odd, s_esc, active && lane_staged,
-                                    crec, cdep, nch, Om, Cm, maxd);
+                                    crec, cdep, nch, Om, Cm, maxd, whole1);
       if (__any(maxd > 2u)) {  // middle levels are found from these masks in their round
         ev[0] = Om.lo, ev[kRBlock] = Om.hi, ev[2 * kRBlock] = Cm.lo, ev[3 * kRBlock] = Cm.hi;
       }
@@ -1209,7 +1229,7 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
         for (int c = 0; c < kMaxTop; c++) {
           if ((uint32_t)c < nch) {
             J.crec[jb + c] = crec[c];
-            J.meta[jb + c] = (uint16_t)(tid | (cdep[c] << 12));
+            J.meta[jb + c] = (uint16_t)(tid | (cdep[c] << 12) | (whole1 ? 0x8000u : 0u));
           }
         }
       }
@@ -1221,7 +1241,7 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
       IE_STAMP(10);
       __syncthreads();
       IE_STAMP(11);
-      const bool fast = pok && combine_chains(J, jb, nch, crec, (uint32_t)sn, d, olen, r);
+      const bool fast = pok && combine_chains(J, jb, nch, crec, (uint32_t)sn, d, olen, r, vid, vflags);
       __syncthreads();  // the job arrays are free (the exact evaluator's scratch)
       IE_STAMP(12);
       slow = active && !fast;
