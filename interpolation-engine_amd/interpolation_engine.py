@@ -25,6 +25,7 @@ import ctypes
 import datetime as _dt
 import json
 import os
+import re
 import time
 
 from . import _native as N
@@ -101,6 +102,7 @@ class InsertsTableSet:
         self.clock = tuple(clock)
         self.dialect = dialect
         self.device = device
+        self.has_dir = bool(has_inserts_dir)
         self.dicts = list(dicts)
         self.keys, self.values, starts = [], [], [0]
         for d in self.dicts:
@@ -186,9 +188,60 @@ class InsertsTableSet:
                 out.append(payload)
             elif st == N.OK_VALUE:
                 out.append(self.value(payload))
+            elif self.has_dir and inserts_dir and (st == N.NEEDS_HOST or (st == N.E_INTERP and _dir_bad)):
+                out.append(self._host_complete(s, t, st))
             else:
                 out.append(_exception(s, st, self.table_keys(t)))
         return out
+
+    def _host_complete(self, s, t, st):
+        """The inserts-directory lookups the device hands to the host (get_interpdata's file
+        fallback, py:452-461). IE_NEEDS_HOST: a key that is not a canonical relative file name
+        (os.path.join may leave the directory, so no snapshot holds it): the host opens the files
+        the string's literal keys name (and keys inside what it read), adds what it finds to the
+        string's dict and resolves the string on the device again; a key whose files are missing is
+        the reference's miss. IE_E_INTERP with unreadable files in the directory: the reference
+        raises that file's error when its key is looked up. Returns a result or an exception."""
+        keys = _literal_keys(s)
+        if st == N.E_INTERP:
+            for k in keys:
+                e = _dir_bad.get(os.path.join(inserts_dir, k))
+                if e is not None:
+                    return e
+            return _exception(s, st, self.table_keys(t))
+        base = self.dicts[t]
+        extras, missing = {}, set()
+        for _ in range(8):
+            found = keys + [k for v in extras.values() if isinstance(v, str) for k in _literal_keys(v)]
+            cands = [k for k in dict.fromkeys(found)
+                     if not _canonical_key(k) and k not in base and k not in extras and k not in missing]
+            if not cands:
+                break
+            for k in cands:
+                try:
+                    extras[k] = _read_dir_key(k)
+                except FileNotFoundError:
+                    missing.add(k)
+                except Exception as e:  # noqa: BLE001 — IsADirectoryError, UnicodeDecodeError, a JSON5 error
+                    return e
+            tbl = InsertsTable(base, dialect=self.dialect, clock=self.clock, device=self.device,
+                               has_inserts_dir=True, extra=extras)
+            try:
+                st2, payload = tbl.run([s])[0]
+                if st2 == N.OK_STR:
+                    return payload
+                if st2 == N.OK_VALUE:
+                    return tbl.value(payload)
+                if st2 != N.NEEDS_HOST:
+                    return _exception(s, st2, tbl.table_keys(0))
+            finally:
+                tbl.close()
+        for k in sorted(missing):
+            try:
+                get_interpdata(base, k)
+            except InterpolationException as e:
+                return e
+        return _exception(s, N.NEEDS_HOST, self.table_keys(t))
 
 
 class InsertsTable(InsertsTableSet):
@@ -272,6 +325,40 @@ _cache = {}  # (id(inserts), dialect, device) -> (inserts, InsertsTable), least 
 _DIR_TTL = 1.0  # seconds a directory snapshot is reused before the directory is read again
 _dir_snap = {}  # path -> (time read, version, {key: value})
 _dir_bad = {}   # file path -> the error reading it raised (left out of the snapshot)
+
+
+_LITERAL_KEY = re.compile(r"\{([^{}]*)\}")
+
+
+def _literal_keys(s):
+    """The innermost brace contents of s: the keys it spells out literally (escapes kept)."""
+    return _LITERAL_KEY.findall(s)
+
+
+def _canonical_key(k):
+    """The device's rule (ie_device.h missing_status): a key that names a file inside the inserts
+    directory (components separated by single '/', none empty, '.' or '..', no NUL); '' is a
+    plain miss."""
+    if k == "":
+        return True
+    return "\0" not in k and all(c not in ("", ".", "..") for c in k.split("/"))
+
+
+def _read_dir_key(key):
+    """get_interpdata's file fallback for one key (py:452-461): `<key>.json5` parsed, else `<key>`
+    stripped, escaped (recursive_escape on the device); raises FileNotFoundError when neither
+    exists, or whatever opening / reading / parsing the file raised."""
+    from .program import loads as json5_loads
+    try:
+        with open(os.path.join(inserts_dir, f"{insertkey_str(key)}.json5")) as f:
+            return recursive_escape(json5_loads(f.read()))
+    except FileNotFoundError:
+        with open(os.path.join(inserts_dir, insertkey_str(key))) as f:
+            return recursive_escape(f.read().strip())
+
+
+def insertkey_str(key):
+    return key if isinstance(key, str) else str(key)
 
 
 def _is_arg_key(k):
@@ -399,13 +486,7 @@ def get_interpdata(inserts, insertkey):
         return inserts[insertkey]
     if inserts_dir:  # py:452-461
         try:
-            try:
-                with open(os.path.join(inserts_dir, f"{insertkey}.json5")) as f:
-                    from .program import loads as json5_loads
-                    return recursive_escape(json5_loads(f.read()))
-            except FileNotFoundError:
-                with open(os.path.join(inserts_dir, insertkey)) as f:
-                    return recursive_escape(f.read().strip())
+            return _read_dir_key(insertkey)
         except FileNotFoundError:
             pass
     detail = " in interpdata" + (" or inserts directory '%s'" % inserts_dir if inserts_dir else "")

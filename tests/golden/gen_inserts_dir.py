@@ -56,7 +56,16 @@ CASES = [
 ]
 
 
-def classify(ie, inserts, s):
+# keys that are not canonical relative file names (os.path.join may leave the directory, py:455-459)
+# and files the reference cannot read: the directory is <base>/dir, these files sit in <base>
+OUTSIDE_FILES = {"outside": "an outside {name} file", "outside_j.json5": "'outside json5'", "dir2/leaf": "second dir"}
+BAD_FILES = {"binary": "fffe00206e6f74207574662d38", "broken.json5": "7b756e7465726d696e617465643a20"}  # hex
+OUTSIDE_CASES = ["{../outside}", "a{../outside}b", "{../outside_j}", "{../nope}", "x{../nope}y", "{sub/../count}",
+                 "{./over}", "{sub//leaf}", "{../dir2/leaf}", "{../dir/plain}", "{binary}", "x{binary}y", "{broken}",
+                 "{q-{../nope}}"]
+
+
+def classify(ie, inserts, s, other_errors=False):
     try:
         r = ie.interpolate_inserts(inserts, s)
     except ie.InterpolationException:
@@ -67,6 +76,10 @@ def classify(ie, inserts, s):
         if "unhashable" in str(e):
             return {"st": "E_UNHASHABLE"}
         raise
+    except Exception as e:  # noqa: BLE001 — a file the reference could not read (its own error)
+        if not other_errors:
+            raise
+        return {"st": "RAISES", "exc": type(e).__name__}
     protected = s.replace("\\{", ".〠").replace("\\}", "〠.")
     if ie.get_simple_insertkey(protected):
         return {"st": "OK_VALUE", "value": r}
@@ -98,9 +111,29 @@ def main():
                 continue  # the clock: covered by the main fixtures
             rec["s"] = s
             cases.append(rec)
+    with tempfile.TemporaryDirectory() as base:
+        d = os.path.join(base, "dir")
+        for rel, text in FILES.items():
+            os.makedirs(os.path.dirname(os.path.join(d, rel)), exist_ok=True)
+            with open(os.path.join(d, rel), "w") as f:
+                f.write(text)
+        for rel, text in OUTSIDE_FILES.items():
+            os.makedirs(os.path.dirname(os.path.join(base, rel)), exist_ok=True)
+            with open(os.path.join(base, rel), "w") as f:
+                f.write(text)
+        for rel, hx in BAD_FILES.items():
+            with open(os.path.join(d, rel), "wb") as f:
+                f.write(bytes.fromhex(hx))
+        ie.inserts_dir = d
+        outside = []
+        for s in OUTSIDE_CASES:
+            rec = classify(ie, dict(INSERTS), s, other_errors=True)
+            rec["s"] = s
+            outside.append(rec)
     with open(os.path.join(HERE, "inserts_dir_py.json"), "w", encoding="utf-8") as f:
-        json.dump({"files": FILES, "inserts": INSERTS, "cases": cases}, f, ensure_ascii=False, indent=0)
-    print("inserts_dir_py.json: %d cases" % len(cases))
+        json.dump({"files": FILES, "inserts": INSERTS, "cases": cases, "outside_files": OUTSIDE_FILES,
+                   "bad_files": BAD_FILES, "outside_cases": outside}, f, ensure_ascii=False, indent=0)
+    print("inserts_dir_py.json: %d cases, %d outside / bad-file cases" % (len(cases), len(outside)))
 
 
 if __name__ == "__main__":

@@ -86,8 +86,40 @@ def test_device_mirror_with_inserts_dir(tmp_path):
         assert M.get_interpdata(dict(FIX["inserts"]), "over") == "from the inserts"
         with pytest.raises(pkg.InterpolationException):
             M.get_interpdata(dict(FIX["inserts"]), "missing")
-        with pytest.raises(NotImplementedError):
-            pkg.interpolate_inserts({}, "{../outside}")
+    finally:
+        M.inserts_dir = old
+
+
+@pytest.mark.gpu
+def test_device_mirror_outside_keys_and_bad_files(tmp_path):
+    """Keys that are not canonical file names under the directory (the device reports
+    IE_NEEDS_HOST; the host opens os.path.join(inserts_dir, key) as py:452-461 does and the
+    device resolves the string again) and files the reference cannot read (its error is raised when
+    the key is looked up), against the reference's own results (gen_inserts_dir.py)."""
+    pkg = G.load_package()
+    from interpolation_engine_amd import interpolation_engine as M
+    d = make_dir(tmp_path / "dir")
+    for rel, text in FIX["outside_files"].items():
+        os.makedirs(os.path.dirname(os.path.join(tmp_path, rel)), exist_ok=True)
+        with open(os.path.join(tmp_path, rel), "w") as f:
+            f.write(text)
+    for rel, hx in FIX["bad_files"].items():
+        with open(os.path.join(d, rel), "wb") as f:
+            f.write(bytes.fromhex(hx))
+    old = M.inserts_dir
+    M.inserts_dir = d
+    try:
+        for c in FIX["outside_cases"]:
+            try:
+                r = pkg.interpolate_inserts(dict(FIX["inserts"]), c["s"])
+            except pkg.InterpolationException:
+                assert c["st"] == "E_INTERP", c
+                continue
+            except Exception as e:  # noqa: BLE001
+                assert c["st"] == "RAISES" and type(e).__name__ == c["exc"], (c, e)
+                continue
+            assert c["st"] in ("OK_STR", "OK_VALUE"), (c, r)
+            assert r == (c["out"] if c["st"] == "OK_STR" else c["value"]), (c, r)
     finally:
         M.inserts_dir = old
 
