@@ -111,19 +111,36 @@ class InsertsTableSet:
             starts.append(len(self.keys))
         self.starts = starts
         n = len(self.keys)
-        arr = (N.KV * max(1, n))()
-        keep = []
-        for i, k in enumerate(self.keys):
-            if not isinstance(k, str):
+        # the ie_kv array as one numpy record array over two byte blobs (keys, splice texts): a
+        # table set of many states holds ~10^5 entries, and one ctypes struct per entry costs more
+        # than the device build
+        import numpy as np
+        texts, kinds = [None] * n, np.empty(max(1, n), np.int32)
+        for i, v in enumerate(self.values):
+            if type(v) is str:
+                texts[i], kinds[i] = v, N.KIND_STR
+            else:
+                kinds[i], texts[i] = render(v, dialect)
+        for k in self.keys:
+            if type(k) is not str:
                 raise TypeError("insert keys must be str")
-            kind, text = render(self.values[i], dialect)
-            kb, tb = N.enc(k), N.enc(text)
-            keep += [kb, tb]
-            arr[i] = N.KV(kb, len(kb), tb, len(tb), kind, 0)
+        kb = [N.enc(k) for k in self.keys]
+        tb = [N.enc(t) for t in texts]
+        kblob, tblob = np.frombuffer(b"".join(kb) + b"\0", np.uint8), np.frombuffer(b"".join(tb) + b"\0", np.uint8)
+        klen = np.fromiter(map(len, kb), np.uint64, n)
+        tlen = np.fromiter(map(len, tb), np.uint64, n)
+        arr = np.zeros(max(1, n), dtype=[("key", "<u8"), ("key_len", "<u8"), ("text", "<u8"), ("text_len", "<u8"),
+                                         ("kind", "<i4"), ("reserved", "<u4")])
+        if n:
+            arr["key"][:n] = kblob.ctypes.data + np.concatenate(([0], np.cumsum(klen)[:-1])).astype(np.uint64)
+            arr["key_len"][:n] = klen
+            arr["text"][:n] = tblob.ctypes.data + np.concatenate(([0], np.cumsum(tlen)[:-1])).astype(np.uint64)
+            arr["text_len"][:n] = tlen
+            arr["kind"][:n] = kinds[:n]
         h = ctypes.c_void_p()
         clk = N.Clock(*self.clock)
         st = (ctypes.c_uint64 * len(starts))(*starts)
-        N.check(N.lib().ie_table_set_build(ctypes.cast(arr, ctypes.c_void_p), st, len(self.dicts),
+        N.check(N.lib().ie_table_set_build(ctypes.c_void_p(arr.ctypes.data), st, len(self.dicts),
                                            N.IE_DIALECT[dialect], ctypes.byref(clk),
                                            N.TABLE_HAS_INSERTS_DIR if has_inserts_dir else 0, device,
                                            ctypes.byref(h)), "ie_table_set_build")

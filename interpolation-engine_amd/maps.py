@@ -56,14 +56,16 @@ def _str_results(tset, strings, ids):
 # ------------------------------------------------------------------------------------------
 # goto_map (py:1689-1711)
 # ------------------------------------------------------------------------------------------
-def goto_map_states(states, task, dialect="py", device=0):
-    """goto_map for each state: [{'goto_target': t} | None | exception instance]."""
+def goto_map_states(states, task, dialect="py", device=0, tables=None):
+    """goto_map for each state: [{'goto_target': t} | None | exception instance]. tables: an
+    InsertsTableSet of exactly these states' dicts, to share between tasks that do not change them
+    (run_map_tasks does); else one is built for this task."""
     maps = task["target_maps"]
     n, m = len(states), len(maps)
     out = [None] * n
     if n == 0:
         return out
-    tset = IE.InsertsTableSet(states, dialect=dialect, device=device)
+    tset = tables or IE.InsertsTableSet(states, dialect=dialect, device=device)
     try:
         # value text, then all keys, then all values, for every state in one batch
         strings, ids = [], []
@@ -74,7 +76,8 @@ def goto_map_states(states, task, dialect="py", device=0):
             ids.extend([s] * (1 + 2 * m))
         res = _str_results(tset, strings, ids)
     finally:
-        tset.close()
+        if tables is None:
+            tset.close()
     texts, keys, vals = [], [], []
     for s in range(n):
         r = res[s * (1 + 2 * m):(s + 1) * (1 + 2 * m)]
@@ -166,9 +169,10 @@ def _rebuild(skel, done):
     return skel
 
 
-def replace_map_states(states, task, dialect="py", device=0):
+def replace_map_states(states, task, dialect="py", device=0, tables=None):
     """replace_map for each state: [(output_name, value) | exception instance]. The caller
-    stores value under output_name (set_interpdata, py:1771-1773); nothing is mutated here."""
+    stores value under output_name (set_interpdata, py:1771-1773); nothing is mutated here.
+    tables: as goto_map_states."""
     maps = task["wildcard_maps"]
     n, m = len(states), len(maps)
     repeat = task.get("repeat_until_done", False)
@@ -177,7 +181,7 @@ def replace_map_states(states, task, dialect="py", device=0):
         return out
     no_value = object()
     value_if_error = ([_first_value(d) for d in maps if _first_key(d) == "NULL"] + [no_value])[0]  # py:1761
-    tset = IE.InsertsTableSet(states, dialect=dialect, device=device)
+    tset = tables or IE.InsertsTableSet(states, dialect=dialect, device=device)
     try:
         names = tset.results([task["output_name"]] * n, list(range(n)))  # py:1715 (no str(): as the reference)
         keys = _str_results(tset, [_first_key(d) for d in maps] * n, [s for s in range(n) for _ in range(m)])
@@ -198,7 +202,8 @@ def replace_map_states(states, task, dialect="py", device=0):
             owner.extend([s] * len(mine))
         done, err = _replace_strings(tset, states, leaves, owner, keys, maps, m, repeat, dialect, device)
     finally:
-        tset.close()
+        if tables is None:
+            tset.close()
     # per state: the first failing leaf in the reference's traversal order decides (py:1763-1771)
     for s in range(n):
         if out[s] is not None:
@@ -275,9 +280,10 @@ def _replace_strings(tset, states, leaves, owner, keys, maps, m, repeat, dialect
                 hits.append((i, p - r[0], caps))
             elif key_err[owner[i]] is not None:  # a key failed before anything matched
                 err[i] = key_err[owner[i]]
-        # 3. the matched maps' values against inserts | captures (py:1736-1738), one table per leaf
+        # 3. the matched maps' values against inserts | captures (py:1736-1738), one table per leaf:
+        #    the captures and the keys the value can reach (not a copy of the whole state)
         if hits:
-            dicts = [dict(states[owner[i]], **{str(k + 1): c for k, c in enumerate(caps)}) for i, _, caps in hits]
+            dicts = [_value_dict(states[owner[i]], vals_raw[p], caps, dialect) for i, p, caps in hits]
             xs = IE.InsertsTableSet(dicts, dialect=dialect, device=device)
             try:
                 vres = _str_results(xs, [vals_raw[p] for _, p, _ in hits], list(range(len(hits))))
@@ -299,6 +305,79 @@ def _replace_strings(tset, states, leaves, owner, keys, maps, m, repeat, dialect
             nxt.append(i)
         active = nxt
     return cur, err
+
+
+def _nested(t):
+    """does some pair of t hold another '{' (a key built from a lookup: {q-{1}})?"""
+    depth = 0
+    for c in t:
+        if c == "{":
+            depth += 1
+            if depth > 1:
+                return True
+        elif c == "}":
+            depth = max(depth - 1, 0)
+    return False
+
+
+def _value_dict(state, value, caps, dialect):
+    """`inserts | extra_inserts` for interpolating one map value (py:1736-1738), reduced to what the
+    interpolation can look up: the captures ('1', '2', ...) and, from the state, the keys the value
+    spells out, closed over the keys spelled out by the values they splice (a spliced '{x}' is
+    resolved again by the reference's loop). A key built from another lookup ({a-{b}}) cannot be
+    known in advance: then the whole state goes in, as in the reference."""
+    extra = {str(k + 1): c for k, c in enumerate(caps)}
+    if not isinstance(value, str) or _nested(value):
+        return dict(state, **extra)
+    out, todo, seen = {}, list(IE._literal_keys(value)), set()
+    while todo:
+        k = todo.pop()
+        if k in seen:
+            continue
+        seen.add(k)
+        if k in extra or k not in state:
+            continue
+        v = state[k]
+        out[k] = v
+        try:
+            text = IE.render(v, dialect)[1]
+        except TypeError:
+            return dict(state, **extra)
+        if "{" in text:
+            if _nested(text):
+                return dict(state, **extra)
+            todo.extend(IE._literal_keys(text))
+    out.update(extra)
+    return out
+
+
+def run_map_tasks(states, tasks, dialect="py", device=0):
+    """goto_map / replace_map tasks in order over many states (the reference's loop applies them
+    one state at a time): one table set per stretch of tasks that leaves the states unchanged, a
+    replace_map's results stored into each state before the next task (set_interpdata,
+    py:470-471). Returns one list of per-state outcomes per task."""
+    outs, tset = [], None
+    try:
+        for task in tasks:
+            if tset is None:
+                tset = IE.InsertsTableSet(states, dialect=dialect, device=device)
+            if task["cmd"] == "goto_map":
+                outs.append(goto_map_states(states, task, dialect, device, tables=tset))
+                continue
+            got = replace_map_states(states, task, dialect, device, tables=tset)
+            outs.append(got)
+            changed = False
+            for st, r in zip(states, got):
+                if not isinstance(r, BaseException):
+                    st[r[0]] = r[1]
+                    changed = True
+            if changed:
+                tset.close()
+                tset = None
+    finally:
+        if tset is not None:
+            tset.close()
+    return outs
 
 
 def replace_map(inserts, task):

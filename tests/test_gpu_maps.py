@@ -77,6 +77,16 @@ def test_text_adventure_maps_match_reference():
     assert not bad, (len(bad), bad[:6])
 
 
+def test_run_map_tasks_matches_reference():
+    """The same program through run_map_tasks (table sets shared while the states do not change;
+    each map value interpolated against the captures and the keys it can reach)."""
+    g = load_golden("maps_py.json")
+    states = [make_state(g["defaults"], j) for j in range(g["states"])]
+    outs = M.run_map_tasks(states, g["tasks"])
+    bad = [(k, j) for k, got in enumerate(outs) for j, r in enumerate(got) if not _check(g["results"][j][k], r)]
+    assert not bad, (len(bad), bad[:6])
+
+
 def test_single_state_entry_points():
     """goto_map / replace_map for one state (the reference's call regime) agree with the batch."""
     g = load_golden("maps_py.json")
