@@ -103,6 +103,8 @@ struct ie_exec {
   uint32_t opt_fast = 1;          // 0: exact evaluator only (IE_FAST)
   int32_t opt_tile = 0;           // k_resolve tile: 0 by call site, 256 or 512 forced (IE_TILE)
   int32_t opt_views = 0;          // host batch APIs resolve into a views layout (IE_VIEWS)
+  int32_t opt_defer = -1;         // views batches: heavy strings to a second pass: -1 adaptive, 0 / 1 (IE_DEFER)
+  bool defer_slow = false;        // the adaptive choice (from an earlier batch's counts)
   int32_t opt_lean = 0;           // views batches: k_lean first, k_resolve on what it lists (IE_LEAN; measured
                                   // slower than k_resolve alone: DESIGN.md, k_lean)
   int32_t lean_grid = 0;          // resident k_lean workgroups on the device (0: not known yet)
@@ -356,11 +358,16 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
     // fail commit: forced by the option (diagnostics, tests), else adaptive on the count of chain
     // failures (misses / unspliceable hits) an earlier batch saw, in either variant
     const bool forced = x->opt_fail_commit >= 0;
-    if (!forced && x->stat_pending && hipEventQuery(x->stat_ev) == hipSuccess) {
+    if (x->stat_pending && hipEventQuery(x->stat_ev) == hipSuccess) {
       x->stat_pending = false;
-      const uint64_t fails = *x->stat_host;
+      const uint64_t fails = x->stat_host[4];  // counters word 8: chain failures
       if (fails * 1024 > x->stat_n) x->fail_commit = true;  // > 0.1 % of the strings
       else if (fails == 0) x->fail_commit = false;
+      // heavy strings (exact evaluator, literal path): above 0.4 % of a views batch they go to a
+      // second pass in tiles of their own; below 1/4096 they stay in their tiles again
+      const uint64_t heavy = (uint64_t)x->stat_host[3] + x->stat_host[0];
+      if (heavy * 256 > x->stat_n) x->defer_slow = true;
+      else if (heavy * 4096 < x->stat_n) x->defer_slow = false;
     }
     W.fail_commit = forced ? (uint32_t)x->opt_fail_commit : (uint32_t)x->fail_commit;
     if (x->timing) IE_HIP(hipEventRecord(x->ev[1], st));
@@ -402,15 +409,25 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
                  hipGetErrorString(le));
         return fail(IE_ERR_HIP, msg);
       }
+    } else if (d_out_len && !x->in_cmd && !x->opt_noeval &&
+               (x->opt_defer == 1 || (x->opt_defer < 0 && x->defer_slow))) {
+      // a views batch with heavy strings: two passes (ie_lean.hip launch_resolve_deferring)
+      IE_HIP(x->u_list.ensure(n * 4 + 4));
+      IE_HIP(x->u_off.ensure(n * 8 + 8));
+      IE_HIP(x->u_len.ensure(n * 4 + 4));
+      if (d_tid) IE_HIP(x->u_tid.ensure(n * 4 + 4));
+      W.udefer_list = (uint32_t*)x->u_list.p;
+      IE_HIP(launch_resolve_deferring(B, W, t->dev, out->bytes, cap, (uint64_t*)x->u_off.p, (uint32_t*)x->u_len.p,
+                                      d_tid ? (uint32_t*)x->u_tid.p : nullptr, st));
     } else {
       IE_HIP(wide ? launch_resolve512(B, W, t->dev, out->bytes, cap, st) : launch_resolve(B, W, t->dev, out->bytes, cap, st));
     }
-    if (!forced && !x->stat_pending) {
+    if (!x->stat_pending) {
       if (!x->stat_host) {
-        IE_HIP(hipHostMalloc((void**)&x->stat_host, 4, hipHostMallocDefault));
+        IE_HIP(hipHostMalloc((void**)&x->stat_host, 64, hipHostMallocDefault));
         IE_HIP(hipEventCreateWithFlags(&x->stat_ev, hipEventDisableTiming));
       }
-      IE_HIP(hipMemcpyAsync(x->stat_host, W.stats + 4, 4, hipMemcpyDeviceToHost, st));
+      IE_HIP(hipMemcpyAsync(x->stat_host, W.stats, 5 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
       IE_HIP(hipEventRecord(x->stat_ev, st));
       x->stat_pending = true;
       x->stat_n = n;
@@ -968,6 +985,7 @@ int ie_exec_create(int32_t device, void* hip_stream, ie_exec** out) {
   if (const char* e = getenv("IE_TILE")) x->opt_tile = atoi(e) == 512 ? 512 : atoi(e) == 256 ? 256 : 0;
   if (const char* e = getenv("IE_VIEWS")) x->opt_views = atoi(e) != 0;
   if (const char* e = getenv("IE_LEAN")) x->opt_lean = atoi(e) != 0;
+  if (const char* e = getenv("IE_DEFER")) x->opt_defer = atoi(e) < 0 ? -1 : atoi(e) != 0 ? 1 : 0;
   if (const char* e = getenv("IE_DEBUG_STAMPS")) x->stamps_path = e;
   if (hip_stream) {
     x->stream = (hipStream_t)hip_stream;
@@ -1098,6 +1116,10 @@ int ie_exec_set_option(ie_exec* x, int32_t option, int64_t value) {
       return IE_SUCCESS;
     case IE_OPT_LEAN:
       x->opt_lean = value ? 1 : 0;
+      return IE_SUCCESS;
+    case IE_OPT_DEFER:
+      if (value < -1 || value > 1) return fail(IE_ERR_INVALID, "defer must be -1, 0 or 1");
+      x->opt_defer = (int32_t)value;
       return IE_SUCCESS;
     default:
       return fail(IE_ERR_INVALID, "unknown exec option");

@@ -77,6 +77,8 @@ struct Work {
   uint64_t* shards;
   uint32_t n_shards;     // a power of two
   uint32_t stripe_log2;
+  uint32_t defer_slow;   // k_resolve on a views batch: strings the chain jobs cannot finish are listed
+                         // in udefer_list for a second pass instead of evaluated in their tile
   uint32_t recurse;      // k_resolve in the unescape command (py dialect): whole-string items whose
                          // result recursive_interpolate walks again report IE_RECURSE
   uint32_t zero_on_overflow; // escape kernels: when the output exceeds its capacity, write every
@@ -118,6 +120,10 @@ hipError_t launch_unescape_cmd(const Batch& B, const Work& W, const DevTable& T,
 hipError_t launch_lean(const Batch& B, const Work& W, const DevTable& T, uint8_t* out, uint64_t cap, uint64_t* sub_off,
                        uint32_t* sub_len, uint32_t* sub_tid, uint32_t grid_cap, hipStream_t st);
 int lean_blocks_per_cu(int multi);
+// k_resolve on a views batch in two passes: the heavy strings listed by the first (W.defer_slow)
+// are resolved by the second as a subset (their views in sub_off / sub_len / sub_tid)
+hipError_t launch_resolve_deferring(const Batch& B, const Work& W, const DevTable& T, uint8_t* out, uint64_t cap,
+                                    uint64_t* sub_off, uint32_t* sub_len, uint32_t* sub_tid, hipStream_t st);
 int lean_failed_stage();
 hipError_t launch_status_carry(const uint8_t* before, uint8_t* after, uint64_t n, hipStream_t st);
 hipError_t launch_debug_probe(const DevTable& T, const uint8_t* key, uint32_t klen, uint64_t* out,

@@ -516,6 +516,28 @@ hipError_t launch_lean(const Batch& B, const Work& W, const DevTable& T, uint8_t
   return launch_resolve(D, W, T, out, cap, st);
 }
 
+hipError_t launch_resolve_deferring(const Batch& B, const Work& W, const DevTable& T, uint8_t* out, uint64_t cap,
+                                    uint64_t* sub_off, uint32_t* sub_len, uint32_t* sub_tid, hipStream_t st) {
+  if (!B.out_len || !B.n) return hipErrorInvalidValue;
+  Work W1 = W;
+  W1.defer_slow = 1;
+  hipError_t e = launch_resolve(B, W1, T, out, cap, st);
+  if (e != hipSuccess) return e;
+  // the windowed-tile list is the second pass's again
+  e = hipMemsetAsync(W.defer_count, 0, sizeof(uint32_t), st);
+  if (e != hipSuccess) return e;
+  const bool multi = B.table_id != nullptr;
+  const uint32_t gb = (uint32_t)((B.n + 255) / 256 < 1024 ? (B.n + 255) / 256 : 1024);
+  hipLaunchKernelGGL(lean::k_lean_gather, dim3(gb), dim3(256), 0, st, B, W, sub_off, sub_len, multi ? sub_tid : nullptr);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  Work W2 = W;
+  W2.defer_slow = 0;
+  const Batch D{B.bytes, sub_off, B.n, B.out_off, B.status, B.value_id, multi ? sub_tid : nullptr, sub_len, B.out_len,
+                W.udefer_list, W.udefer_count};
+  return launch_resolve(D, W2, T, out, cap, st);
+}
+
 int lean_blocks_per_cu(int multi) {
   int nb = 0;
   hipError_t e = multi ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lean::k_lean<true>, (int)lean::kTile, 0)

@@ -1248,6 +1248,16 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
     }
     const uint64_t fail_m = __ballot(chain_fail);
     if (fail_m && lane == 0) atomicAdd(W.stats + 4, (uint32_t)__popcll(fail_m));  // misses: rare
+    // a views batch with heavy strings (W.defer_slow, chosen per batch by the host): the strings the
+    // chain jobs could not finish go to a second pass, in tiles of their own, instead of holding up
+    // this tile (and its 255 other strings) in the exact evaluator or the literal path
+    const bool dslow = VIEWS && !UNESC && W.defer_slow != 0u;
+    if (dslow) {
+      const uint64_t dm = __ballot(slow);
+      if (dm && lane == 0) atomicAdd(W.stats + 3, (uint32_t)__popcll(dm));
+      if (slow) r = kStatusDeferred;
+      slow = false;
+    }
     // the rest: the exact evaluator (scratch: the lane's own chain-evaluator columns)
     const uint64_t slow_m = __ballot(slow);
     if (slow_m) {
@@ -1263,11 +1273,12 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
       if (slow) r = r2, olen = o2;
     }
     if (active) st = r;
-    if (UNESC && i < B.n && st == kStatusPending) {
+    if ((UNESC || dslow) && i < B.n && st == kStatusPending) {
       // the fused unescape command finishes in the stage only: the rest goes to the deferred pass
+      // (so do the literal-path strings of a deferring views batch)
       st = kStatusDeferred;
     }
-    if (UNESC) {
+    if (UNESC || dslow) {
       const bool dfr = i < B.n && st == kStatusDeferred;
       const uint64_t m = __ballot(dfr);
       if (m) {

@@ -242,7 +242,9 @@ def test_config5_10k_states_vs_oracle():
     rst, rlen, rhash = np.zeros(n, np.uint8), np.zeros(n, np.uint64), np.zeros(n, np.uint64)
     rvid = np.zeros(n, np.uint32)
     O.run_batch_sets(oracles, ids, buf, offs, THREADS, rst, rlen, rhash, rvid)
-    for views in (False, True):
+    for views, defer in ((False, -1), (True, 0), (True, 1)):
+        # views: heavy strings in their tiles (IE_OPT_DEFER 0) and in a second pass of their own (1)
+        x.set_option(N.OPT_DEFER, defer)
         o = interpolate(x, tset.h, d_bytes, d_off, n, 16 * len(blob) + (1 << 20), views, d_ids.ptr)
         st, _, _ = assert_matches_oracle(o, rst, rlen, rhash)
         # typed whole-string results ({scenario}, {stage}, {history_list}): the same insert; the

@@ -30,9 +30,10 @@ def run_product(table_dict, strings, dialect="py", has_dir=False):
     return t.run(strings), t
 
 
-@pytest.fixture(params=["0", "1", "1w", "0v", "1v", "0lv"],
+@pytest.fixture(params=["0", "1", "1w", "0v", "1v", "0lv", "0dv", "1dv"],
                 ids=["chain-fail-exact", "chain-fail-commit", "chain-fail-commit-512", "chain-fail-exact-views",
-                     "chain-fail-commit-views", "chain-fail-exact-views-lean"])
+                     "chain-fail-commit-views", "chain-fail-exact-views-lean", "chain-fail-exact-views-defer",
+                     "chain-fail-commit-views-defer"])
 def fail_commit(request, monkeypatch):
     """Both k_resolve variants: chain failures sent to the exact evaluator, or committed in the
     chain evaluator (the library picks one adaptively; IE_FAIL_COMMIT / IE_OPT_FAIL_COMMIT force it);
@@ -43,7 +44,9 @@ def fail_commit(request, monkeypatch):
     fc, tile = request.param[0], 512 if request.param.endswith("w") else 0
     views = 1 if request.param.endswith("v") else 0
     lean = 1 if "l" in request.param else 0  # k_lean first (ie_lean.hip), k_resolve on what it leaves
+    defer = 1 if "d" in request.param else 0  # heavy strings to a second pass (IE_OPT_DEFER)
     monkeypatch.setenv("IE_LEAN", str(lean))
+    monkeypatch.setenv("IE_DEFER", str(defer))
     monkeypatch.setenv("IE_FAIL_COMMIT", fc)
     monkeypatch.setenv("IE_TILE", str(tile))
     monkeypatch.setenv("IE_VIEWS", str(views))
@@ -52,10 +55,12 @@ def fail_commit(request, monkeypatch):
     x.set_option(N.OPT_TILE, tile)
     x.set_option(N.OPT_VIEWS, views)
     x.set_option(N.OPT_LEAN, lean)
+    x.set_option(N.OPT_DEFER, defer)
     VIEWS[0] = bool(views)
     yield fc
     VIEWS[0] = False
     x.set_option(N.OPT_LEAN, 0)
+    x.set_option(N.OPT_DEFER, -1)
     x.set_option(N.OPT_FAIL_COMMIT, -1)
     x.set_option(N.OPT_TILE, 0)
     x.set_option(N.OPT_VIEWS, 0)
