@@ -204,9 +204,10 @@ int ie_exec_timing(ie_exec* x, ie_timing* out); /* syncs */
 #define IE_OPT_TILE 4
 #define IE_OPT_VIEWS 5 /* 1: the host batch APIs resolve into a views layout (no look-back) and pack
                           the results in input order on the host; 0 (default): packed on the device */
-#define IE_OPT_DEFER 7 /* views batches: -1 (default) adaptive, 1: strings the chain jobs cannot finish
-                          go to a second pass in tiles of their own (the exact evaluator and the
-                          literal path then run on full tiles of such strings), 0: in their tiles */
+#define IE_OPT_DEFER 7 /* views batches: 1: strings the chain jobs cannot finish go to a second pass in
+                          tiles of their own (the exact evaluator and the literal path then run on
+                          full tiles of such strings); -1 adaptive (above 0.4 % of a batch); 0
+                          (default): in their tiles (config 5 measured 2.5x slower deferred) */
 #define IE_OPT_LEAN 6  /* 1: a views batch runs k_lean (one wave per 64 strings, the common string shape,
                           output claimed in striped shards: *total is then the extent used, gaps
                           included) and then k_resolve on the strings it left; 0 (default): k_resolve */
