@@ -20,3 +20,5 @@ tail -1 gpurun_out/${TAG}_pytest_gpu.log
 NOTEST=1 TAG=$TAG bash tools/gpu_all.sh || exit 1
 timeout -k 10 300 python -u tools/mirror_latency.py > gpurun_out/${TAG}_mirror.json 2> gpurun_out/${TAG}_mirror.err || { tail -20 gpurun_out/${TAG}_mirror.err; exit 1; }
 cat gpurun_out/${TAG}_mirror.json
+timeout -k 10 400 python -u tools/task_times.py > gpurun_out/${TAG}_task_times.json 2> gpurun_out/${TAG}_task_times.err || { tail -20 gpurun_out/${TAG}_task_times.err; exit 1; }
+cat gpurun_out/${TAG}_task_times.json
