@@ -42,6 +42,12 @@
 #define IE_RNS r256
 #endif
 
+// issue the first value text's loads before the output scan (config 4 first resolve 1.80 -> 1.76 ms,
+// configs 2 and 3 unchanged: profiles/r03/early_text/)
+#ifndef IE_EARLY_TEXT
+#define IE_EARLY_TEXT 1
+#endif
+
 namespace ie {
 // everything of one tile size lives in its own namespace: ie_resolve512.hip compiles this file
 // again with 512-string tiles (IE_RBLOCK=512, IE_RNS=r512, IE_RESOLVE_WIDE)
@@ -1368,6 +1374,21 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
     d.vk[0] = (kValPool << 30) | olen;
     d.vs[0] = s_lit[tid];
   }
+#if IE_EARLY_TEXT
+  // value 0's entry text in flight across the scan's barriers (its latency no longer opens the build)
+  const bool mine = i < B.n && st == IE_OK_STR && olen;
+  uint32_t tt[2][8];
+  auto load_text = [&](int j, uint32_t (&t)[8]) {
+    const bool need = mine && (uint32_t)j < d.ntop && (d.vk[j] >> 30) == kValEntry;
+    if (__any(need)) {
+      const uint4* tp = (const uint4*)(T.entries + (need ? d.vs[j] : 0u)) + 2;
+      const uint4 t2 = gld4(tp), t3 = gld4(tp + 1);
+      t[0] = t2.x, t[1] = t2.y, t[2] = t2.z, t[3] = t2.w;
+      t[4] = t3.x, t[5] = t3.y, t[6] = t3.z, t[7] = 0;
+    }
+  };
+  load_text(0, tt[0]);
+#endif
   uint64_t tile_total;
   const uint64_t local = block_scan(olen, s_red, &tile_total);  // (its barriers also retire s_lit)
   uint64_t lb_early = 0;
@@ -1384,10 +1405,13 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
   // ---- 5. the tile's output bytes into the LDS stage (tile-relative offsets) while the
   //      look-back is pending; tiles whose output does not fit store straight to HBM later ----
   const bool in_stage = tile_total <= (uint64_t)kOutStage;
+#if !IE_EARLY_TEXT
   const bool mine = i < B.n && st == IE_OK_STR && olen;
+#endif
   if (in_stage) {
     // entry texts of the values (inline, <= kInlineText bytes): into registers, value j's loads
     // issued one value ahead of its use
+#if !IE_EARLY_TEXT
     uint32_t tt[2][8];
     auto load_text = [&](int j, uint32_t (&t)[8]) {
       const bool need = mine && (uint32_t)j < d.ntop && (d.vk[j] >> 30) == kValEntry;
@@ -1399,6 +1423,7 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
       }
     };
     load_text(0, tt[0]);
+#endif
     lds_u8* const dd = (lds_u8*)(s_u + (mine ? local : 0));
     const lds_u8* const ls = (const lds_u8*)s;
     const uint32_t ntop = mine ? d.ntop : 0u;

@@ -388,6 +388,8 @@ def read_inserts_dir(path):
     (nested files as 'sub/name'; `<key>.json5` first, as py:455-459 tries it first). Keys the
     lookup never sends to the directory ('', 'HH:MM', 'HH:MM:SS', ARGn) are left out."""
     from .program import loads as json5_loads  # the builder's JSON5 reader (json5 is absent here)
+    for p in [p for p in _dir_bad if p.startswith(os.path.join(path, ""))]:
+        del _dir_bad[p]  # (read again below: a file fixed since reads fine now)
     plain, j5 = {}, {}
     seen = set()
     for root, dirs, files in os.walk(path, followlinks=True):  # open() follows links too

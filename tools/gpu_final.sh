@@ -22,3 +22,7 @@ timeout -k 10 300 python -u tools/mirror_latency.py > gpurun_out/${TAG}_mirror.j
 cat gpurun_out/${TAG}_mirror.json
 timeout -k 10 400 python -u tools/task_times.py > gpurun_out/${TAG}_task_times.json 2> gpurun_out/${TAG}_task_times.err || { tail -20 gpurun_out/${TAG}_task_times.err; exit 1; }
 cat gpurun_out/${TAG}_task_times.json
+# the multi-rank control plane on one card (two ranks on device 0; the 8-GPU curve is the driver's)
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 \
+  bench.py --gpus 2 --device 0 --steps 10 --warmup 2 --no-cpu > gpurun_out/${TAG}_bench_2ranks.log 2>&1 || { tail -20 gpurun_out/${TAG}_bench_2ranks.log; exit 1; }
+tail -1 gpurun_out/${TAG}_bench_2ranks.log
