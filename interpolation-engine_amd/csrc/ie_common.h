@@ -122,7 +122,10 @@ constexpr uint32_t kTidShift = 12;
 constexpr uint32_t kMaxTables = 1u << (32 - kTidShift);
 
 // DevTable.flags
-enum : uint32_t { TF_HAS_DIR = 1u };
+enum : uint32_t {
+  TF_HAS_DIR = 1u,
+  TF_LONG_KEYS = 2u,  // some key is 17-32 bytes long: k_resolve's chain jobs compare key tails (LK)
+};
 
 constexpr uint32_t kInlineKey = 16;   // bytes of key kept inline in an entry
 constexpr uint32_t kInlineText = 28;  // bytes of splice text kept inline in an entry

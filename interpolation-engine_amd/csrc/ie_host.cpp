@@ -644,7 +644,9 @@ int upload_table(const std::vector<Ent>& ents, uint32_t n_tables, int32_t dialec
   std::vector<Entry> items;
   items.reserve(ents.size());
   uint64_t maxtext = 8;
+  bool long_keys = false;
   for (const Ent& e : ents) {
+    long_keys |= e.key.size() > kInlineKey && e.key.size() <= 2 * kInlineKey;
     while (arena.size() & 3) arena.push_back(0);  // texts 4-byte aligned (dword copies)
     if (e.flags & EF_RAWALT) {  // [raw text][u32 raw length] right before the splice text
       arena.insert(arena.end(), e.raw.begin(), e.raw.end());
@@ -722,7 +724,7 @@ int upload_table(const std::vector<Ent>& ents, uint32_t n_tables, int32_t dialec
   t->dev.n_entries = (uint32_t)ents.size();
   t->dev.n_tables = n_tables;
   t->dev.dialect = (uint32_t)dialect;
-  t->dev.flags = (flags & IE_TABLE_HAS_INSERTS_DIR) ? TF_HAS_DIR : 0u;
+  t->dev.flags = ((flags & IE_TABLE_HAS_INSERTS_DIR) ? TF_HAS_DIR : 0u) | (long_keys ? TF_LONG_KEYS : 0u);
   t->dev.maxtext = maxtext;
   *out = t;
   return IE_SUCCESS;

@@ -422,7 +422,7 @@ constexpr uint32_t kResWhole = 1u << 27;  // a whole-string '{key}' (res_s: the 
 // inserts-dir or an unspliceable hit, recorded with its pair's opening offset) or at anything the
 // exact evaluator must decide (kResReject: a long key or text, a non-inert value, a failure when
 // !FAILC, a miss an inserts-dir might resolve).
-template <bool FAILC>
+template <bool FAILC, bool LK>
 __device__ void resolve_jobs(const DevTable& T, const lds_u8* tile, const ChainJobs J, uint32_t j0, uint32_t njobs,
                              bool& chain_fail, uint64_t* stamp) {
   constexpr int NJ = 2;
@@ -455,6 +455,8 @@ __device__ void resolve_jobs(const DevTable& T, const lds_u8* tile, const ChainJ
     uint32_t open[NJ], close[NJ], la[NJ], lb[NJ], klen[NJ], slot[NJ];
     u32x4 ka[NJ], kb[NJ], kw[NJ];
     uint64_t h[NJ];
+    u32x4 kw2[NJ];  // bytes 16..31 of an innermost key longer than the entry's inline copy
+    bool lk[NJ];
 #pragma unroll
     for (int q = 0; q < NJ; q++) {
       on[q] = !done[q] && r < dep[q];
@@ -481,7 +483,11 @@ __device__ void resolve_jobs(const DevTable& T, const lds_u8* tile, const ChainJ
 #pragma unroll
     for (int q = 0; q < NJ; q++) {
       klen[q] = la[q] + (r != 0 ? ctl[q] + lb[q] : 0u);
-      if (on[q] && klen[q] > 16u) {  // longer keys live in the arena: exact evaluator
+      // LK (a table with 17-32 byte keys): an innermost key (template bytes only) that long has
+      // its tail compared with the arena's copy of the entry's key once the entry is in
+      lk[q] = LK && on[q] && r == 0 && klen[q] > 16u && klen[q] <= 32u;
+      kw2[q] = lk[q] ? keep_bytes(ld16a(s[q] + open[q] + 17), klen[q] - 16u) : u32x4{0, 0, 0, 0};
+      if (on[q] && klen[q] > 16u && !lk[q]) {  // longer keys live in the arena: exact evaluator
         on[q] = false;
         done[q] = true;
       }
@@ -497,6 +503,10 @@ __device__ void resolve_jobs(const DevTable& T, const lds_u8* tile, const ChainJ
       if (klen[q] > 4u) hh = hash_word(hh, kw[q].y);
       if (klen[q] > 8u) hh = hash_word(hh, kw[q].z);
       if (klen[q] > 12u) hh = hash_word(hh, kw[q].w);
+      if (LK && klen[q] > 16u) hh = hash_word(hh, kw2[q].x);
+      if (LK && klen[q] > 20u) hh = hash_word(hh, kw2[q].y);
+      if (LK && klen[q] > 24u) hh = hash_word(hh, kw2[q].z);
+      if (LK && klen[q] > 28u) hh = hash_word(hh, kw2[q].w);
       h[q] = hh;
     }
     if (stamp && threadIdx.x == 0 && r == 0) {  // diagnostic: keys hashed
@@ -534,8 +544,16 @@ __device__ void resolve_jobs(const DevTable& T, const lds_u8* tile, const ChainJ
     for (int q = 0; q < NJ; q++) {
       if (!__any(on[q])) continue;
       const Probe& E = P[q];
-      const bool hit = on[q] && (entry_head_ok(E.q0, klen[q], tb[q]) & (E.q1.x == kw[q].x) & (E.q1.y == kw[q].y) &
-                                 (E.q1.z == kw[q].z) & (E.q1.w == kw[q].w));
+      bool hit = on[q] && (entry_head_ok(E.q0, klen[q], tb[q]) & (E.q1.x == kw[q].x) & (E.q1.y == kw[q].y) &
+                           (E.q1.z == kw[q].z) & (E.q1.w == kw[q].w));
+      if (LK && __any(lk[q] && hit)) {  // the tail of a long key: the arena's copy (key_off_of), bytes 16..
+        u32x4 tail{0, 0, 0, 0};
+        if (lk[q] && hit) {
+          const uint32_t* kp = (const uint32_t*)(T.arena + key_off_of(E.q0.w, E.q0.y) + 16u);
+          tail = keep_bytes(u32x4{gld(kp), gld(kp + 1), gld(kp + 2), gld(kp + 3)}, klen[q] - 16u);
+        }
+        hit = hit && (!lk[q] || ((tail.x == kw2[q].x) & (tail.y == kw2[q].y) & (tail.z == kw2[q].z) & (tail.w == kw2[q].w)));
+      }
       const uint32_t flags = E.q0.z, tlen = E.q0.y;
       // (a whole-string '{key}' takes any hit: its result is the raw value, nothing is spliced)
       const bool good = hit && (wh[q] || ((flags & EF_SPLICE_OK) && (flags & EF_INERT)));
@@ -1100,7 +1118,7 @@ __global__ __launch_bounds__(kRBlock) void k_emit_windows(Batch B0, Work W, DevT
 // UNESC (with VIEWS): the unescape command's resolve, fused with its recursive_unescape: the tile
 // is unescaped in the LDS stage (unescape_stage) and then resolved; strings that cannot be finished
 // there (not staged, or needing the literal path) go to W.udefer_list for the deferred pass.
-template <bool FAILC, bool MULTI, bool VIEWS, bool UNESC = false>
+template <bool FAILC, bool MULTI, bool VIEWS, bool UNESC = false, bool LK = false>
 __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES_PER_EU))) void k_resolve(Batch B0, Work W, DevTable T, uint8_t* out,
                                                     uint64_t cap) {
   // a deferred subset counts its strings on the device (the grid is sized for B0.n)
@@ -1243,7 +1261,7 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
       J.tbl[tid] = tid_s;
       __syncthreads();
       IE_STAMP(9);
-      for (uint32_t j0 = 0; j0 < njobs; j0 += 2 * kRBlock) resolve_jobs<FAILC>(T, (const lds_u8*)s_in, J, j0, njobs, chain_fail, j0 == 0 ? stamp_row : nullptr);
+      for (uint32_t j0 = 0; j0 < njobs; j0 += 2 * kRBlock) resolve_jobs<FAILC, LK>(T, (const lds_u8*)s_in, J, j0, njobs, chain_fail, j0 == 0 ? stamp_row : nullptr);
       IE_STAMP(10);
       __syncthreads();
       IE_STAMP(11);
@@ -1606,18 +1624,28 @@ hipError_t launch_resolve_impl(const Batch& B, const Work& W, const DevTable& T,
     hipLaunchKernelGGL(k_emit_windows, dim3(grid < 512u ? grid : 512u), dim3(kRBlock), 0, st, B, W, T, out);
     return hipGetLastError();
   }
-  const int variant = (W.fail_commit ? 4 : 0) | (multi ? 2 : 0) | (B.out_len ? 1 : 0);
+  // LK: a table with 17-32 byte keys gets the instances whose chain jobs take such keys (they cost
+  // config 3 3 %: their registers; config 5 -32 %: its long keys leave the exact evaluator)
+  const int variant = ((T.flags & TF_LONG_KEYS) ? 8 : 0) | (W.fail_commit ? 4 : 0) | (multi ? 2 : 0) | (B.out_len ? 1 : 0);
   switch (variant) {
-#define IE_LAUNCH(V, F, M, S) \
-  case V: hipLaunchKernelGGL((k_resolve<F, M, S>), dim3(grid), dim3(kRBlock), 0, st, B, W, T, out, cap); break;
-    IE_LAUNCH(0, false, false, false)
-    IE_LAUNCH(1, false, false, true)
-    IE_LAUNCH(2, false, true, false)
-    IE_LAUNCH(3, false, true, true)
-    IE_LAUNCH(4, true, false, false)
-    IE_LAUNCH(5, true, false, true)
-    IE_LAUNCH(6, true, true, false)
-    IE_LAUNCH(7, true, true, true)
+#define IE_LAUNCH(V, F, M, S, L) \
+  case V: hipLaunchKernelGGL((k_resolve<F, M, S, false, L>), dim3(grid), dim3(kRBlock), 0, st, B, W, T, out, cap); break;
+    IE_LAUNCH(0, false, false, false, false)
+    IE_LAUNCH(1, false, false, true, false)
+    IE_LAUNCH(2, false, true, false, false)
+    IE_LAUNCH(3, false, true, true, false)
+    IE_LAUNCH(4, true, false, false, false)
+    IE_LAUNCH(5, true, false, true, false)
+    IE_LAUNCH(6, true, true, false, false)
+    IE_LAUNCH(7, true, true, true, false)
+    IE_LAUNCH(8, false, false, false, true)
+    IE_LAUNCH(9, false, false, true, true)
+    IE_LAUNCH(10, false, true, false, true)
+    IE_LAUNCH(11, false, true, true, true)
+    IE_LAUNCH(12, true, false, false, true)
+    IE_LAUNCH(13, true, false, true, true)
+    IE_LAUNCH(14, true, true, false, true)
+    IE_LAUNCH(15, true, true, true, true)
 #undef IE_LAUNCH
   }
   // the deferred (oversized) tiles' bytes (exits at once when there are none); views: the total
