@@ -1050,7 +1050,12 @@ __global__ __launch_bounds__(kRBlock) void k_emit_windows(Batch B0, Work W, DevT
   const uint32_t tid = threadIdx.x;
   // views output: the bytes every tile claimed are the batch's total (k_resolve has finished)
   if (B.out_len && blockIdx.x == 0 && tid == 0) *W.total = *W.cursor;
-  for (uint32_t slot = blockIdx.x; slot < count; slot += gridDim.x) {
+  // fewer deferred tiles than workgroups: each tile's windows are shared by `per` workgroups (a
+  // tile of multi-KB outputs is hundreds of windows: one workgroup alone would take them in turn)
+  const uint32_t per = count && count < gridDim.x ? gridDim.x / count : 1u;
+  const uint32_t slot0 = per > 1u ? blockIdx.x / per : blockIdx.x, wk = per > 1u ? blockIdx.x % per : 0u;
+  const uint32_t slot_step = per > 1u ? count : gridDim.x;  // (per > 1: one slot per workgroup)
+  for (uint32_t slot = slot0; slot < count; slot += slot_step) {
     const uint32_t tile = gld(W.defer_tiles + slot);
     const uint64_t first = (uint64_t)tile * kRBlock, last = min(first + (uint64_t)kRBlock, B.n), i = first + tid;
     // (a deferred subset's results sit at out_index[] of the batch)
@@ -1082,7 +1087,7 @@ __global__ __launch_bounds__(kRBlock) void k_emit_windows(Batch B0, Work W, DevT
     }
     const bool mine = olen != 0;
     lds_u8* const win = (lds_u8*)s_win;
-    for (uint64_t w0 = 0; w0 < tile_total; w0 += (uint64_t)kRStageBytes) {
+    for (uint64_t w0 = (uint64_t)wk * kRStageBytes; w0 < tile_total; w0 += (uint64_t)per * kRStageBytes) {
       const uint32_t wl = (uint32_t)min((uint64_t)kRStageBytes, tile_total - w0);
       const int64_t rel0 = (int64_t)local - (int64_t)w0;  // this lane's output, window-relative
       const bool on = mine && rel0 < (int64_t)wl && rel0 + (int64_t)olen > 0;
