@@ -233,6 +233,14 @@ constexpr int kMaxTop = 3;
 constexpr int kChainDepth = 4;
 constexpr uint32_t kChainMax = 112;
 
+// A chain record: first open | first close << 8 | innermost open << 16 | last close << 24 (strings
+// of <= kChainMax bytes), or, for a flat pair of a long string, kLongRec | open | close << 14.
+constexpr uint32_t kLongRec = 1u << 31;
+__device__ __forceinline__ uint32_t cr_first_open(uint32_t r) { return (r & kLongRec) ? r & 0x3FFFu : r & 0xFFu; }
+__device__ __forceinline__ uint32_t cr_first_close(uint32_t r) { return (r & kLongRec) ? (r >> 14) & 0x3FFFu : (r >> 8) & 0xFFu; }
+__device__ __forceinline__ uint32_t cr_inner_open(uint32_t r) { return (r & kLongRec) ? r & 0x3FFFu : (r >> 16) & 0xFFu; }
+__device__ __forceinline__ uint32_t cr_last_close(uint32_t r) { return (r & kLongRec) ? (r >> 14) & 0x3FFFu : r >> 24; }
+
 // the string's chains (<= kMaxTop, depth <= kChainDepth; records as in ChainJobs::crec). False:
 // the string is not a chain-only clean string (the exact evaluator decides it).
 __device__ __forceinline__ bool parse_chains(const lds_u8* tile, uint32_t p0, uint32_t n, const lds_u32* cm,
@@ -241,23 +249,50 @@ __device__ __forceinline__ bool parse_chains(const lds_u8* tile, uint32_t p0, ui
                                              Ev& Om_out, Ev& Cm_out, uint32_t& maxd_out, bool& whole_out) {
   whole_out = false;
   if (active && n > kChainMax) {
-    // a long string is copied verbatim when none of its bytes is a brace and its chunks hold no
-    // U+3020 lead byte (no pair to resolve, no placeholder to collide with: py:505-540 leave it
-    // unchanged); otherwise the exact evaluator decides it
+    // A long string (a prompt template): copied verbatim when none of its bytes is a brace and its
+    // chunks hold no U+3020 lead byte (py:505-540 leave it unchanged). One with up to kMaxTop FLAT
+    // pairs ({key} with no brace inside, no '\\' near any of them) is chain-shaped too: each pair is
+    // a one-level chain whose record holds 14-bit positions (kLongRec). Anything else: the exact
+    // evaluator.
     nch = 0;
 #pragma unroll
     for (int c = 0; c < kMaxTop; c++) crec[c] = cdep[c] = 0;
     const uint32_t c0 = p0 >> 4, cl = (p0 + n - 1) >> 4;
-    bool clean = true;
-    for (uint32_t c = c0; c <= cl && clean; c++) {
-      const uint32_t m = cm[c];  // bits 0-15 '{', 16-31 '}' of the chunk's bytes
+    bool ok = n < (1u << 14), braces = false, esc = false, inside = false;
+    uint32_t a = 0;
+    for (uint32_t c = c0; c <= cl && ok; c++) {
       const uint32_t b_lo = c == c0 ? (p0 & 15u) : 0u, b_hi = c == cl ? ((p0 + n - 1) & 15u) : 15u;
       const uint32_t bm = ((2u << b_hi) - 1u) & ~((1u << b_lo) - 1u);  // the string's bytes in the chunk
-      clean = (((m | (m >> 16)) & bm) == 0u) && !((oddbits[c >> 5] >> (c & 31u)) & 1u);
+      uint32_t op = cm[c] & bm, cls = (cm[c] >> 16) & bm;  // '{' / '}' bytes of the chunk
+      if ((oddbits[c >> 5] >> (c & 31u)) & 1u) ok = false;
+      esc |= ((escbits[c >> 5] >> (c & 31u)) & 1u) != 0u;
+      braces |= (op | cls) != 0u;
+      while ((op | cls) && ok) {  // the chunk's events in byte order
+        const uint32_t k = (uint32_t)__builtin_ctz(op | cls), pos = 16u * c + k - p0;
+        if ((op >> k) & 1u) {
+          ok = !inside;  // a brace inside a pair: nesting (the exact evaluator)
+          inside = true;
+          a = pos;
+          op &= op - 1u;
+        } else {
+          ok = inside && nch < (uint32_t)kMaxTop;  // a '}' before its '{', or too many pairs
+          if (ok) {
+            crec[nch] = kLongRec | a | (pos << 14);
+            cdep[nch] = 1u;
+            nch++;
+          }
+          inside = false;
+          cls &= cls - 1u;
+        }
+      }
     }
+    ok = ok && !inside && !(braces && esc);
+    // a single pair that is the whole string: get_simple_insertkey's typed result (exact evaluator)
+    ok = ok && !(nch == 1u && (crec[0] & 0x3FFFu) == 0u && ((crec[0] >> 14) & 0x3FFFu) == n - 1u);
+    if (!ok) nch = 0;
     Om_out = Cm_out = Ev{0ull, 0ull};
-    maxd_out = 0;
-    return clean;
+    maxd_out = ok && nch ? 1u : 0u;
+    return ok;
   }
   bool ok = active && n <= kChainMax;
   // ---- 1. the string's open / close events as 128-bit windows ----

@@ -463,8 +463,8 @@ __device__ void resolve_jobs(const DevTable& T, const lds_u8* tile, const ChainJ
       // level r: the innermost pair in round 0, the outermost in the last round; a middle level is
       // the open before the previous level's and the close after it (from the string's masks)
       const bool top = r + 1 == dep[q];
-      uint32_t o = r == 0 ? (cr[q] >> 16) & 0xFFu : top ? cr[q] & 0xFFu : 0u;
-      uint32_t c = r == 0 ? (cr[q] >> 8) & 0xFFu : top ? cr[q] >> 24 : 0u;
+      uint32_t o = r == 0 ? cr_inner_open(cr[q]) : top ? cr_first_open(cr[q]) : 0u;
+      uint32_t c = r == 0 ? cr_first_close(cr[q]) : top ? cr_last_close(cr[q]) : 0u;
       const bool mid = on[q] && r != 0 && !top;
       if (__any(mid)) {
         if (mid) {
@@ -617,11 +617,11 @@ __device__ bool combine_chains(const ChainJobs J, uint32_t jb, uint32_t nch, con
   for (int c = 0; c < kMaxTop; c++) {
     if ((uint32_t)c >= nch) continue;
     const uint32_t rk = J.res_k[jb + c], rs = J.res_s[jb + c];
-    const uint32_t a = crec[c] & 0xFFu, e = crec[c] >> 24;
+    const uint32_t a = cr_first_open(crec[c]), e = cr_last_close(crec[c]);
     if (rk & kResReject) {
       ok = false;
     } else if ((rk >> 30) == 0u) {  // failed at the pair opening at (rk >> 8) & 0xFF
-      const uint32_t op = (rk >> 8) & 0xFFu;
+      const uint32_t op = (rk >> 8) & 0x3FFFu;  // (14 bits: the flat pairs of long strings)
       if ((fw & 0xFFu) == 0u || op > (fw >> 8)) fw = (op << 8) | (rk & 0xFFu);
     } else {
       d.open[c] = a;
