@@ -413,7 +413,6 @@ struct ChainJobs {  // LDS views, tile-wide
 constexpr uint32_t kJobCap = kMaxTop * kRBlock;
 constexpr uint32_t kResFail = 1u << 29, kResReject = 1u << 28;
 constexpr uint32_t kResWhole = 1u << 27;  // a whole-string '{key}' (res_s: the value id; kind bits 0-2)
-constexpr uint32_t kSubsetGrid = 1024;  // workgroups for a deferred views subset (4 per CU)
 
 // The jobs [j0, j0 + 2 * kRBlock) of the tile: lane t takes jobs j0 + t and j0 + kRBlock + t. Round r
 // resolves level r of each job (the innermost pair in round 0); the key of a level is A | T | B
@@ -1124,7 +1123,7 @@ __global__ __launch_bounds__(kRBlock) void k_emit_windows(Batch B0, Work W, DevT
 // UNESC (with VIEWS): the unescape command's resolve, fused with its recursive_unescape: the tile
 // is unescaped in the LDS stage (unescape_stage) and then resolved; strings that cannot be finished
 // there (not staged, or needing the literal path) go to W.udefer_list for the deferred pass.
-template <bool FAILC, bool MULTI, bool VIEWS, bool UNESC = false, bool LK = false, bool SUB = false>
+template <bool FAILC, bool MULTI, bool VIEWS, bool UNESC = false, bool LK = false>
 __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES_PER_EU))) void k_resolve(Batch B0, Work W, DevTable T, uint8_t* out,
                                                     uint64_t cap) {
   // a deferred subset counts its strings on the device (the grid is sized for B0.n)
@@ -1148,16 +1147,13 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
   const uint32_t ntiles = (uint32_t)((B.n + kRBlock - 1) / kRBlock);
   // Tile = workgroup index: workgroups are dispatched in index order, so every tile a look-back
-  // waits on is already resident (no ticket: a single-address atomic serializes chip-wide). A
-  // deferred views subset (its size counted on the device) runs on a bounded grid instead, each
-  // workgroup looping over tiles (no look-back there), so that a near-empty subset costs little.
-  constexpr bool loop = VIEWS && SUB;  // (its own instances: the loop's registers stay out of the rest)
-  for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  // waits on is already resident (no ticket: a single-address atomic serializes chip-wide).
+  const uint32_t tile = blockIdx.x;
   const TileGeo geo = load_geo(B, tile, tid);
   TilePrefetch<kStageV> pre;
   pre.nv = 0;
-  pre.issue(B, geo, tid);
-  {
+  if (tile < ntiles) pre.issue(B, geo, tid);
+  if (tile < ntiles) {
   uint64_t t_start = 0;
   if (tid == 0) {
     if (W.stamps) t_start = __builtin_amdgcn_s_memrealtime();
@@ -1534,9 +1530,6 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
   IE_STAMP(5);
 #undef IE_STAMP
   }
-  if (!loop) break;  // one tile per workgroup (the look-back's dispatch-order argument)
-  __syncthreads();   // the next tile reuses the LDS
-  }
 }
 
 // diagnostic: one key through the device lookups. out[0..1] hash, out[2] slot, out[3] find_bytes,
@@ -1624,7 +1617,7 @@ hipError_t launch_resolve_impl(const Batch& B, const Work& W, const DevTable& T,
   const uint64_t tiles = (B.n + kRBlock - 1) / kRBlock;
   if (!tiles) return hipSuccess;
   if (tiles > 0xFFFFFFFFull) return hipErrorInvalidValue;
-  uint32_t grid = (uint32_t)tiles;
+  const uint32_t grid = (uint32_t)tiles;
   const bool multi = B.table_id != nullptr;
   if (unesc) {  // the fused unescape command (views only)
     if (!B.out_len) return hipErrorInvalidValue;
@@ -1638,17 +1631,6 @@ hipError_t launch_resolve_impl(const Batch& B, const Work& W, const DevTable& T,
   }
   // LK: a table with 17-32 byte keys gets the instances whose chain jobs take such keys (they cost
   // config 3 3 %: their registers; config 5 -32 %: its long keys leave the exact evaluator)
-  // a deferred views subset: at most a residency's worth of workgroups, looping over the tiles
-  if (B.n_dev && B.out_len) {
-    if (grid > kSubsetGrid) grid = kSubsetGrid;
-    const int v = (W.fail_commit ? 2 : 0) | (multi ? 1 : 0);
-    if (v == 0) hipLaunchKernelGGL((k_resolve<false, false, true, false, false, true>), dim3(grid), dim3(kRBlock), 0, st, B, W, T, out, cap);
-    if (v == 1) hipLaunchKernelGGL((k_resolve<false, true, true, false, false, true>), dim3(grid), dim3(kRBlock), 0, st, B, W, T, out, cap);
-    if (v == 2) hipLaunchKernelGGL((k_resolve<true, false, true, false, false, true>), dim3(grid), dim3(kRBlock), 0, st, B, W, T, out, cap);
-    if (v == 3) hipLaunchKernelGGL((k_resolve<true, true, true, false, false, true>), dim3(grid), dim3(kRBlock), 0, st, B, W, T, out, cap);
-    hipLaunchKernelGGL(k_emit_windows, dim3(grid < 512u ? grid : 512u), dim3(kRBlock), 0, st, B, W, T, out);
-    return hipGetLastError();
-  }
   const int variant = ((T.flags & TF_LONG_KEYS) ? 8 : 0) | (W.fail_commit ? 4 : 0) | (multi ? 2 : 0) | (B.out_len ? 1 : 0);
   switch (variant) {
 #define IE_LAUNCH(V, F, M, S, L) \
