@@ -330,7 +330,9 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(IE_LEAN_W
     bool ok = parse_chains((const lds_u8*)s_stage, staged ? p0 : 0u, staged ? n32 : 0u, (const lds_u32*)s_cm,
                            (const lds_u32*)s_odd, (const lds_u32*)s_esc, staged, crec, cdep, nch, Om, Cm, maxd,
                            whole1);
-    ok = ok && !whole1 && n32 <= kChainMax;  // (long templates' flat pairs: k_resolve's chain jobs)
+    // (long templates with flat pairs have wide chain records: k_resolve's chain jobs take them;
+    // a long brace-free string is copied here)
+    ok = ok && !whole1 && (n32 <= kChainMax || nch == 0u);
     const lds_u8* const s = (const lds_u8*)s_stage + (staged ? p0 : 0u);
     uint32_t rk[kMaxTop], rs[kMaxTop];  // per chain: value kind << 30 | text length; entry / arena offset
     bool rej = false;
