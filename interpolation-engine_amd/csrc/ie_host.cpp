@@ -274,7 +274,8 @@ int set_device(int32_t dev) {
 constexpr uint32_t kLeanShards = 16;  // k_lean's cursor shards, 128 B apart after the counters
 constexpr uint64_t kCounterBytes = 64 + kLeanShards * 128;
 int ensure_work(ie_exec* x, int op, uint64_t n) {
-  const uint64_t tiles = (n + kBlock - 1) / kBlock + 1;  // (kRBlock >= kBlock: enough for k_resolve too)
+  // (k_resolve tiles of 128 strings or more: enough look-back words and deferred-tile slots)
+  const uint64_t tiles = (n + 127) / 128 + 1;
   // counters, then (interpolation) the look-back words: one buffer, zeroed by one memset per call
   IE_HIP(x->counters.ensure(kCounterBytes + (op == kOpInterp ? tiles * sizeof(uint64_t) : 0)));
   if (op == kOpInterp) {
@@ -282,7 +283,7 @@ int ensure_work(ie_exec* x, int op, uint64_t n) {
     // room for every tile to be deferred (64 B of descriptor per string; grow-only, never read
     // unless written, so only HBM capacity is spent)
     IE_HIP(x->defer_tiles.ensure(tiles * sizeof(uint32_t)));
-    IE_HIP(x->defer_desc.ensure(tiles * kBlock * 64));  // tiles * kBlock >= resolve tiles * kRBlock
+    IE_HIP(x->defer_desc.ensure(tiles * 128 * 64));  // whole tiles of kRBlock >= 128 strings
   } else {
     IE_HIP(x->out_len.ensure((n + 1) * sizeof(uint32_t)));
     IE_HIP(x->tile_sum.ensure(tiles * sizeof(uint64_t)));
@@ -350,7 +351,7 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
   const uint64_t cap = out->bytes ? out->bytes_cap : 0;
   if (x->timing) IE_HIP(hipEventRecord(x->ev[0], st));
   // the counters and, for a packed interpolation, the look-back words (one fill instead of two)
-  const uint64_t zero_tiles = (op == kOpInterp && n && !d_out_len) ? (n + kRBlock - 1) / kRBlock : 0;
+  const uint64_t zero_tiles = (op == kOpInterp && n && !d_out_len) ? (n + 127) / 128 : 0;  // (ensure_work)
   IE_HIP(hipMemsetAsync(x->counters.p, 0, kCounterBytes + zero_tiles * sizeof(uint64_t), st));
   if (n == 0) {
     if (!d_out_len) IE_HIP(hipMemsetAsync(out->offsets, 0, sizeof(uint64_t), st));

@@ -20,8 +20,8 @@ constexpr int kStageBytes = 20480;   // escape kernels: LDS output stage
 #define IE_RBLOCK 256
 #endif
 constexpr int kRBlock = IE_RBLOCK;
-constexpr int kRTileBytes = 17664 * (IE_RBLOCK / 256);   // LDS input stage: the tile's first bytes
-constexpr int kRStageBytes = 20480 * (IE_RBLOCK / 256);  // LDS output stage; larger outputs: k_emit_windows
+constexpr int kRTileBytes = 17664 * IE_RBLOCK / 256;   // LDS input stage: the tile's first bytes
+constexpr int kRStageBytes = 20480 * IE_RBLOCK / 256;  // LDS output stage; larger outputs: k_emit_windows
 
 enum { kOpInterp = 0, kOpUnescape = 1, kOpEscape = 2 };
 
