@@ -1,14 +1,13 @@
 // ie_common.h — types shared by the host table builder and the gfx950 kernels.
 //
 // Device data layout of one inserts table (built once per get_interpdata snapshot, read-only):
-//   pilots[nb]      uint16 per pilot group: the displacement that sends every key of the group to
-//                   its own entry (a perfect hash: each key has exactly ONE candidate entry).
-//                   Tables of up to kLdsPilotKeys keys use at most kLdsPilots groups, so the kernel
-//                   keeps the pilots in LDS (a lookup is then one memory round trip, not two)
+//   pilots[nb]      uint16 per pilot group (about 4 keys per group): the displacement that sends
+//                   every key of the group to its own entry (a perfect hash: each key has exactly
+//                   ONE candidate entry). A lookup is two dependent reads, the pilot (L2-resident:
+//                   50 KB for 100k keys) and then the entry
 //   entries[m]      Entry (64 B): lengths, flags, arena offset, inline copies of the key (<= 16 B)
 //                   and splice text (<= 28 B), value id; a lookup reads the first 48 bytes (the
-//                   first 16 text bytes are all an inner nesting level needs);
-//                   m ~ 1.25 * keys (about 4 keys per group) or 2 * keys (the LDS pilot sizing)
+//                   first 16 text bytes are all an inner nesting level needs); m ~ 1.25 * keys
 //   arena[...]      every splice text (4-byte aligned) followed by its key (4-byte aligned)
 // Lookup of key k in table t of the set: h = hash_key(k, seed, t); group g = ph_group(h, nb);
 // slot = ph_slot(h, pilots[g]); the key is present iff entries[slot] holds it for table t (full
