@@ -106,6 +106,7 @@ struct ie_exec {
   int32_t opt_defer = 0;          // views batches: heavy strings to a second pass: -1 adaptive, 0 (default:
                                   // measured slower on config 5) / 1 (IE_DEFER)
   bool defer_slow = false;        // the adaptive choice (from an earlier batch's counts)
+  int32_t opt_small = 1;          // host batches of <= 1024 strings / 64 KB: one pinned copy each way (IE_SMALL_HOST)
   int32_t opt_lean = 0;           // views batches: k_lean first, k_resolve on what it lists (IE_LEAN; measured
                                   // slower than k_resolve alone: DESIGN.md, k_lean)
   int32_t lean_grid = 0;          // resident k_lean workgroups on the device (0: not known yet)
@@ -131,7 +132,13 @@ struct ie_exec {
   DevBuf s_lens, s_part;
   DevBuf stamps;        // diagnostic phase stamps (env IE_DEBUG_STAMPS=<file>)
   uint64_t stamp_tiles = 0;
+  // small host batches: one device block and one pinned host block (inputs, then outputs)
+  DevBuf sm_dev;
+  uint8_t* sm_host = nullptr;
+  uint64_t sm_host_bytes = 0;
   ~ie_exec() {
+    sm_dev.release();
+    if (sm_host) (void)hipHostFree(sm_host);
     for (DevBuf* b : {&u_list, &u_off, &u_len, &u_tid}) b->release();
     for (DevBuf* b : {&counters, &pool, &out_len, &tile_sum, &tile_base, &defer_tiles, &defer_desc, &in_bytes,
                       &in_off, &in_tid, &o_bytes, &o_off, &o_len, &o_status, &o_vid, &o_total, &wc_range, &wc_match, &wc_ncap, &wc_caps,
@@ -455,6 +462,71 @@ int check_device_error(ie_exec* x) {
   return IE_SUCCESS;
 }
 
+// Small host batches (the mirror's one-string calls, reference py:1691-1697 / 1722-1734): the
+// inputs packed into one pinned block and sent with one copy, every output array read back with
+// one copy, one synchronisation (the generic path below issues a pageable copy per array and
+// synchronises three times). Leaves b null when the output outgrew its first-guess capacity: the
+// generic path then runs the batch.
+constexpr uint64_t kSmallN = 1024, kSmallBytes = 1ull << 16;
+inline uint64_t al256(uint64_t v) { return (v + 255) & ~255ull; }
+
+int run_host_small(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, const uint64_t* offsets,
+                   uint64_t n, const uint32_t* table_id, bool views, ie_batch*& b, std::vector<uint32_t>& lens,
+                   uint64_t& total) {
+  const uint64_t base = offsets[0], in_bytes = offsets[n] - base, cap = 2 * in_bytes + 4096;
+  // input block: offsets | table ids | bytes (the device block keeps room for the loads' over-read)
+  const uint64_t i_tid = al256((n + 1) * 8), i_bytes = i_tid + al256(table_id ? n * 4 : 0);
+  const uint64_t in_size = i_bytes + al256(in_bytes + 64);
+  // output block: total | offsets | lengths (views) | statuses | value ids | bytes; then the
+  // device error word, read with a copy of its own
+  const uint64_t o_off = 256, o_len = o_off + al256((n + 1) * 8), o_st = o_len + al256(views ? n * 4 : 0),
+                 o_vid = o_st + al256(n + 1), o_bytes = o_vid + al256((n + 1) * 4), o_err = o_bytes + al256(cap);
+  const uint64_t need = in_size + o_err + 256;
+  IE_HIP(x->sm_dev.ensure(std::max<uint64_t>(need, 1ull << 19)));
+  if (x->sm_host_bytes < need) {
+    if (x->sm_host) (void)hipHostFree(x->sm_host);
+    x->sm_host = nullptr;
+    x->sm_host_bytes = 0;
+    const uint64_t want = std::max<uint64_t>(need, 1ull << 19);
+    IE_HIP(hipHostMalloc((void**)&x->sm_host, want, hipHostMallocDefault));
+    x->sm_host_bytes = want;
+  }
+  uint8_t* const h = x->sm_host;
+  uint8_t* const ho = h + in_size;
+  uint64_t* const hoff = (uint64_t*)h;
+  for (uint64_t i = 0; i <= n; i++) hoff[i] = offsets[i] - base;
+  if (table_id) memcpy(h + i_tid, table_id, n * 4);
+  if (in_bytes) memcpy(h + i_bytes, bytes + base, in_bytes);
+  uint8_t* const dv = (uint8_t*)x->sm_dev.p;
+  uint8_t* const dout = dv + in_size;
+  IE_HIP(hipMemcpyAsync(dv, h, i_bytes + in_bytes, hipMemcpyHostToDevice, x->stream));
+  ie_dev_out o{dout + o_bytes, cap, (uint64_t*)(dout + o_off), dout + o_st, (uint32_t*)(dout + o_vid), (uint64_t*)dout};
+  int rc = run_device(x, op, t, dv + i_bytes, (const uint64_t*)dv, n, &o,
+                      table_id ? (const uint32_t*)(dv + i_tid) : nullptr, views ? (uint32_t*)(dout + o_len) : nullptr);
+  if (rc) return rc;
+  IE_HIP(hipMemcpyAsync(ho, dout, o_err, hipMemcpyDeviceToHost, x->stream));
+  IE_HIP(hipMemcpyAsync(ho + o_err, (uint32_t*)x->counters.p + 1, 4, hipMemcpyDeviceToHost, x->stream));
+  IE_HIP(hipStreamSynchronize(x->stream));
+  const uint32_t err = *(const uint32_t*)(ho + o_err);  // (check_device_error's rules)
+  if (err & 2u) return fail(IE_ERR_CAPACITY, "a step's output did not fit its caller-sized buffer");
+  if (err) return fail(IE_ERR_TIMEOUT, "look-back spin timed out (a predecessor tile never published)");
+  total = *(const uint64_t*)ho;
+  if (total > cap) return IE_SUCCESS;
+  b = new ie_batch{};
+  b->n = n;
+  b->bytes_len = total;
+  b->bytes = new uint8_t[total + 1];
+  b->offsets = new uint64_t[n + 1];
+  b->status = new uint8_t[n + 1];
+  b->value_id = new uint32_t[n + 1];
+  if (total) memcpy(b->bytes, ho + o_bytes, total);
+  memcpy(b->offsets, ho + o_off, (views ? n : n + 1) * 8);
+  if (views) lens.assign((const uint32_t*)(ho + o_len), (const uint32_t*)(ho + o_len) + n);
+  memcpy(b->status, ho + o_st, n);
+  memcpy(b->value_id, ho + o_vid, n * 4);
+  return IE_SUCCESS;
+}
+
 // synchronous host batch: H2D, run, D2H; grows the output buffer and re-runs overflowed
 // literal-path strings with the full working space until every status is final.
 int run_host(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, const uint64_t* offsets,
@@ -465,72 +537,80 @@ int run_host(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, const 
   if (table_id && t)
     for (uint64_t i = 0; i < n; i++)
       if (table_id[i] >= t->n_tables) return fail(IE_ERR_INVALID, "table id beyond the table set");
-  const uint32_t* d_tid = nullptr;
-  if (table_id && n) {
-    IE_HIP(x->in_tid.ensure(n * 4));
-    IE_HIP(hipMemcpyAsync(x->in_tid.p, table_id, n * 4, hipMemcpyHostToDevice, x->stream));
-    d_tid = (const uint32_t*)x->in_tid.p;
-  }
   const uint64_t base = n ? offsets[0] : 0;
   const uint64_t in_bytes = n ? offsets[n] - base : 0;
-  std::vector<uint64_t> off(n + 1);
-  for (uint64_t i = 0; i <= n; i++) off[i] = n ? offsets[i] - base : 0;
-  IE_HIP(x->in_bytes.ensure(in_bytes + 16));
-  IE_HIP(x->in_off.ensure((n + 1) * 8));
-  IE_HIP(x->o_off.ensure((n + 1) * 8));
-  IE_HIP(x->o_status.ensure(n + 1));
-  IE_HIP(x->o_vid.ensure((n + 1) * 4));
-  IE_HIP(x->o_total.ensure(8));
-  if (in_bytes) IE_HIP(hipMemcpyAsync(x->in_bytes.p, bytes + base, in_bytes, hipMemcpyHostToDevice, x->stream));
-  IE_HIP(hipMemcpyAsync(x->in_off.p, off.data(), (n + 1) * 8, hipMemcpyHostToDevice, x->stream));
-  uint64_t cap = std::max<uint64_t>(2 * in_bytes + 4096, x->o_bytes.bytes);
-  IE_HIP(x->o_bytes.ensure(cap));
-  cap = x->o_bytes.bytes;
-  ie_dev_out o{(uint8_t*)x->o_bytes.p, cap, (uint64_t*)x->o_off.p, (uint8_t*)x->o_status.p,
-               (uint32_t*)x->o_vid.p, (uint64_t*)x->o_total.p};
   // views: the device writes each string where its tile claimed room; packed on the host below
-  uint32_t* d_len = nullptr;
-  if (op == kOpInterp && x->opt_views && n) {
-    IE_HIP(x->o_len.ensure(n * 4));
-    d_len = (uint32_t*)x->o_len.p;
-  }
-  rc = run_device(x, op, t, (const uint8_t*)x->in_bytes.p, (const uint64_t*)x->in_off.p, n, &o, d_tid, d_len);
-  if (rc) return rc;
+  const bool views = op == kOpInterp && x->opt_views && n;
+  ie_batch* b = nullptr;
+  std::vector<uint32_t> lens;
   uint64_t total = 0;
-  IE_HIP(hipMemcpyAsync(&total, o.total, 8, hipMemcpyDeviceToHost, x->stream));
-  IE_HIP(hipStreamSynchronize(x->stream));
-  if ((rc = check_device_error(x))) return rc;
-  if (total > cap) {  // grow and re-run
-    IE_HIP(x->o_bytes.ensure(total + 4096));
-    o.bytes = (uint8_t*)x->o_bytes.p;
-    o.bytes_cap = x->o_bytes.bytes;
+  if (x->opt_small && n && n <= kSmallN && in_bytes <= kSmallBytes) {
+    rc = run_host_small(x, op, t, bytes, offsets, n, table_id, views, b, lens, total);
+    if (rc) return rc;
+  }
+  if (!b) {
+    const uint32_t* d_tid = nullptr;
+    if (table_id && n) {
+      IE_HIP(x->in_tid.ensure(n * 4));
+      IE_HIP(hipMemcpyAsync(x->in_tid.p, table_id, n * 4, hipMemcpyHostToDevice, x->stream));
+      d_tid = (const uint32_t*)x->in_tid.p;
+    }
+    std::vector<uint64_t> off(n + 1);
+    for (uint64_t i = 0; i <= n; i++) off[i] = n ? offsets[i] - base : 0;
+    IE_HIP(x->in_bytes.ensure(in_bytes + 16));
+    IE_HIP(x->in_off.ensure((n + 1) * 8));
+    IE_HIP(x->o_off.ensure((n + 1) * 8));
+    IE_HIP(x->o_status.ensure(n + 1));
+    IE_HIP(x->o_vid.ensure((n + 1) * 4));
+    IE_HIP(x->o_total.ensure(8));
+    if (in_bytes) IE_HIP(hipMemcpyAsync(x->in_bytes.p, bytes + base, in_bytes, hipMemcpyHostToDevice, x->stream));
+    IE_HIP(hipMemcpyAsync(x->in_off.p, off.data(), (n + 1) * 8, hipMemcpyHostToDevice, x->stream));
+    uint64_t cap = std::max<uint64_t>(2 * in_bytes + 4096, x->o_bytes.bytes);
+    IE_HIP(x->o_bytes.ensure(cap));
+    cap = x->o_bytes.bytes;
+    ie_dev_out o{(uint8_t*)x->o_bytes.p, cap, (uint64_t*)x->o_off.p, (uint8_t*)x->o_status.p,
+                 (uint32_t*)x->o_vid.p, (uint64_t*)x->o_total.p};
+    uint32_t* d_len = nullptr;
+    if (views) {
+      IE_HIP(x->o_len.ensure(n * 4));
+      d_len = (uint32_t*)x->o_len.p;
+    }
     rc = run_device(x, op, t, (const uint8_t*)x->in_bytes.p, (const uint64_t*)x->in_off.p, n, &o, d_tid, d_len);
     if (rc) return rc;
     IE_HIP(hipMemcpyAsync(&total, o.total, 8, hipMemcpyDeviceToHost, x->stream));
     IE_HIP(hipStreamSynchronize(x->stream));
     if ((rc = check_device_error(x))) return rc;
-    if (total > o.bytes_cap) return fail(IE_ERR_CAPACITY, "output grew between runs");
+    if (total > cap) {  // grow and re-run
+      IE_HIP(x->o_bytes.ensure(total + 4096));
+      o.bytes = (uint8_t*)x->o_bytes.p;
+      o.bytes_cap = x->o_bytes.bytes;
+      rc = run_device(x, op, t, (const uint8_t*)x->in_bytes.p, (const uint64_t*)x->in_off.p, n, &o, d_tid, d_len);
+      if (rc) return rc;
+      IE_HIP(hipMemcpyAsync(&total, o.total, 8, hipMemcpyDeviceToHost, x->stream));
+      IE_HIP(hipStreamSynchronize(x->stream));
+      if ((rc = check_device_error(x))) return rc;
+      if (total > o.bytes_cap) return fail(IE_ERR_CAPACITY, "output grew between runs");
+    }
+    b = new ie_batch{};
+    b->n = n;
+    b->bytes_len = total;
+    b->bytes = new uint8_t[total + 1];
+    b->offsets = new uint64_t[n + 1];
+    b->status = new uint8_t[n + 1];
+    b->value_id = new uint32_t[n + 1];
+    if (total) IE_HIP(hipMemcpyAsync(b->bytes, o.bytes, total, hipMemcpyDeviceToHost, x->stream));
+    if (d_len) {
+      lens.resize(n);
+      IE_HIP(hipMemcpyAsync(b->offsets, o.offsets, n * 8, hipMemcpyDeviceToHost, x->stream));
+      IE_HIP(hipMemcpyAsync(lens.data(), d_len, n * 4, hipMemcpyDeviceToHost, x->stream));
+    } else {
+      IE_HIP(hipMemcpyAsync(b->offsets, o.offsets, (n + 1) * 8, hipMemcpyDeviceToHost, x->stream));
+    }
+    if (n) IE_HIP(hipMemcpyAsync(b->status, o.status, n, hipMemcpyDeviceToHost, x->stream));
+    if (n) IE_HIP(hipMemcpyAsync(b->value_id, o.value_id, n * 4, hipMemcpyDeviceToHost, x->stream));
+    IE_HIP(hipStreamSynchronize(x->stream));
   }
-  ie_batch* b = new ie_batch{};
-  b->n = n;
-  b->bytes_len = total;
-  b->bytes = new uint8_t[total + 1];
-  b->offsets = new uint64_t[n + 1];
-  b->status = new uint8_t[n + 1];
-  b->value_id = new uint32_t[n + 1];
-  if (total) IE_HIP(hipMemcpyAsync(b->bytes, o.bytes, total, hipMemcpyDeviceToHost, x->stream));
-  std::vector<uint32_t> lens;
-  if (d_len) {
-    lens.resize(n);
-    IE_HIP(hipMemcpyAsync(b->offsets, o.offsets, n * 8, hipMemcpyDeviceToHost, x->stream));
-    IE_HIP(hipMemcpyAsync(lens.data(), d_len, n * 4, hipMemcpyDeviceToHost, x->stream));
-  } else {
-    IE_HIP(hipMemcpyAsync(b->offsets, o.offsets, (n + 1) * 8, hipMemcpyDeviceToHost, x->stream));
-  }
-  if (n) IE_HIP(hipMemcpyAsync(b->status, o.status, n, hipMemcpyDeviceToHost, x->stream));
-  if (n) IE_HIP(hipMemcpyAsync(b->value_id, o.value_id, n * 4, hipMemcpyDeviceToHost, x->stream));
-  IE_HIP(hipStreamSynchronize(x->stream));
-  if (d_len) {  // views -> packed in input order
+  if (views) {  // views -> packed in input order
     uint8_t* packed = new uint8_t[total + 1];
     uint64_t w = 0;
     for (uint64_t i = 0; i < n; i++) {
@@ -989,6 +1069,7 @@ int ie_exec_create(int32_t device, void* hip_stream, ie_exec** out) {
   if (const char* e = getenv("IE_TILE")) x->opt_tile = atoi(e) == 512 ? 512 : atoi(e) == 256 ? 256 : 0;
   if (const char* e = getenv("IE_VIEWS")) x->opt_views = atoi(e) != 0;
   if (const char* e = getenv("IE_LEAN")) x->opt_lean = atoi(e) != 0;
+  if (const char* e = getenv("IE_SMALL_HOST")) x->opt_small = atoi(e) != 0;
   if (const char* e = getenv("IE_DEFER")) x->opt_defer = atoi(e) < 0 ? -1 : atoi(e) != 0 ? 1 : 0;
   if (const char* e = getenv("IE_DEBUG_STAMPS")) x->stamps_path = e;
   if (hip_stream) {
