@@ -1,0 +1,93 @@
+"""The small-batch host path (ie_host.cpp run_host_small: inputs in one pinned block, every output
+array back with one copy, one synchronisation) against the per-array path (IE_SMALL_HOST=0) and the
+C oracle on the same batches: identical statuses, bytes and value ids, packed and views, with table
+ids, and with an output larger than the small path's first-guess capacity (it hands the batch to the
+per-array path)."""
+import random
+
+import pytest
+
+import __graft_entry__ as G
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+G.build()
+PKG = G.load_package()
+N = PKG._native
+CLOCK = (7, 8, 9)
+
+
+def _exec(monkeypatch, small, views):
+    monkeypatch.setenv("IE_SMALL_HOST", "1" if small else "0")
+    x = N.Exec(0)
+    x.set_option(N.OPT_VIEWS, views)
+    return x
+
+
+def _batch(rng, n):
+    keys = ["k%d" % j for j in range(40)]
+    out = []
+    for _ in range(n):
+        parts = []
+        for _ in range(rng.randrange(0, 4)):
+            r = rng.random()
+            if r < 0.5:
+                parts.append("{%s}" % rng.choice(keys))
+            elif r < 0.7:
+                parts.append("{n-{%s}}" % rng.choice(keys[:8]))
+            elif r < 0.8:
+                parts.append("{missing%d}" % rng.randrange(5))
+            elif r < 0.9:
+                parts.append("\\{lit\\}")
+            else:
+                parts.append("{big}")
+            parts.append("".join(rng.choice("abc xyz") for _ in range(rng.randrange(0, 12))))
+        out.append("".join(parts))
+    return out
+
+
+TABLE = dict({"k%d" % j: "v%d" % j for j in range(40)}, **{"n-v%d" % j: "nested%d" % j for j in range(8)},
+             big="B" * 3000, num=17)
+
+
+@pytest.mark.parametrize("views", [0, 1])
+@pytest.mark.parametrize("n", [1, 7, 300, 1024])
+def test_small_path_matches_per_array_path(monkeypatch, views, n):
+    rng = random.Random(1000 * n + views)
+    strings = _batch(rng, n)
+    t = PKG.InsertsTable(TABLE, clock=CLOCK)
+    small = t.run(strings, exec_=_exec(monkeypatch, True, views))
+    generic = t.run(strings, exec_=_exec(monkeypatch, False, views))
+    assert small == generic
+    ref = O.Oracle(TABLE, "py", clock=CLOCK)
+    for s, (st, payload) in zip(strings, small):
+        rst, rout, _ = ref.interpolate(s)
+        assert N.STATUS_NAMES[st] == rst, s
+        if rst == "OK_STR":
+            assert payload == rout, s
+
+
+@pytest.mark.parametrize("views", [0, 1])
+def test_small_path_output_past_first_capacity(monkeypatch, views):
+    # 12 x 3000 bytes of output from a 60-byte input: more than 2 x input + 4096
+    strings = ["{big}" * 12, "x{k1}y"]
+    t = PKG.InsertsTable(TABLE, clock=CLOCK)
+    got = t.run(strings, exec_=_exec(monkeypatch, True, views))
+    assert got == [(N.OK_STR, "B" * 36000), (N.OK_STR, "xv1y")]
+
+
+def test_small_path_table_ids(monkeypatch):
+    dicts = [{"a": "A%d" % i, "b": "{a}-%d" % i} for i in range(5)]
+    ts = PKG.InsertsTableSet(dicts, clock=CLOCK)
+    rng = random.Random(5)
+    strings = [rng.choice(["{a}", "<{b}>", "{c}", "t{a}{b}"]) for _ in range(200)]
+    ids = [rng.randrange(5) for _ in strings]
+    small = ts.run(strings, ids, exec_=_exec(monkeypatch, True, 0))
+    generic = ts.run(strings, ids, exec_=_exec(monkeypatch, False, 0))
+    assert small == generic
+    for s, i, (st, payload) in zip(strings, ids, small):
+        rst, rout, _ = O.Oracle(dicts[i], "py", clock=CLOCK).interpolate(s)
+        assert N.STATUS_NAMES[st] == rst, (s, i)
+        if rst == "OK_STR":
+            assert payload == rout, (s, i)
