@@ -79,8 +79,12 @@ struct ie_table {
   DevTable dev{};
   // the clock entries ('HH:MM', 'HH:MM:SS' of every table): slot, host copy (ie_table_set_clock)
   std::vector<std::pair<uint32_t, Entry>> clock_entries;
-  DevBuf block;  // entries | pilots | arena: one allocation, one upload, one free
-  ~ie_table() { block.release(); }
+  DevBuf entries, pilots, arena;
+  ~ie_table() {
+    entries.release();
+    pilots.release();
+    arena.release();
+  }
 };
 
 struct ie_exec {
@@ -766,21 +770,13 @@ int upload_table(const std::vector<Ent>& ents, uint32_t n_tables, int32_t dialec
     if (attempt & 1) m += m / 4;
     else seed = fmix64_host(seed + 0x9E3779B97F4A7C15ull);
   }
-  for (int pad = 0; pad < 16; pad++) arena.push_back(0);  // dword reads past the last text
-  // the device image: entries | pilots | arena (256-byte aligned parts), built in place and sent
-  // with one copy into one allocation (a table rebuilt per dict mutation pays one hipMalloc and
-  // one hipFree, not three)
-  const uint64_t e_bytes = m * sizeof(Entry), p_bytes = pilots.size() * sizeof(uint16_t);
-  const uint64_t p_off = (e_bytes + 255) & ~255ull, a_off = p_off + ((p_bytes + 255) & ~255ull);
-  std::vector<uint8_t> image(a_off + arena.size() + 16, 0);
-  Entry* const entries = (Entry*)image.data();
+  std::vector<Entry> entries(m);
   for (size_t i = 0; i < items.size(); i++) entries[slot_of[i]] = items[i];
-  if (p_bytes) memcpy(image.data() + p_off, pilots.data(), p_bytes);
-  memcpy(image.data() + a_off, arena.data(), arena.size());
   std::vector<std::pair<uint32_t, Entry>> clock_entries;
   for (size_t i = 0; i < items.size(); i++)
     if (items[i].vid == IE_VID_CLOCK_HHMM || items[i].vid == IE_VID_CLOCK_HHMMSS)
       clock_entries.emplace_back(slot_of[i], items[i]);
+  for (int pad = 0; pad < 16; pad++) arena.push_back(0);  // dword reads past the last text
   ie_table* t = new ie_table();
   t->device = device;
   t->dialect = dialect;
@@ -788,15 +784,21 @@ int upload_table(const std::vector<Ent>& ents, uint32_t n_tables, int32_t dialec
   t->n_entries = ents.size();
   t->n_tables = n_tables;
   t->clock_entries = std::move(clock_entries);
-  hipError_t e = t->block.ensure(image.size());
-  if (e == hipSuccess) e = hipMemcpy(t->block.p, image.data(), image.size(), hipMemcpyHostToDevice);
-  if (e != hipSuccess) {
+  auto up = [&](DevBuf& b, const void* src, uint64_t bytes) -> hipError_t {
+    hipError_t e = b.ensure(bytes + 16);
+    if (e != hipSuccess) return e;
+    return bytes ? hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice) : hipSuccess;
+  };
+  hipError_t e1 = up(t->entries, entries.data(), entries.size() * sizeof(Entry));
+  hipError_t e2 = e1 == hipSuccess ? up(t->pilots, pilots.data(), pilots.size() * sizeof(uint16_t)) : e1;
+  hipError_t e3 = e2 == hipSuccess ? up(t->arena, arena.data(), arena.size()) : e2;
+  if (e3 != hipSuccess) {
     delete t;
-    return fail(IE_ERR_HIP, std::string("table upload: ") + hipGetErrorString(e));
+    return fail(IE_ERR_HIP, std::string("table upload: ") + hipGetErrorString(e3));
   }
-  t->dev.entries = (const Entry*)t->block.p;
-  t->dev.pilots = (const uint16_t*)((const uint8_t*)t->block.p + p_off);
-  t->dev.arena = (const uint8_t*)t->block.p + a_off;
+  t->dev.entries = (const Entry*)t->entries.p;
+  t->dev.pilots = (const uint16_t*)t->pilots.p;
+  t->dev.arena = (const uint8_t*)t->arena.p;
   t->dev.seed = seed;
   t->dev.nb = nb;
   t->dev.m = (uint32_t)m;
@@ -990,19 +992,22 @@ int ie_table_replicate(const ie_table* t, int32_t device, ie_table** out) {
   c->n_tables = t->n_tables;
   c->clock_entries = t->clock_entries;
   c->dev = t->dev;
-  hipError_t e = c->block.ensure(t->block.bytes);
-  if (e == hipSuccess) e = hipMemcpyPeer(c->block.p, device, t->block.p, t->device, t->block.bytes);
+  auto copy = [&](DevBuf& dst, const DevBuf& src) -> hipError_t {
+    hipError_t e = dst.ensure(src.bytes);
+    if (e != hipSuccess || !src.bytes) return e;
+    return hipMemcpyPeer(dst.p, device, src.p, t->device, src.bytes);
+  };
+  hipError_t e = copy(c->entries, t->entries);
+  if (e == hipSuccess) e = copy(c->pilots, t->pilots);
+  if (e == hipSuccess) e = copy(c->arena, t->arena);
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) {
     delete c;
     return fail(IE_ERR_HIP, std::string("table replicate: ") + hipGetErrorString(e));
   }
-  // the same image layout at the copy's base
-  const uint8_t* const tb = (const uint8_t*)t->block.p;
-  const uint8_t* const cb = (const uint8_t*)c->block.p;
-  c->dev.entries = (const Entry*)(cb + ((const uint8_t*)t->dev.entries - tb));
-  c->dev.pilots = (const uint16_t*)(cb + ((const uint8_t*)t->dev.pilots - tb));
-  c->dev.arena = cb + (t->dev.arena - tb);
+  c->dev.entries = (const Entry*)c->entries.p;
+  c->dev.pilots = (const uint16_t*)c->pilots.p;
+  c->dev.arena = (const uint8_t*)c->arena.p;
   *out = c;
   return IE_SUCCESS;
 }
@@ -1042,8 +1047,8 @@ int ie_table_set_clock(ie_table* t, const ie_clock* now) {
     const char* txt = e.vid == IE_VID_CLOCK_HHMM ? hhmm : hhmmss;
     if (strlen(txt) != e.text_len) return fail(IE_ERR_INVALID, "clock field out of range");
     memcpy(e.text, txt, e.text_len);
-    IE_HIP(hipMemcpy((Entry*)t->dev.entries + ce.first, &e, sizeof(Entry), hipMemcpyHostToDevice));
-    IE_HIP(hipMemcpy((uint8_t*)t->dev.arena + e.text_off, txt, e.text_len, hipMemcpyHostToDevice));
+    IE_HIP(hipMemcpy((Entry*)t->entries.p + ce.first, &e, sizeof(Entry), hipMemcpyHostToDevice));
+    IE_HIP(hipMemcpy((uint8_t*)t->arena.p + e.text_off, txt, e.text_len, hipMemcpyHostToDevice));
   }
   return IE_SUCCESS;
 }
