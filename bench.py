@@ -12,9 +12,14 @@ One step = one pass of the hot path over one batch of synthetic strings already 
             replace_map first-round strings, from the reference-recorded trees in
             tests/golden/config5_trees.json) against one inserts dict per state, all states in
             one table set, a table id per string
-Multi-GPU: one process per GPU, each resolving its own shard (weak scaling; the table is built
-per rank, no data-path collective — only the barrier and the max-over-ranks time go over
-torch.distributed, gloo on the host).
+Multi-GPU: one process per GPU, each resolving its own shard (the table is built per rank, no
+data-path collective — only the barrier and the max-over-ranks time go over torch.distributed,
+gloo on the host). `--gpus N` with N > 1 and no launcher around it starts the N rank processes
+itself (torch.distributed.run as a child process, before this process loads the library or makes
+any HIP call); under a launcher WORLD_SIZE must equal N. Rank r drives device LOCAL_RANK unless
+`--device` makes ranks share one; `n_gpus` counts distinct devices, `ranks` the processes.
+`--scaling weak` (configs 2-4 by default: every rank owns n strings, so config 4 at 8 GPUs is the
+100M batch) or `strong` (config 5 by default: the 10k states are the global batch, split by state).
 
 Prints ONE JSON line (rank 0): `value` = interpolated MB/s (input payload, 1 MB = 1e6 B) over
 all ranks; `roofline` prices the resolve pipeline against HBM (algorithmic bytes
@@ -48,11 +53,66 @@ WORKLOADS = {
        "first-round strings, ~180), one inserts dict per state in one table set",
 }
 DEFAULT_N = {2: 1_000_000, 3: 10_000_000, 4: 12_500_000, 5: 10_000}  # strings (configs 2-4) / states (5)
+# the batch BASELINE.json names for each config (weak: per GPU; strong: over all GPUs)
+DEFAULT_SCALING = {2: "weak", 3: "weak", 4: "weak", 5: "strong"}
 
 
 def shard_first(rank, n_per_rank):
     """First global index (string or state) of a rank's shard: every rank owns n (weak scaling)."""
     return rank * n_per_rank
+
+
+def shard_range(rank, world, n, scaling):
+    """(first, count) of a rank's shard of the global unit (string / state) index space: weak
+    scaling gives every rank n units, strong scaling splits n units over the world."""
+    if scaling == "weak":
+        return shard_first(rank, n), n
+    lo, hi = rank * n // world, (rank + 1) * n // world
+    return lo, hi - lo
+
+
+def launch_ranks(args, argv):
+    """`--gpus N` (N > 1) without a launcher: start the N ranks as child processes with the
+    environment torch.distributed.run gives them (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_*), wait
+    for all of them and return the first non-zero exit code (the others are then stopped). This
+    process never loads the library or initialises HIP (no exec from a process that touched the
+    GPU); the ranks are the ones that do."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in pending:  # a failed rank leaves the others waiting at a barrier
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def rank_devices(args, world, local, ndev):
+    """This rank's device, or SystemExit when the request cannot be met: N ranks need N visible
+    devices unless --device makes them share one explicitly."""
+    if args.device >= 0:
+        if args.device >= ndev:
+            raise SystemExit("device %d requested, %d visible" % (args.device, ndev))
+        return args.device
+    if world > ndev:
+        raise SystemExit("--gpus %d needs %d devices, %d visible (--device D shares one device)" % (world, world, ndev))
+    return local
 
 
 def max_over_ranks(x, dist):
@@ -63,6 +123,16 @@ def max_over_ranks(x, dist):
     t = torch.tensor([x], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def sum_over_ranks(xs, dist):
+    """Sums of integers over all ranks (the whole job's bytes and strings)."""
+    if dist is None:
+        return list(xs)
+    import torch
+    t = torch.tensor(list(xs), dtype=torch.int64)
+    dist.all_reduce(t)
+    return [int(v) for v in t.tolist()]
 
 
 def parse(argv=None):
@@ -79,6 +149,12 @@ def parse(argv=None):
     ap.add_argument("--layout", choices=["views", "packed"], default="",
                     help="output layout (default views; config 4 views runs the fused unescape command): views = each tile claims its "
                          "output range with one atomic (no look-back), packed = input order (look-back)")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="",
+                    help="weak: --n units per GPU; strong: --n units over all GPUs (default per config: DEFAULT_SCALING)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="control plane only (launcher, rank/device assignment, barrier, max over ranks): no library, "
+                         "no GPU; --dry-devices devices are taken as visible")
+    ap.add_argument("--dry-devices", type=int, default=-1)
     return ap.parse_args(argv)
 
 
@@ -199,11 +275,57 @@ class States:
         self.tset.close()
 
 
-def main():
-    args = parse()
+def dry_run(args, world, rank, local):
+    """The multi-rank control plane without the library or a GPU (tests/test_bench_launch.py):
+    device assignment, the barrier and the max-over-ranks time, and the line's rank fields."""
+    ndev = args.dry_devices if args.dry_devices >= 0 else world
+    dev = rank_devices(args, world, local, ndev)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    devs = gather_devices(dev, world, dist)
+    cfg = args.config
+    scaling = args.scaling or DEFAULT_SCALING[cfg]
+    first, n = shard_range(rank, world, args.n or DEFAULT_N[cfg], scaling)
+    units = [None] * world
+    if dist:
+        dist.all_gather_object(units, (first, n))
+        dist.barrier()
+    else:
+        units = [(first, n)]
+    wall = max_over_ranks(0.001 * (rank + 1), dist)
+    if rank == 0:
+        print(json.dumps({"metric": "interpolated MB/s + strings/s on synthetic batches at 1/2/4/8 MI355X", "value": None,
+                          "unit": "MB/s", "n_gpus": len(set(devs)), "ranks": world, "devices": devs, "dry_run": True,
+                          "scaling": scaling, "shards": units, "wall_max_s": wall}), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def gather_devices(dev, world, dist):
+    """Every rank's device (rank order)."""
+    if dist is None:
+        return [dev]
+    out = [None] * world
+    dist.all_gather_object(out, dev)
+    return out
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args, argv))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("--gpus %d but WORLD_SIZE is %d" % (args.gpus, world))
+    if args.dry_run:
+        return dry_run(args, world, rank, local)
 
     # the library (and with it the HIP runtime it links) is loaded before anything imports torch:
     # torch bundles a HIP runtime of the same soname, and which one binds depends on load order
@@ -213,19 +335,22 @@ def main():
     N = pkg._native
     L = N.lib()
     ndev = L.ie_device_count()
-    dev = args.device if args.device >= 0 else local
-    if ndev <= 0 or dev >= ndev:
-        raise SystemExit("device %d requested, %d visible" % (dev, ndev))
+    if ndev <= 0:
+        raise SystemExit("no HIP device visible")
+    dev = rank_devices(args, world, local, ndev)
 
     dist = None
     if world > 1:
         # control plane only (barrier + max-over-ranks time): the shards are independent
         import torch.distributed as dist
         dist.init_process_group("gloo")
+    devs = gather_devices(dev, world, dist)
 
     cfg = args.config
-    n_units = args.n or DEFAULT_N[cfg]
-    first = shard_first(rank, n_units)  # this rank's shard of the global string / state index space
+    scaling = args.scaling or DEFAULT_SCALING[cfg]
+    # this rank's shard of the global string / state index space
+    first, n_units = shard_range(rank, world, args.n or DEFAULT_N[cfg], scaling)
+    total_units = n_units * world if scaling == "weak" else (args.n or DEFAULT_N[cfg])
     x = N.Exec(dev)
     # literal-path scratch sized for the workload (the call stays asynchronous; the statuses below
     # prove no string ran out of it)
@@ -321,8 +446,9 @@ def main():
     id_bytes = 4 * n if ids is not None else 0
     alg_bytes = in_bytes + out_bytes + 17 * n + id_bytes  # |in| + |out| + 16 (offsets) + 1 (status)
     achieved_gbs = alg_bytes / (gpu_ms * 1e-3) / 1e9
-    value = in_bytes * world / wall_max * args.steps / 1e6  # MB/s over all ranks
-    strings_per_s = n * world * args.steps / wall_max
+    all_bytes, all_strings = sum_over_ranks([in_bytes, n], dist)
+    value = all_bytes / wall_max * args.steps / 1e6  # MB/s over all ranks
+    strings_per_s = all_strings * args.steps / wall_max
 
     cpu = None
     if rank == 0 and not args.no_cpu:
@@ -348,18 +474,21 @@ def main():
             "metric": "interpolated MB/s + strings/s on synthetic batches at 1/2/4/8 MI355X",
             "value": round(value, 1),
             "unit": "MB/s",
-            "n_gpus": world,
+            "n_gpus": len(set(devs)),
+            "ranks": world,
+            "devices": devs,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(wall_max / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (SURVEY §8d generators; configs 2-4 splitmix64 seed 0x1E5EED00+config generated in "
                     "HBM; config 5 seeded states + the reference-recorded call stream)",
             "config": {"workload": WORKLOADS[cfg], "layout": layout, "strings_per_gpu": n, "input_bytes_per_gpu": in_bytes,
                        "output_bytes_per_gpu": out_bytes, "inserts": W.inserts, "parallelism": "shard%d" % world,
+                       "units_total": total_units, "input_bytes_total": all_bytes,
                        "statuses": status_counts, "table_build_s": round(W.build_s, 3)},
             "strings_per_s": round(strings_per_s, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,

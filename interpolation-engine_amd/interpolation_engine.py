@@ -96,6 +96,7 @@ class InsertsTableSet:
     This is the batch form of get_interpdata for many forked interpreter states (config 5)."""
 
     def __init__(self, dicts, dialect="py", clock=None, device=0, has_inserts_dir=False):
+        self.clock_pinned = clock is not None  # else the wall clock at build (set_clock re-reads it)
         if clock is None:
             now = _dt.datetime.now()
             clock = (now.hour, now.minute, now.second)

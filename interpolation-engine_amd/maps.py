@@ -25,9 +25,9 @@ Semantics kept from the reference, step by step:
               ... in `inserts | extra_inserts` to interpolate the value, repeated until nothing
               changes when repeat_until_done (py:1720-1745); an InterpolationException anywhere
               sets the raw 'NULL' value instead (py:1761-1771), or fails the task's assertion.
-Known difference: the reference re-interpolates the map keys on every pass of its loop; the
-inserts cannot change inside the command, so the keys are interpolated once per state (only a
-clock key read in a key could differ between passes).
+The map keys are interpolated again on every pass of the loop, as the reference does (py:1728),
+with the clock re-read (a table set built without a pinned clock); the inserts cannot change
+inside the command, so only a clock key read in a key can make two passes differ.
 """
 import copy
 
@@ -206,6 +206,11 @@ def replace_map_states(states, task, dialect="py", device=0, tables=None):
             tset.close()
     # per state: the first failing leaf in the reference's traversal order decides (py:1763-1771)
     for s in range(n):
+        if isinstance(names[s], BaseException):
+            # output_name is interpolated before the reference's try (py:1715, 1762): its error
+            # reaches the caller as it is, whatever 'NULL' says
+            out[s] = names[s]
+            continue
         if out[s] is not None:
             e = out[s]
         else:
@@ -218,8 +223,6 @@ def replace_map_states(states, task, dialect="py", device=0, tables=None):
             if value_if_error is no_value:  # py:1765-1766
                 out[s] = AssertionError("%s: replace_map encountered an interpolation error without 'NULL' key: %r"
                                         % (task.get("traceback_label"), e))
-            elif isinstance(names[s], BaseException):
-                out[s] = names[s]
             else:
                 out[s] = (names[s], copy.deepcopy(value_if_error))
         else:
@@ -235,14 +238,13 @@ def _replace_strings(tset, states, leaves, owner, keys, maps, m, repeat, dialect
     err = [None] * L
     active = list(range(L))
     vals_raw = [_first_value(d) for d in maps]
-    # per state: the keys before the first key that failed to interpolate (later keys are never
-    # tried once one fails: the failure propagates) and that failure
-    key_ok, key_err = {}, {}
-    for s in set(owner):
-        ks = keys[s * m:(s + 1) * m]
-        f = next((j for j, k in enumerate(ks) if isinstance(k, BaseException)), m)
-        key_ok[s] = f
-        key_err[s] = ks[f] if f < m else None
+    raw_keys = [_first_key(d) for d in maps]
+    # the reference interpolates the map keys inside its loop (py:1728): every pass again. They
+    # can only differ between passes through the clock keys, so the keys of the first pass are the
+    # ones replace_map_states computed; later passes re-read the clock and interpolate them again
+    # (in the same batch as the leaves) when some key text holds a brace.
+    live_keys = any("{" in k for k in raw_keys)
+    pinned = getattr(tset, "clock_pinned", False)
     passes = 0
     while active:
         passes += 1
@@ -250,8 +252,29 @@ def _replace_strings(tset, states, leaves, owner, keys, maps, m, repeat, dialect
             for i in active:
                 err[i] = RecursionError("replace_map does not reach a fixed point")
             break
-        # 1. interpolate (py:1722)
-        res = _str_results(tset, [cur[i] for i in active], [owner[i] for i in active])
+        # 1. interpolate (py:1722); the keys of this pass (py:1728)
+        batch, ids = [cur[i] for i in active], [owner[i] for i in active]
+        kstates = sorted(set(ids)) if passes > 1 and live_keys else []
+        if kstates:
+            if not pinned:
+                now = IE._dt.datetime.now()
+                tset.set_clock((now.hour, now.minute, now.second))
+            for s in kstates:
+                batch.extend(raw_keys)
+                ids.extend([s] * m)
+        res = _str_results(tset, batch, ids)
+        for j, s in enumerate(kstates):
+            base = len(active) + j * m
+            keys[s * m:(s + 1) * m] = res[base:base + m]
+        res = res[:len(active)]
+        # per state: the keys before the first key that fails to interpolate (later keys are never
+        # tried once one fails: the failure propagates) and that failure
+        key_ok, key_err = {}, {}
+        for s in set(ids):
+            ks = keys[s * m:(s + 1) * m]
+            f = next((j for j, k in enumerate(ks) if isinstance(k, BaseException)), m)
+            key_ok[s] = f
+            key_err[s] = ks[f] if f < m else None
         alive = []
         for i, r in zip(active, res):
             if isinstance(r, BaseException):

@@ -75,6 +75,52 @@ def fnv(s):
     return h
 
 
+# Edge cases of the two commands' error order (py:1689-1773) on one small state: an output_name
+# that fails (interpolated before replace_map's try, py:1715), failing item leaves and keys with and
+# without a 'NULL' map, a key that matches before a failing key, repeat_until_done on captures.
+EDGE_STATE = {"a": "apple", "n": 3, "who": "guard", "greet": "hello {who}"}
+EDGE_TASKS = [
+    {"cmd": "replace_map", "item": "apple pie", "output_name": "{missing_name}",
+     "wildcard_maps": [{"apple*": "fruit{1}"}], "traceback_label": "E1"},
+    {"cmd": "replace_map", "item": "apple pie", "output_name": "{missing_name}",
+     "wildcard_maps": [{"apple*": "x"}, {"NULL": "n"}], "traceback_label": "E2"},
+    {"cmd": "replace_map", "item": "x{missing}", "output_name": "out", "wildcard_maps": [{"*": "y"}],
+     "traceback_label": "E3"},
+    {"cmd": "replace_map", "item": "x{missing}", "output_name": "out", "wildcard_maps": [{"*": "y"}, {"NULL": "nv"}],
+     "traceback_label": "E4"},
+    {"cmd": "replace_map", "item": "pear", "output_name": "out", "wildcard_maps": [{"{nokey}": "y"}, {"NULL": "nv"}],
+     "traceback_label": "E5"},
+    {"cmd": "replace_map", "item": "pear", "output_name": "out", "wildcard_maps": [{"p*": "P{1}"}, {"{nokey}": "y"}],
+     "traceback_label": "E6"},
+    {"cmd": "replace_map", "item": "{a}", "output_name": "res_{n}", "wildcard_maps": [{"app*": "<{1}>"}],
+     "traceback_label": "E7"},
+    {"cmd": "replace_map", "item": ["{greet}!", {"k{n}": "{a}"}], "output_name": "out",
+     "wildcard_maps": [{"hello *": "hi {1}"}, {"*": "[{1}]"}], "traceback_label": "E8"},
+    {"cmd": "replace_map", "item": "aaab", "output_name": "out", "repeat_until_done": True,
+     "wildcard_maps": [{"a*": "{1}"}], "traceback_label": "E9"},
+    {"cmd": "goto_map", "text": "{missing}", "target_maps": [{"x": "t1"}, {"NULL": "tn"}], "traceback_label": "E10"},
+    {"cmd": "goto_map", "text": "{missing}", "target_maps": [{"x": "t1"}], "traceback_label": "E11"},
+    {"cmd": "goto_map", "text": "abc", "target_maps": [{"{nokey}": "t1"}], "traceback_label": "E12"},
+    {"cmd": "goto_map", "text": "{greet}", "target_maps": [{"hello *": "{who}"}], "traceback_label": "E13"},
+]
+
+
+def run_task(ie, state, t):
+    """One task through the reference's execute_task: an outcome record (see the module doc)."""
+    try:
+        before = dict(state["inserts"])
+        r = asyncio.run(ie.execute_task(state, copy.deepcopy(t), {}, {}, "x"))
+        if t["cmd"] == "goto_map":
+            return {"goto": r["goto_target"] if r else None}
+        name = next(k for k in state["inserts"] if k not in before or state["inserts"][k] is not before[k])
+        val = state["inserts"][name]
+        if isinstance(val, str) and len(val) > 256:
+            return {"set": [name, None], "len": len(val), "fnv": fnv(val)}
+        return {"set": [name, val]}
+    except Exception as e:  # noqa: BLE001 — the class is the outcome
+        return {"err": type(e).__name__}
+
+
 def map_tasks(program):
     out = []
 
@@ -121,7 +167,9 @@ def main():
             except Exception as e:  # noqa: BLE001 — the class is the outcome
                 row.append({"err": type(e).__name__})
         results.append(row)
-    out = {"tasks": tasks, "defaults": defaults, "states": args.states, "results": results}
+    edge = [run_task(ie, {"order_index": 1, "inserts": copy.deepcopy(EDGE_STATE), "output": ""}, t) for t in EDGE_TASKS]
+    out = {"tasks": tasks, "defaults": defaults, "states": args.states, "results": results,
+           "edge": {"state": EDGE_STATE, "tasks": EDGE_TASKS, "results": edge}}
     with open(os.path.join(HERE, "maps_py.json"), "w", encoding="utf-8") as f:
         json.dump(out, f, ensure_ascii=False, indent=0)
     from collections import Counter

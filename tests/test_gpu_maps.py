@@ -103,3 +103,19 @@ def test_single_state_entry_points():
         elif "err" not in want:
             M.replace_map(ins, task)
             assert _check(want, (want["set"][0], ins[want["set"][0]]))
+
+
+def test_error_order_edges_match_reference():
+    """Reference-generated edge cases (tests/golden/gen_maps.py EDGE_TASKS): an output_name that
+    fails raises its InterpolationException whatever 'NULL' says (py:1715 is before the try), item
+    leaves and keys that fail with and without 'NULL', a key matching before a failing key,
+    repeat_until_done over captures, goto_map's text / key failures."""
+    import copy
+    e = load_golden("maps_py.json")["edge"]
+    bad = []
+    for task, want in zip(e["tasks"], e["results"]):
+        fn = M.goto_map_states if task["cmd"] == "goto_map" else M.replace_map_states
+        got = fn([copy.deepcopy(e["state"])], task)[0]
+        if not _check(want, got):
+            bad.append((task["traceback_label"], want, repr(got)[:200]))
+    assert not bad, bad
