@@ -15,8 +15,8 @@ One step = one pass of the hot path over one batch of synthetic strings already 
 Multi-GPU: one process per GPU, each resolving its own shard (the table is built per rank, no
 data-path collective — only the barrier and the max-over-ranks time go over torch.distributed,
 gloo on the host). `--gpus N` with N > 1 and no launcher around it starts the N rank processes
-itself (torch.distributed.run as a child process, before this process loads the library or makes
-any HIP call); under a launcher WORLD_SIZE must equal N. Rank r drives device LOCAL_RANK unless
+itself (child processes with torch.distributed.run's environment, started before this process
+loads the library or makes any HIP call); under a launcher WORLD_SIZE must equal N. Rank r drives device LOCAL_RANK unless
 `--device` makes ranks share one; `n_gpus` counts distinct devices, `ranks` the processes.
 `--scaling weak` (configs 2-4 by default: every rank owns n strings, so config 4 at 8 GPUs is the
 100M batch) or `strong` (config 5 by default: the 10k states are the global batch, split by state).
@@ -149,6 +149,9 @@ def parse(argv=None):
     ap.add_argument("--layout", choices=["views", "packed"], default="",
                     help="output layout (default views; config 4 views runs the fused unescape command): views = each tile claims its "
                          "output range with one atomic (no look-back), packed = input order (look-back)")
+    ap.add_argument("--reserve", type=int, default=32,
+                    help="views output: IE_OPT_RESERVE (F x16: tile t writes at F x its input offset, no claim "
+                         "atomic; 0 = one claim per tile on one cursor)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="",
                     help="weak: --n units per GPU; strong: --n units over all GPUs (default per config: DEFAULT_SCALING)")
     ap.add_argument("--dry-run", action="store_true",
@@ -369,6 +372,8 @@ def main(argv=None):
     layout = args.layout or "views"
     views = layout == "views"
     d_olen = N.DeviceBuffer(x, 4 * n + 4) if views else None
+    reserve = args.reserve if views and (args.reserve * in_bytes) // 16 + (in_bytes >> 2) + (64 << 20) <= out_cap else 0
+    N.check(L.ie_exec_set_option(x.h, N.OPT_RESERVE, reserve), "IE_OPT_RESERVE")
     if views:
         o = N.DevViews(d_out.ptr, out_cap, d_ooff.ptr, d_olen.ptr, d_st.ptr, d_vid.ptr, d_tot.ptr)
     else:
@@ -486,7 +491,9 @@ def main(argv=None):
             "dtype": "u8",
             "data": "synthetic (SURVEY §8d generators; configs 2-4 splitmix64 seed 0x1E5EED00+config generated in "
                     "HBM; config 5 seeded states + the reference-recorded call stream)",
-            "config": {"workload": WORKLOADS[cfg], "layout": layout, "strings_per_gpu": n, "input_bytes_per_gpu": in_bytes,
+            "config": {"workload": WORKLOADS[cfg], "layout": layout,
+                       "claim": ("reserved ranges at %g x the input offsets" % (reserve / 16)) if reserve else
+                                ("one atomic per tile" if views else "look-back"), "strings_per_gpu": n, "input_bytes_per_gpu": in_bytes,
                        "output_bytes_per_gpu": out_bytes, "inserts": W.inserts, "parallelism": "shard%d" % world,
                        "units_total": total_units, "input_bytes_total": all_bytes,
                        "statuses": status_counts, "table_build_s": round(W.build_s, 3)},

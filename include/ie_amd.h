@@ -32,7 +32,9 @@
 extern "C" {
 #endif
 
-#define IE_ABI_VERSION 1
+/* 2: ie_timing gained n_deferred; ie_unescape_cmd_device may report IE_RECURSE; IE_OPT_LEAN (6) was
+ *    removed and IE_OPT_RESERVE (8) added. */
+#define IE_ABI_VERSION 2
 
 /* ---- dialects: which reference implementation's rules to follow ---- */
 enum ie_dialect {
@@ -151,7 +153,7 @@ typedef struct ie_timing {
   uint64_t n_polls;      /* look-back poll rounds that found a predecessor not yet published */
   uint64_t n_exact;      /* strings the level evaluator handed to the exact event evaluator */
   uint64_t n_chain_fail; /* strings whose chain evaluation met a miss or an unspliceable hit */
-  uint64_t n_deferred;   /* views batches: strings k_lean left to k_resolve (the fused unescape
+  uint64_t n_deferred;   /* views batches: strings left to a second pass (the fused unescape
                             command: strings left to its deferred pass) */
 } ie_timing;
 
@@ -208,9 +210,14 @@ int ie_exec_timing(ie_exec* x, ie_timing* out); /* syncs */
                           tiles of their own (the exact evaluator and the literal path then run on
                           full tiles of such strings); -1 adaptive (above 0.4 % of a batch); 0
                           (default): in their tiles (config 5 measured 2.5x slower deferred) */
-#define IE_OPT_LEAN 6  /* 1: a views batch runs k_lean (one wave per 64 strings, the common string shape,
-                          output claimed in striped shards: *total is then the extent used, gaps
-                          included) and then k_resolve on the strings it left; 0 (default): k_resolve */
+#define IE_OPT_RESERVE 8 /* views output of a packed batch: 0 (default): each tile claims its range on one
+                          cursor (the bytes packed without gaps, *total = sum of lengths); F in 16..1024:
+                          tile t writes at F/16 x its input span's offset from the batch's first byte
+                          when its output fits the span x F/16 (no atomic), else in an overflow region
+                          after the whole reservation (a claim on the cursor): gaps between tiles,
+                          *total = sum of lengths still; a tile that did not fit bytes_cap makes
+                          ie_exec_sync report IE_ERR_CAPACITY. Size bytes_cap >= F/16 x the input bytes
+                          plus the overflow's share. */
 int ie_exec_set_option(ie_exec* x, int32_t option, int64_t value);
 /* Literal-path scratch pool size. Setting it makes ie_interpolate_device fully asynchronous: it no
  * longer waits to check the pool's demand, and strings that ran out of it report IE_E_OVERFLOW. */

@@ -107,9 +107,8 @@ struct ie_exec {
                                   // measured slower on config 5) / 1 (IE_DEFER)
   bool defer_slow = false;        // the adaptive choice (from an earlier batch's counts)
   int32_t opt_small = 1;          // host batches of <= 1024 strings / 64 KB: one pinned copy each way (IE_SMALL_HOST)
-  int32_t opt_lean = 0;           // views batches: k_lean first, k_resolve on what it lists (IE_LEAN; measured
-                                  // slower than k_resolve alone: DESIGN.md, k_lean)
-  int32_t lean_grid = 0;          // resident k_lean workgroups on the device (0: not known yet)
+  uint32_t opt_reserve = 0;       // views output of a packed batch: reserved ranges at opt_reserve / 16 x the
+                                  // input offsets (IE_OPT_RESERVE; 0: one claim per tile on one cursor)
   bool in_cmd = false;            // inside the unescape command's second resolve
   bool cmd_first = false;         // the unescape command's unescape step (offsets zeroed on overflow)
   bool cmd_fused = false;         // the fused unescape command (views): launch_unescape_cmd
@@ -278,8 +277,8 @@ int set_device(int32_t dev) {
 // [2..3] pool bytes used (u64), [4..8] telemetry (literal strings, deferred tiles, look-back polls,
 // exact-path strings, chain failures), [9] deferred-tile count, [10..11] views output cursor (u64),
 // [12] the fused unescape command's deferred-string count; zeroed on every call.
-constexpr uint32_t kLeanShards = 16;  // k_lean's cursor shards, 128 B apart after the counters
-constexpr uint64_t kCounterBytes = 64 + kLeanShards * 128;
+constexpr uint32_t kSumShards = 16;  // reserved-range tile sums (IE_OPT_RESERVE), 128 B apart after the counters
+constexpr uint64_t kCounterBytes = 64 + kSumShards * 128;
 int ensure_work(ie_exec* x, int op, uint64_t n) {
   // (k_resolve tiles of 128 strings or more: enough look-back words and deferred-tile slots)
   const uint64_t tiles = (n + 127) / 128 + 1;
@@ -314,10 +313,10 @@ Work make_work(ie_exec* x, uint64_t* total) {
   W.defer_desc = (uint4*)x->defer_desc.p;
   W.tile_state = (uint64_t*)((uint8_t*)x->counters.p + kCounterBytes);
   W.shards = (uint64_t*)((uint8_t*)x->counters.p + 64);
-  W.n_shards = kLeanShards;
-  W.stripe_log2 = 18;
+  W.n_shards = kSumShards;
   W.cursor = (uint64_t*)x->counters.p + 5;  // words 10-11
   W.udefer_count = (uint32_t*)x->counters.p + 12;
+  W.res_ovf = (uint64_t*)x->counters.p + 7;  // words 14-15
   W.zero_on_overflow = x->cmd_first ? 1u : 0u;
   W.pool = (uint8_t*)x->pool.p;
   W.pool_bytes = x->pool.bytes;
@@ -329,9 +328,11 @@ Work make_work(ie_exec* x, uint64_t* total) {
 }
 
 // d_out_len / d_in_len (k_resolve only): views output / views input (ie_interpolate_device_views)
+// reserve_ok: the caller is ie_interpolate_device_views (the only entry whose caller sized the output
+// for IE_OPT_RESERVE; the host batch APIs read back *total bytes and keep one claim per tile)
 int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, const uint64_t* d_off,
                uint64_t n, const ie_dev_out* out, const uint32_t* d_tid = nullptr, uint32_t* d_out_len = nullptr,
-               const uint32_t* d_in_len = nullptr) {
+               const uint32_t* d_in_len = nullptr, bool reserve_ok = false) {
   if (!x || !d_off || !out || !out->offsets || !out->status || !out->total || (op == kOpInterp && !t))
     return fail(IE_ERR_INVALID, "null argument");
   if (n && !d_bytes) return fail(IE_ERR_INVALID, "null input bytes");
@@ -354,6 +355,8 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
   Batch B{d_bytes, d_off, n, out->offsets, out->status, out->value_id, d_tid, d_in_len, d_out_len};
   Work W = make_work(x, out->total);
   W.recurse = op == kOpInterp && x->in_cmd && t->dialect == IE_DIALECT_PY ? 1u : 0u;
+  // reserved output ranges: a views output of a packed interpolation batch (not the unescape command)
+  W.reserve16 = reserve_ok && op == kOpInterp && d_out_len && !d_in_len && !x->in_cmd && !x->cmd_fused ? x->opt_reserve : 0u;
   hipStream_t st = x->stream;
   const uint64_t cap = out->bytes ? out->bytes_cap : 0;
   if (x->timing) IE_HIP(hipEventRecord(x->ev[0], st));
@@ -392,35 +395,9 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
       W.udefer_list = (uint32_t*)x->u_list.p;
       IE_HIP(launch_unescape_cmd(B, W, t->dev, out->bytes, cap, (uint64_t*)x->u_off.p, (uint32_t*)x->u_len.p,
                                  d_tid ? (uint32_t*)x->u_tid.p : nullptr, st));
-    } else if (d_out_len && x->opt_lean && !x->in_cmd && !x->opt_noeval) {
-      // a views batch: k_lean, then k_resolve on the strings it listed. Stripes of 2^18 bytes (at
-      // most 16 x 256 KB of the output left unused at the shards' ends), fewer for small batches
-      // (sized from the string count, ~64 B a string: no wait for the input's byte count)
-      uint32_t slog = 14;
-      while (slog < 18 && (1ull << slog) * kLeanShards < n * 64) slog++;
-      W.stripe_log2 = slog;
-      if (!x->lean_grid) {
-        int ncu = 0;
-        IE_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, x->device));
-        const int nb = lean_blocks_per_cu(0);  // (both variants: the same registers and LDS)
-        x->lean_grid = (nb > 0 ? nb : 8) * (ncu > 0 ? ncu : 256);
-      }
-      IE_HIP(x->u_list.ensure(n * 4 + 4));
-      IE_HIP(x->u_off.ensure(n * 8 + 8));
-      IE_HIP(x->u_len.ensure(n * 4 + 4));
-      if (d_tid) IE_HIP(x->u_tid.ensure(n * 4 + 4));
-      W.udefer_list = (uint32_t*)x->u_list.p;
-      const hipError_t le = launch_lean(B, W, t->dev, out->bytes, cap, (uint64_t*)x->u_off.p, (uint32_t*)x->u_len.p,
-                                        d_tid ? (uint32_t*)x->u_tid.p : nullptr, (uint32_t)x->lean_grid, st);
-      if (le != hipSuccess) {
-        char msg[160];
-        snprintf(msg, sizeof msg, "launch_lean (step %d, grid %d): %s", lean_failed_stage(), x->lean_grid,
-                 hipGetErrorString(le));
-        return fail(IE_ERR_HIP, msg);
-      }
     } else if (d_out_len && !x->in_cmd && !x->opt_noeval &&
                (x->opt_defer == 1 || (x->opt_defer < 0 && x->defer_slow))) {
-      // a views batch with heavy strings: two passes (ie_lean.hip launch_resolve_deferring)
+      // a views batch with heavy strings: two passes (launch_resolve_deferring)
       IE_HIP(x->u_list.ensure(n * 4 + 4));
       IE_HIP(x->u_off.ensure(n * 8 + 8));
       IE_HIP(x->u_len.ensure(n * 4 + 4));
@@ -626,7 +603,7 @@ int run_host(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, const 
     b->offsets[n] = w;
     delete[] b->bytes;
     b->bytes = packed;
-    b->bytes_len = w;  // (a views total is the extent the device used: k_lean's stripes leave gaps)
+    b->bytes_len = w;
     if (w > total) {
       ie_batch_free(b);
       return fail(IE_ERR_HIP, "views output lengths exceed its total");
@@ -1068,7 +1045,10 @@ int ie_exec_create(int32_t device, void* hip_stream, ie_exec** out) {
   if (const char* e = getenv("IE_DEBUG_NOEVAL")) x->opt_noeval = (uint32_t)atoi(e);
   if (const char* e = getenv("IE_TILE")) x->opt_tile = atoi(e) == 512 ? 512 : atoi(e) == 256 ? 256 : 0;
   if (const char* e = getenv("IE_VIEWS")) x->opt_views = atoi(e) != 0;
-  if (const char* e = getenv("IE_LEAN")) x->opt_lean = atoi(e) != 0;
+  if (const char* e = getenv("IE_RESERVE")) {
+    const int v = atoi(e);
+    x->opt_reserve = v >= 16 && v <= 1024 ? (uint32_t)v : 0u;
+  }
   if (const char* e = getenv("IE_SMALL_HOST")) x->opt_small = atoi(e) != 0;
   if (const char* e = getenv("IE_DEFER")) x->opt_defer = atoi(e) < 0 ? -1 : atoi(e) != 0 ? 1 : 0;
   if (const char* e = getenv("IE_DEBUG_STAMPS")) x->stamps_path = e;
@@ -1199,8 +1179,9 @@ int ie_exec_set_option(ie_exec* x, int32_t option, int64_t value) {
     case IE_OPT_VIEWS:
       x->opt_views = value ? 1 : 0;
       return IE_SUCCESS;
-    case IE_OPT_LEAN:
-      x->opt_lean = value ? 1 : 0;
+    case IE_OPT_RESERVE:
+      if (value != 0 && (value < 16 || value > 1024)) return fail(IE_ERR_INVALID, "reserve must be 0 or 16..1024");
+      x->opt_reserve = (uint32_t)value;
       return IE_SUCCESS;
     case IE_OPT_DEFER:
       if (value < -1 || value > 1) return fail(IE_ERR_INVALID, "defer must be -1, 0 or 1");
@@ -1295,7 +1276,7 @@ int ie_interpolate_device_views(ie_exec* x, const ie_table* t, const uint32_t* d
                                 const ie_dev_views* out) {
   if (!out || (n && (!out->offsets || !out->lengths))) return fail(IE_ERR_INVALID, "null argument");
   const ie_dev_out o{out->bytes, out->bytes_cap, out->offsets, out->status, out->value_id, out->total};
-  int rc = run_device(x, kOpInterp, t, d_bytes, d_offsets, n, &o, d_table_id, out->lengths, d_lengths);
+  int rc = run_device(x, kOpInterp, t, d_bytes, d_offsets, n, &o, d_table_id, out->lengths, d_lengths, true);
   if (rc || !n || x->pool_fixed) return rc;
   // the literal path's scratch demand, as ie_interpolate_device_ids
   uint64_t used = 0;
@@ -1303,7 +1284,7 @@ int ie_interpolate_device_views(ie_exec* x, const ie_table* t, const uint32_t* d
   IE_HIP(hipStreamSynchronize(x->stream));
   if (used <= x->pool.bytes) return IE_SUCCESS;
   x->pool_request = std::max<uint64_t>(x->pool_request, used + used / 8 + (1ull << 20));
-  return run_device(x, kOpInterp, t, d_bytes, d_offsets, n, &o, d_table_id, out->lengths, d_lengths);
+  return run_device(x, kOpInterp, t, d_bytes, d_offsets, n, &o, d_table_id, out->lengths, d_lengths, true);
 }
 
 int ie_interpolate_batch_ids(ie_exec* x, const ie_table* t, const uint32_t* table_id, const uint8_t* bytes,

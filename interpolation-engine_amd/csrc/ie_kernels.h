@@ -72,13 +72,16 @@ struct Work {
   // staged, or needing the literal path) are listed here for the deferred pass
   uint32_t* udefer_list;  // n
   uint32_t* udefer_count; // 1
-  // k_lean (views output): R cursor shards (u64 words 16 apart; shard r owns the output stripes
-  // r, r + R, ... of 2^stripe_log2 bytes), zeroed per call
-  uint64_t* shards;
-  uint32_t n_shards;     // a power of two
-  uint32_t stripe_log2;
+  uint64_t* shards;      // 16 u64 words 16 apart (reserved ranges' tile sums), zeroed per call
+  uint32_t n_shards;
   uint32_t defer_slow;   // k_resolve on a views batch: strings the chain jobs cannot finish are listed
                          // in udefer_list for a second pass instead of evaluated in their tile
+  // views output of a packed batch, reserved ranges (IE_OPT_RESERVE): a tile's output goes to
+  // reserve16 / 16 times its input span's offset from the batch's first byte when it fits there (no
+  // atomic), else to the overflow region after the whole batch's reservation (W.cursor); the tile
+  // sums go to the 16 `shards` words (u64, 128 B apart) and k_emit_windows adds them into *total
+  uint32_t reserve16;
+  uint64_t* res_ovf;     // 1   the overflow region's start (written by the reserved pass)
   uint32_t recurse;      // k_resolve in the unescape command (py dialect): whole-string items whose
                          // result recursive_interpolate walks again report IE_RECURSE
   uint32_t zero_on_overflow; // escape kernels: when the output exceeds its capacity, write every
@@ -115,16 +118,10 @@ hipError_t launch_cap_check(const uint64_t* total, uint64_t cap, uint32_t* err, 
 // staging), then the deferred strings: unescaped into the pool (k_unesc_deferred), resolved again
 hipError_t launch_unescape_cmd(const Batch& B, const Work& W, const DevTable& T, uint8_t* out, uint64_t cap,
                                uint64_t* sub_off, uint32_t* sub_len, uint32_t* sub_tid, hipStream_t st);
-// k_lean on a views batch (ie_lean.hip), then k_resolve on the strings it listed (their views in
-// sub_off / sub_len / sub_tid); grid_cap: resident 64-lane workgroups of the device
-hipError_t launch_lean(const Batch& B, const Work& W, const DevTable& T, uint8_t* out, uint64_t cap, uint64_t* sub_off,
-                       uint32_t* sub_len, uint32_t* sub_tid, uint32_t grid_cap, hipStream_t st);
-int lean_blocks_per_cu(int multi);
 // k_resolve on a views batch in two passes: the heavy strings listed by the first (W.defer_slow)
 // are resolved by the second as a subset (their views in sub_off / sub_len / sub_tid)
 hipError_t launch_resolve_deferring(const Batch& B, const Work& W, const DevTable& T, uint8_t* out, uint64_t cap,
                                     uint64_t* sub_off, uint32_t* sub_len, uint32_t* sub_tid, hipStream_t st);
-int lean_failed_stage();
 hipError_t launch_status_carry(const uint8_t* before, uint8_t* after, uint64_t n, hipStream_t st);
 hipError_t launch_debug_probe(const DevTable& T, const uint8_t* key, uint32_t klen, uint64_t* out,
                               hipStream_t st);

@@ -48,6 +48,11 @@
 #define IE_EARLY_TEXT 1
 #endif
 
+// chain jobs with wave-uniform skips (empty job slots, no template after the child, short keys)
+#ifndef IE_JOBS_V2
+#define IE_JOBS_V2 0
+#endif
+
 namespace ie {
 // everything of one tile size lives in its own namespace: ie_resolve512.hip compiles this file
 // again with 512-string tiles (IE_RBLOCK=512, IE_RNS=r512, IE_RESOLVE_WIDE)
@@ -477,8 +482,16 @@ __device__ void resolve_jobs(const DevTable& T, const lds_u8* tile, const ChainJ
       close[q] = on[q] ? c : 0u;
       la[q] = on[q] ? (r == 0 ? close[q] : co_[q]) - open[q] - 1 : 0u;
       lb[q] = on[q] && r != 0 ? close[q] - cl_[q] - 1 : 0u;
+#if IE_JOBS_V2
+      // (uniform skips: a slot no lane of the wave uses, the template after the child when no lane
+      // has one, e.g. config 3's {q-{iM}})
+      ka[q] = kb[q] = u32x4{0, 0, 0, 0};
+      if (__any(on[q])) ka[q] = ld16a(s[q] + open[q] + 1);
+      if (r != 0 && __any(lb[q] != 0u)) kb[q] = ld16a(s[q] + cl_[q] + 1);
+#else
       ka[q] = ld16a(s[q] + open[q] + 1);
       kb[q] = r != 0 ? ld16a(s[q] + cl_[q] + 1) : u32x4{0, 0, 0, 0};
+#endif
     }
 #pragma unroll
     for (int q = 0; q < NJ; q++) {
@@ -491,6 +504,30 @@ __device__ void resolve_jobs(const DevTable& T, const lds_u8* tile, const ChainJ
         on[q] = false;
         done[q] = true;
       }
+#if IE_JOBS_V2
+      h[q] = 0;
+      kw[q] = u32x4{0, 0, 0, 0};
+      if (!__any(on[q])) continue;
+      // the parts are exact (template bytes masked, the child's text zero past its length, shifts
+      // drop what passes 16 bytes): no final mask
+      u32x4 k = keep_bytes(ka[q], la[q]);
+      if (r != 0) {
+        const u32x4 t = shl_bytes(u32x4{ct[q][0], ct[q][1], ct[q][2], ct[q][3]}, la[q]);
+        k = u32x4{k.x | t.x, k.y | t.y, k.z | t.z, k.w | t.w};
+        if (__any(lb[q] != 0u)) {
+          const u32x4 b = shl_bytes(keep_bytes(kb[q], lb[q]), la[q] + ctl[q]);
+          k = u32x4{k.x | b.x, k.y | b.y, k.z | b.z, k.w | b.w};
+        }
+      }
+      kw[q] = k;
+      uint64_t hh = hash_init(klen[q], T.seed, tb[q]);
+      if (klen[q] > 0u) hh = hash_word(hh, kw[q].x);
+      if (klen[q] > 4u) hh = hash_word(hh, kw[q].y);
+      if (__any(klen[q] > 8u)) {
+        if (klen[q] > 8u) hh = hash_word(hh, kw[q].z);
+        if (klen[q] > 12u) hh = hash_word(hh, kw[q].w);
+      }
+#else
       u32x4 k = keep_bytes(ka[q], la[q]);
       if (r != 0) {
         const u32x4 t = shl_bytes(u32x4{ct[q][0], ct[q][1], ct[q][2], ct[q][3]}, la[q]);
@@ -503,6 +540,7 @@ __device__ void resolve_jobs(const DevTable& T, const lds_u8* tile, const ChainJ
       if (klen[q] > 4u) hh = hash_word(hh, kw[q].y);
       if (klen[q] > 8u) hh = hash_word(hh, kw[q].z);
       if (klen[q] > 12u) hh = hash_word(hh, kw[q].w);
+#endif
       if (LK && klen[q] > 16u) hh = hash_word(hh, kw2[q].x);
       if (LK && klen[q] > 20u) hh = hash_word(hh, kw2[q].y);
       if (LK && klen[q] > 24u) hh = hash_word(hh, kw2[q].z);
@@ -1049,7 +1087,12 @@ __global__ __launch_bounds__(kRBlock) void k_emit_windows(Batch B0, Work W, DevT
   const uint32_t count = __hip_atomic_load(W.defer_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t tid = threadIdx.x;
   // views output: the bytes every tile claimed are the batch's total (k_resolve has finished)
-  if (B.out_len && blockIdx.x == 0 && tid == 0) *W.total = *W.cursor;
+  if (B.out_len && blockIdx.x == 0 && tid == 0) {
+    uint64_t t = 0;  // reserved ranges: the tiles' sums (the cursor counts the overflow region only)
+    if (W.reserve16)
+      for (uint32_t k = 0; k < 16; k++) t += W.shards[16u * k];
+    *W.total = W.reserve16 ? t : *W.cursor;
+  }
   // fewer deferred tiles than workgroups: each tile's windows are shared by `per` workgroups (a
   // tile of multi-KB outputs is hundreds of windows: one workgroup alone would take them in turn)
   const uint32_t per = count && count < gridDim.x ? gridDim.x / count : 1u;
@@ -1416,10 +1459,31 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
   const uint64_t local = block_scan(olen, s_red, &tile_total);  // (its barriers also retire s_lit)
   uint64_t lb_early = 0;
   if (VIEWS) {
-    // the tile's output range: one atomic, its answer consumed after the build
-    if (tid == 0)
-      lb_early = (W.debug_noeval & 2u) ? 2 * lo  // diagnostic: no claim (a range from the input's)
-                                       : atomicAdd((unsigned long long*)W.cursor, (unsigned long long)tile_total);
+    // the tile's output range: one atomic, its answer consumed after the build; or (reserved
+    // ranges) the tile's own part of the output, no atomic unless it overflows its reservation
+    if (tid == 0) {
+      if (W.debug_noeval & 2u) {
+        lb_early = 2 * lo;  // diagnostic: no claim (a range from the input's)
+      } else if (W.reserve16) {
+        // the reserved pass (packed input) computes the overflow region's start itself (two words
+        // every tile reads: L2-resident) and tile 0 leaves it for later subset passes
+        uint64_t rb = 0, ovf;
+        bool own = false;
+        if (!B.in_len && !B.out_index) {
+          const uint64_t res_base = gld(B.in_off);
+          ovf = ((((gld(B.in_off + B.n) - res_base) * W.reserve16) >> 4) + 15) & ~15ull;
+          rb = ((lo - res_base) * W.reserve16) >> 4;
+          own = tile_total <= (((geo.hi - res_base) * W.reserve16) >> 4) - rb;
+          if (tile == 0) __hip_atomic_store(W.res_ovf, ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          ovf = __hip_atomic_load(W.res_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        lb_early = own ? rb : ovf + atomicAdd((unsigned long long*)W.cursor, (unsigned long long)tile_total);
+        __hip_atomic_fetch_add(W.shards + 16u * (tile & 15u), tile_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        lb_early = atomicAdd((unsigned long long*)W.cursor, (unsigned long long)tile_total);
+      }
+    }
   } else if (wave == 0) {
     publish_aggregate(W.tile_state, tile, tile_total);
     if (tile != 0) lb_early = lb_poll(W.tile_state, (int64_t)tile - 1);  // consumed after the build
@@ -1505,6 +1569,8 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
     *W.total = base + tile_total;
   }
   const bool write_bytes = base + tile_total <= cap;  // caller's buffer too small: offsets only
+  // (reserved ranges: *total is the sum of lengths, not the extent, so the flag tells the caller)
+  if (VIEWS && W.reserve16 && !write_bytes && tid == 0) atomicOr(W.err, 2u);
 
   // ---- 6. stream out: 16-byte stores at 16-byte aligned addresses, each assembled from the
   //      two stage blocks it straddles (the shift is uniform over the tile) ----
@@ -1676,6 +1742,44 @@ hipError_t launch_unescape_cmd(const Batch& B, const Work& W, const DevTable& T,
                      W, sub_off, sub_len, sub_tid);
   Batch D{W.pool, sub_off, B.n, B.out_off, B.status, B.value_id, sub_tid, sub_len, B.out_len, W.udefer_list, W.udefer_count};
   return IE_RNS::launch_resolve_impl(D, W, T, out, cap, st, false);
+}
+#endif
+
+#if !defined(IE_RESOLVE_WIDE)
+// the listed strings (W.udefer_list) as a views subset of the batch (their bytes where they are)
+__global__ void k_gather_listed(Batch B, Work W, uint64_t* sub_off, uint32_t* sub_len, uint32_t* sub_tid) {
+  const uint32_t count = __hip_atomic_load(W.udefer_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < count; j += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t idx = W.udefer_list[j];
+    const uint64_t so = gld(B.in_off + idx);
+    sub_off[j] = so;
+    sub_len[j] = B.in_len ? gld(B.in_len + idx) : (uint32_t)min(gld(B.in_off + idx + 1) - so, (uint64_t)0xFFFFFFFFu);
+    if (sub_tid) sub_tid[j] = B.table_id ? gld(B.table_id + idx) : 0u;
+  }
+}
+
+// k_resolve on a views batch in two passes (IE_OPT_DEFER): the strings the chain jobs could not
+// finish are listed by the first (W.defer_slow) and resolved by the second as a subset
+hipError_t launch_resolve_deferring(const Batch& B, const Work& W, const DevTable& T, uint8_t* out, uint64_t cap,
+                                    uint64_t* sub_off, uint32_t* sub_len, uint32_t* sub_tid, hipStream_t st) {
+  if (!B.out_len || !B.n) return hipErrorInvalidValue;
+  Work W1 = W;
+  W1.defer_slow = 1;
+  hipError_t e = IE_RNS::launch_resolve_impl(B, W1, T, out, cap, st);
+  if (e != hipSuccess) return e;
+  // the windowed-tile list is the second pass's again
+  e = hipMemsetAsync(W.defer_count, 0, sizeof(uint32_t), st);
+  if (e != hipSuccess) return e;
+  const bool multi = B.table_id != nullptr;
+  const uint32_t gb = (uint32_t)((B.n + 255) / 256 < 1024 ? (B.n + 255) / 256 : 1024);
+  hipLaunchKernelGGL(k_gather_listed, dim3(gb), dim3(256), 0, st, B, W, sub_off, sub_len, multi ? sub_tid : nullptr);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  Work W2 = W;
+  W2.defer_slow = 0;
+  const Batch D{B.bytes, sub_off, B.n, B.out_off, B.status, B.value_id, multi ? sub_tid : nullptr, sub_len, B.out_len,
+                W.udefer_list, W.udefer_count};
+  return IE_RNS::launch_resolve_impl(D, W2, T, out, cap, st);
 }
 #endif
 

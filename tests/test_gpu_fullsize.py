@@ -91,7 +91,9 @@ class Out:
     def read(self):
         st = self.status.to_numpy(np.uint8, self.n)
         starts, lens = self.spans()
-        blob = self.bytes.to_numpy(np.uint8, self.total())
+        # (views: the extent the results reach; reserved ranges leave gaps, *total = sum of lengths)
+        ext = int((starts + lens).max()) if self.views and self.n else self.total()
+        blob = self.bytes.to_numpy(np.uint8, max(ext, self.total()))
         return st, starts, lens, blob
 
 
@@ -115,8 +117,9 @@ def assert_matches_oracle(o, ref_st, ref_len, ref_hash):
     ok = st == 0
     bad = np.flatnonzero(ok & (lens != ref_len))
     assert bad.size == 0, ("length", bad.size, bad[:8])
-    if o.views:  # a views payload: disjoint results inside the extent used (k_lean leaves gaps)
-        assert_views_disjoint(starts, lens, o.total())
+    if o.views:  # a views payload: disjoint results (reserved ranges leave gaps), *total = sum of lengths
+        assert int(lens.sum()) == o.total()
+        assert_views_disjoint(starts, lens, blob.size)
     else:
         assert int(lens.sum()) == o.total()  # nothing but the results in the payload
     hs = O.hash_spans(blob, starts, lens, st, THREADS)
@@ -135,29 +138,32 @@ def assert_views_disjoint(starts, lens, total):
     assert np.all(s[o][1:] >= (s[o] + l[o])[:-1])
 
 
-def assert_views_packing(starts, lens, total, n, tile=256):
-    """A views output's 256-string tiles: each tile's strings lie together in input order, except
-    the rare string k_lean moved off a stripe boundary; the gaps (stripe ends) stay small."""
+def assert_views_packing(starts, lens, n, tile=256, gaps=False):
+    """A views output's 256-string tiles: each tile's strings lie together in input order; without
+    reserved ranges the tiles lie together too (no gaps: the extent is the sum of lengths)."""
     starts, lens = starts.astype(np.int64), lens.astype(np.int64)
-    assert total - int(lens.sum()) <= max(int(lens.sum()) // 50, 8 << 20)
+    if not gaps:
+        assert int((starts + lens).max()) == int(lens.sum())
     idx = np.arange(n)
     same_tile = (idx[1:] // tile) == (idx[:-1] // tile)
     follows = starts[1:] == starts[:-1] + lens[:-1]
-    assert np.count_nonzero(~follows[same_tile]) <= 2 * (total >> 14) + 16
+    assert np.count_nonzero(~follows[same_tile]) == 0
 
 
-@pytest.mark.parametrize("layout", ["packed", "views", "views-lean"])
+@pytest.mark.parametrize("layout", ["packed", "views", "views-reserve"])
 @pytest.mark.parametrize("config,n", [(2, 1_000_000), (3, 10_000_000)], ids=["cfg2-1M", "cfg3-10M"])
-def test_full_batch_vs_oracle(config, n, layout, monkeypatch):
-    """Every string of the BASELINE-size batch against the oracle (status, length, bytes); views-lean:
-    k_lean first (IE_LEAN), k_resolve on what it leaves."""
-    monkeypatch.setenv("IE_LEAN", "1" if layout == "views-lean" else "0")
+def test_full_batch_vs_oracle(config, n, layout):
+    """Every string of the BASELINE-size batch against the oracle (status, length, bytes); views-reserve:
+    reserved output ranges at 2x the input offsets (IE_OPT_RESERVE 32, the bench's claim)."""
     h, kvp, nkv = _synth(config)
     table = _table(kvp, nkv)
     x = N.Exec(0)
+    reserve = layout == "views-reserve"
+    if reserve:
+        x.set_option(N.OPT_RESERVE, 32)
     d_off, d_bytes, in_total = _device_strings(x, h, 0, n)
     views = layout.startswith("views")
-    o = interpolate(x, table, d_bytes, d_off, n, 2 * in_total + (1 << 20), views)
+    o = interpolate(x, table, d_bytes, d_off, n, (3 if reserve else 2) * in_total + (1 << 20), views)
     buf = d_bytes.to_numpy(np.uint8, in_total + 1)
     offs = d_off.to_numpy(np.uint64, n + 1)
     ref = O.Oracle.from_kv(ctypes.cast(kvp, ctypes.c_void_p), nkv, "py", clock=CLOCK)
@@ -166,7 +172,7 @@ def test_full_batch_vs_oracle(config, n, layout, monkeypatch):
     st, starts, lens = assert_matches_oracle(o, rst, rlen, rhash)
     assert int(np.count_nonzero(st)) == 0  # the synthetic configs resolve every string
     if views:
-        assert_views_packing(starts, lens, o.total(), n)
+        assert_views_packing(starts, lens, n, gaps=reserve)
     N.lib().ie_table_free(table)
     N.lib().ie_synth_free(h)
 

@@ -30,10 +30,10 @@ def run_product(table_dict, strings, dialect="py", has_dir=False):
     return t.run(strings), t
 
 
-@pytest.fixture(params=["0", "1", "1w", "0v", "1v", "0lv", "0dv", "1dv"],
+@pytest.fixture(params=["0", "1", "1w", "0v", "1v", "0rv", "1rv", "0dv", "1dv"],
                 ids=["chain-fail-exact", "chain-fail-commit", "chain-fail-commit-512", "chain-fail-exact-views",
-                     "chain-fail-commit-views", "chain-fail-exact-views-lean", "chain-fail-exact-views-defer",
-                     "chain-fail-commit-views-defer"])
+                     "chain-fail-commit-views", "chain-fail-exact-views-reserve", "chain-fail-commit-views-reserve",
+                     "chain-fail-exact-views-defer", "chain-fail-commit-views-defer"])
 def fail_commit(request, monkeypatch):
     """Both k_resolve variants: chain failures sent to the exact evaluator, or committed in the
     chain evaluator (the library picks one adaptively; IE_FAIL_COMMIT / IE_OPT_FAIL_COMMIT force it);
@@ -43,9 +43,11 @@ def fail_commit(request, monkeypatch):
     cached exec is set directly. Yields the fail-commit digit; VIEWS[0] tells _device_run."""
     fc, tile = request.param[0], 512 if request.param.endswith("w") else 0
     views = 1 if request.param.endswith("v") else 0
-    lean = 1 if "l" in request.param else 0  # k_lean first (ie_lean.hip), k_resolve on what it leaves
+    # reserved output ranges (IE_OPT_RESERVE: tiles write at 2x their input offsets, no claim atomic;
+    # ie_interpolate_device_views only)
+    reserve = 32 if "r" in request.param else 0
     defer = 1 if "d" in request.param else 0  # heavy strings to a second pass (IE_OPT_DEFER)
-    monkeypatch.setenv("IE_LEAN", str(lean))
+    monkeypatch.setenv("IE_RESERVE", str(reserve))
     monkeypatch.setenv("IE_DEFER", str(defer))
     monkeypatch.setenv("IE_FAIL_COMMIT", fc)
     monkeypatch.setenv("IE_TILE", str(tile))
@@ -54,12 +56,12 @@ def fail_commit(request, monkeypatch):
     x.set_option(N.OPT_FAIL_COMMIT, int(fc))
     x.set_option(N.OPT_TILE, tile)
     x.set_option(N.OPT_VIEWS, views)
-    x.set_option(N.OPT_LEAN, lean)
+    x.set_option(N.OPT_RESERVE, reserve)
     x.set_option(N.OPT_DEFER, defer)
     VIEWS[0] = bool(views)
     yield fc
     VIEWS[0] = False
-    x.set_option(N.OPT_LEAN, 0)
+    x.set_option(N.OPT_RESERVE, 0)
     x.set_option(N.OPT_DEFER, -1)
     x.set_option(N.OPT_FAIL_COMMIT, -1)
     x.set_option(N.OPT_TILE, 0)
@@ -405,7 +407,7 @@ def assert_views_disjoint(starts, lens, total):
 def _device_run(x, table, d_bytes, d_off, n, cap=None):
     """A packed result; with the views fixture the device writes views, packed here on the host in
     input order (the check then runs on the same packed form)."""
-    r = DevResult(x, n, cap if cap is not None else int(d_bytes.nbytes * 2 + 4096))
+    r = DevResult(x, n, cap if cap is not None else int(d_bytes.nbytes * 3 + 4096))
     if not VIEWS[0]:
         N.check(N.lib().ie_interpolate_device(x.h, table, d_bytes.ptr, d_off.ptr, n, ctypes.byref(r.out)),
                 "ie_interpolate_device")
@@ -419,8 +421,10 @@ def _device_run(x, table, d_bytes, d_off, n, cap=None):
     tot = r.total()
     starts = r.off.to_numpy(np.uint64, n)
     ln = lens.to_numpy(np.uint32, n).astype(np.uint64)
-    blob = r.bytes.to_numpy(np.uint8, tot)
-    assert_views_disjoint(starts, ln, tot)
+    assert int(ln.sum()) == tot  # *total = sum of lengths (reserved ranges: gaps between tiles)
+    ext = int((starts + ln).max()) if n else 0
+    blob = r.bytes.to_numpy(np.uint8, max(ext, tot))
+    assert_views_disjoint(starts, ln, blob.size)
     packed = np.concatenate([blob[int(starts[i]):int(starts[i] + ln[i])] for i in range(n)]) if n else blob
     offs = np.zeros(n + 1, np.uint64)
     offs[1:] = np.cumsum(ln)
