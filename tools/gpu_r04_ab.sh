@@ -12,7 +12,7 @@ if [ -x tools/exp/lds_ubench ] && [ -z "${NO_UBENCH:-}" ]; then
   timeout -k 10 120 tools/exp/lds_ubench > $O/ubench.txt 2>&1 || exit $?
 fi
 if [ -n "${PYTEST_K:-}" ]; then
-  timeout -k 10 900 python -u -m pytest ${PYTEST_FILES:-tests/test_gpu_parity.py tests/test_gpu_fullsize.py} -m gpu -x -q -k "$PYTEST_K" --timeout 600 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+  IE_LIB_PATH=${PYTEST_LIB:-} timeout -k 10 900 python -u -m pytest ${PYTEST_FILES:-tests/test_gpu_parity.py tests/test_gpu_fullsize.py} -m gpu -x -q -k "$PYTEST_K" --timeout 600 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 fi
 PMC="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY"
 for v in ${VARIANTS:-main}; do
