@@ -184,6 +184,15 @@ int ie_shard_bounds(const uint64_t* offsets, uint64_t n, uint32_t n_shards, uint
  * place (values that read the clock, also through nested keys, are never pre-resolved at build,
  * so every lookup sees the new time). Waits for the device first: no batch may be in flight. */
 int ie_table_set_clock(ie_table* t, const ie_clock* now);
+/* set_interpdata on a built table or table set (py:470-471 `inserts[key] = value`, the replace_map /
+ * user_input / set stores of py:1566-1568, 1770-1773; rust-project/src/runtime.rs:700-701 snapshots
+ * the map per task): entry i sets kv[i] (kind < 0: deletes the key) in table table_id[i], value id
+ * vid[i], without a rebuild: a key the table has is rewritten in place, a new key re-places its
+ * pilot group. Synchronous (waits for the device first, like ie_table_set_clock). A brace-bearing
+ * value is not pre-resolved, and the pre-resolved values of every changed table return to their raw
+ * text (both then resolve through the exact evaluator, in the reference's order). IE_ERR_CAPACITY:
+ * some new key found no placement (those keys were not applied; rebuild the table). */
+int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, const uint32_t* vid, uint64_t n);
 uint64_t ie_table_entries(const ie_table* t);
 uint32_t ie_table_tables(const ie_table* t);
 int32_t ie_table_dialect(const ie_table* t);

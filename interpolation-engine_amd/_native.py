@@ -23,7 +23,7 @@ OPT_FAIL_COMMIT, OPT_FAST, OPT_DEBUG_NOEVAL, OPT_TILE, OPT_VIEWS, OPT_DEFER, OPT
 # every symbol include/ie_amd.h declares (tests check the .so exports exactly these)
 EXPORTS = [
     "ie_abi_version", "ie_build_id", "ie_last_error", "ie_device_count",
-    "ie_table_build", "ie_table_set_build", "ie_table_set_clock", "ie_table_free", "ie_table_entries", "ie_table_tables",
+    "ie_table_build", "ie_table_set_build", "ie_table_set_clock", "ie_table_set_update", "ie_table_free", "ie_table_entries", "ie_table_tables",
     "ie_table_dialect",
     "ie_exec_create", "ie_exec_destroy", "ie_exec_sync", "ie_exec_set_timing", "ie_exec_timing",
     "ie_exec_set_scratch", "ie_exec_set_option",
@@ -94,6 +94,7 @@ def signatures():
         "ie_table_set_build": (ctypes.c_int, [vp, vp, u32, i32, ctypes.POINTER(Clock), u32, i32, pvp]),
         "ie_table_free": (None, [vp]),
         "ie_table_set_clock": (ctypes.c_int, [vp, ctypes.POINTER(Clock)]),
+        "ie_table_set_update": (ctypes.c_int, [vp, vp, vp, vp, u64]),
         "ie_table_tables": (u32, [vp]),
         "ie_table_entries": (u64, [vp]),
         "ie_table_dialect": (i32, [vp]),
@@ -156,6 +157,9 @@ def lib():
         f.argtypes = args
     _lib = L
     return L
+
+
+ERR_CAPACITY = -6  # IE_ERR_CAPACITY
 
 
 def check(rc, what):

@@ -77,9 +77,18 @@ struct ie_table {
   uint64_t n_entries = 0;
   uint32_t n_tables = 1;  // inserts dicts in the set
   DevTable dev{};
-  // the clock entries ('HH:MM', 'HH:MM:SS' of every table): slot, host copy (ie_table_set_clock)
-  std::vector<std::pair<uint32_t, Entry>> clock_entries;
+  // the clock entries ('HH:MM', 'HH:MM:SS' of every table): their slots (ie_table_set_clock)
+  std::vector<uint32_t> clock_slots;
   DevBuf entries, pilots, arena;
+  // host mirror of the device table (ie_table_set_update, ie_table_set_clock): entries, pilots,
+  // the arena (device capacity arena_cap), the slots of each pilot group, and per table of the set
+  // the slots of its pre-resolved (EF_RAWALT) entries
+  std::vector<Entry> h_entries;
+  std::vector<uint16_t> h_pilots;
+  std::vector<uint8_t> h_arena;
+  uint64_t arena_cap = 0;
+  std::vector<std::vector<uint32_t>> groups;
+  std::unordered_map<uint32_t, std::vector<uint32_t>> rawalt;
   ~ie_table() {
     entries.release();
     pilots.release();
@@ -695,6 +704,77 @@ struct Ent {
   std::string_view raw;  // EF_RAWALT: the raw value behind a pre-resolved splice text
 };
 
+// Byte patches of a device buffer, applied by one upload and one kernel (k_patch): patch k writes
+// len[k] bytes of data (at soff[k]) to dst + doff[k]. Synchronous.
+struct Patches {
+  std::vector<uint8_t> data;
+  std::vector<uint64_t> doff;
+  std::vector<uint32_t> soff, len;
+  void add(uint64_t dst_off, const void* src, uint32_t n) {
+    doff.push_back(dst_off);
+    soff.push_back((uint32_t)data.size());
+    len.push_back(n);
+    data.insert(data.end(), (const uint8_t*)src, (const uint8_t*)src + n);
+    while (data.size() & 15) data.push_back(0);
+  }
+};
+
+int apply_patches(void* dst, const Patches& P) {
+  const uint64_t n = P.doff.size();
+  if (!n) return IE_SUCCESS;
+  if (P.data.size() >= (1ull << 32)) return fail(IE_ERR_INVALID, "patch set above 4 GiB");
+  const uint64_t o_doff = (P.data.size() + 15) & ~15ull, o_soff = o_doff + 8 * n, o_len = o_soff + 4 * n;
+  std::vector<uint8_t> blob(o_len + 4 * n);
+  memcpy(blob.data(), P.data.data(), P.data.size());
+  memcpy(blob.data() + o_doff, P.doff.data(), 8 * n);
+  memcpy(blob.data() + o_soff, P.soff.data(), 4 * n);
+  memcpy(blob.data() + o_len, P.len.data(), 4 * n);
+  DevBuf d;
+  IE_HIP(d.ensure(blob.size()));
+  hipError_t e = hipMemcpy(d.p, blob.data(), blob.size(), hipMemcpyHostToDevice);
+  const uint8_t* base = (const uint8_t*)d.p;
+  if (e == hipSuccess)
+    e = launch_patch((uint8_t*)dst, base, (const uint64_t*)(base + o_doff), (const uint32_t*)(base + o_soff),
+                     (const uint32_t*)(base + o_len), (uint32_t)n, nullptr);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  d.release();
+  if (e != hipSuccess) return fail(IE_ERR_HIP, std::string("table patch: ") + hipGetErrorString(e));
+  return IE_SUCCESS;
+}
+
+extern "C++" {
+// the key stored at a slot of the host mirror (inline up to kInlineKey bytes, else the arena copy)
+std::string_view mirror_key(const ie_table* t, const Entry& e) {
+  if (e.key_len <= kInlineKey) return std::string_view((const char*)e.key, e.key_len);
+  return std::string_view((const char*)t->h_arena.data() + key_off_of(e.text_off, e.text_len), e.key_len);
+}
+
+// [text][pad to 4][key] appended to the mirror's arena: the new text's offset (kernels read a long
+// key at key_off_of(text_off, text_len))
+uint32_t arena_append(ie_table* t, std::string_view text, std::string_view key) {
+  std::vector<uint8_t>& a = t->h_arena;
+  while (a.size() & 3) a.push_back(0);
+  const uint32_t off = (uint32_t)a.size();
+  a.insert(a.end(), text.begin(), text.end());
+  while (a.size() & 3) a.push_back(0);
+  a.insert(a.end(), key.begin(), key.end());
+  return off;
+}
+
+Entry make_entry(ie_table* t, std::string_view key, std::string_view text, uint32_t flags, uint32_t vid, uint32_t tb) {
+  Entry b{};
+  b.key_len = (uint32_t)key.size();
+  b.text_len = (uint32_t)text.size();
+  b.vid = vid;
+  b.flags = flags | EF_OCCUPIED | (tb << kTidShift);
+  b.text_off = arena_append(t, text, key);
+  memcpy(b.key, key.data(), std::min<size_t>(key.size(), kInlineKey));
+  memcpy(b.text, text.data(), std::min<size_t>(text.size(), kInlineText));
+  return b;
+}
+
+}  // extern "C++"
+
 // Entries -> perfect-hash table on the device.
 int upload_table(const std::vector<Ent>& ents, uint32_t n_tables, int32_t dialect, uint32_t flags,
                  int32_t device, ie_table** out) {
@@ -749,26 +829,32 @@ int upload_table(const std::vector<Ent>& ents, uint32_t n_tables, int32_t dialec
   }
   std::vector<Entry> entries(m);
   for (size_t i = 0; i < items.size(); i++) entries[slot_of[i]] = items[i];
-  std::vector<std::pair<uint32_t, Entry>> clock_entries;
-  for (size_t i = 0; i < items.size(); i++)
-    if (items[i].vid == IE_VID_CLOCK_HHMM || items[i].vid == IE_VID_CLOCK_HHMMSS)
-      clock_entries.emplace_back(slot_of[i], items[i]);
-  for (int pad = 0; pad < 16; pad++) arena.push_back(0);  // dword reads past the last text
   ie_table* t = new ie_table();
+  t->groups.assign(nb, {});
+  for (size_t i = 0; i < items.size(); i++) {
+    if (items[i].vid == IE_VID_CLOCK_HHMM || items[i].vid == IE_VID_CLOCK_HHMMSS) t->clock_slots.push_back(slot_of[i]);
+    if (items[i].flags & EF_RAWALT) t->rawalt[ents[i].tid].push_back(slot_of[i]);
+    t->groups[ph_group(key_hash(ents[i].key, seed, ents[i].tid), nb)].push_back(slot_of[i]);
+  }
   t->device = device;
   t->dialect = dialect;
   t->flags = flags;
   t->n_entries = ents.size();
   t->n_tables = n_tables;
-  t->clock_entries = std::move(clock_entries);
-  auto up = [&](DevBuf& b, const void* src, uint64_t bytes) -> hipError_t {
-    hipError_t e = b.ensure(bytes + 16);
+  auto up = [&](DevBuf& b, const void* src, uint64_t bytes, uint64_t cap) -> hipError_t {
+    hipError_t e = b.ensure(cap + 16);
     if (e != hipSuccess) return e;
     return bytes ? hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice) : hipSuccess;
   };
-  hipError_t e1 = up(t->entries, entries.data(), entries.size() * sizeof(Entry));
-  hipError_t e2 = e1 == hipSuccess ? up(t->pilots, pilots.data(), pilots.size() * sizeof(uint16_t)) : e1;
-  hipError_t e3 = e2 == hipSuccess ? up(t->arena, arena.data(), arena.size()) : e2;
+  // the arena keeps room for the texts ie_table_set_update appends (16 pad bytes past the end:
+  // dword reads past the last text)
+  t->arena_cap = arena.size() + std::max<uint64_t>(arena.size() / 4, 1ull << 16);
+  hipError_t e1 = up(t->entries, entries.data(), entries.size() * sizeof(Entry), entries.size() * sizeof(Entry));
+  hipError_t e2 = e1 == hipSuccess ? up(t->pilots, pilots.data(), pilots.size() * sizeof(uint16_t), pilots.size() * 2) : e1;
+  hipError_t e3 = e2;
+  if (e3 == hipSuccess) e3 = t->arena.ensure(t->arena_cap + 16);
+  if (e3 == hipSuccess) e3 = hipMemset(t->arena.p, 0, t->arena_cap + 16);
+  if (e3 == hipSuccess && !arena.empty()) e3 = hipMemcpy(t->arena.p, arena.data(), arena.size(), hipMemcpyHostToDevice);
   if (e3 != hipSuccess) {
     delete t;
     return fail(IE_ERR_HIP, std::string("table upload: ") + hipGetErrorString(e3));
@@ -784,6 +870,9 @@ int upload_table(const std::vector<Ent>& ents, uint32_t n_tables, int32_t dialec
   t->dev.dialect = (uint32_t)dialect;
   t->dev.flags = ((flags & IE_TABLE_HAS_INSERTS_DIR) ? TF_HAS_DIR : 0u) | (long_keys ? TF_LONG_KEYS : 0u);
   t->dev.maxtext = maxtext;
+  t->h_entries = std::move(entries);
+  t->h_pilots = std::move(pilots);
+  t->h_arena = std::move(arena);
   *out = t;
   return IE_SUCCESS;
 }
@@ -967,7 +1056,13 @@ int ie_table_replicate(const ie_table* t, int32_t device, ie_table** out) {
   c->flags = t->flags;
   c->n_entries = t->n_entries;
   c->n_tables = t->n_tables;
-  c->clock_entries = t->clock_entries;
+  c->clock_slots = t->clock_slots;
+  c->h_entries = t->h_entries;
+  c->h_pilots = t->h_pilots;
+  c->h_arena = t->h_arena;
+  c->arena_cap = t->arena_cap;
+  c->groups = t->groups;
+  c->rawalt = t->rawalt;
   c->dev = t->dev;
   auto copy = [&](DevBuf& dst, const DevBuf& src) -> hipError_t {
     hipError_t e = dst.ensure(src.bytes);
@@ -1019,15 +1114,174 @@ int ie_table_set_clock(ie_table* t, const ie_clock* now) {
   char hhmm[16], hhmmss[16];
   snprintf(hhmm, sizeof hhmm, "%02d:%02d", now->hour, now->minute);
   snprintf(hhmmss, sizeof hhmmss, "%02d:%02d:%02d", now->hour, now->minute, now->second);
-  for (auto& ce : t->clock_entries) {
-    Entry& e = ce.second;
+  Patches pe, pa;  // every table's two clock entries and their arena texts: one upload each
+  for (uint32_t slot : t->clock_slots) {
+    Entry& e = t->h_entries[slot];
     const char* txt = e.vid == IE_VID_CLOCK_HHMM ? hhmm : hhmmss;
     if (strlen(txt) != e.text_len) return fail(IE_ERR_INVALID, "clock field out of range");
     memcpy(e.text, txt, e.text_len);
-    IE_HIP(hipMemcpy((Entry*)t->entries.p + ce.first, &e, sizeof(Entry), hipMemcpyHostToDevice));
-    IE_HIP(hipMemcpy((uint8_t*)t->arena.p + e.text_off, txt, e.text_len, hipMemcpyHostToDevice));
+    memcpy(t->h_arena.data() + e.text_off, txt, e.text_len);
+    pe.add((uint64_t)slot * sizeof(Entry), &e, sizeof(Entry));
+    pa.add(e.text_off, txt, e.text_len);
   }
-  return IE_SUCCESS;
+  if ((rc = apply_patches(t->entries.p, pe))) return rc;
+  return apply_patches(t->arena.p, pa);
+}
+
+// set_interpdata on a built table (set): py:470-471 `inserts[key] = value` (and `del`) on state
+// table_id[i], without a rebuild. A key already in that table is rewritten in place (its slot is
+// fixed by the perfect hash); a new key re-places its pilot group (about four keys) around it; a
+// group with no free placement reports IE_ERR_CAPACITY and nothing of that key is applied (the
+// caller rebuilds). Values are taken as given: a brace-bearing value is not pre-resolved (the
+// exact evaluator resolves it in the reference's order), and the pre-resolved values of every
+// table that changed go back to their raw text, since they were resolved against the old dict.
+int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, const uint32_t* vid, uint64_t n) {
+  if (!t || (n && (!kv || !table_id || !vid))) return fail(IE_ERR_INVALID, "null argument");
+  int rc = set_device(t->device);
+  if (rc) return rc;
+  IE_HIP(hipDeviceSynchronize());  // no batch may still read the table
+  const uint64_t arena0 = t->h_arena.size();
+  const uint64_t seed = t->dev.seed;
+  const uint32_t nb = t->dev.nb, m = t->dev.m;
+  std::vector<uint32_t> dirty;             // entry slots to upload
+  std::vector<uint32_t> dirty_groups;      // pilots to upload
+  std::vector<uint32_t> touched;           // tables whose pre-resolved values must go raw
+  int status = IE_SUCCESS;
+  auto is_clock = [](uint32_t v) { return v == IE_VID_CLOCK_HHMM || v == IE_VID_CLOCK_HHMMSS; };
+  for (uint64_t i = 0; i < n; i++) {
+    const uint32_t tb = table_id[i];
+    if (tb >= t->n_tables) return fail(IE_ERR_INVALID, "table id beyond the table set");
+    std::string_view key(kv[i].key ? kv[i].key : "", kv[i].key_len);
+    if (key.empty() || key == "HH:MM" || key == "HH:MM:SS") continue;  // never looked up (py:433-446)
+    if (kv[i].kind > IE_KIND_DICT) return fail(IE_ERR_INVALID, "bad kind");
+    if (vid[i] >= IE_VID_CLOCK_HHMMSS && kv[i].kind >= 0) return fail(IE_ERR_INVALID, "value id out of range");
+    const uint64_t h = key_hash(key, seed, tb);
+    const uint32_t g = ph_group(h, nb), slot = ph_slot(h, t->h_pilots[g], m);
+    Entry& cur = t->h_entries[slot];
+    const bool present = (cur.flags & EF_OCCUPIED) && (cur.flags >> kTidShift) == tb && mirror_key(t, cur) == key;
+    if (kv[i].kind < 0) {  // del inserts[key]
+      if (!present) continue;
+      auto& gs = t->groups[g];
+      gs.erase(std::remove(gs.begin(), gs.end(), slot), gs.end());
+      cur = Entry{};
+      dirty.push_back(slot);
+      t->n_entries--;
+      touched.push_back(tb);
+      continue;
+    }
+    std::string_view text(kv[i].text ? kv[i].text : "", kv[i].text_len);
+    if (key.size() >= 0xFFFFFFF0ull || text.size() >= 0xFFFFFFF0ull) return fail(IE_ERR_INVALID, "key or text above 4 GiB");
+    const uint32_t flags = kind_flags(kv[i].kind, t->dialect) | text_flags(text);
+    touched.push_back(tb);
+    if (present) {
+      cur = make_entry(t, key, text, flags, vid[i], tb);
+      dirty.push_back(slot);
+    } else {
+      // re-place the group with the new key: a pilot that sends every member to a distinct slot
+      // that is free or one of the group's own
+      std::vector<uint32_t>& gs = t->groups[g];
+      std::vector<uint64_t> hs;
+      for (uint32_t s2 : gs) {
+        const Entry& e = t->h_entries[s2];
+        hs.push_back(key_hash(mirror_key(t, e), seed, e.flags >> kTidShift));
+      }
+      hs.push_back(h);
+      std::vector<uint32_t> cand(hs.size());
+      bool found = false;
+      uint32_t pilot = 0;
+      for (uint32_t p = 0; p < 65536 && !found; p++) {
+        bool ok = true;
+        for (size_t k = 0; k < hs.size() && ok; k++) {
+          const uint32_t c = ph_slot(hs[k], p, m);
+          ok = !(t->h_entries[c].flags & EF_OCCUPIED) || std::find(gs.begin(), gs.end(), c) != gs.end();
+          for (size_t j = 0; j < k && ok; j++) ok = cand[j] != c;
+          cand[k] = c;
+        }
+        if (ok) found = true, pilot = p;
+      }
+      if (!found) {
+        status = fail(IE_ERR_CAPACITY, "no free placement for a new key's pilot group: rebuild the table");
+        continue;
+      }
+      std::vector<Entry> moved;
+      for (uint32_t s2 : gs) moved.push_back(t->h_entries[s2]);
+      for (uint32_t s2 : gs) {
+        t->h_entries[s2] = Entry{};
+        dirty.push_back(s2);
+      }
+      for (size_t k = 0; k < moved.size(); k++) {
+        const uint32_t from = gs[k], to = cand[k];
+        t->h_entries[to] = moved[k];
+        dirty.push_back(to);
+        if (from != to) {
+          for (uint32_t& cs : t->clock_slots)
+            if (cs == from && is_clock(moved[k].vid)) cs = to;
+          auto it = t->rawalt.find(moved[k].flags >> kTidShift);
+          if (it != t->rawalt.end())
+            for (uint32_t& rs : it->second)
+              if (rs == from) rs = to;
+        }
+      }
+      t->h_entries[cand.back()] = make_entry(t, key, text, flags, vid[i], tb);
+      dirty.push_back(cand.back());
+      gs.assign(cand.begin(), cand.end());
+      t->h_pilots[g] = (uint16_t)pilot;
+      dirty_groups.push_back(g);
+      t->n_entries++;
+    }
+    if (key.size() > kInlineKey && key.size() <= 2 * kInlineKey) t->dev.flags |= TF_LONG_KEYS;
+    t->dev.maxtext = std::max<uint64_t>(t->dev.maxtext, text.size());
+  }
+  // values pre-resolved against the old dict of a changed table: back to their raw text
+  std::sort(touched.begin(), touched.end());
+  touched.erase(std::unique(touched.begin(), touched.end()), touched.end());
+  for (uint32_t tb : touched) {
+    auto it = t->rawalt.find(tb);
+    if (it == t->rawalt.end()) continue;
+    for (uint32_t s2 : it->second) {
+      Entry& e = t->h_entries[s2];
+      if (!(e.flags & EF_RAWALT)) continue;
+      const uint8_t* a = t->h_arena.data();
+      uint32_t rl;
+      memcpy(&rl, a + e.text_off - 4, 4);
+      const uint32_t roff = e.text_off - 4 - ((rl + 3u) & ~3u);
+      const std::string raw((const char*)a + roff, rl), key(mirror_key(t, e));
+      const uint32_t kflags = e.flags & (EF_KIND_MASK | EF_SPLICE_OK | EF_KEY_STR | EF_KEY_UNHASHABLE);
+      e = make_entry(t, key, raw, kflags | text_flags(raw), e.vid, tb);
+      t->dev.maxtext = std::max<uint64_t>(t->dev.maxtext, raw.size());
+      dirty.push_back(s2);
+    }
+    t->rawalt.erase(it);
+  }
+  // upload: the appended arena bytes, the changed entries, the changed pilots
+  if (t->h_arena.size() > t->arena_cap) {  // grow the device arena (the whole mirror goes up again)
+    DevBuf na;
+    const uint64_t cap = t->h_arena.size() + std::max<uint64_t>(t->h_arena.size() / 4, 1ull << 16);
+    IE_HIP(na.ensure(cap + 16));
+    IE_HIP(hipMemset(na.p, 0, cap + 16));
+    IE_HIP(hipMemcpy(na.p, t->h_arena.data(), t->h_arena.size(), hipMemcpyHostToDevice));
+    t->arena.release();
+    t->arena = na;
+    na.p = nullptr;
+    t->arena_cap = cap;
+    t->dev.arena = (const uint8_t*)t->arena.p;
+  } else if (t->h_arena.size() > arena0) {
+    IE_HIP(hipMemcpy((uint8_t*)t->arena.p + arena0, t->h_arena.data() + arena0, t->h_arena.size() - arena0,
+                     hipMemcpyHostToDevice));
+  }
+  std::sort(dirty.begin(), dirty.end());
+  dirty.erase(std::unique(dirty.begin(), dirty.end()), dirty.end());
+  if (dirty.size() * 8 > t->h_entries.size()) {  // many: the whole entry array in one copy
+    IE_HIP(hipMemcpy(t->entries.p, t->h_entries.data(), t->h_entries.size() * sizeof(Entry), hipMemcpyHostToDevice));
+  } else {
+    Patches pe;
+    for (uint32_t s2 : dirty) pe.add((uint64_t)s2 * sizeof(Entry), &t->h_entries[s2], sizeof(Entry));
+    if ((rc = apply_patches(t->entries.p, pe))) return rc;
+  }
+  if (!dirty_groups.empty())
+    IE_HIP(hipMemcpy(t->pilots.p, t->h_pilots.data(), t->h_pilots.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+  t->dev.n_entries = (uint32_t)t->n_entries;
+  return status;
 }
 
 uint64_t ie_table_entries(const ie_table* t) { return t ? t->n_entries : 0; }

@@ -870,13 +870,24 @@ __device__ __forceinline__ void stream_stage(uint8_t* g, const uint8_t* stage, u
   const uint32_t nv = (uint32_t)((b_down - a_up) >> 4);
   constexpr int kOutV = (kOutStage + kRBlock * 16 - 1) / (kRBlock * 16);
   uint4 v[kOutV];
+  if (head == 0) {  // (uniform) a 16-aligned destination, e.g. reserved ranges: the stage's blocks as they are
 #pragma unroll
-  for (int k = 0; k < kOutV; k++) {
-    const uint32_t c = tid + (uint32_t)k * kRBlock;
-    if (c < nv) {
-      const lds_u128* blk = (const lds_u128*)(const lds_u8*)stage + c;
-      const u32x4 x = blk[0], y = blk[1];
-      v[k] = bytes_at(x, y, head);
+    for (int k = 0; k < kOutV; k++) {
+      const uint32_t c = tid + (uint32_t)k * kRBlock;
+      if (c < nv) {
+        const u32x4 x = ((const lds_u128*)(const lds_u8*)stage)[c];
+        v[k] = make_uint4(x.x, x.y, x.z, x.w);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kOutV; k++) {
+      const uint32_t c = tid + (uint32_t)k * kRBlock;
+      if (c < nv) {
+        const lds_u128* blk = (const lds_u128*)(const lds_u8*)stage + c;
+        const u32x4 x = blk[0], y = blk[1];
+        v[k] = bytes_at(x, y, head);
+      }
     }
   }
   uint4* dstv = (uint4*)a_up;
@@ -1472,13 +1483,15 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
         if (!B.in_len && !B.out_index) {
           const uint64_t res_base = gld(B.in_off);
           ovf = ((((gld(B.in_off + B.n) - res_base) * W.reserve16) >> 4) + 15) & ~15ull;
-          rb = ((lo - res_base) * W.reserve16) >> 4;
-          own = tile_total <= (((geo.hi - res_base) * W.reserve16) >> 4) - rb;
+          // (16-aligned: the stream-out then moves the stage's blocks as they are)
+          rb = ((((lo - res_base) * W.reserve16) >> 4) + 15) & ~15ull;
+          const uint64_t re = ((geo.hi - res_base) * W.reserve16) >> 4;
+          own = rb <= re && tile_total <= re - rb;
           if (tile == 0) __hip_atomic_store(W.res_ovf, ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
           ovf = __hip_atomic_load(W.res_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        lb_early = own ? rb : ovf + atomicAdd((unsigned long long*)W.cursor, (unsigned long long)tile_total);
+        lb_early = own ? rb : ovf + atomicAdd((unsigned long long*)W.cursor, (unsigned long long)((tile_total + 15) & ~15ull));
         __hip_atomic_fetch_add(W.shards + 16u * (tile & 15u), tile_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
         lb_early = atomicAdd((unsigned long long*)W.cursor, (unsigned long long)tile_total);
@@ -1746,6 +1759,28 @@ hipError_t launch_unescape_cmd(const Batch& B, const Work& W, const DevTable& T,
 #endif
 
 #if !defined(IE_RESOLVE_WIDE)
+// host-built patches of a device table (ie_table_set_update, ie_table_set_clock): one lane per patch
+__global__ void k_patch(uint8_t* dst, const uint8_t* src, const uint64_t* doff, const uint32_t* soff, const uint32_t* len,
+                        uint32_t n) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  uint8_t* d = dst + doff[k];
+  const uint8_t* s = src + soff[k];
+  const uint32_t l = len[k];
+  if (l == sizeof(Entry) && ((uintptr_t)d & 15u) == 0) {  // a whole entry: four 16-byte moves
+    for (uint32_t j = 0; j < sizeof(Entry) / 16; j++) gst4((uint4*)d + j, gld4((const uint4*)s + j));
+    return;
+  }
+  for (uint32_t j = 0; j < l; j++) d[j] = s[j];
+}
+
+hipError_t launch_patch(uint8_t* dst, const uint8_t* src, const uint64_t* doff, const uint32_t* soff,
+                        const uint32_t* len, uint32_t n, hipStream_t st) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_patch, dim3((n + 255) / 256), dim3(256), 0, st, dst, src, doff, soff, len, n);
+  return hipGetLastError();
+}
+
 // the listed strings (W.udefer_list) as a views subset of the batch (their bytes where they are)
 __global__ void k_gather_listed(Batch B, Work W, uint64_t* sub_off, uint32_t* sub_len, uint32_t* sub_tid) {
   const uint32_t count = __hip_atomic_load(W.udefer_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -36,6 +36,9 @@ escape = "\\"
 inserts_dir = None  # py:44 — when set, get_interpdata falls back to its files (py:452-461)
 
 
+DELETE = object()  # InsertsTableSet.update: remove the key (`del inserts[key]`)
+
+
 class InterpolationException(Exception):
     # Caught in goto_map to trigger the 'NULL' key (py:426-428).
     pass
@@ -170,7 +173,49 @@ class InsertsTableSet:
         return self.values[vid]
 
     def table_keys(self, t):
-        return self.keys[self.starts[t]:self.starts[t + 1]]
+        return list(self.dicts[t].keys())  # the live dict (as py:467's message reads it)
+
+    def update(self, changes):
+        """set_interpdata on the device copy (py:470-471 `inserts[key] = value`, or DELETE for
+        `del`), without a rebuild (ie_table_set_update): changes = [(dict index, key, value)].
+        The caller's dicts are not touched (the states the table set was built from are usually the
+        caller's own, already updated). False when the library found no placement for a new key:
+        then rebuild the table set."""
+        import numpy as np
+        n = len(changes)
+        if n == 0:
+            return True
+        kb, tb, kinds, tids, vids = [], [], np.zeros(n, np.int32), np.zeros(n, np.uint32), np.zeros(n, np.uint32)
+        for i, (t, k, v) in enumerate(changes):
+            if type(k) is not str:
+                raise TypeError("insert keys must be str")
+            if t < 0 or t >= len(self.dicts):
+                raise IndexError("dict index beyond the table set")
+            tids[i] = t
+            kb.append(N.enc(k))
+            if v is DELETE:
+                kinds[i], text = -1, ""
+            else:
+                kinds[i], text = (N.KIND_STR, v) if type(v) is str else render(v, self.dialect)
+                vids[i] = len(self.values)
+                self.values.append(v)
+            tb.append(N.enc(text))
+        kblob = np.frombuffer(b"".join(kb) + b"\0", np.uint8)
+        tblob = np.frombuffer(b"".join(tb) + b"\0", np.uint8)
+        klen = np.fromiter(map(len, kb), np.uint64, n)
+        tlen = np.fromiter(map(len, tb), np.uint64, n)
+        arr = np.zeros(n, dtype=[("key", "<u8"), ("key_len", "<u8"), ("text", "<u8"), ("text_len", "<u8"),
+                                 ("kind", "<i4"), ("reserved", "<u4")])
+        arr["key"] = kblob.ctypes.data + np.concatenate(([0], np.cumsum(klen)[:-1])).astype(np.uint64)
+        arr["key_len"] = klen
+        arr["text"] = tblob.ctypes.data + np.concatenate(([0], np.cumsum(tlen)[:-1])).astype(np.uint64)
+        arr["text_len"] = tlen
+        arr["kind"] = kinds
+        rc = N.lib().ie_table_set_update(self.h, ctypes.c_void_p(arr.ctypes.data), tids.ctypes.data, vids.ctypes.data, n)
+        if rc == N.ERR_CAPACITY:
+            return False
+        N.check(rc, "ie_table_set_update")
+        return True
 
     # --------------------------------------------------------------------------------------
     def run(self, strings, table_ids=None, exec_=None):

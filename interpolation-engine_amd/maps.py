@@ -389,12 +389,14 @@ def run_map_tasks(states, tasks, dialect="py", device=0):
                 continue
             got = replace_map_states(states, task, dialect, device, tables=tset)
             outs.append(got)
-            changed = False
-            for st, r in zip(states, got):
+            changes = []
+            for s, (st, r) in enumerate(zip(states, got)):
                 if not isinstance(r, BaseException):
-                    st[r[0]] = r[1]
-                    changed = True
-            if changed:
+                    st[r[0]] = r[1]  # set_interpdata (py:470-471)
+                    changes.append((s, r[0], r[1]))
+            # the same stores on the device copy (ie_table_set_update), or a rebuild when a new
+            # key found no placement
+            if changes and not tset.update(changes):
                 tset.close()
                 tset = None
     finally:
