@@ -213,8 +213,8 @@ int ie_exec_timing(ie_exec* x, ie_timing* out); /* syncs */
 #define IE_OPT_FAST 2
 #define IE_OPT_DEBUG_NOEVAL 3
 #define IE_OPT_TILE 4
-#define IE_OPT_VIEWS 5 /* 1: the host batch APIs resolve into a views layout (no look-back) and pack
-                          the results in input order on the host; 0 (default): packed on the device */
+#define IE_OPT_VIEWS 5 /* 1 (default): the host batch APIs resolve into a views layout (no look-back) and
+                          pack the results in input order on the host; 0: packed on the device */
 #define IE_OPT_DEFER 7 /* views batches: 1: strings the chain jobs cannot finish go to a second pass in
                           tiles of their own (the exact evaluator and the literal path then run on
                           full tiles of such strings); -1 adaptive (above 0.4 % of a batch); 0

@@ -111,7 +111,7 @@ struct ie_exec {
   int32_t opt_fail_commit = -1;   // -1 adaptive, 0 / 1 forced (IE_FAIL_COMMIT)
   uint32_t opt_fast = 1;          // 0: exact evaluator only (IE_FAST)
   int32_t opt_tile = 0;           // k_resolve tile: 0 by call site, 256 or 512 forced (IE_TILE)
-  int32_t opt_views = 0;          // host batch APIs resolve into a views layout (IE_VIEWS)
+  int32_t opt_views = 1;          // host batch APIs resolve into a views layout (IE_VIEWS; 0: packed on the device)
   int32_t opt_defer = 0;          // views batches: heavy strings to a second pass: -1 adaptive, 0 (default:
                                   // measured slower on config 5) / 1 (IE_DEFER)
   bool defer_slow = false;        // the adaptive choice (from an earlier batch's counts)

@@ -1,12 +1,12 @@
 // ie_resolve.hip — k_resolve: interpolate_inserts (py:497-541 / rust-project/src/interp.rs:31-89)
 // over a packed batch in ONE pass over HBM.
 //
-// One 256-lane workgroup per tile of 256 consecutive strings; the tile is the workgroup index and
-// tiles are chained with a decoupled look-back over 8-byte {flag, value} words published by
-// agent-scope atomics. Forward progress relies on the dispatcher starting workgroups in index
-// order (observed on gfx950; HIP does not promise it): a tile only waits on lower-numbered tiles,
-// which are then already resident. The wait is bounded (10 s): a violation sets the exec's error
-// word, which ie_exec_sync / the host APIs report as IE_ERR_TIMEOUT. Per tile:
+// One 256-lane workgroup per tile of 256 consecutive strings. Packed output: tiles are chained with a
+// decoupled look-back over 8-byte {flag, value} words published by agent-scope atomics, and the tile
+// index is a ticket each workgroup takes when it starts, so a tile only waits on tiles that have
+// started (no assumption about dispatch order). The wait is bounded (10 s): a violation sets the
+// exec's error word, which ie_exec_sync / the host APIs report as IE_ERR_TIMEOUT.
+// Views output: no look-back, tile = workgroup index. Per tile:
 //   1. stage the tile's input bytes in LDS (16-byte loads) and classify every 16-byte chunk into
 //      an open-brace and a close-brace mask (plus one "odd byte" bit per chunk: '\' or 0xE3);
 //   2. every lane evaluates its string. Clean strings (no odd byte, brace pairs forming chains
@@ -1200,9 +1200,15 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
 
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
   const uint32_t ntiles = (uint32_t)((B.n + kRBlock - 1) / kRBlock);
-  // Tile = workgroup index: workgroups are dispatched in index order, so every tile a look-back
-  // waits on is already resident (no ticket: a single-address atomic serializes chip-wide).
-  const uint32_t tile = blockIdx.x;
+  // Views: tile = workgroup index (no tile waits on another). Packed output: the tile index is a
+  // ticket taken when the workgroup starts, so every tile a look-back waits on has started (HIP
+  // promises no dispatch order; one atomic per tile, on the packed path only)
+  uint32_t tile = blockIdx.x;
+  if (!VIEWS) {
+    if (tid == 0) s_misc[0] = atomicAdd(W.tile_ticket, 1u);
+    __syncthreads();
+    tile = s_misc[0];
+  }
   const TileGeo geo = load_geo(B, tile, tid);
   TilePrefetch<kStageV> pre;
   pre.nv = 0;

@@ -14,6 +14,9 @@ fi
 if [ -n "${PYTEST_K:-}" ]; then
   IE_LIB_PATH=${PYTEST_LIB:-} timeout -k 10 900 python -u -m pytest ${PYTEST_FILES:-tests/test_gpu_parity.py tests/test_gpu_fullsize.py} -m gpu -x -q -k "$PYTEST_K" --timeout 600 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 fi
+if [ -n "${PYTEST2_FILES:-}" ]; then
+  timeout -k 10 600 python -u -m pytest $PYTEST2_FILES -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest2.log 2>&1 || { tail -30 $O/pytest2.log; exit 1; }
+fi
 PMC="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY"
 for v in ${VARIANTS:-main}; do
   if [ "$v" = main ]; then LIBP=""; else LIBP=interpolation-engine_amd/libie_amd_$v.so; fi
