@@ -89,10 +89,12 @@ struct ie_table {
   uint64_t arena_cap = 0;
   std::vector<std::vector<uint32_t>> groups;
   std::unordered_map<uint32_t, std::vector<uint32_t>> rawalt;
+  DevBuf patch_staging;  // ie_table_set_update / _set_clock uploads
   ~ie_table() {
     entries.release();
     pilots.release();
     arena.release();
+    patch_staging.release();
   }
 };
 
@@ -704,40 +706,44 @@ struct Ent {
   std::string_view raw;  // EF_RAWALT: the raw value behind a pre-resolved splice text
 };
 
-// Byte patches of a device buffer, applied by one upload and one kernel (k_patch): patch k writes
-// len[k] bytes of data (at soff[k]) to dst + doff[k]. Synchronous.
+// Byte patches of device memory, applied by one upload and one kernel (k_patch): patch k writes
+// len[k] (<= 256) bytes of data (at soff[k]) to the device address dst[k]. Synchronous. The upload
+// goes through a grow-only staging buffer of the caller's (a table's).
 struct Patches {
   std::vector<uint8_t> data;
-  std::vector<uint64_t> doff;
+  std::vector<uint64_t> dst;
   std::vector<uint32_t> soff, len;
-  void add(uint64_t dst_off, const void* src, uint32_t n) {
-    doff.push_back(dst_off);
-    soff.push_back((uint32_t)data.size());
-    len.push_back(n);
-    data.insert(data.end(), (const uint8_t*)src, (const uint8_t*)src + n);
-    while (data.size() & 15) data.push_back(0);
+  void add(void* dst_ptr, const void* src, uint64_t n) {
+    const uint8_t* s8 = (const uint8_t*)src;
+    for (uint64_t k = 0; k < n; k += 256) {
+      const uint32_t l = (uint32_t)std::min<uint64_t>(256, n - k);
+      dst.push_back((uint64_t)(uintptr_t)dst_ptr + k);
+      soff.push_back((uint32_t)data.size());
+      len.push_back(l);
+      data.insert(data.end(), s8 + k, s8 + k + l);
+      while (data.size() & 15) data.push_back(0);
+    }
   }
+  bool empty() const { return dst.empty(); }
 };
 
-int apply_patches(void* dst, const Patches& P) {
-  const uint64_t n = P.doff.size();
+int apply_patches(DevBuf& staging, const Patches& P) {
+  const uint64_t n = P.dst.size();
   if (!n) return IE_SUCCESS;
   if (P.data.size() >= (1ull << 32)) return fail(IE_ERR_INVALID, "patch set above 4 GiB");
-  const uint64_t o_doff = (P.data.size() + 15) & ~15ull, o_soff = o_doff + 8 * n, o_len = o_soff + 4 * n;
+  const uint64_t o_dst = (P.data.size() + 15) & ~15ull, o_soff = o_dst + 8 * n, o_len = o_soff + 4 * n;
   std::vector<uint8_t> blob(o_len + 4 * n);
   memcpy(blob.data(), P.data.data(), P.data.size());
-  memcpy(blob.data() + o_doff, P.doff.data(), 8 * n);
+  memcpy(blob.data() + o_dst, P.dst.data(), 8 * n);
   memcpy(blob.data() + o_soff, P.soff.data(), 4 * n);
   memcpy(blob.data() + o_len, P.len.data(), 4 * n);
-  DevBuf d;
-  IE_HIP(d.ensure(blob.size()));
-  hipError_t e = hipMemcpy(d.p, blob.data(), blob.size(), hipMemcpyHostToDevice);
-  const uint8_t* base = (const uint8_t*)d.p;
+  IE_HIP(staging.ensure(blob.size()));
+  hipError_t e = hipMemcpy(staging.p, blob.data(), blob.size(), hipMemcpyHostToDevice);
+  const uint8_t* base = (const uint8_t*)staging.p;
   if (e == hipSuccess)
-    e = launch_patch((uint8_t*)dst, base, (const uint64_t*)(base + o_doff), (const uint32_t*)(base + o_soff),
+    e = launch_patch(base, (const uint64_t*)(base + o_dst), (const uint32_t*)(base + o_soff),
                      (const uint32_t*)(base + o_len), (uint32_t)n, nullptr);
   if (e == hipSuccess) e = hipDeviceSynchronize();
-  d.release();
   if (e != hipSuccess) return fail(IE_ERR_HIP, std::string("table patch: ") + hipGetErrorString(e));
   return IE_SUCCESS;
 }
@@ -1114,18 +1120,17 @@ int ie_table_set_clock(ie_table* t, const ie_clock* now) {
   char hhmm[16], hhmmss[16];
   snprintf(hhmm, sizeof hhmm, "%02d:%02d", now->hour, now->minute);
   snprintf(hhmmss, sizeof hhmmss, "%02d:%02d:%02d", now->hour, now->minute, now->second);
-  Patches pe, pa;  // every table's two clock entries and their arena texts: one upload each
+  Patches pe;  // every table's two clock entries and their arena texts: one upload
   for (uint32_t slot : t->clock_slots) {
     Entry& e = t->h_entries[slot];
     const char* txt = e.vid == IE_VID_CLOCK_HHMM ? hhmm : hhmmss;
     if (strlen(txt) != e.text_len) return fail(IE_ERR_INVALID, "clock field out of range");
     memcpy(e.text, txt, e.text_len);
     memcpy(t->h_arena.data() + e.text_off, txt, e.text_len);
-    pe.add((uint64_t)slot * sizeof(Entry), &e, sizeof(Entry));
-    pa.add(e.text_off, txt, e.text_len);
+    pe.add((Entry*)t->entries.p + slot, &e, sizeof(Entry));
+    pe.add((uint8_t*)t->arena.p + e.text_off, txt, e.text_len);
   }
-  if ((rc = apply_patches(t->entries.p, pe))) return rc;
-  return apply_patches(t->arena.p, pa);
+  return apply_patches(t->patch_staging, pe);
 }
 
 // set_interpdata on a built table (set): py:470-471 `inserts[key] = value` (and `del`) on state
@@ -1254,7 +1259,8 @@ int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
     t->rawalt.erase(it);
   }
   // upload: the appended arena bytes, the changed entries, the changed pilots
-  if (t->h_arena.size() > t->arena_cap) {  // grow the device arena (the whole mirror goes up again)
+  const bool grown = t->h_arena.size() > t->arena_cap;
+  if (grown) {  // grow the device arena (the whole mirror goes up again)
     DevBuf na;
     const uint64_t cap = t->h_arena.size() + std::max<uint64_t>(t->h_arena.size() / 4, 1ull << 16);
     IE_HIP(na.ensure(cap + 16));
@@ -1265,21 +1271,23 @@ int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
     na.p = nullptr;
     t->arena_cap = cap;
     t->dev.arena = (const uint8_t*)t->arena.p;
-  } else if (t->h_arena.size() > arena0) {
-    IE_HIP(hipMemcpy((uint8_t*)t->arena.p + arena0, t->h_arena.data() + arena0, t->h_arena.size() - arena0,
-                     hipMemcpyHostToDevice));
   }
+  // one upload and one kernel for the appended texts, the changed entries and pilots (the whole
+  // entry array in one copy when many changed)
+  Patches pe;
+  if (t->h_arena.size() > arena0 && !grown)
+    pe.add((uint8_t*)t->arena.p + arena0, t->h_arena.data() + arena0, t->h_arena.size() - arena0);
   std::sort(dirty.begin(), dirty.end());
   dirty.erase(std::unique(dirty.begin(), dirty.end()), dirty.end());
-  if (dirty.size() * 8 > t->h_entries.size()) {  // many: the whole entry array in one copy
+  if (dirty.size() * 8 > t->h_entries.size()) {
     IE_HIP(hipMemcpy(t->entries.p, t->h_entries.data(), t->h_entries.size() * sizeof(Entry), hipMemcpyHostToDevice));
   } else {
-    Patches pe;
-    for (uint32_t s2 : dirty) pe.add((uint64_t)s2 * sizeof(Entry), &t->h_entries[s2], sizeof(Entry));
-    if ((rc = apply_patches(t->entries.p, pe))) return rc;
+    for (uint32_t s2 : dirty) pe.add((Entry*)t->entries.p + s2, &t->h_entries[s2], sizeof(Entry));
   }
-  if (!dirty_groups.empty())
-    IE_HIP(hipMemcpy(t->pilots.p, t->h_pilots.data(), t->h_pilots.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+  std::sort(dirty_groups.begin(), dirty_groups.end());
+  dirty_groups.erase(std::unique(dirty_groups.begin(), dirty_groups.end()), dirty_groups.end());
+  for (uint32_t g : dirty_groups) pe.add((uint16_t*)t->pilots.p + g, &t->h_pilots[g], sizeof(uint16_t));
+  if ((rc = apply_patches(t->patch_staging, pe))) return rc;
   t->dev.n_entries = (uint32_t)t->n_entries;
   return status;
 }

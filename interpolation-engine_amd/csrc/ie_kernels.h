@@ -122,9 +122,10 @@ hipError_t launch_unescape_cmd(const Batch& B, const Work& W, const DevTable& T,
 // are resolved by the second as a subset (their views in sub_off / sub_len / sub_tid)
 hipError_t launch_resolve_deferring(const Batch& B, const Work& W, const DevTable& T, uint8_t* out, uint64_t cap,
                                     uint64_t* sub_off, uint32_t* sub_len, uint32_t* sub_tid, hipStream_t st);
-// patch k writes len[k] bytes of src + soff[k] to dst + doff[k] (ie_table_set_update / _set_clock)
-hipError_t launch_patch(uint8_t* dst, const uint8_t* src, const uint64_t* doff, const uint32_t* soff,
-                        const uint32_t* len, uint32_t n, hipStream_t st);
+// patch k writes len[k] (<= 256) bytes of src + soff[k] to the device address dst[k]
+// (ie_table_set_update / _set_clock)
+hipError_t launch_patch(const uint8_t* src, const uint64_t* dst, const uint32_t* soff, const uint32_t* len, uint32_t n,
+                        hipStream_t st);
 hipError_t launch_status_carry(const uint8_t* before, uint8_t* after, uint64_t n, hipStream_t st);
 hipError_t launch_debug_probe(const DevTable& T, const uint8_t* key, uint32_t klen, uint64_t* out,
                               hipStream_t st);

@@ -1766,24 +1766,24 @@ hipError_t launch_unescape_cmd(const Batch& B, const Work& W, const DevTable& T,
 
 #if !defined(IE_RESOLVE_WIDE)
 // host-built patches of a device table (ie_table_set_update, ie_table_set_clock): one lane per patch
-__global__ void k_patch(uint8_t* dst, const uint8_t* src, const uint64_t* doff, const uint32_t* soff, const uint32_t* len,
-                        uint32_t n) {
+// of <= 256 bytes (whole 64-byte entries as four 16-byte moves)
+__global__ void k_patch(const uint8_t* src, const uint64_t* dst, const uint32_t* soff, const uint32_t* len, uint32_t n) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
-  uint8_t* d = dst + doff[k];
+  uint8_t* d = (uint8_t*)(uintptr_t)dst[k];
   const uint8_t* s = src + soff[k];
   const uint32_t l = len[k];
-  if (l == sizeof(Entry) && ((uintptr_t)d & 15u) == 0) {  // a whole entry: four 16-byte moves
+  if (l == sizeof(Entry) && ((uintptr_t)d & 15u) == 0) {
     for (uint32_t j = 0; j < sizeof(Entry) / 16; j++) gst4((uint4*)d + j, gld4((const uint4*)s + j));
     return;
   }
   for (uint32_t j = 0; j < l; j++) d[j] = s[j];
 }
 
-hipError_t launch_patch(uint8_t* dst, const uint8_t* src, const uint64_t* doff, const uint32_t* soff,
-                        const uint32_t* len, uint32_t n, hipStream_t st) {
+hipError_t launch_patch(const uint8_t* src, const uint64_t* dst, const uint32_t* soff, const uint32_t* len, uint32_t n,
+                        hipStream_t st) {
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL(k_patch, dim3((n + 255) / 256), dim3(256), 0, st, dst, src, doff, soff, len, n);
+  hipLaunchKernelGGL(k_patch, dim3((n + 255) / 256), dim3(256), 0, st, src, dst, soff, len, n);
   return hipGetLastError();
 }
 

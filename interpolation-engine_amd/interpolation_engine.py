@@ -266,13 +266,19 @@ class InsertsTableSet:
         the reference's miss. IE_E_INTERP with unreadable files in the directory: the reference
         raises that file's error when its key is looked up. Returns a result or an exception."""
         keys = _literal_keys(s)
-        if st == N.E_INTERP:
-            for k in keys:
-                e = _dir_bad.get(os.path.join(inserts_dir, k))
-                if e is not None:
-                    return e
-            return _exception(s, st, self.table_keys(t))
         base = self.dicts[t]
+        if st == N.E_INTERP:
+            # the reference looks keys up innermost-rightmost first (py:520, rfind): the first
+            # literal key, in that order, that neither the dict nor the snapshot holds is the
+            # lookup that failed; a file the snapshot could not read raises its own error there
+            snap = _dir_snap.get(inserts_dir)
+            have = snap[2] if snap else {}
+            for k in reversed(keys):
+                if k in base or k in have:
+                    continue
+                e = _dir_bad.get(os.path.join(inserts_dir, k))
+                return e if e is not None else _exception(s, st, self.table_keys(t))
+            return _exception(s, st, self.table_keys(t))
         extras, missing = {}, set()
         for _ in range(8):
             found = keys + [k for v in extras.values() if isinstance(v, str) for k in _literal_keys(v)]
@@ -318,6 +324,23 @@ class InsertsTable(InsertsTableSet):
         self._snapshot = (dict(inserts), {k: render(v, dialect)[1] for k, v in inserts.items()
                                           if isinstance(v, (list, dict))})
         self._version = getattr(inserts, "version", None)
+
+    def refresh(self, inserts):
+        """Bring this snapshot up to date with `inserts` in place (ie_table_set_update) when only a
+        few keys changed: False when a rebuild is the better (or the only) way."""
+        if self.dicts[0] is not inserts:  # (a merged inserts-directory snapshot, or another dict)
+            return False
+        snap, mutable = self._snapshot
+        changes = [(0, k, v) for k, v in inserts.items()
+                   if k not in snap or snap[k] is not v
+                   or (k in mutable and render(v, self.dialect)[1] != mutable[k])]
+        changes += [(0, k, DELETE) for k in snap if k not in inserts]
+        if len(changes) > max(64, len(inserts) // 4) or not self.update(changes):
+            return False
+        self._snapshot = (dict(inserts), {k: render(v, self.dialect)[1] for k, v in inserts.items()
+                                          if isinstance(v, (list, dict))})
+        self._version = getattr(inserts, "version", None)
+        return True
 
     def matches(self, inserts):
         """Is this still a snapshot of `inserts`? O(1) for a VersionedInserts, else O(len)."""
@@ -385,8 +408,7 @@ class VersionedInserts(dict):
 
 _CACHE_SIZE = 8
 _cache = {}  # (id(inserts), dialect, device) -> (inserts, InsertsTable), least recently used first
-_DIR_TTL = 1.0  # seconds a directory snapshot is reused before the directory is read again
-_dir_snap = {}  # path -> (time read, version, {key: value})
+_dir_snap = {}  # path -> (stat signature, version, {key: value})
 _dir_bad = {}   # file path -> the error reading it raised (left out of the snapshot)
 
 
@@ -438,6 +460,7 @@ def read_inserts_dir(path):
         del _dir_bad[p]  # (read again below: a file fixed since reads fine now)
     plain, j5 = {}, {}
     seen = set()
+    subdirs = []
     for root, dirs, files in os.walk(path, followlinks=True):  # open() follows links too
         real = os.path.realpath(root)
         if real in seen:  # a link cycle
@@ -450,6 +473,17 @@ def read_inserts_dir(path):
             plain[rel] = os.path.join(root, f)
             if rel.endswith(".json5"):
                 j5[rel[:-len(".json5")]] = os.path.join(root, f)
+        for d in dirs:
+            subdirs.append(d if rel_root == "." else "/".join(rel_root.split(os.sep) + [d]))
+    # a key naming a subdirectory (and no `<key>.json5` file): py:457 opens the directory, which
+    # raises IsADirectoryError when that key is looked up
+    for rel in subdirs:
+        if rel in j5 or rel in plain:
+            continue
+        try:
+            open(os.path.join(path, rel)).close()
+        except OSError as e:
+            _dir_bad[os.path.join(path, rel)] = e
     raw = {}
     for key in sorted(set(plain) | set(j5)):
         if key in ("", "HH:MM", "HH:MM:SS") or _is_arg_key(key):
@@ -471,22 +505,47 @@ def read_inserts_dir(path):
 
 def inserts_dir_snapshot(path):
     """(version, {key: recursive_escape(value)}) for read_inserts_dir(path), the escape on the
-    device; re-read at most every _DIR_TTL seconds (the reference reads at every lookup)."""
-    now = time.monotonic()
+    device. The reference reads the files at every lookup; here the directory is re-read when its
+    stat signature (every entry's path, type, size and modification time) changed since the last
+    call, which sees every write that changes a file's mtime or size."""
+    sig = _dir_signature(path)
     hit = _dir_snap.get(path)
-    if hit is not None and now - hit[0] < _DIR_TTL:
+    if hit is not None and hit[0] == sig:
         return hit[1], hit[2]
     raw = read_inserts_dir(path)
     keys = list(raw)
     snap = dict(zip(keys, recursive_escape([raw[k] for k in keys]))) if keys else {}
     version = 0 if hit is None else hit[1] + (hit[2] != snap)
-    _dir_snap[path] = (now, version, snap)
+    _dir_snap[path] = (sig, version, snap)
     return version, snap
 
 
+def _dir_signature(path):
+    """(relative path, is a directory, size, mtime_ns) of every entry under path (links followed,
+    as open() does), sorted."""
+    out, seen = [], set()
+    for root, dirs, files in os.walk(path, followlinks=True):
+        real = os.path.realpath(root)
+        if real in seen:
+            dirs[:] = []
+            continue
+        seen.add(real)
+        for name in dirs + files:
+            p = os.path.join(root, name)
+            try:
+                st = os.stat(p)
+            except OSError:
+                out.append((p, None))
+                continue
+            out.append((p, name in dirs, st.st_size, st.st_mtime_ns))
+    out.sort(key=lambda x: x[0])
+    return tuple(out)
+
+
 def table_for(inserts, dialect="py", device=0):
-    """The device table for this dict: rebuilt only when the dict changed; a new clock second
-    rewrites the two clock entries in place (ie_table_set_clock). At most _CACHE_SIZE tables stay
+    """The device table for this dict: updated in place when a few keys changed
+    (ie_table_set_update), rebuilt when many did; a new clock second rewrites the two clock entries
+    in place (ie_table_set_clock). At most _CACHE_SIZE tables stay
     alive (the dict is held with its table, so its id cannot be reused while cached). With
     `inserts_dir` set the table also holds the directory's snapshot, after the inserts."""
     now = _dt.datetime.now()
@@ -498,7 +557,7 @@ def table_for(inserts, dialect="py", device=0):
     key = (id(inserts), dialect, device)
     hit = _cache.pop(key, None)
     t = hit[1] if hit is not None and hit[0] is inserts else None
-    if t is not None and (t.dir_key != dir_key or not t.matches(inserts)):
+    if t is not None and (t.dir_key != dir_key or (not t.matches(inserts) and not (dir_key is None and t.refresh(inserts)))):
         t.close()
         t = None
     if t is not None and t.clock != clock and not t.set_clock(clock):

@@ -62,7 +62,8 @@ OUTSIDE_FILES = {"outside": "an outside {name} file", "outside_j.json5": "'outsi
 BAD_FILES = {"binary": "fffe00206e6f74207574662d38", "broken.json5": "7b756e7465726d696e617465643a20"}  # hex
 OUTSIDE_CASES = ["{../outside}", "a{../outside}b", "{../outside_j}", "{../nope}", "x{../nope}y", "{sub/../count}",
                  "{./over}", "{sub//leaf}", "{../dir2/leaf}", "{../dir/plain}", "{binary}", "x{binary}y", "{broken}",
-                 "{q-{../nope}}"]
+                 "{q-{../nope}}", "{sub}", "x{sub}y", "{binary}{missing}", "{missing}{binary}", "{binary}{sub}",
+                 "{sub}{count}"]
 
 
 def classify(ie, inserts, s, other_errors=False):

@@ -138,3 +138,36 @@ def test_bad_file_stays_out_of_the_snapshot(tmp_path):
     assert "binary" not in raw and "broken" not in raw
     assert raw["count"] == 42
     assert os.path.join(d, "binary") in M._dir_bad and os.path.join(d, "broken") in M._dir_bad
+
+
+@pytest.mark.gpu
+def test_directory_changes_are_seen_at_the_next_call(tmp_path):
+    """The reference opens the file at every lookup (py:452-461): a file written, rewritten (same
+    size too), added or removed between two calls is what the next call sees."""
+    pkg = G.load_package()
+    from interpolation_engine_amd import interpolation_engine as M
+    d = str(tmp_path)
+    p = os.path.join(d, "v")
+    old = M.inserts_dir
+    M.inserts_dir = d
+    try:
+        with open(p, "w") as f:
+            f.write("one")
+        ins = {"name": "Tom"}
+        assert pkg.interpolate_inserts(ins, "<{v}>") == "<one>"
+        st = os.stat(p)
+        with open(p, "w") as f:
+            f.write("two")  # same size: the modification time tells
+        os.utime(p, ns=(st.st_atime_ns, st.st_mtime_ns + 1_000_000_000))
+        assert pkg.interpolate_inserts(ins, "<{v}>") == "<two>"
+        with open(os.path.join(d, "w.json5"), "w") as f:
+            f.write("'added'")
+        assert pkg.interpolate_inserts(ins, "{w}|{v}") == "added|two"
+        os.remove(p)
+        with pytest.raises(pkg.InterpolationException):
+            pkg.interpolate_inserts(ins, "<{v}>")
+        os.makedirs(os.path.join(d, "v"))
+        with pytest.raises(IsADirectoryError):
+            pkg.interpolate_inserts(ins, "<{v}>")
+    finally:
+        M.inserts_dir = old
