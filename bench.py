@@ -263,7 +263,7 @@ class States:
         self.ids = np.asarray(ids, dtype=np.uint32)
         self.n = len(strings)
         t0 = time.perf_counter()
-        self.tset = pkg.InsertsTableSet(self.states, clock=CLOCK, device=dev)
+        self.tset = pkg.InsertsTableSet(self.states, clock=CLOCK, device=dev, mutable=False)
         self.build_s = time.perf_counter() - t0
         self.table = self.tset.h
         blob, offs = N.pack(strings)

@@ -115,6 +115,7 @@ typedef struct ie_clock {
 } ie_clock;
 
 #define IE_TABLE_HAS_INSERTS_DIR 1u /* missing keys report IE_NEEDS_HOST instead of IE_E_INTERP */
+#define IE_TABLE_MUTABLE 2u         /* room for ie_table_set_update's new keys (entries at load 0.5, not 0.8) */
 
 typedef struct ie_table ie_table; /* immutable after build; read-only on device; thread-safe */
 typedef struct ie_exec ie_exec;   /* one per host thread: device, stream, workspace           */
@@ -191,7 +192,8 @@ int ie_table_set_clock(ie_table* t, const ie_clock* now);
  * pilot group. Synchronous (waits for the device first, like ie_table_set_clock). A brace-bearing
  * value is not pre-resolved, and the pre-resolved values of every changed table return to their raw
  * text (both then resolve through the exact evaluator, in the reference's order). IE_ERR_CAPACITY:
- * some new key found no placement (those keys were not applied; rebuild the table). */
+ * a new key found no placement (the entries before it were applied, it and the rest were not:
+ * rebuild the table; a table built with IE_TABLE_MUTABLE keeps room for new keys). */
 int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, const uint32_t* vid, uint64_t n);
 uint64_t ie_table_entries(const ie_table* t);
 uint32_t ie_table_tables(const ie_table* t);

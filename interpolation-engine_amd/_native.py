@@ -18,6 +18,7 @@ STATUS_NAMES = ["OK_STR", "OK_VALUE", "E_INTERP", "E_ASSERT_BRACES", "E_ASSERT_T
                 "E_UNHASHABLE", "E_RS_PANIC", "NEEDS_HOST", "DIVERGED", "E_OVERFLOW", "RECURSE"]
 VID_NONE, VID_HHMM, VID_HHMMSS = 0xFFFFFFFF, 0xFFFFFFFE, 0xFFFFFFFD
 TABLE_HAS_INSERTS_DIR = 1
+TABLE_MUTABLE = 2
 OPT_FAIL_COMMIT, OPT_FAST, OPT_DEBUG_NOEVAL, OPT_TILE, OPT_VIEWS, OPT_DEFER, OPT_RESERVE = 1, 2, 3, 4, 5, 7, 8
 
 # every symbol include/ie_amd.h declares (tests check the .so exports exactly these)

@@ -821,7 +821,8 @@ int upload_table(const std::vector<Ent>& ents, uint32_t n_tables, int32_t dialec
   // (two keys with one 64-bit hash can never be separated) and then grows the table.
   const uint64_t nk = items.size();
   const uint32_t nb = (uint32_t)std::max<uint64_t>(1, (nk + 3) / 4);
-  uint64_t m = std::max<uint64_t>(16, nk + nk / 4 + 1);
+  // (IE_TABLE_MUTABLE: load 0.5, so that a pilot group can be placed again around new keys)
+  uint64_t m = std::max<uint64_t>(16, (flags & IE_TABLE_MUTABLE) ? 2 * nk + 16 : nk + nk / 4 + 1);
   uint64_t seed = 0xA0761D6478BD642Full;
   std::vector<uint16_t> pilots;
   std::vector<uint32_t> slot_of;
@@ -1206,7 +1207,8 @@ int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
       }
       if (!found) {
         status = fail(IE_ERR_CAPACITY, "no free placement for a new key's pilot group: rebuild the table");
-        continue;
+        n = i;  // apply (upload) what came before, stop here
+        break;
       }
       std::vector<Entry> moved;
       for (uint32_t s2 : gs) moved.push_back(t->h_entries[s2]);

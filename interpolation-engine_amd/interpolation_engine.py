@@ -98,7 +98,7 @@ class InsertsTableSet:
     include/ie_amd.h ie_table_set_build): every string names the dict it resolves against.
     This is the batch form of get_interpdata for many forked interpreter states (config 5)."""
 
-    def __init__(self, dicts, dialect="py", clock=None, device=0, has_inserts_dir=False):
+    def __init__(self, dicts, dialect="py", clock=None, device=0, has_inserts_dir=False, mutable=True):
         self.clock_pinned = clock is not None  # else the wall clock at build (set_clock re-reads it)
         if clock is None:
             now = _dt.datetime.now()
@@ -146,7 +146,8 @@ class InsertsTableSet:
         st = (ctypes.c_uint64 * len(starts))(*starts)
         N.check(N.lib().ie_table_set_build(ctypes.c_void_p(arr.ctypes.data), st, len(self.dicts),
                                            N.IE_DIALECT[dialect], ctypes.byref(clk),
-                                           N.TABLE_HAS_INSERTS_DIR if has_inserts_dir else 0, device,
+                                           (N.TABLE_HAS_INSERTS_DIR if has_inserts_dir else 0) |
+                                           (N.TABLE_MUTABLE if mutable else 0), device,
                                            ctypes.byref(h)), "ie_table_set_build")
         self.h = h
 
