@@ -152,6 +152,9 @@ def parse(argv=None):
     ap.add_argument("--reserve", type=int, default=32,
                     help="views output: IE_OPT_RESERVE (F x16: tile t writes at F x its input offset, no claim "
                          "atomic; 0 = one claim per tile on one cursor)")
+    ap.add_argument("--replay", type=int, default=3,
+                    help="config 5: loop iterations replayed after the timed steps, each mutating every state "
+                         "(ie_table_set_update) and resolving the batch again (0: none)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="",
                     help="weak: --n units per GPU; strong: --n units over all GPUs (default per config: DEFAULT_SCALING)")
     ap.add_argument("--dry-run", action="store_true",
@@ -461,6 +464,11 @@ def main(argv=None):
                      d_olen2 if cmd else d_olen, d_tot2 if cmd else d_tot)
         cpu = cpu_baseline(args, W, N, res)
 
+    replay = None
+    if rank == 0 and cfg == 5 and args.replay > 0:
+        res = Result(N, n, d_out, d_ooff, d_st, d_olen, d_tot)
+        replay = replay_states(args, W, x, resolve, res)
+
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic_cfg%d.json" % cfg)
     if os.path.exists(pmc_path):
@@ -510,6 +518,7 @@ def main(argv=None):
         }
         if cfg == 5:
             line["config"]["states_per_gpu"] = n_units
+            line["replay"] = replay
         if cmd:
             ob2 = int(d_tot2.to_numpy(np.uint64, 1)[0])
             ums = float(np.mean(cmd_ms))
@@ -548,7 +557,9 @@ class Result:
         if not np.array_equal(gst, st) or not np.array_equal(lens[gst == 0], ln[gst == 0]):
             return False
         total = int(self.d_tot.to_numpy(np.uint64, 1)[0])
-        blob = self.d_out.to_numpy(np.uint8, total)
+        # (views: the results' extent; reserved ranges leave gaps, *total is the sum of lengths)
+        ext = int((starts + lens).max()) if m else 0
+        blob = self.d_out.to_numpy(np.uint8, max(total, ext))
         return bool(np.array_equal(O.hash_spans(blob, starts, lens, gst, threads), hs))
 
 
@@ -584,6 +595,55 @@ def cpu_baseline(args, W, N, res):
                       "single-thread on the first %d (%.2f s)%s; GPU results identical on all %d: %s"
                       % (m, int(offs[m]), threads, wall, m1, wall1,
                          "; each OK result then through the unescape command" if cmd else "", m, same)}
+
+
+def replay_states(args, W, x, resolve, res):
+    """Config 5 as the loop runs it (not a frozen snapshot): between two iterations every state
+    takes the stores an iteration makes (set_interpdata, py:470-471; user_input py:1566-1568; the
+    model's output and the history replace_maps py:1770-1773): new_user_input, maybe_input, output,
+    the appended history_text_llm and length_history. The stores go to the device table set in place
+    (ie_table_set_update, no rebuild), then the iteration's strings are resolved again. Per
+    iteration: the host's store time (packing + the library call), the library call alone, and the
+    resolve; after the last iteration every string is compared with the oracle on the mutated
+    states."""
+    from interpolation_engine_amd import workloads as Wk
+    from oracle import oracle as O
+    upd, nat, rsv, nch = [], [], [], 0
+    for it in range(args.replay):
+        changes = []
+        for j, ins in enumerate(W.states):
+            r = Wk._Rng(0xC0FFEE ^ (j * 0x9E3779B1) ^ (it << 40))
+            inp, out = r.words(2, 8), r.words(15, 55)
+            hist = ins["history_text_llm"] + "\n\n<action>" + inp + "</action>\n\n<action-output>" + out + "</action-output>"
+            for k, v in (("new_user_input", inp), ("maybe_input", inp), ("output", out), ("history_text_llm", hist),
+                         ("length_history", ins["length_history"] + 2)):
+                ins[k] = v
+                changes.append((j, k, v))
+        nch = len(changes)
+        t0 = time.perf_counter()
+        if not W.tset.update(changes):
+            raise RuntimeError("replay: a new key found no placement")
+        t1 = time.perf_counter()
+        x.sync()
+        t2 = time.perf_counter()
+        resolve()
+        x.sync()
+        t3 = time.perf_counter()
+        upd.append(t1 - t0)
+        nat.append(W.tset.last_update_native_s)
+        rsv.append(t3 - t2)
+    threads, _ = cpu_share()
+    oracles = [O.Oracle(ins, "py", clock=CLOCK) for ins in W.states]
+    buf = np.frombuffer(W.blob + bytes(1), np.uint8)
+    st, ln, hs = np.zeros(W.n, np.uint8), np.zeros(W.n, np.uint64), np.zeros(W.n, np.uint64)
+    O.run_batch_sets(oracles, W.ids, buf, W.offs, threads, st, ln, hs)
+    same = res.compare(W.n, st, ln, hs, threads)
+    return {"iterations": args.replay, "stores_per_iteration": nch,
+            "store_ms": [round(1e3 * v, 3) for v in upd], "store_library_ms": [round(1e3 * v, 3) for v in nat],
+            "resolve_ms": [round(1e3 * v, 3) for v in rsv],
+            "identical_to_oracle_after_replay": same,
+            "note": "store_ms = InsertsTableSet.update (Python packing + ie_table_set_update); resolve_ms = wall "
+                    "time of one batch (launch + sync)"}
 
 
 def cpu_baseline_states(args, W, N, res, model, budget, threads):

@@ -212,7 +212,9 @@ class InsertsTableSet:
         arr["text"] = tblob.ctypes.data + np.concatenate(([0], np.cumsum(tlen)[:-1])).astype(np.uint64)
         arr["text_len"] = tlen
         arr["kind"] = kinds
+        t0 = time.perf_counter()
         rc = N.lib().ie_table_set_update(self.h, ctypes.c_void_p(arr.ctypes.data), tids.ctypes.data, vids.ctypes.data, n)
+        self.last_update_native_s = time.perf_counter() - t0
         if rc == N.ERR_CAPACITY:
             return False
         N.check(rc, "ie_table_set_update")

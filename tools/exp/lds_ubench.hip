@@ -7,6 +7,7 @@
 //   mode 3: 1 ds_read_b128 unaligned source, 1 ds_write_b128 aligned dst
 //   mode 4: integer mix: v_mul_lo_u32 chain (hash_word-like), 8 per iteration
 //   mode 5: the same work with v_mul_u32_u24
+//   modes 6 / 7 / 8: throughput of 32 independent v_mul_lo_u32 / v_mul_u32_u24 / (xor + add) per iteration
 // Prints cycles per iteration per wave (median over workgroups) and checks the copies.
 // Build: hipcc --offload-arch=gfx950 -O3 tools/exp/lds_ubench.hip -o tools/exp/lds_ubench
 #include <hip/hip_runtime.h>
@@ -24,6 +25,12 @@ typedef u32x4 __attribute__((aligned(1))) u32x4_ua;
 typedef __attribute__((address_space(3))) u32x4_ua lds_v4u;
 
 constexpr int kIters = 256;
+
+__device__ __forceinline__ uint32_t mul24_asm(uint32_t x) {
+  uint32_t r;
+  asm volatile("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "v"(x), "v"(0x9E3779u));
+  return r;
+}
 
 template <int MODE>
 __global__ __launch_bounds__(256) void k_bench(uint64_t* cyc, uint32_t* sink) {
@@ -68,9 +75,34 @@ __global__ __launch_bounds__(256) void k_bench(uint64_t* cyc, uint32_t* sink) {
     } else if (MODE == 4) {
 #pragma unroll
       for (int k = 0; k < 8; k++) acc = (acc ^ (uint32_t)k) * 0x9E3779B1u;
-    } else {
+    } else if (MODE == 5) {
 #pragma unroll
       for (int k = 0; k < 8; k++) acc = ((acc ^ (uint32_t)k) & 0xFFFFFFu) * 0x9E3779u + (acc >> 24);
+    } else if (MODE == 6 || MODE == 7) {
+      // throughput: 8 independent chains of 4 multiplies (v_mul_lo_u32 / v_mul_u32_u24)
+      uint32_t a[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) a[k] = acc + (uint32_t)k;
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          if (MODE == 6) a[k] = a[k] * 0x9E3779B1u;
+          else a[k] = mul24_asm(a[k]);
+        }
+#pragma unroll
+      for (int k = 0; k < 8; k++) acc ^= a[k];
+    } else {
+      // throughput: 8 independent chains of 4 xor-add pairs (full-rate reference)
+      uint32_t a[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) a[k] = acc + (uint32_t)k;
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int k = 0; k < 8; k++) a[k] = (a[k] ^ 0x9E3779B1u) + 0x7F4A7C15u;
+#pragma unroll
+      for (int k = 0; k < 8; k++) acc ^= a[k];
     }
     so = (so + 13u) & 8191u;
     dof = 8192u + ((dof + 7u) & 4095u);
@@ -116,5 +148,8 @@ int main() {
   run<3>(blocks);
   run<4>(blocks);
   run<5>(blocks);
+  run<6>(blocks);
+  run<7>(blocks);
+  run<8>(blocks);
   return 0;
 }
