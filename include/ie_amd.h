@@ -233,6 +233,12 @@ int ie_exec_set_option(ie_exec* x, int32_t option, int64_t value);
 /* Literal-path scratch pool size. Setting it makes ie_interpolate_device fully asynchronous: it no
  * longer waits to check the pool's demand, and strings that ran out of it report IE_E_OVERFLOW. */
 int ie_exec_set_scratch(ie_exec* x, uint64_t bytes);
+/* Keys only the host can look up (get_interpdata's file fallback for a key that is not a canonical
+ * relative file name under the inserts directory, py:452-461): for every string of the exec's last
+ * interpolation call that reported IE_NEEDS_HOST, the key its failing lookup used (also one built
+ * from looked-up values), as records {uint32 string index, uint32 key length, key bytes padded to
+ * 4}. Copies min(cap, *used) bytes of records to buf; *used = the records' size. Synchronous. */
+int ie_exec_host_keys(ie_exec* x, uint8_t* buf, uint64_t cap, uint64_t* used);
 
 /* Diagnostic (no reference counterpart): one key through the device lookups next to the host's
  * view of the same table; out[12] as documented in ie_host.cpp. */

@@ -27,7 +27,7 @@ EXPORTS = [
     "ie_table_build", "ie_table_set_build", "ie_table_set_clock", "ie_table_set_update", "ie_table_free", "ie_table_entries", "ie_table_tables",
     "ie_table_dialect",
     "ie_exec_create", "ie_exec_destroy", "ie_exec_sync", "ie_exec_set_timing", "ie_exec_timing",
-    "ie_exec_set_scratch", "ie_exec_set_option",
+    "ie_exec_set_scratch", "ie_exec_set_option", "ie_exec_host_keys",
     "ie_dev_alloc", "ie_dev_free", "ie_copy_h2d", "ie_copy_d2h", "ie_memset_d", "ie_exec_mark",
     "ie_exec_elapsed",
     "ie_interpolate_device", "ie_interpolate_batch", "ie_interpolate", "ie_interpolate_device_ids",
@@ -106,6 +106,7 @@ def signatures():
         "ie_exec_timing": (ctypes.c_int, [vp, ctypes.POINTER(Timing)]),
         "ie_exec_set_scratch": (ctypes.c_int, [vp, u64]),
         "ie_exec_set_option": (ctypes.c_int, [vp, i32, ctypes.c_int64]),
+        "ie_exec_host_keys": (ctypes.c_int, [vp, vp, u64, ctypes.POINTER(u64)]),
         "ie_dev_alloc": (ctypes.c_int, [i32, u64, pvp]),
         "ie_dev_free": (None, [vp]),
         "ie_copy_h2d": (ctypes.c_int, [vp, vp, vp, u64]),
@@ -185,6 +186,23 @@ class Exec:
         check(lib().ie_exec_create(device, stream, ctypes.byref(h)), "ie_exec_create")
         self.h = h
         self.device = device
+
+    def host_keys(self):
+        """{string index: [key, ...]}: the keys the last interpolation call could not look up on
+        the device (IE_NEEDS_HOST), ie_exec_host_keys."""
+        used = ctypes.c_uint64()
+        check(lib().ie_exec_host_keys(self.h, None, 0, ctypes.byref(used)), "ie_exec_host_keys")
+        if not used.value:
+            return {}
+        buf = ctypes.create_string_buffer(used.value)
+        check(lib().ie_exec_host_keys(self.h, buf, used.value, ctypes.byref(used)), "ie_exec_host_keys")
+        raw, out, k = buf.raw, {}, 0
+        while k + 8 <= len(raw):
+            idx = int.from_bytes(raw[k:k + 4], "little")
+            n = int.from_bytes(raw[k + 4:k + 8], "little")
+            out.setdefault(idx, []).append(dec(raw[k + 8:k + 8 + n]))
+            k += 8 + ((n + 3) & ~3)
+        return out
 
     def close(self):
         if getattr(self, "h", None):

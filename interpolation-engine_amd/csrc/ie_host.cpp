@@ -134,6 +134,11 @@ struct ie_exec {
   hipEvent_t stat_ev = nullptr;
   // workspace
   DevBuf counters, pool, out_len, tile_sum, tile_base, defer_tiles, defer_desc;
+  // keys only the host can look up (IE_NEEDS_HOST): [u64 bytes used | pad][records] (ie_exec_host_keys);
+  // a host batch call keeps its records (all its device passes, indices of its own batch) in hk
+  DevBuf host_keys;
+  std::vector<uint8_t> hk;
+  bool hk_host = false;
   // the fused unescape command's deferred pass: list, views into the pool, table ids
   DevBuf u_list, u_off, u_len, u_tid;
   // host-API staging
@@ -149,7 +154,7 @@ struct ie_exec {
   ~ie_exec() {
     sm_dev.release();
     if (sm_host) (void)hipHostFree(sm_host);
-    for (DevBuf* b : {&u_list, &u_off, &u_len, &u_tid}) b->release();
+    for (DevBuf* b : {&u_list, &u_off, &u_len, &u_tid, &host_keys}) b->release();
     for (DevBuf* b : {&counters, &pool, &out_len, &tile_sum, &tile_base, &defer_tiles, &defer_desc, &in_bytes,
                       &in_off, &in_tid, &o_bytes, &o_off, &o_len, &o_status, &o_vid, &o_total, &wc_range, &wc_match, &wc_ncap, &wc_caps,
                       &s_lens, &s_part, &stamps})
@@ -339,6 +344,35 @@ Work make_work(ie_exec* x, uint64_t* total) {
 }
 
 // d_out_len / d_in_len (k_resolve only): views output / views input (ie_interpolate_device_views)
+// a device pass starts a new host-key list
+int reset_host_keys(ie_exec* x) {
+  if (x->host_keys.p) IE_HIP(hipMemsetAsync(x->host_keys.p, 0, 16, x->stream));
+  return IE_SUCCESS;
+}
+
+// the device's host-key records of the last pass (synchronises)
+int read_host_keys(ie_exec* x, std::vector<uint8_t>& out) {
+  out.clear();
+  if (!x->host_keys.p) return IE_SUCCESS;
+  uint64_t used = 0;
+  IE_HIP(hipMemcpyAsync(&used, x->host_keys.p, 8, hipMemcpyDeviceToHost, x->stream));
+  IE_HIP(hipStreamSynchronize(x->stream));
+  used = std::min<uint64_t>(used, x->host_keys.bytes - 16);  // (records past the list's end were dropped)
+  out.resize(used);
+  if (used) IE_HIP(hipMemcpy(out.data(), (uint8_t*)x->host_keys.p + 16, used, hipMemcpyDeviceToHost));
+  // keep whole records only
+  uint64_t k = 0;
+  while (k + 8 <= out.size()) {
+    uint32_t len;
+    memcpy(&len, out.data() + k + 4, 4);
+    const uint64_t next = k + 8 + ((len + 3ull) & ~3ull);
+    if (next > out.size()) break;
+    k = next;
+  }
+  out.resize(k);
+  return IE_SUCCESS;
+}
+
 // reserve_ok: the caller is ie_interpolate_device_views (the only entry whose caller sized the output
 // for IE_OPT_RESERVE; the host batch APIs read back *total bytes and keep one claim per tile)
 int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, const uint64_t* d_off,
@@ -365,6 +399,15 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
   if (n && d_out_len == nullptr && out->offsets == nullptr) return fail(IE_ERR_INVALID, "null offsets");
   Batch B{d_bytes, d_off, n, out->offsets, out->status, out->value_id, d_tid, d_in_len, d_out_len};
   Work W = make_work(x, out->total);
+  if (op == kOpInterp && (t->dev.flags & TF_HAS_DIR)) {  // the literal path records IE_NEEDS_HOST keys
+    if (!x->host_keys.p) {
+      IE_HIP(x->host_keys.ensure(1ull << 20));
+      IE_HIP(hipMemsetAsync(x->host_keys.p, 0, 16, x->stream));
+    }
+    W.host_keys = (uint8_t*)x->host_keys.p + 16;
+    W.host_keys_used = (uint64_t*)x->host_keys.p;
+    W.host_keys_cap = x->host_keys.bytes - 16;
+  }
   W.recurse = op == kOpInterp && x->in_cmd && t->dialect == IE_DIALECT_PY ? 1u : 0u;
   // reserved output ranges: a views output of a packed interpolation batch (not the unescape command)
   W.reserve16 = reserve_ok && op == kOpInterp && d_out_len && !d_in_len && !x->in_cmd && !x->cmd_fused ? x->opt_reserve : 0u;
@@ -522,6 +565,9 @@ int run_host(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, const 
   if (!x || !outp || (n && (!bytes || !offsets))) return fail(IE_ERR_INVALID, "null argument");
   int rc = set_device(x->device);
   if (rc) return rc;
+  if ((rc = reset_host_keys(x))) return rc;
+  x->hk_host = true;
+  x->hk.clear();
   if (table_id && t)
     for (uint64_t i = 0; i < n; i++)
       if (table_id[i] >= t->n_tables) return fail(IE_ERR_INVALID, "table id beyond the table set");
@@ -622,6 +668,11 @@ int run_host(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, const 
   }
   for (uint64_t i = 0; i < n; i++)
     if (b->status[i] != IE_OK_VALUE && b->status[i] != IE_RECURSE) b->value_id[i] = IE_VID_NONE;
+  std::vector<uint8_t> recs;  // this batch's host-key records (the device pass above)
+  if (op == kOpInterp && t && (t->dev.flags & TF_HAS_DIR) && (rc = read_host_keys(x, recs))) {
+    ie_batch_free(b);
+    return rc;
+  }
 
   // literal-path strings that ran out of scratch: re-run them alone with the full working space
   if (op == kOpInterp) {
@@ -651,6 +702,17 @@ int run_host(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, const 
         ie_batch_free(b);
         return rc;
       }
+      for (uint64_t k = 0; k + 8 <= x->hk.size();) {  // the re-run's records, at their batch indices
+        uint32_t idx, len;
+        memcpy(&idx, x->hk.data() + k, 4);
+        memcpy(&len, x->hk.data() + k + 4, 4);
+        const uint64_t rl = 8 + ((len + 3ull) & ~3ull);
+        const uint32_t at = idx < redo.size() ? (uint32_t)redo[idx] : idx;
+        const size_t o = recs.size();
+        recs.insert(recs.end(), x->hk.data() + k, x->hk.data() + k + rl);
+        memcpy(recs.data() + o, &at, 4);
+        k += rl;
+      }
       // splice the re-run results back in
       std::vector<uint8_t> nb;
       std::vector<uint64_t> noff(n + 1, 0);
@@ -676,6 +738,8 @@ int run_host(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, const 
       memcpy(b->offsets, noff.data(), (n + 1) * 8);
     }
   }
+  x->hk.swap(recs);
+  x->hk_host = true;
   *outp = b;
   return IE_SUCCESS;
 }
@@ -1294,6 +1358,21 @@ int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
   return status;
 }
 
+int ie_exec_host_keys(ie_exec* x, uint8_t* buf, uint64_t cap, uint64_t* used) {
+  if (!x || !used || (cap && !buf)) return fail(IE_ERR_INVALID, "null argument");
+  int rc = set_device(x->device);
+  if (rc) return rc;
+  std::vector<uint8_t> dev;
+  const std::vector<uint8_t>* src = &x->hk;
+  if (!x->hk_host) {
+    if ((rc = read_host_keys(x, dev))) return rc;
+    src = &dev;
+  }
+  *used = src->size();
+  if (!src->empty() && cap) memcpy(buf, src->data(), std::min<uint64_t>(cap, src->size()));
+  return IE_SUCCESS;
+}
+
 uint64_t ie_table_entries(const ie_table* t) { return t ? t->n_entries : 0; }
 uint32_t ie_table_tables(const ie_table* t) { return t ? t->n_tables : 0; }
 int32_t ie_table_dialect(const ie_table* t) { return t ? t->dialect : -1; }
@@ -1515,7 +1594,10 @@ int ie_exec_elapsed(ie_exec* x, uint32_t a, uint32_t b, float* ms) {
 
 int ie_interpolate_device_ids(ie_exec* x, const ie_table* t, const uint32_t* d_table_id, const uint8_t* d_bytes,
                               const uint64_t* d_offsets, uint64_t n, const ie_dev_out* out) {
-  int rc = run_device(x, kOpInterp, t, d_bytes, d_offsets, n, out, d_table_id);
+  if (!x) return fail(IE_ERR_INVALID, "null exec");
+  x->hk_host = false;
+  int rc = reset_host_keys(x);
+  if (!rc) rc = run_device(x, kOpInterp, t, d_bytes, d_offsets, n, out, d_table_id);
   if (rc || !n || x->pool_fixed) return rc;
   // The literal path reserves scratch with one atomic per string, so the counter ends at the
   // batch's whole demand even when the pool ran out. A demand above the pool means some strings
@@ -1527,6 +1609,7 @@ int ie_interpolate_device_ids(ie_exec* x, const ie_table* t, const uint32_t* d_t
   IE_HIP(hipStreamSynchronize(x->stream));
   if (used <= x->pool.bytes) return IE_SUCCESS;
   x->pool_request = std::max<uint64_t>(x->pool_request, used + used / 8 + (1ull << 20));
+  if ((rc = reset_host_keys(x))) return rc;
   return run_device(x, kOpInterp, t, d_bytes, d_offsets, n, out, d_table_id);
 }
 
@@ -1540,7 +1623,10 @@ int ie_interpolate_device_views(ie_exec* x, const ie_table* t, const uint32_t* d
                                 const ie_dev_views* out) {
   if (!out || (n && (!out->offsets || !out->lengths))) return fail(IE_ERR_INVALID, "null argument");
   const ie_dev_out o{out->bytes, out->bytes_cap, out->offsets, out->status, out->value_id, out->total};
-  int rc = run_device(x, kOpInterp, t, d_bytes, d_offsets, n, &o, d_table_id, out->lengths, d_lengths, true);
+  if (!x) return fail(IE_ERR_INVALID, "null exec");
+  x->hk_host = false;
+  int rc = reset_host_keys(x);
+  if (!rc) rc = run_device(x, kOpInterp, t, d_bytes, d_offsets, n, &o, d_table_id, out->lengths, d_lengths, true);
   if (rc || !n || x->pool_fixed) return rc;
   // the literal path's scratch demand, as ie_interpolate_device_ids
   uint64_t used = 0;
@@ -1548,6 +1634,7 @@ int ie_interpolate_device_views(ie_exec* x, const ie_table* t, const uint32_t* d
   IE_HIP(hipStreamSynchronize(x->stream));
   if (used <= x->pool.bytes) return IE_SUCCESS;
   x->pool_request = std::max<uint64_t>(x->pool_request, used + used / 8 + (1ull << 20));
+  if ((rc = reset_host_keys(x))) return rc;
   return run_device(x, kOpInterp, t, d_bytes, d_offsets, n, &o, d_table_id, out->lengths, d_lengths, true);
 }
 
@@ -1595,7 +1682,10 @@ int ie_unescape_cmd_device_views(ie_exec* x, const ie_table* t, const uint32_t* 
                                  const uint8_t* d_status_in, const ie_dev_views* out) {
   if (!x || !out || !out->status || (n && (!out->offsets || !out->lengths))) return fail(IE_ERR_INVALID, "null argument");
   const ie_dev_out o{out->bytes, out->bytes_cap, out->offsets, out->status, out->value_id, out->total};
+  x->hk_host = false;
   auto run = [&]() -> int {
+    const int r0 = reset_host_keys(x);
+    if (r0) return r0;
     x->in_cmd = true;
     x->cmd_fused = true;
     const int r = run_device(x, kOpInterp, t, d_bytes, d_offsets, n, &o, d_table_id, out->lengths, d_lengths);

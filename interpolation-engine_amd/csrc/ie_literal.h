@@ -216,7 +216,11 @@ __device__ LitOut w_literal(const DevTable T, uint32_t tid, const uint8_t* s, ui
     const uint64_t k2 = w_replace<kPatRestoreClose>(K, k1, K2, cap);
     Hit E;
     const int32_t e = find_bytes(T, tid, K2, (uint32_t)k2, E);                // py:529
-    if (e < 0) { r.status = missing_status(T, K2, (uint32_t)k2); return r; }
+    if (e < 0) {  // (IE_NEEDS_HOST: the key's bytes stay at res_off for the host, k_resolve records them)
+      r.status = missing_status(T, K2, (uint32_t)k2);
+      if (r.status == IE_NEEDS_HOST) r.res_off = pool_off + 3 * cap, r.res_len = k2;
+      return r;
+    }
     if (!(E.flags & EF_SPLICE_OK)) { r.status = IE_E_ASSERT_TYPE; return r; }  // py:530
     // py:531-535: prefix (protected already, never ends in '\') + protect(text | seam) + suffix
     uint8_t* dst = R[si ^ 1];
@@ -249,7 +253,11 @@ __device__ LitOut w_literal(const DevTable T, uint32_t tid, const uint8_t* s, ui
   uint8_t st = 0;
   Hit cur_hit;
   int32_t e = find_bytes(T, tid, K, (uint32_t)f2, cur_hit);
-  if (e < 0) { r.status = missing_status(T, K, (uint32_t)f2); return r; }
+  if (e < 0) {
+    r.status = missing_status(T, K, (uint32_t)f2);
+    if (r.status == IE_NEEDS_HOST) r.res_off = pool_off + 2 * cap, r.res_len = f2;
+    return r;
+  }
   for (uint32_t k = 1; k < W; k++) {
     Hit nh;
     e = find_raw(T, tid, cur_hit, st, nh);  // rs: every raw value has EF_KEY_STR (value_to_string)

@@ -53,6 +53,12 @@
 #define IE_JOBS_V2 0
 #endif
 
+// three workgroup barriers fewer per tile (the two scans' trailing barriers, the literal path's when
+// no string took it)
+#ifndef IE_FEWER_BARRIERS
+#define IE_FEWER_BARRIERS 0
+#endif
+
 namespace ie {
 // everything of one tile size lives in its own namespace: ie_resolve512.hip compiles this file
 // again with 512-string tiles (IE_RBLOCK=512, IE_RNS=r512, IE_RESOLVE_WIDE)
@@ -227,7 +233,8 @@ __device__ uint8_t eval_exact(const DevTable& T, uint32_t tid, const Src<STAGED>
     if (nopen == 0) return IE_OK_STR;
     if (nopen != nclose) return IE_E_ASSERT_BRACES;
     if (negclose) return kStatusPending;  // balanced but '}{': py break / rs panic
-    if (err_off >= 0) return err_cls;
+    // (a key only the host can look up, IE_NEEDS_HOST: the literal path reports it with the key)
+    if (err_off >= 0) return err_cls == IE_NEEDS_HOST ? kStatusPending : err_cls;
     if (wrapped) {
       vid = wrap_h.vid;
       vflags = wrap_h.flags;
@@ -742,6 +749,9 @@ __device__ uint64_t look_back(uint64_t* state, uint32_t tile, uint64_t agg, uint
 // ------------------------------------------------------------------------------------------
 // workgroup scan helper
 // ------------------------------------------------------------------------------------------
+// TRAIL: a second barrier so that lds_w can be written again at once; without it the caller
+// guarantees a barrier before the next write of lds_w
+template <bool TRAIL = true>
 __device__ uint64_t block_scan(uint64_t v, uint64_t* lds_w, uint64_t* total) {
   const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
   const uint64_t inc = wave_incl_scan(v);
@@ -754,7 +764,7 @@ __device__ uint64_t block_scan(uint64_t v, uint64_t* lds_w, uint64_t* total) {
     if (w < wid) base += x;
     tot += x;
   }
-  __syncthreads();
+  if (TRAIL) __syncthreads();
   *total = tot;
   return base + inc - v;
 }
@@ -1306,7 +1316,9 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
         ev[0] = Om.lo, ev[kRBlock] = Om.hi, ev[2 * kRBlock] = Cm.lo, ev[3 * kRBlock] = Cm.hi;
       }
       uint64_t njobs64;
-      const uint32_t jb = (uint32_t)block_scan(pok ? nch : 0u, s_red, &njobs64);  // barriers: masks read
+      // (its barrier: every wave has read the chunk masks the job records overwrite; the records'
+      // barrier below comes before s_red is written again)
+      const uint32_t jb = (uint32_t)block_scan<IE_FEWER_BARRIERS == 0>(pok ? nch : 0u, s_red, &njobs64);
       const uint32_t njobs = (uint32_t)njobs64;
       IE_STAMP(8);
       const ChainJobs J{(lds_u32*)(lds_u8*)(s_u + kCmOff), (lds_u16*)(lds_u8*)(s_u + 8 * kJobCap),
@@ -1420,6 +1432,22 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
                     W.lit_cap_max != 0);
     if (r.status == IE_OK_STR && (r.res_len > kLenMask || (r.res_off >> 4) > 0xFFFFFFFFull))
       r.status = IE_E_OVERFLOW;
+    if (r.status == IE_NEEDS_HOST && W.host_keys && r.res_len) {
+      // the key the host must look up (get_interpdata's file fallback, py:452-461): a record
+      // {string index, key length, key bytes} in the exec's host-key list
+      const uint64_t need = 8 + ((r.res_len + 3) & ~3ull);
+      uint64_t at = 0;
+      if (lane == 0) at = atomicAdd((unsigned long long*)W.host_keys_used, (unsigned long long)need);
+      at = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(at >> 32), 0, 64) << 32) | (uint32_t)__shfl((int)(uint32_t)at, 0, 64);
+      if (at + need <= W.host_keys_cap) {
+        if (lane == 0) {
+          uint32_t* hdr = (uint32_t*)(W.host_keys + at);
+          hdr[0] = B.out_index ? gld(B.out_index + gi) : (uint32_t)gi;
+          hdr[1] = (uint32_t)r.res_len;
+        }
+        for (uint64_t k = lane; k < r.res_len; k += 64) W.host_keys[at + 8 + k] = W.pool[r.res_off + k];
+      }
+    }
 
     if (lane == 0) {
       uint64_t ko, kl;  // W.recurse: get_simple_insertkey on the item as written (py:1463)
@@ -1443,7 +1471,7 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
     d.vs[q] = park[(10 + q) * kRBlock];
   }
   }
-  __syncthreads();
+  if (!IE_FEWER_BARRIERS || npend) __syncthreads();  // (nothing was written since the last barrier otherwise)
   IE_STAMP(3);
 
   // ---- 4. offsets: workgroup scan; the aggregate goes out at once ----
@@ -1473,7 +1501,8 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
   load_text(0, tt[0]);
 #endif
   uint64_t tile_total;
-  const uint64_t local = block_scan(olen, s_red, &tile_total);  // (its barriers also retire s_lit)
+  // (its barrier also retires s_lit; s_red[kRBlock / 64] below is another word than the scan's)
+  const uint64_t local = block_scan<IE_FEWER_BARRIERS == 0>(olen, s_red, &tile_total);
   uint64_t lb_early = 0;
   if (VIEWS) {
     // the tile's output range: one atomic, its answer consumed after the build; or (reserved

@@ -249,18 +249,21 @@ class InsertsTableSet:
         """Like interpolate_inserts on each string; failures come back as exception instances."""
         ids = [0] * len(strings) if table_ids is None else list(table_ids)
         out = []
-        for s, t, (st, payload) in zip(strings, ids, self.run(strings, table_ids)):
+        got = self.run(strings, table_ids)
+        # the keys the device could not look up (IE_NEEDS_HOST), also those built from values
+        host_keys = get_exec(self.device).host_keys() if self.has_dir and any(st == N.NEEDS_HOST for st, _ in got) else {}
+        for i, (s, t, (st, payload)) in enumerate(zip(strings, ids, got)):
             if st == N.OK_STR:
                 out.append(payload)
             elif st == N.OK_VALUE:
                 out.append(self.value(payload))
             elif self.has_dir and inserts_dir and (st == N.NEEDS_HOST or (st == N.E_INTERP and _dir_bad)):
-                out.append(self._host_complete(s, t, st))
+                out.append(self._host_complete(s, t, st, host_keys.get(i, [])))
             else:
                 out.append(_exception(s, st, self.table_keys(t)))
         return out
 
-    def _host_complete(self, s, t, st):
+    def _host_complete(self, s, t, st, device_keys=()):
         """The inserts-directory lookups the device hands to the host (get_interpdata's file
         fallback, py:452-461). IE_NEEDS_HOST: a key that is not a canonical relative file name
         (os.path.join may leave the directory, so no snapshot holds it): the host opens the files
@@ -284,7 +287,7 @@ class InsertsTableSet:
             return _exception(s, st, self.table_keys(t))
         extras, missing = {}, set()
         for _ in range(8):
-            found = keys + [k for v in extras.values() if isinstance(v, str) for k in _literal_keys(v)]
+            found = list(device_keys) + keys + [k for v in extras.values() if isinstance(v, str) for k in _literal_keys(v)]
             cands = [k for k in dict.fromkeys(found)
                      if not _canonical_key(k) and k not in base and k not in extras and k not in missing]
             if not cands:
@@ -306,6 +309,8 @@ class InsertsTableSet:
                     return tbl.value(payload)
                 if st2 != N.NEEDS_HOST:
                     return _exception(s, st2, tbl.table_keys(0))
+                # the next key the device could not look up (built from what was just added too)
+                device_keys = list(device_keys) + get_exec(self.device).host_keys().get(0, [])
             finally:
                 tbl.close()
         for k in sorted(missing):

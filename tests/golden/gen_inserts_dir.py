@@ -63,7 +63,11 @@ BAD_FILES = {"binary": "fffe00206e6f74207574662d38", "broken.json5": "7b756e7465
 OUTSIDE_CASES = ["{../outside}", "a{../outside}b", "{../outside_j}", "{../nope}", "x{../nope}y", "{sub/../count}",
                  "{./over}", "{sub//leaf}", "{../dir2/leaf}", "{../dir/plain}", "{binary}", "x{binary}y", "{broken}",
                  "{q-{../nope}}", "{sub}", "x{sub}y", "{binary}{missing}", "{missing}{binary}", "{binary}{sub}",
-                 "{sub}{count}"]
+                 "{sub}{count}",
+                 # keys built from looked-up values that leave the directory (the device records them)
+                 "{{up}/outside}", "x{{up}/nope}y", "<{{up}/dir2/leaf}>", "{{up}/{sub_k}}", "{{up}/outside_j}"]
+# the values those keys are built from (added to the inserts of the outside cases only)
+OUTSIDE_INSERTS = {"up": "..", "sub_k": "dir"}
 
 
 def classify(ie, inserts, s, other_errors=False):
@@ -128,12 +132,13 @@ def main():
         ie.inserts_dir = d
         outside = []
         for s in OUTSIDE_CASES:
-            rec = classify(ie, dict(INSERTS), s, other_errors=True)
+            rec = classify(ie, dict(INSERTS, **OUTSIDE_INSERTS), s, other_errors=True)
             rec["s"] = s
             outside.append(rec)
     with open(os.path.join(HERE, "inserts_dir_py.json"), "w", encoding="utf-8") as f:
         json.dump({"files": FILES, "inserts": INSERTS, "cases": cases, "outside_files": OUTSIDE_FILES,
-                   "bad_files": BAD_FILES, "outside_cases": outside}, f, ensure_ascii=False, indent=0)
+                   "bad_files": BAD_FILES, "outside_inserts": OUTSIDE_INSERTS, "outside_cases": outside}, f,
+                  ensure_ascii=False, indent=0)
     print("inserts_dir_py.json: %d cases, %d outside / bad-file cases" % (len(cases), len(outside)))
 
 

@@ -93,8 +93,8 @@ def test_device_mirror_with_inserts_dir(tmp_path):
 @pytest.mark.gpu
 def test_device_mirror_outside_keys_and_bad_files(tmp_path):
     """Keys that are not canonical file names under the directory (the device reports
-    IE_NEEDS_HOST; the host opens os.path.join(inserts_dir, key) as py:452-461 does and the
-    device resolves the string again) and files the reference cannot read (its error is raised when
+    IE_NEEDS_HOST and records the key, also one built from looked-up values; the host opens
+    os.path.join(inserts_dir, key) as py:452-461 does and the device resolves the string again) and files the reference cannot read (its error is raised when
     the key is looked up), against the reference's own results (gen_inserts_dir.py)."""
     pkg = G.load_package()
     from interpolation_engine_amd import interpolation_engine as M
@@ -111,7 +111,7 @@ def test_device_mirror_outside_keys_and_bad_files(tmp_path):
     try:
         for c in FIX["outside_cases"]:
             try:
-                r = pkg.interpolate_inserts(dict(FIX["inserts"]), c["s"])
+                r = pkg.interpolate_inserts(dict(FIX["inserts"], **FIX.get("outside_inserts", {})), c["s"])
             except pkg.InterpolationException:
                 assert c["st"] == "E_INTERP", c
                 continue
