@@ -884,9 +884,11 @@ int upload_table(const std::vector<Ent>& ents, uint32_t n_tables, int32_t dialec
   // table is 8 MB of entries and 50 KB of L2-resident pilots). A failed search changes the seed
   // (two keys with one 64-bit hash can never be separated) and then grows the table.
   const uint64_t nk = items.size();
-  const uint32_t nb = (uint32_t)std::max<uint64_t>(1, (nk + 3) / 4);
-  // (IE_TABLE_MUTABLE: load 0.5, so that a pilot group can be placed again around new keys)
-  uint64_t m = std::max<uint64_t>(16, (flags & IE_TABLE_MUTABLE) ? 2 * nk + 16 : nk + nk / 4 + 1);
+  // (IE_TABLE_MUTABLE: load 0.5 and groups sized for the capacity, about 2 keys each at the build
+  // and 4 when the table is full, so that a group can be placed again around new keys)
+  const bool mut = (flags & IE_TABLE_MUTABLE) != 0;
+  uint64_t m = std::max<uint64_t>(16, mut ? 2 * nk + 16 : nk + nk / 4 + 1);
+  const uint32_t nb = (uint32_t)std::max<uint64_t>(1, ((mut ? m : nk) + 3) / 4);
   uint64_t seed = 0xA0761D6478BD642Full;
   std::vector<uint16_t> pilots;
   std::vector<uint32_t> slot_of;

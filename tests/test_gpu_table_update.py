@@ -110,12 +110,33 @@ def test_clock_entries_follow_replaced_groups():
     states = [{"k": "v"} for _ in range(64)]
     tset = IE.InsertsTableSet(states, clock=CLOCK)
     try:
-        changes = [(t, "new%d_%d" % (t, j), "x") for t in range(64) for j in range(6)]
+        # within the headroom IE_TABLE_MUTABLE leaves (slots for twice the built keys)
+        changes = [(t, "new%d_%d" % (t, j), "x") for t in range(64) for j in range(2)]
         for t, k, v in changes:
             states[t][k] = v
         assert tset.update(changes)
         assert tset.set_clock((1, 2, 3))
-        got = tset.results(["{HH:MM}|{HH:MM:SS}|{new%d_5}" % t for t in range(64)], list(range(64)))
+        got = tset.results(["{HH:MM}|{HH:MM:SS}|{new%d_1}" % t for t in range(64)], list(range(64)))
         assert got == ["01:02|01:02:03|x"] * 64
+    finally:
+        tset.close()
+
+
+def test_updates_beyond_the_headroom_ask_for_a_rebuild():
+    # more new keys than the table set has free slots: update says so (False), and a rebuilt table
+    # set answers for the grown dicts
+    states = [{"k": "v"} for _ in range(64)]
+    tset = IE.InsertsTableSet(states, clock=CLOCK)
+    try:
+        changes = [(t, "new%d_%d" % (t, j), "x") for t in range(64) for j in range(8)]
+        for t, k, v in changes:
+            states[t][k] = v
+        assert not tset.update(changes)
+    finally:
+        tset.close()
+    tset = IE.InsertsTableSet(states, clock=CLOCK)
+    try:
+        got = tset.results(["{k}{new%d_7}" % t for t in range(64)], list(range(64)))
+        assert got == ["vx"] * 64
     finally:
         tset.close()

@@ -30,3 +30,15 @@ for v in ${VARIANTS:-main}; do
       python3 bench.py --steps 3 --warmup 1 --no-cpu ${PMC_ARGS:---reserve=32} > $O/pmc_$v.log 2>&1 || exit $?
   fi
 done
+# FETCH_SIZE calibration on known byte counts (streaming vs random 64-B entry gathers) and the
+# config-4 fetch split (full vs IE_DEBUG_NOEVAL, i.e. without the table lookups)
+if [ -n "${GATHER:-}" ]; then
+  timeout -k 10 60 tools/exp/gather_ubench > $O/gather.txt 2>&1 || exit $?
+  timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/gather_fetch -o run -- tools/exp/gather_ubench > $O/gather_fetch.log 2>&1 || exit $?
+  timeout -s KILL 60 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $O/gather_hit -o run -- tools/exp/gather_ubench > $O/gather_hit.log 2>&1 || exit $?
+fi
+if [ -n "${CFG4_PMC:-}" ]; then
+  timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/c4_fetch -o run -- python3 bench.py --config 4 --steps 2 --warmup 1 --no-cpu > $O/c4_fetch.log 2>&1 || exit $?
+  IE_DEBUG_NOEVAL=1 timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/c4_fetch_noeval -o run -- python3 bench.py --config 4 --steps 2 --warmup 1 --no-cpu > $O/c4_fetch_noeval.log 2>&1 || exit $?
+  timeout -s KILL 150 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum --output-format csv -d $O/c4_hit -o run -- python3 bench.py --config 4 --steps 2 --warmup 1 --no-cpu > $O/c4_hit.log 2>&1 || exit $?
+fi
