@@ -40,5 +40,5 @@ fi
 if [ -n "${CFG4_PMC:-}" ]; then
   timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/c4_fetch -o run -- python3 bench.py --config 4 --steps 2 --warmup 1 --no-cpu > $O/c4_fetch.log 2>&1 || exit $?
   IE_DEBUG_NOEVAL=1 timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/c4_fetch_noeval -o run -- python3 bench.py --config 4 --steps 2 --warmup 1 --no-cpu > $O/c4_fetch_noeval.log 2>&1 || exit $?
-  timeout -s KILL 150 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum --output-format csv -d $O/c4_hit -o run -- python3 bench.py --config 4 --steps 2 --warmup 1 --no-cpu > $O/c4_hit.log 2>&1 || exit $?
+  timeout -s KILL 150 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $O/c4_hit -o run -- python3 bench.py --config 4 --steps 2 --warmup 1 --no-cpu > $O/c4_hit.log 2>&1 || exit $?
 fi
