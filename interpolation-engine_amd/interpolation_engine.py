@@ -810,8 +810,8 @@ def _walk_states(states, xs, owner, tables, depth):
     for i in range(n):
         try:
             skels[i] = _tree_leaves(states[owner[i]], xs[i], leaves, ids, owner[i])
-        except (InterpolationException, AssertionError, TypeError, KeyError) as e:
-            fails[i] = e  # the loop-command branch's get_interpdata (py:1483-1488)
+        except Exception as e:  # noqa: BLE001 — fails this state only, not the batch
+            fails[i] = e
     res = tables.results(leaves, ids) if leaves else []
     # leaves whose result the reference walks again (py:1463-1464): the next batch
     again = [k for k, leaf in enumerate(leaves) if not isinstance(res[k], BaseException) and get_simple_insertkey(leaf)]
@@ -853,12 +853,17 @@ def _tree_leaves(inserts, v, leaves, ids, i):
         if cmd in ("goto_map", "replace_map"):  # py:1471-1477
             return (_LEAF + "const", v)
         if cmd in _LOOP_CMDS:  # py:1479-1489
-            v = copy.deepcopy(v)
-            if (k := get_simple_insertkey(v["tasks"])):
-                v["tasks"] = get_interpdata(inserts, k)
-            for j in range(len(v["tasks"])):
-                if (k := get_simple_insertkey(v["tasks"][j])):
-                    v["tasks"][j] = get_interpdata(inserts, k)
+            # a failing lookup is raised where the reference's walk reaches it (_tree_rebuild), so
+            # an earlier leaf's error still comes first
+            try:
+                v = copy.deepcopy(v)
+                if (k := get_simple_insertkey(v["tasks"])):
+                    v["tasks"] = get_interpdata(inserts, k)
+                for j in range(len(v["tasks"])):
+                    if (k := get_simple_insertkey(v["tasks"][j])):
+                        v["tasks"][j] = get_interpdata(inserts, k)
+            except Exception as e:  # noqa: BLE001
+                return (_LEAF + "raise", e)
             return (_LEAF + "const", v)
         return (_LEAF + "dict", [(_tree_leaves(inserts, k, leaves, ids, i), _tree_leaves(inserts, vv, leaves, ids, i))
                                  for k, vv in v.items()])
@@ -876,4 +881,6 @@ def _tree_rebuild(skel, res):
         return r
     if tag == _LEAF + "dict":
         return {_tree_rebuild(k, res): _tree_rebuild(vv, res) for k, vv in val}
+    if tag == _LEAF + "raise":
+        raise val
     return val

@@ -312,6 +312,19 @@ def _replace_strings(tset, states, leaves, owner, keys, maps, m, repeat, dialect
                 vres = _str_results(xs, [vals_raw[p] for _, p, _ in hits], list(range(len(hits))))
             finally:
                 xs.close()
+            # a failure's message lists the table's keys (py:467): those again against the whole
+            # `inserts | extra_inserts`, so that the text is the reference's
+            bad = [j for j, v in enumerate(vres) if isinstance(v, BaseException)]
+            if bad:
+                full = [dict(states[owner[hits[j][0]]], **{str(k + 1): c for k, c in enumerate(hits[j][2])})
+                        for j in bad]
+                xs = IE.InsertsTableSet(full, dialect=dialect, device=device)
+                try:
+                    again = _str_results(xs, [vals_raw[hits[j][1]] for j in bad], list(range(len(bad))))
+                finally:
+                    xs.close()
+                for j, v in zip(bad, again):
+                    vres[j] = v
             for (i, _, _), v in zip(hits, vres):
                 if isinstance(v, BaseException):
                     err[i] = v

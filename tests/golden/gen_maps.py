@@ -102,6 +102,11 @@ EDGE_TASKS = [
     {"cmd": "goto_map", "text": "{missing}", "target_maps": [{"x": "t1"}], "traceback_label": "E11"},
     {"cmd": "goto_map", "text": "abc", "target_maps": [{"{nokey}": "t1"}], "traceback_label": "E12"},
     {"cmd": "goto_map", "text": "{greet}", "target_maps": [{"hello *": "{who}"}], "traceback_label": "E13"},
+    # a matched value that fails: the message lists every key of `inserts | extra_inserts` (py:467)
+    {"cmd": "replace_map", "item": "apple", "output_name": "out", "wildcard_maps": [{"app*": "{1}{missing_v}"}],
+     "traceback_label": "E14"},
+    {"cmd": "replace_map", "item": "apple", "output_name": "out", "wildcard_maps": [{"app*": "{greet}{missing_v}"}],
+     "traceback_label": "E15"},
 ]
 
 
@@ -117,8 +122,8 @@ def run_task(ie, state, t):
         if isinstance(val, str) and len(val) > 256:
             return {"set": [name, None], "len": len(val), "fnv": fnv(val)}
         return {"set": [name, val]}
-    except Exception as e:  # noqa: BLE001 — the class is the outcome
-        return {"err": type(e).__name__}
+    except Exception as e:  # noqa: BLE001 — the class (and the message) is the outcome
+        return {"err": type(e).__name__, "msg": str(e)}
 
 
 def map_tasks(program):

@@ -114,3 +114,20 @@ def test_config5_prepass_trees_of_all_states_in_one_batch():
             bad.append((w["x"], w["st"], repr(r)[:200]))
     assert not bad, (len(bad), bad[:3])
     assert len(want) >= 200
+
+
+def test_errors_come_in_the_walk_order():
+    """py:1462-1494 walks a list in order: a missing key in an earlier leaf is raised before the
+    loop command's get_interpdata (py:1483-1488) of a later element, and a failing state does not
+    fail the other states of the batch."""
+    inserts = {"name": "tom"}
+    x = ["{missing_a}", {"cmd": "for", "tasks": "{missing_b}"}]
+    with pytest.raises(PKG.InterpolationException) as e:
+        PKG.recursive_interpolate(inserts, x)
+    assert "missing_a" in str(e.value) and "missing_b" not in str(e.value)
+    # the loop command's lookup first when it comes first
+    with pytest.raises(PKG.InterpolationException) as e:
+        PKG.recursive_interpolate(inserts, [{"cmd": "for", "tasks": "{missing_b}"}, "{missing_a}"])
+    assert "missing_b" in str(e.value)
+    got = PKG.recursive_interpolate_states([inserts, inserts], [x, ["{name}"]])
+    assert isinstance(got[0], PKG.InterpolationException) and got[1] == ["tom"]
