@@ -189,11 +189,13 @@ int ie_table_set_clock(ie_table* t, const ie_clock* now);
  * user_input / set stores of py:1566-1568, 1770-1773; rust-project/src/runtime.rs:700-701 snapshots
  * the map per task): entry i sets kv[i] (kind < 0: deletes the key) in table table_id[i], value id
  * vid[i], without a rebuild: a key the table has is rewritten in place, a new key re-places its
- * pilot group. Synchronous (waits for the device first, like ie_table_set_clock). A brace-bearing
+ * pilot group (or, when that group has no free placement, the whole table is placed again at the
+ * same capacity: entries and pilots uploaded whole). Synchronous (waits for the device first, like ie_table_set_clock). A brace-bearing
  * value is not pre-resolved, and the pre-resolved values of every changed table return to their raw
  * text (both then resolve through the exact evaluator, in the reference's order). IE_ERR_CAPACITY:
  * a new key found no placement (the entries before it were applied, it and the rest were not:
- * rebuild the table; a table built with IE_TABLE_MUTABLE keeps room for new keys). */
+ * rebuild the table; a table built with IE_TABLE_MUTABLE keeps room for about as many new keys as it
+ * was built with). */
 int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, const uint32_t* vid, uint64_t n);
 uint64_t ie_table_entries(const ie_table* t);
 uint32_t ie_table_tables(const ie_table* t);

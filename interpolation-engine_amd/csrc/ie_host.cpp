@@ -843,6 +843,52 @@ Entry make_entry(ie_table* t, std::string_view key, std::string_view text, uint3
   return b;
 }
 
+// Whole-table re-placement at the same capacity (ie_table_set_update, when a group found no pilot
+// around a new key): every live entry and `extra` placed again under a new seed. The slot lists
+// (groups, clock entries, pre-resolved values) follow their entries; the caller uploads entries
+// and pilots whole. False when no seed of a few tried places them all (the table is too full).
+bool replace_all(ie_table* t, const Entry& extra) {
+  const uint32_t m = t->dev.m, nb = t->dev.nb;
+  std::vector<Entry> live;
+  std::vector<uint32_t> from;
+  for (uint32_t s = 0; s < m; s++)
+    if (t->h_entries[s].flags & EF_OCCUPIED) live.push_back(t->h_entries[s]), from.push_back(s);
+  live.push_back(extra);
+  from.push_back(UINT32_MAX);
+  std::vector<std::string> keys(live.size());
+  for (size_t i = 0; i < live.size(); i++) keys[i] = std::string(mirror_key(t, live[i]));
+  std::vector<uint64_t> hs(live.size());
+  std::vector<uint16_t> pilots;
+  std::vector<uint32_t> slot_of;
+  uint64_t seed = t->dev.seed;
+  for (int attempt = 0; attempt < 8; attempt++) {
+    seed = fmix64_host(seed + 0x9E3779B97F4A7C15ull);
+    for (size_t i = 0; i < live.size(); i++) hs[i] = key_hash(keys[i], seed, live[i].flags >> kTidShift);
+    if (!ph_place(hs, m, nb, pilots, slot_of)) continue;
+    std::vector<Entry> ne(m);
+    std::unordered_map<uint32_t, uint32_t> moved;
+    t->groups.assign(nb, {});
+    for (size_t i = 0; i < live.size(); i++) {
+      ne[slot_of[i]] = live[i];
+      if (from[i] != UINT32_MAX) moved[from[i]] = slot_of[i];
+      t->groups[ph_group(hs[i], nb)].push_back(slot_of[i]);
+    }
+    for (uint32_t& cs : t->clock_slots)
+      if (moved.count(cs)) cs = moved[cs];
+    for (auto& kv : t->rawalt) {  // (a deleted entry's slot is dropped)
+      std::vector<uint32_t> keep;
+      for (uint32_t rs : kv.second)
+        if (moved.count(rs)) keep.push_back(moved[rs]);
+      kv.second = std::move(keep);
+    }
+    t->h_entries = std::move(ne);
+    t->h_pilots = std::move(pilots);
+    t->dev.seed = seed;
+    return true;
+  }
+  return false;
+}
+
 }  // extern "C++"
 
 // Entries -> perfect-hash table on the device.
@@ -1202,9 +1248,10 @@ int ie_table_set_clock(ie_table* t, const ie_clock* now) {
 
 // set_interpdata on a built table (set): py:470-471 `inserts[key] = value` (and `del`) on state
 // table_id[i], without a rebuild. A key already in that table is rewritten in place (its slot is
-// fixed by the perfect hash); a new key re-places its pilot group (about four keys) around it; a
-// group with no free placement reports IE_ERR_CAPACITY and nothing of that key is applied (the
-// caller rebuilds). Values are taken as given: a brace-bearing value is not pre-resolved (the
+// fixed by the perfect hash); a new key re-places its pilot group (a few keys) around it, or, when
+// the group finds no pilot, the whole table is placed again under a new seed at the same capacity
+// (replace_all); only when that fails too IE_ERR_CAPACITY is reported and nothing of that key is
+// applied (the caller rebuilds). Values are taken as given: a brace-bearing value is not pre-resolved (the
 // exact evaluator resolves it in the reference's order), and the pre-resolved values of every
 // table that changed go back to their raw text, since they were resolved against the old dict.
 int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, const uint32_t* vid, uint64_t n) {
@@ -1213,8 +1260,9 @@ int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
   if (rc) return rc;
   IE_HIP(hipDeviceSynchronize());  // no batch may still read the table
   const uint64_t arena0 = t->h_arena.size();
-  const uint64_t seed = t->dev.seed;
+  uint64_t seed = t->dev.seed;
   const uint32_t nb = t->dev.nb, m = t->dev.m;
+  bool whole = false;                      // entries and pilots re-placed: upload them whole
   std::vector<uint32_t> dirty;             // entry slots to upload
   std::vector<uint32_t> dirty_groups;      // pilots to upload
   std::vector<uint32_t> touched;           // tables whose pre-resolved values must go raw
@@ -1272,9 +1320,18 @@ int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
         if (ok) found = true, pilot = p;
       }
       if (!found) {
-        status = fail(IE_ERR_CAPACITY, "no free placement for a new key's pilot group: rebuild the table");
-        n = i;  // apply (upload) what came before, stop here
-        break;
+        // every entry placed again under a new seed, at the same capacity
+        if (!replace_all(t, make_entry(t, key, text, flags, vid[i], tb))) {
+          status = fail(IE_ERR_CAPACITY, "no free placement for a new key: rebuild the table with more room");
+          n = i;  // apply (upload) what came before, stop here
+          break;
+        }
+        seed = t->dev.seed;
+        whole = true;
+        t->n_entries++;
+        if (key.size() > kInlineKey && key.size() <= 2 * kInlineKey) t->dev.flags |= TF_LONG_KEYS;
+        t->dev.maxtext = std::max<uint64_t>(t->dev.maxtext, text.size());
+        continue;
       }
       std::vector<Entry> moved;
       for (uint32_t s2 : gs) moved.push_back(t->h_entries[s2]);
@@ -1347,14 +1404,18 @@ int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
     pe.add((uint8_t*)t->arena.p + arena0, t->h_arena.data() + arena0, t->h_arena.size() - arena0);
   std::sort(dirty.begin(), dirty.end());
   dirty.erase(std::unique(dirty.begin(), dirty.end()), dirty.end());
-  if (dirty.size() * 8 > t->h_entries.size()) {
+  if (whole || dirty.size() * 8 > t->h_entries.size()) {
     IE_HIP(hipMemcpy(t->entries.p, t->h_entries.data(), t->h_entries.size() * sizeof(Entry), hipMemcpyHostToDevice));
   } else {
     for (uint32_t s2 : dirty) pe.add((Entry*)t->entries.p + s2, &t->h_entries[s2], sizeof(Entry));
   }
-  std::sort(dirty_groups.begin(), dirty_groups.end());
-  dirty_groups.erase(std::unique(dirty_groups.begin(), dirty_groups.end()), dirty_groups.end());
-  for (uint32_t g : dirty_groups) pe.add((uint16_t*)t->pilots.p + g, &t->h_pilots[g], sizeof(uint16_t));
+  if (whole) {
+    IE_HIP(hipMemcpy(t->pilots.p, t->h_pilots.data(), t->h_pilots.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+  } else {
+    std::sort(dirty_groups.begin(), dirty_groups.end());
+    dirty_groups.erase(std::unique(dirty_groups.begin(), dirty_groups.end()), dirty_groups.end());
+    for (uint32_t g : dirty_groups) pe.add((uint16_t*)t->pilots.p + g, &t->h_pilots[g], sizeof(uint16_t));
+  }
   if ((rc = apply_patches(t->patch_staging, pe))) return rc;
   t->dev.n_entries = (uint32_t)t->n_entries;
   return status;
