@@ -231,15 +231,19 @@ int ie_exec_timing(ie_exec* x, ie_timing* out); /* syncs */
                           *total = sum of lengths still; a tile that did not fit bytes_cap makes
                           ie_exec_sync report IE_ERR_CAPACITY. Size bytes_cap >= F/16 x the input bytes
                           plus the overflow's share. */
+#define IE_OPT_ERROR_KEYS 9 /* 1: every IE_E_INTERP string of an interpolation call also leaves the
+                          missing key its message names (py:467, "Could not find variable '<key>'")
+                          in ie_exec_host_keys; such strings take the literal path (0, the default:
+                          no keys, misses stay on the fast evaluators) */
 int ie_exec_set_option(ie_exec* x, int32_t option, int64_t value);
 /* Literal-path scratch pool size. Setting it makes ie_interpolate_device fully asynchronous: it no
  * longer waits to check the pool's demand, and strings that ran out of it report IE_E_OVERFLOW. */
 int ie_exec_set_scratch(ie_exec* x, uint64_t bytes);
 /* Keys only the host can look up (get_interpdata's file fallback for a key that is not a canonical
  * relative file name under the inserts directory, py:452-461): for every string of the exec's last
- * interpolation call that reported IE_NEEDS_HOST, the key its failing lookup used (also one built
- * from looked-up values), as records {uint32 string index, uint32 key length, key bytes padded to
- * 4}. Copies min(cap, *used) bytes of records to buf; *used = the records' size. Synchronous. */
+ * interpolation call that reported IE_NEEDS_HOST (and, with IE_OPT_ERROR_KEYS, IE_E_INTERP), the key
+ * its failing lookup used (also one built from looked-up values), as records {uint32 string index,
+ * uint32 key length, key bytes padded to 4}. Copies min(cap, *used) bytes of records to buf; *used = the records' size. Synchronous. */
 int ie_exec_host_keys(ie_exec* x, uint8_t* buf, uint64_t cap, uint64_t* used);
 
 /* Diagnostic (no reference counterpart): one key through the device lookups next to the host's

@@ -118,6 +118,7 @@ struct ie_exec {
                                   // measured slower on config 5) / 1 (IE_DEFER)
   bool defer_slow = false;        // the adaptive choice (from an earlier batch's counts)
   int32_t opt_small = 1;          // host batches of <= 1024 strings / 64 KB: one pinned copy each way (IE_SMALL_HOST)
+  int32_t opt_err_keys = 0;       // IE_OPT_ERROR_KEYS: record the missing key of every IE_E_INTERP string
   uint32_t opt_reserve = 0;       // views output of a packed batch: reserved ranges at opt_reserve / 16 x the
                                   // input offsets (IE_OPT_RESERVE; 0: one claim per tile on one cursor)
   bool in_cmd = false;            // inside the unescape command's second resolve
@@ -399,7 +400,8 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
   if (n && d_out_len == nullptr && out->offsets == nullptr) return fail(IE_ERR_INVALID, "null offsets");
   Batch B{d_bytes, d_off, n, out->offsets, out->status, out->value_id, d_tid, d_in_len, d_out_len};
   Work W = make_work(x, out->total);
-  if (op == kOpInterp && (t->dev.flags & TF_HAS_DIR)) {  // the literal path records IE_NEEDS_HOST keys
+  // the literal path records IE_NEEDS_HOST keys (and, IE_OPT_ERROR_KEYS, the missing keys of IE_E_INTERP)
+  if (op == kOpInterp && ((t->dev.flags & TF_HAS_DIR) || x->opt_err_keys)) {
     if (!x->host_keys.p) {
       IE_HIP(x->host_keys.ensure(1ull << 20));
       IE_HIP(hipMemsetAsync(x->host_keys.p, 0, 16, x->stream));
@@ -408,6 +410,7 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
     W.host_keys_used = (uint64_t*)x->host_keys.p;
     W.host_keys_cap = x->host_keys.bytes - 16;
   }
+  W.err_keys = op == kOpInterp && x->opt_err_keys ? 1u : 0u;
   W.recurse = op == kOpInterp && x->in_cmd && t->dialect == IE_DIALECT_PY ? 1u : 0u;
   // reserved output ranges: a views output of a packed interpolation batch (not the unescape command)
   W.reserve16 = reserve_ok && op == kOpInterp && d_out_len && !d_in_len && !x->in_cmd && !x->cmd_fused ? x->opt_reserve : 0u;
@@ -436,6 +439,7 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
       else if (heavy * 4096 < x->stat_n) x->defer_slow = false;
     }
     W.fail_commit = forced ? (uint32_t)x->opt_fail_commit : (uint32_t)x->fail_commit;
+    if (W.err_keys) W.fail_commit = 0;  // misses go through the exact evaluator to the literal path
     if (x->timing) IE_HIP(hipEventRecord(x->ev[1], st));
     // 512-string tiles halve the look-back hops: the unescape command's second resolve (its input
     // is interpolation output, so its evaluation is light and the look-back bounds it) takes them
@@ -669,7 +673,7 @@ int run_host(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, const 
   for (uint64_t i = 0; i < n; i++)
     if (b->status[i] != IE_OK_VALUE && b->status[i] != IE_RECURSE) b->value_id[i] = IE_VID_NONE;
   std::vector<uint8_t> recs;  // this batch's host-key records (the device pass above)
-  if (op == kOpInterp && t && (t->dev.flags & TF_HAS_DIR) && (rc = read_host_keys(x, recs))) {
+  if (op == kOpInterp && t && ((t->dev.flags & TF_HAS_DIR) || x->opt_err_keys) && (rc = read_host_keys(x, recs))) {
     ie_batch_free(b);
     return rc;
   }
@@ -1592,6 +1596,9 @@ int ie_exec_set_option(ie_exec* x, int32_t option, int64_t value) {
     case IE_OPT_DEFER:
       if (value < -1 || value > 1) return fail(IE_ERR_INVALID, "defer must be -1, 0 or 1");
       x->opt_defer = (int32_t)value;
+      return IE_SUCCESS;
+    case IE_OPT_ERROR_KEYS:
+      x->opt_err_keys = value ? 1 : 0;
       return IE_SUCCESS;
     default:
       return fail(IE_ERR_INVALID, "unknown exec option");

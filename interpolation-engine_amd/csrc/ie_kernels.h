@@ -80,11 +80,13 @@ struct Work {
   // reserve16 / 16 times its input span's offset from the batch's first byte when it fits there (no
   // atomic), else to the overflow region after the whole batch's reservation (W.cursor); the tile
   // sums go to the 16 `shards` words (u64, 128 B apart) and k_emit_windows adds them into *total
-  // keys only the host can look up (IE_NEEDS_HOST, inserts-dir tables): records {u32 string index,
+  // keys only the host can look up (IE_NEEDS_HOST, inserts-dir tables) and, with err_keys
+  // (IE_OPT_ERROR_KEYS), the missing key of every IE_E_INTERP string: records {u32 string index,
   // u32 length, bytes padded to 4} appended by the literal path (ie_exec_host_keys)
   uint8_t* host_keys;
   uint64_t host_keys_cap;
   uint64_t* host_keys_used;
+  uint32_t err_keys;     // IE_E_INTERP strings go to the literal path, which records their key
   uint32_t reserve16;
   uint64_t* res_ovf;     // 1   the overflow region's start (written by the reserved pass)
   uint32_t recurse;      // k_resolve in the unescape command (py dialect): whole-string items whose

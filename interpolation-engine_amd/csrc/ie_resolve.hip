@@ -59,6 +59,13 @@
 #define IE_FEWER_BARRIERS 0
 #endif
 
+// views launches as persistent workgroups (as many as are resident): each loops over the tiles
+// blockIdx.x, + gridDim.x, ... and has the next tile's offsets and input chunks in flight while it
+// evaluates, builds and streams out the current one
+#ifndef IE_PERSIST
+#define IE_PERSIST 0
+#endif
+
 namespace ie {
 // everything of one tile size lives in its own namespace: ie_resolve512.hip compiles this file
 // again with 512-string tiles (IE_RBLOCK=512, IE_RNS=r512, IE_RESOLVE_WIDE)
@@ -208,7 +215,8 @@ __device__ __forceinline__ void copy_bytes(uint8_t* __restrict__ dst, const uint
 // ------------------------------------------------------------------------------------------
 template <bool STAGED>
 __device__ uint8_t eval_exact(const DevTable& T, uint32_t tid, const Src<STAGED> s, uint32_t n, bool active, lds_u8* kbuf,
-                              lds_u32* stack, Desc& d, uint32_t& out_len, uint32_t& vid, uint32_t& vflags) {
+                              lds_u32* stack, Desc& d, uint32_t& out_len, uint32_t& vid, uint32_t& vflags,
+                              bool err_keys) {
   constexpr uint8_t kRunning = 0xFF;
   uint8_t status = active ? kRunning : (uint8_t)IE_OK_STR;
   uint32_t depth = 0, klen = 0, vsum = 0, span = 0, ntop = 0;
@@ -233,8 +241,9 @@ __device__ uint8_t eval_exact(const DevTable& T, uint32_t tid, const Src<STAGED>
     if (nopen == 0) return IE_OK_STR;
     if (nopen != nclose) return IE_E_ASSERT_BRACES;
     if (negclose) return kStatusPending;  // balanced but '}{': py break / rs panic
-    // (a key only the host can look up, IE_NEEDS_HOST: the literal path reports it with the key)
-    if (err_off >= 0) return err_cls == IE_NEEDS_HOST ? kStatusPending : err_cls;
+    // (a key only the host can look up, IE_NEEDS_HOST, or, err_keys, the missing key of an
+    // IE_E_INTERP: the literal path reports it with the key)
+    if (err_off >= 0) return err_cls == IE_NEEDS_HOST || (err_keys && err_cls == IE_E_INTERP) ? kStatusPending : err_cls;
     if (wrapped) {
       vid = wrap_h.vid;
       vflags = wrap_h.flags;
@@ -1219,11 +1228,26 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
     __syncthreads();
     tile = s_misc[0];
   }
-  const TileGeo geo = load_geo(B, tile, tid);
+  TileGeo geo = load_geo(B, tile, tid);
   TilePrefetch<kStageV> pre;
   pre.nv = 0;
   if (tile < ntiles) pre.issue(B, geo, tid);
-  if (tile < ntiles) {
+  // persistent (views): this workgroup's tiles in turn; the next one's geometry loads now, its
+  // input chunks once this tile's evaluation is done
+  constexpr bool kLoop = IE_PERSIST && VIEWS;
+  while (tile < ntiles) {
+#if IE_PERSIST
+  // the lane index, opaque per tile: what derives from it is computed in the loop, not kept live
+  // across it
+  uint32_t tid_o;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(tid_o) : "v"(threadIdx.x));
+  const uint32_t tid = tid_o, wave = tid >> 6, lane = tid & 63u;
+#endif
+  const uint32_t ntile = tile + gridDim.x;
+  TileGeo ngeo{0, 0, 0, 0};
+  if (kLoop && IE_PERSIST != 3) ngeo = load_geo(B, ntile, tid);  // (IE_PERSIST 1 / 2: the chunks before / after the build)
+  TilePrefetch<kStageV> npre;
+  npre.nv = 0;
   uint64_t t_start = 0;
   if (tid == 0) {
     if (W.stamps) t_start = __builtin_amdgcn_s_memrealtime();
@@ -1369,7 +1393,7 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
       uint8_t r2 = kStatusPending;
 #ifndef IE_EXP_NOEXACT
       // staged strings through a generic pointer into the stage, the rest in global memory
-      r2 = eval_exact<false>(T, tid_s, Src<false>{s}, (uint32_t)sn, slow, kb, stk, d, o2, vid, vflags);
+      r2 = eval_exact<false>(T, tid_s, Src<false>{s}, (uint32_t)sn, slow, kb, stk, d, o2, vid, vflags, W.err_keys != 0u);
 #endif
       if (slow) r = r2, olen = o2;
     }
@@ -1422,7 +1446,7 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
     uint64_t pbase = 0;
     if (lane == 0) pbase = atomicAdd((unsigned long long*)W.pool_used, (unsigned long long)(4 * rcap));
     pbase = __shfl(pbase, 0, 64);
-    LitOut r{IE_E_OVERFLOW, 0, 0, IE_VID_NONE};
+    LitOut r{IE_E_OVERFLOW, 0, 0, IE_VID_NONE, 0, false};
 #ifndef IE_EXP_NOLIT
     if (rcap && pbase + 4 * rcap <= W.pool_bytes)
 #else
@@ -1432,9 +1456,10 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
                     W.lit_cap_max != 0);
     if (r.status == IE_OK_STR && (r.res_len > kLenMask || (r.res_off >> 4) > 0xFFFFFFFFull))
       r.status = IE_E_OVERFLOW;
-    if (r.status == IE_NEEDS_HOST && W.host_keys && r.res_len) {
-      // the key the host must look up (get_interpdata's file fallback, py:452-461): a record
-      // {string index, key length, key bytes} in the exec's host-key list
+    if ((r.status == IE_NEEDS_HOST || (W.err_keys && r.status == IE_E_INTERP)) && W.host_keys && r.has_key) {
+      // the key the host must look up (get_interpdata's file fallback, py:452-461), or the missing
+      // key an IE_E_INTERP message names (py:467): a record {string index, key length, key bytes}
+      // in the exec's host-key list
       const uint64_t need = 8 + ((r.res_len + 3) & ~3ull);
       uint64_t at = 0;
       if (lane == 0) at = atomicAdd((unsigned long long*)W.host_keys_used, (unsigned long long)need);
@@ -1473,6 +1498,9 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
   }
   if (!IE_FEWER_BARRIERS || npend) __syncthreads();  // (nothing was written since the last barrier otherwise)
   IE_STAMP(3);
+#if IE_PERSIST == 1
+  if (kLoop && ntile < ntiles) npre.issue(B, ngeo, tid);  // in flight through the build and stream-out
+#endif
 
   // ---- 4. offsets: workgroup scan; the aggregate goes out at once ----
   const uint8_t st = s_st[tid];
@@ -1590,6 +1618,14 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
     }
   }
   IE_STAMP(4);
+#if IE_PERSIST == 2
+  if (kLoop && ntile < ntiles) npre.issue(B, ngeo, tid);  // in flight through the stream-out
+#elif IE_PERSIST == 3
+  if (kLoop && ntile < ntiles) {
+    ngeo = load_geo(B, ntile, tid);
+    npre.issue(B, ngeo, tid);
+  }
+#endif
   if (VIEWS) {
     if (tid == 0) s_red[kRBlock / 64] = lb_early;
   } else if (wave == 0) {
@@ -1643,6 +1679,11 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
   }
   IE_STAMP(5);
 #undef IE_STAMP
+  if (!kLoop) break;
+  __syncthreads();  // every wave is done with this tile's LDS
+  tile = ntile;
+  geo = ngeo;
+  pre = npre;
   }
 }
 
@@ -1726,12 +1767,33 @@ __global__ __launch_bounds__(kRBlock) void k_unesc_deferred(Batch B, Work W, uin
   }
 }
 
+// resident workgroups of k_resolve on this device (IE_PERSIST): CUs x workgroups per CU (the
+// 256-lane instance at IE_WAVES_PER_EU waves per SIMD, LDS permitting)
+uint32_t persist_grid(uint32_t tiles) {
+  thread_local int dev_cached = -1;
+  thread_local uint32_t resident = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return tiles;
+  if (dev != dev_cached) {
+    int cus = 0, per_cu = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return tiles;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_resolve<false, false, true, false, false>,
+                                                     kRBlock, 0) != hipSuccess || per_cu < 1)
+      per_cu = 1;
+    resident = (uint32_t)(cus * per_cu);
+    dev_cached = dev;
+  }
+  return tiles < resident ? tiles : resident;
+}
+
 hipError_t launch_resolve_impl(const Batch& B, const Work& W, const DevTable& T, uint8_t* out, uint64_t cap,
                                hipStream_t st, bool unesc = false) {
   const uint64_t tiles = (B.n + kRBlock - 1) / kRBlock;
   if (!tiles) return hipSuccess;
   if (tiles > 0xFFFFFFFFull) return hipErrorInvalidValue;
   const uint32_t grid = (uint32_t)tiles;
+  // persistent views launches: as many workgroups as the device holds at once
+  const uint32_t vgrid = IE_PERSIST && B.out_len ? persist_grid(grid) : grid;
   const bool multi = B.table_id != nullptr;
   if (unesc) {  // the fused unescape command (views only)
     if (!B.out_len) return hipErrorInvalidValue;
@@ -1748,7 +1810,7 @@ hipError_t launch_resolve_impl(const Batch& B, const Work& W, const DevTable& T,
   const int variant = ((T.flags & TF_LONG_KEYS) ? 8 : 0) | (W.fail_commit ? 4 : 0) | (multi ? 2 : 0) | (B.out_len ? 1 : 0);
   switch (variant) {
 #define IE_LAUNCH(V, F, M, S, L) \
-  case V: hipLaunchKernelGGL((k_resolve<F, M, S, false, L>), dim3(grid), dim3(kRBlock), 0, st, B, W, T, out, cap); break;
+  case V: hipLaunchKernelGGL((k_resolve<F, M, S, false, L>), dim3(S ? vgrid : grid), dim3(kRBlock), 0, st, B, W, T, out, cap); break;
     IE_LAUNCH(0, false, false, false, false)
     IE_LAUNCH(1, false, false, true, false)
     IE_LAUNCH(2, false, true, false, false)

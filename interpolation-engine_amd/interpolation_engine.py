@@ -90,6 +90,8 @@ def get_exec(device=0):
     x = _execs.get(device)
     if x is None:
         x = _execs[device] = N.Exec(device)
+        # the missing key of every failed lookup comes back with its string (the message names it)
+        x.set_option(N.OPT_ERROR_KEYS, 1)
     return x
 
 
@@ -250,8 +252,10 @@ class InsertsTableSet:
         ids = [0] * len(strings) if table_ids is None else list(table_ids)
         out = []
         got = self.run(strings, table_ids)
-        # the keys the device could not look up (IE_NEEDS_HOST), also those built from values
-        host_keys = get_exec(self.device).host_keys() if self.has_dir and any(st == N.NEEDS_HOST for st, _ in got) else {}
+        # the keys the device could not look up (IE_NEEDS_HOST), also those built from values, and
+        # the missing keys of the failed lookups (IE_E_INTERP, IE_OPT_ERROR_KEYS)
+        need = any(st == N.E_INTERP or (self.has_dir and st == N.NEEDS_HOST) for st, _ in got)
+        host_keys = get_exec(self.device).host_keys() if need else {}
         for i, (s, t, (st, payload)) in enumerate(zip(strings, ids, got)):
             if st == N.OK_STR:
                 out.append(payload)
@@ -260,7 +264,7 @@ class InsertsTableSet:
             elif self.has_dir and inserts_dir and (st == N.NEEDS_HOST or (st == N.E_INTERP and _dir_bad)):
                 out.append(self._host_complete(s, t, st, host_keys.get(i, [])))
             else:
-                out.append(_exception(s, st, self.table_keys(t)))
+                out.append(_exception(s, st, self.table_keys(t), host_keys.get(i), self.has_dir))
         return out
 
     def _host_complete(self, s, t, st, device_keys=()):
@@ -283,8 +287,8 @@ class InsertsTableSet:
                 if k in base or k in have:
                     continue
                 e = _dir_bad.get(os.path.join(inserts_dir, k))
-                return e if e is not None else _exception(s, st, self.table_keys(t))
-            return _exception(s, st, self.table_keys(t))
+                return e if e is not None else _exception(s, st, self.table_keys(t), device_keys, True)
+            return _exception(s, st, self.table_keys(t), device_keys, True)
         extras, missing = {}, set()
         for _ in range(8):
             found = list(device_keys) + keys + [k for v in extras.values() if isinstance(v, str) for k in _literal_keys(v)]
@@ -367,8 +371,12 @@ class InsertsTable(InsertsTableSet):
         return True
 
 
-def _exception(s, st, keys):
+def _exception(s, st, keys, missing=None, has_dir=False):
+    """The exception the reference raises for a string the device reported as `st`; `missing`: the
+    keys the device recorded for it (IE_OPT_ERROR_KEYS), the last one is the failed lookup."""
     if st == N.E_INTERP:
+        if missing:
+            return _missing_key_exception(missing[-1], keys, has_dir)
         return InterpolationException(
             "Could not resolve an interpolation in %r. Available interpolation data keys are %r." % (s, keys))
     if st == N.E_ASSERT_BRACES:
@@ -385,6 +393,19 @@ def _exception(s, st, keys):
         return NotImplementedError("a key of %r names a path outside the inserts directory's snapshot "
                                    "('/', '.', '..' or NUL in the key): not resolved on the device path" % s)
     return RuntimeError("device status %s for %r" % (N.STATUS_NAMES[st] if st < len(N.STATUS_NAMES) else st, s))
+
+
+def _missing_key_exception(key, keys, has_dir):
+    """get_interpdata's messages for a key it does not find (py:430-467): an ARGn key, the empty
+    key, or any other (with the inserts directory it also looked in)."""
+    if _is_arg_key(key):
+        return InterpolationException("Argument interpolation key '%s' is used, but the user passed less than %s "
+                                      "program arguments." % (key, key[3:]))
+    if key == "":
+        return InterpolationException("Tried to interpolate empty string ''.")
+    detail = " in interpdata" + (" or inserts directory '%s'" % inserts_dir if has_dir and inserts_dir else "")
+    return InterpolationException("Could not find variable '%s'%s. Available interpolation data keys are %r."
+                                  % (key, detail, list(keys)))
 
 
 class VersionedInserts(dict):

@@ -65,6 +65,13 @@ def _alarm(signum, frame):
     raise _Timeout()
 
 
+def fnv1a(text):
+    h = 0xCBF29CE484222325
+    for b in text.encode("utf-8", "surrogatepass"):
+        h = ((h ^ b) * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
 def classify(ie, inserts, s):
     """Run the reference on one string; return a JSON-able record of its outcome."""
     protected = s.replace("\\{", ".〠").replace("\\}", "〠.")
@@ -75,8 +82,10 @@ def classify(ie, inserts, s):
         r = ie.interpolate_inserts(inserts, s)
     except _Timeout:
         return {"st": "DIVERGED"}
-    except ie.InterpolationException:
-        return {"st": "E_INTERP"}
+    except ie.InterpolationException as e:
+        # the message names the failed lookup's key and lists the table's keys (py:430-467): its
+        # first 96 characters and an FNV-1a of the whole
+        return {"st": "E_INTERP", "msg_head": str(e)[:96], "msg_fnv": fnv1a(str(e))}
     except AssertionError as e:
         msg = str(e)
         if "trying to interpolate variable" in msg:

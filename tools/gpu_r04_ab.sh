@@ -42,3 +42,14 @@ if [ -n "${CFG4_PMC:-}" ]; then
   IE_DEBUG_NOEVAL=1 timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/c4_fetch_noeval -o run -- python3 bench.py --config 4 --steps 2 --warmup 1 --no-cpu > $O/c4_fetch_noeval.log 2>&1 || exit $?
   timeout -s KILL 150 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $O/c4_hit -o run -- python3 bench.py --config 4 --steps 2 --warmup 1 --no-cpu > $O/c4_hit.log 2>&1 || exit $?
 fi
+# traffic passes (main build): FETCH_SIZE and WRITE_SIZE, full and IE_DEBUG_NOEVAL (the streaming
+# calibration on a known byte count), per config in TRAFFIC_CFGS
+for c in ${TRAFFIC_CFGS:-}; do
+  for ctr in FETCH_SIZE WRITE_SIZE; do
+    timeout -s KILL 150 rocprofv3 --pmc $ctr --output-format csv -d $O/tr_c${c}_$ctr -o run -- python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu > $O/tr_c${c}_$ctr.log 2>&1 || exit $?
+    IE_DEBUG_NOEVAL=1 timeout -s KILL 150 rocprofv3 --pmc $ctr --output-format csv -d $O/tr_c${c}_${ctr}_noeval -o run -- python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu > $O/tr_c${c}_${ctr}_noeval.log 2>&1 || exit $?
+  done
+done
+if [ -n "${PYTEST_ALL:-}" ]; then
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread -p no:cacheprovider > $O/pytest_all.log 2>&1 || { tail -30 $O/pytest_all.log; exit 1; }
+fi
