@@ -425,7 +425,8 @@ def main(argv=None):
     st_final = (d_st2 if cmd else d_st).to_numpy(np.uint8, n)
     names = N.STATUS_NAMES
     status_counts = {names[k]: int(c) for k, c in enumerate(np.bincount(st_final, minlength=len(names))[:len(names)]) if c}
-    assert "E_OVERFLOW" not in status_counts, "scratch too small"
+    # (diagnostic IE_DEBUG_NOEVAL runs leave statuses unwritten or verbatim: not checked)
+    assert "E_OVERFLOW" not in status_counts or os.environ.get("IE_DEBUG_NOEVAL"), "scratch too small"
 
     if dist:
         dist.barrier()

@@ -53,3 +53,13 @@ done
 if [ -n "${PYTEST_ALL:-}" ]; then
   timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread -p no:cacheprovider > $O/pytest_all.log 2>&1 || { tail -30 $O/pytest_all.log; exit 1; }
 fi
+# write split per config in WSPLIT_CFGS: WRITE_SIZE without the byte stream-out (IE_DEBUG_NOEVAL=4)
+# and without the per-string stores (=8); with STW set, the status-word variant's full WRITE_SIZE
+for c in ${WSPLIT_CFGS:-}; do
+  for m in 4 8; do
+    IE_DEBUG_NOEVAL=$m timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/ws_c${c}_m$m -o run -- python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu --replay 0 > $O/ws_c${c}_m$m.log 2>&1 || exit $?
+  done
+  if [ -n "${STW:-}" ]; then
+    IE_LIB_PATH=interpolation-engine_amd/libie_amd_$STW.so timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/ws_c${c}_$STW -o run -- python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu > $O/ws_c${c}_$STW.log 2>&1 || exit $?
+  fi
+done
