@@ -205,6 +205,9 @@ def replace_map_states(states, task, dialect="py", device=0, tables=None):
         if tables is None:
             tset.close()
     # per state: the first failing leaf in the reference's traversal order decides (py:1763-1771)
+    counts = [0] * n
+    for o in owner:
+        counts[o] += 1
     for s in range(n):
         if isinstance(names[s], BaseException):
             # output_name is interpolated before the reference's try (py:1715, 1762): its error
@@ -215,8 +218,7 @@ def replace_map_states(states, task, dialect="py", device=0, tables=None):
             e = out[s]
         else:
             skel, base = skels[s]
-            cnt = sum(1 for o in owner if o == s)
-            e = next((err[base + k] for k in range(cnt) if err[base + k] is not None), None)
+            e = next((err[base + k] for k in range(counts[s]) if err[base + k] is not None), None)
         if e is None:
             out[s] = (names[s], _rebuild(skels[s][0], done[skels[s][1]:]))
         elif isinstance(e, IE.InterpolationException):

@@ -44,9 +44,21 @@ def main():
         best = None
         for rep in range(2):
             st = [dict(s) for s in states]
+            prof = None
+            if rep and n == 10_000 and os.environ.get("IE_TASK_PROFILE"):  # where the host time goes
+                import cProfile
+                prof = cProfile.Profile()
+                prof.enable()
             t0 = time.perf_counter()
             M.run_map_tasks(st, g["tasks"])
             dt = time.perf_counter() - t0
+            if prof:
+                prof.disable()
+                import io
+                import pstats
+                buf = io.StringIO()
+                pstats.Stats(prof, stream=buf).sort_stats("tottime").print_stats(25)
+                sys.stderr.write(buf.getvalue())
             best = dt if best is None else min(best, dt)
         out["states_%d" % n] = {"us_per_state_task": [round(1e6 * x / n, 2) for x in per_task],
                                 "us_per_state_program_task_by_task": round(1e6 * sum(per_task) / n, 2),
