@@ -46,6 +46,17 @@ def _first_value(d):
     return next(iter(d.values()))
 
 
+def _pattern_range(pats, blocks, keys):
+    """The [lo, hi) of `keys` in the pattern list `pats`, appended once per distinct key list (the
+    map keys are usually the same text in every state)."""
+    t = tuple(keys)
+    r = blocks.get(t)
+    if r is None:
+        r = blocks[t] = (len(pats), len(pats) + len(t))
+        pats.extend(t)
+    return r
+
+
 def _str_results(tset, strings, ids):
     """interpolate_inserts on the device, then str() (py:1692, 1698-1699, 1722, 1738)."""
     if not strings:
@@ -84,8 +95,9 @@ def goto_map_states(states, task, dialect="py", device=0, tables=None):
         texts.append(r[0])
         keys.append(r[1:1 + m])
         vals.append(r[1 + m:])
-    # every matching test of every state in one launch: state s tries keys [s*m, (s+1)*m)
-    pending, pats, ranges = [], [], []
+    # every matching test of every state in one launch: state s tries its keys (states whose
+    # interpolated keys are the same share one block of patterns)
+    pending, pats, ranges, blocks = [], [], [], {}
     for s in range(n):
         t = texts[s]
         if isinstance(t, BaseException) and not isinstance(t, IE.InterpolationException):
@@ -104,8 +116,7 @@ def goto_map_states(states, task, dialect="py", device=0, tables=None):
             out[s] = {"goto_target": target} if target != "CONTINUE" else None
             continue
         pending.append(s)
-        ranges.append((len(pats), len(pats) + m))
-        pats.extend(keys[s])
+        ranges.append(_pattern_range(pats, blocks, keys[s]))
     if pending:
         w = Wildcards(pats, device=device, dialect=dialect)
         try:
@@ -285,11 +296,10 @@ def _replace_strings(tset, states, leaves, owner, keys, maps, m, repeat, dialect
                 cur[i] = r
                 alive.append(i)
         # 2. the first map whose key matches (py:1725-1735), all leaves in one launch
-        pats, ranges, tried = [], [], []
+        pats, ranges, tried, blocks = [], [], [], {}
         for i in alive:
             s = owner[i]
-            ranges.append((len(pats), len(pats) + key_ok[s]))
-            pats.extend(keys[s * m:s * m + key_ok[s]])
+            ranges.append(_pattern_range(pats, blocks, keys[s * m:s * m + key_ok[s]]))
             tried.append(i)
         hits = []
         if pats:
