@@ -63,3 +63,8 @@ for c in ${WSPLIT_CFGS:-}; do
     IE_LIB_PATH=interpolation-engine_amd/libie_amd_$STW.so timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/ws_c${c}_$STW -o run -- python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu > $O/ws_c${c}_$STW.log 2>&1 || exit $?
   fi
 done
+# the skeleton's instruction counts (IE_DEBUG_NOEVAL=1: stage, classify, build, stream-out only)
+if [ -n "${PMC_NOEVAL:-}" ]; then
+  IE_DEBUG_NOEVAL=1 timeout -s KILL 90 rocprofv3 --pmc $PMC --output-format csv -d $O/pmc_main_noeval -o run -- \
+    python3 bench.py --steps 3 --warmup 1 --no-cpu --reserve=32 > $O/pmc_main_noeval.log 2>&1 || exit $?
+fi
