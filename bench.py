@@ -446,6 +446,9 @@ def main(argv=None):
     x.set_timing(True)  # one more call with the library's own events for the telemetry
     if cmd and not views and os.environ.get("IE_DIAG_CMD_RESOLVE"):  # diagnostic: the command's second resolve instead
         N.check(L.ie_interpolate_device(x.h, W.table, d_u.ptr, d_uoff.ptr, n, ctypes.byref(o2)), "timing")
+    elif cmd and views and os.environ.get("IE_DIAG_CMD_RESOLVE"):  # diagnostic: the fused command (its stamps)
+        N.check(L.ie_unescape_cmd_device_views(x.h, W.table, None, d_out.ptr, d_ooff.ptr, d_olen.ptr, n, d_st.ptr,
+                                               ctypes.byref(o2)), "timing")
     else:
         N.check(resolve(), "timing")
     tm = x.timing()

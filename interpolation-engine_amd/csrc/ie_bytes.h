@@ -1,12 +1,7 @@
-// ie_bytes.h — byte and event-mask building blocks shared by the gfx950 kernels (k_resolve,
-// k_lean): LDS-typed views, unaligned LDS moves, chunk classification, 128-bit event masks.
+// ie_bytes.h — byte and event-mask building blocks of the gfx950 kernels (k_resolve,
+// k_emit_windows): LDS-typed views, unaligned LDS moves, chunk classification, 128-bit event masks.
 #pragma once
 #include "ie_device.h"
-
-// parse_chains: chains by one pass over the events (1) or by mask scans per chain (0)
-#ifndef IE_PARSE_LOOP
-#define IE_PARSE_LOOP 0
-#endif
 
 namespace ie {
 
@@ -369,66 +364,6 @@ __device__ __forceinline__ bool parse_chains(const lds_u8* tile, uint32_t p0, ui
   }
   const Ev Om{O[0] | ((uint64_t)O[1] << 32), O[2] | ((uint64_t)O[3] << 32)};
   const Ev Cm{C[0] | ((uint64_t)C[1] << 32), C[2] | ((uint64_t)C[3] << 32)};
-#if IE_PARSE_LOOP
-  // ---- 2. chains, one pass over the events in byte order (32 bits of the event mask at a time,
-  //      one event per step): a chain is a block O^d C^d (each pair has at most one child); an
-  //      open after the block's first close while it is still open (a second child), a close with
-  //      nothing open, more than kMaxTop chains, a chain deeper than kChainDepth or an open left
-  //      unclosed: not chain-shaped (the exact evaluator) ----
-  {
-    uint32_t depth = 0, dd = 0, a = 0, o0 = 0, c1 = 0, maxd = 0;
-    bool closing = false, bad = !ok;
-    nch = 0;
-#pragma unroll
-    for (int c = 0; c < kMaxTop; c++) crec[c] = cdep[c] = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      uint32_t w = bad ? 0u : (O[k] | C[k]);
-      const uint32_t ow = O[k];
-      while (__any(w != 0u)) {
-        if (w) {
-          const uint32_t b = (uint32_t)__builtin_ctz(w), pos = 32u * (uint32_t)k + b;
-          w &= w - 1u;
-          if ((ow >> b) & 1u) {  // '{'
-            bad |= closing;      // a second child of a chain still open
-            a = depth == 0u ? pos : a;
-            o0 = pos;
-            depth++;
-          } else if (depth == 0u) {  // '}' with nothing open
-            bad = true;
-          } else {  // '}'
-            if (!closing) c1 = pos, dd = depth;
-            closing = true;
-            depth--;
-            if (depth == 0u) {  // the chain is complete
-              bad |= nch >= (uint32_t)kMaxTop || dd > (uint32_t)kChainDepth;
-              const uint32_t rec = a | (c1 << 8) | (o0 << 16) | (pos << 24);
-#pragma unroll
-              for (int c = 0; c < kMaxTop; c++) {
-                crec[c] = nch == (uint32_t)c ? rec : crec[c];
-                cdep[c] = nch == (uint32_t)c ? dd : cdep[c];
-              }
-              nch++;
-              maxd = dd > maxd ? dd : maxd;
-              closing = false;
-            }
-          }
-          if (bad) w = 0u;
-        }
-      }
-    }
-    bad |= depth != 0u;
-    if (bad) nch = maxd = 0;
-    const bool whole = !bad && nch == 1u && (crec[0] & 0xFFu) == 0u && (crec[0] >> 24) == n - 1u;
-    const bool whole1 = whole && cdep[0] == 1u && !any_esc && ((crec[0] >> 8) & 0xFFu) > 1u;
-    ok = !bad && (!whole || whole1);
-    whole_out = ok && whole1;
-    Om_out = Om, Cm_out = Cm;
-    maxd_out = ok ? maxd : 0u;
-    if (!ok) nch = 0;
-    return ok;
-  }
-#endif
   // ---- 2. chains: the events of a chain-only string are blocks O^d C^d (each pair has at most
   //      one child), so chain c is located by a few mask scans: its first '{' (a), its first '}'
   //      (c1), the opens in [a, c1) (its depth), the closes before the next '{' (as many). ----

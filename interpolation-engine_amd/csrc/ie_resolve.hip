@@ -65,13 +65,6 @@
 #define IE_STATUS_WORDS 0
 #endif
 
-// views launches as persistent workgroups (as many as are resident): each loops over the tiles
-// blockIdx.x, + gridDim.x, ... and has the next tile's offsets and input chunks in flight while it
-// evaluates, builds and streams out the current one
-#ifndef IE_PERSIST
-#define IE_PERSIST 0
-#endif
-
 namespace ie {
 // everything of one tile size lives in its own namespace: ie_resolve512.hip compiles this file
 // again with 512-string tiles (IE_RBLOCK=512, IE_RNS=r512, IE_RESOLVE_WIDE)
@@ -1234,26 +1227,11 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
     __syncthreads();
     tile = s_misc[0];
   }
-  TileGeo geo = load_geo(B, tile, tid);
+  const TileGeo geo = load_geo(B, tile, tid);
   TilePrefetch<kStageV> pre;
   pre.nv = 0;
   if (tile < ntiles) pre.issue(B, geo, tid);
-  // persistent (views): this workgroup's tiles in turn; the next one's geometry loads now, its
-  // input chunks once this tile's evaluation is done
-  constexpr bool kLoop = IE_PERSIST && VIEWS;
-  while (tile < ntiles) {
-#if IE_PERSIST
-  // the lane index, opaque per tile: what derives from it is computed in the loop, not kept live
-  // across it
-  uint32_t tid_o;
-  asm volatile("v_mov_b32 %0, %1" : "=v"(tid_o) : "v"(threadIdx.x));
-  const uint32_t tid = tid_o, wave = tid >> 6, lane = tid & 63u;
-#endif
-  const uint32_t ntile = tile + gridDim.x;
-  TileGeo ngeo{0, 0, 0, 0};
-  if (kLoop && IE_PERSIST != 3) ngeo = load_geo(B, ntile, tid);  // (IE_PERSIST 1 / 2: the chunks before / after the build)
-  TilePrefetch<kStageV> npre;
-  npre.nv = 0;
+  if (tile < ntiles) {
   uint64_t t_start = 0;
   if (tid == 0) {
     if (W.stamps) t_start = __builtin_amdgcn_s_memrealtime();
@@ -1504,9 +1482,6 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
   }
   if (!IE_FEWER_BARRIERS || npend) __syncthreads();  // (nothing was written since the last barrier otherwise)
   IE_STAMP(3);
-#if IE_PERSIST == 1
-  if (kLoop && ntile < ntiles) npre.issue(B, ngeo, tid);  // in flight through the build and stream-out
-#endif
 
   // ---- 4. offsets: workgroup scan; the aggregate goes out at once ----
   const uint8_t st = s_st[tid];
@@ -1624,14 +1599,6 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
     }
   }
   IE_STAMP(4);
-#if IE_PERSIST == 2
-  if (kLoop && ntile < ntiles) npre.issue(B, ngeo, tid);  // in flight through the stream-out
-#elif IE_PERSIST == 3
-  if (kLoop && ntile < ntiles) {
-    ngeo = load_geo(B, ntile, tid);
-    npre.issue(B, ngeo, tid);
-  }
-#endif
   if (VIEWS) {
     if (tid == 0) s_red[kRBlock / 64] = lb_early;
   } else if (wave == 0) {
@@ -1692,11 +1659,6 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
   }
   IE_STAMP(5);
 #undef IE_STAMP
-  if (!kLoop) break;
-  __syncthreads();  // every wave is done with this tile's LDS
-  tile = ntile;
-  geo = ngeo;
-  pre = npre;
   }
 }
 
@@ -1780,33 +1742,12 @@ __global__ __launch_bounds__(kRBlock) void k_unesc_deferred(Batch B, Work W, uin
   }
 }
 
-// resident workgroups of k_resolve on this device (IE_PERSIST): CUs x workgroups per CU (the
-// 256-lane instance at IE_WAVES_PER_EU waves per SIMD, LDS permitting)
-uint32_t persist_grid(uint32_t tiles) {
-  thread_local int dev_cached = -1;
-  thread_local uint32_t resident = 0;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return tiles;
-  if (dev != dev_cached) {
-    int cus = 0, per_cu = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return tiles;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_resolve<false, false, true, false, false>,
-                                                     kRBlock, 0) != hipSuccess || per_cu < 1)
-      per_cu = 1;
-    resident = (uint32_t)(cus * per_cu);
-    dev_cached = dev;
-  }
-  return tiles < resident ? tiles : resident;
-}
-
 hipError_t launch_resolve_impl(const Batch& B, const Work& W, const DevTable& T, uint8_t* out, uint64_t cap,
                                hipStream_t st, bool unesc = false) {
   const uint64_t tiles = (B.n + kRBlock - 1) / kRBlock;
   if (!tiles) return hipSuccess;
   if (tiles > 0xFFFFFFFFull) return hipErrorInvalidValue;
   const uint32_t grid = (uint32_t)tiles;
-  // persistent views launches: as many workgroups as the device holds at once
-  const uint32_t vgrid = IE_PERSIST && B.out_len ? persist_grid(grid) : grid;
   const bool multi = B.table_id != nullptr;
   if (unesc) {  // the fused unescape command (views only)
     if (!B.out_len) return hipErrorInvalidValue;
@@ -1823,7 +1764,7 @@ hipError_t launch_resolve_impl(const Batch& B, const Work& W, const DevTable& T,
   const int variant = ((T.flags & TF_LONG_KEYS) ? 8 : 0) | (W.fail_commit ? 4 : 0) | (multi ? 2 : 0) | (B.out_len ? 1 : 0);
   switch (variant) {
 #define IE_LAUNCH(V, F, M, S, L) \
-  case V: hipLaunchKernelGGL((k_resolve<F, M, S, false, L>), dim3(S ? vgrid : grid), dim3(kRBlock), 0, st, B, W, T, out, cap); break;
+  case V: hipLaunchKernelGGL((k_resolve<F, M, S, false, L>), dim3(grid), dim3(kRBlock), 0, st, B, W, T, out, cap); break;
     IE_LAUNCH(0, false, false, false, false)
     IE_LAUNCH(1, false, false, true, false)
     IE_LAUNCH(2, false, true, false, false)
