@@ -5,10 +5,18 @@ bench.py reads for `roofline.traffic`.
 Which dispatches count: the k_resolve dispatches of the batch (the largest grid; the table
 build's small pre-resolution dispatch is left out). In config 4 every step launches k_resolve
 twice (the interpolation, then the unescape command's second resolve): the roofline kernel is the
-first, so every other batch-sized dispatch counts, starting with the first. FETCH_SIZE is doubled
-(MI355X_MICROARCH.md: gfx950 tallies 128-byte reads as 64 B); both counters are in KB.
+first, so every other batch-sized dispatch counts, starting with the first. Both counters are in KB.
 
-  python3 tools/pmc_traffic.py C N <fetch_dir> <write_dir> <build_id>
+Reads. gfx950 tallies a wide streaming read at half its bytes (MI355X_MICROARCH.md) but a random
+64-byte entry read at its bytes (tools/exp/gather_ubench.hip, profiles/r04/gather_calibration.txt),
+and other widths are uncalibrated, so doubling the whole FETCH_SIZE over-counts a kernel that does
+both. With a FETCH_SIZE pass of the same batch under IE_DEBUG_NOEVAL (the strings copied verbatim:
+the kernel then reads exactly the streamed bytes S = input + offsets (+ table ids), a calibration on
+a known byte count in this kernel's own access pattern), the reads are S + (FETCH - FETCH_noeval):
+the evaluation's own reads (pilots, entries, arena texts, scratch) counted as tallied. Without that
+pass: FETCH_SIZE doubled (the round-3 method, an upper bound). WRITE_SIZE as is.
+
+  python3 tools/pmc_traffic.py C N <fetch_dir> <write_dir> <build_id> [<fetch_noeval_dir> <S bytes>]
 """
 import csv
 import glob
@@ -53,6 +61,7 @@ def main():
     cfg, n, fdir, wdir, bid = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], sys.argv[5]
     fetch, nf = per_dispatch(fdir, "FETCH_SIZE", cfg)
     write, nw = per_dispatch(wdir, "WRITE_SIZE", cfg)
+    doubled = int(round((2 * fetch + write) * 1024))
     out = {
         "config": cfg,
         "n": n,
@@ -60,12 +69,24 @@ def main():
         "k_resolve_launches": [nf, nw],
         "fetch_size_kb": round(fetch),
         "write_size_kb": round(write),
-        "hbm_bytes_per_step": int(round((2 * fetch + write) * 1024)),
-        "how": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes over bench.py --config %d "
-               "(tools/gpu_round.sh); per k_resolve launch of the batch (the roofline kernel; config 4: the "
-               "first resolve of each step); FETCH_SIZE doubled per MI355X_MICROARCH.md, WRITE_SIZE as is" % cfg,
+        "hbm_bytes_per_step_fetch_doubled": doubled,
         "source": [os.path.relpath(fdir), os.path.relpath(wdir)],
     }
+    if len(sys.argv) > 7:
+        ndir, stream = sys.argv[6], int(sys.argv[7])
+        fetch0, _ = per_dispatch(ndir, "FETCH_SIZE", cfg)
+        reads = stream + (fetch - fetch0) * 1024
+        out.update({"fetch_noeval_kb": round(fetch0), "stream_read_bytes": stream, "read_bytes": int(round(reads)),
+                    "hbm_bytes_per_step": int(round(reads + write * 1024)),
+                    "how": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes over bench.py --config %d, "
+                           "per k_resolve launch of the batch (config 4: the first resolve of each step); reads = the "
+                           "streamed bytes S + (FETCH_SIZE - FETCH_SIZE under IE_DEBUG_NOEVAL), writes = WRITE_SIZE "
+                           "(tools/pmc_traffic.py docstring)" % cfg})
+        out["source"].append(os.path.relpath(ndir))
+    else:
+        out.update({"hbm_bytes_per_step": doubled,
+                    "how": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes over bench.py --config %d; "
+                           "per k_resolve launch of the batch; FETCH_SIZE doubled, WRITE_SIZE as is" % cfg})
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "pmc_traffic_cfg%d.json" % cfg)
     json.dump(out, open(path, "w"), indent=1)
     print(path, out["hbm_bytes_per_step"])
