@@ -197,6 +197,18 @@ __device__ uint8_t missing_status(const DevTable& T, const uint8_t* k, uint32_t 
 
 // lookup with the RAW value of bucket `prev` as the key (nested whole-string form,
 // py:511-512: the object itself; interp.rs:47-48: value_to_string of it)
+// the raw value's text: a str value as it is (a pre-resolved one: its raw text), any other the
+// text the reference's message shows for it (str() of the object, py:467)
+__device__ __forceinline__ const uint8_t* raw_text(const DevTable& T, const Hit& prev, uint32_t& kl) {
+  const uint8_t* k = T.arena + prev.text_off;
+  kl = prev.text_len;
+  if (prev.flags & EF_RAWALT) {  // a pre-resolved splice text: the key is the raw value
+    kl = gld((const uint32_t*)(k - 4));
+    k -= 4 + ((kl + 3u) & ~3u);
+  }
+  return k;
+}
+
 __device__ int32_t find_raw(const DevTable& T, uint32_t tid, const Hit& prev, uint8_t& st, Hit& h) {
   if (!(prev.flags & EF_KEY_STR)) {
     st = (prev.flags & EF_KEY_UNHASHABLE) ? (uint8_t)IE_E_UNHASHABLE
@@ -204,12 +216,8 @@ __device__ int32_t find_raw(const DevTable& T, uint32_t tid, const Hit& prev, ui
                                           : (uint8_t)IE_E_INTERP;
     return -1;
   }
-  const uint8_t* k = T.arena + prev.text_off;
-  uint32_t kl = prev.text_len;
-  if (prev.flags & EF_RAWALT) {  // a pre-resolved splice text: the key is the raw value
-    kl = gld((const uint32_t*)(k - 4));
-    k -= 4 + ((kl + 3u) & ~3u);
-  }
+  uint32_t kl;
+  const uint8_t* k = raw_text(T, prev, kl);
   const int32_t b = find_bytes(T, tid, k, kl, h);
   if (b < 0) st = missing_status(T, k, kl);
   return b;

@@ -164,14 +164,15 @@ struct LitOut {
   uint64_t res_len;
   uint32_t vid;
   uint32_t flags;    // the entry flags of an IE_OK_VALUE result
-  bool has_key;      // IE_NEEDS_HOST / IE_E_INTERP: res_off / res_len hold the missing key
+  const uint8_t* key;  // IE_NEEDS_HOST / IE_E_INTERP: the missing key's bytes (pool or arena), key_len
+  uint32_t key_len;
 };
 
 // One complex string, executed by all 64 lanes of a wave with uniform control flow.
 // Scratch: four regions of `cap` bytes at R[0..3] (pool offset `pool_off` of R[0]).
 __device__ LitOut w_literal(const DevTable T, uint32_t tid, const uint8_t* s, uint64_t n, uint8_t* R0,
                             uint64_t cap, uint64_t pool_off, bool max_mode) {
-  LitOut r{0, 0, 0, IE_VID_NONE, 0, false};
+  LitOut r{0, 0, 0, IE_VID_NONE, 0, nullptr, 0};
   uint8_t* R[4] = {R0, R0 + cap, R0 + 2 * cap, R0 + 3 * cap};
   uint8_t* K = R[2];
   uint8_t* K2 = R[3];
@@ -217,9 +218,9 @@ __device__ LitOut w_literal(const DevTable T, uint32_t tid, const uint8_t* s, ui
     const uint64_t k2 = w_replace<kPatRestoreClose>(K, k1, K2, cap);
     Hit E;
     const int32_t e = find_bytes(T, tid, K2, (uint32_t)k2, E);                // py:529
-    if (e < 0) {  // (the key's bytes stay at res_off: k_resolve records them for the host)
+    if (e < 0) {  // (the key stays in K2: k_resolve records it for the host)
       r.status = missing_status(T, K2, (uint32_t)k2);
-      r.res_off = pool_off + 3 * cap, r.res_len = k2, r.has_key = true;
+      r.key = K2, r.key_len = (uint32_t)k2;
       return r;
     }
     if (!(E.flags & EF_SPLICE_OK)) { r.status = IE_E_ASSERT_TYPE; return r; }  // py:530
@@ -256,13 +257,17 @@ __device__ LitOut w_literal(const DevTable T, uint32_t tid, const uint8_t* s, ui
   int32_t e = find_bytes(T, tid, K, (uint32_t)f2, cur_hit);
   if (e < 0) {
     r.status = missing_status(T, K, (uint32_t)f2);
-    r.res_off = pool_off + 2 * cap, r.res_len = f2, r.has_key = true;
+    r.key = K, r.key_len = (uint32_t)f2;
     return r;
   }
   for (uint32_t k = 1; k < W; k++) {
     Hit nh;
     e = find_raw(T, tid, cur_hit, st, nh);  // rs: every raw value has EF_KEY_STR (value_to_string)
-    if (e < 0) { r.status = st; return r; }
+    if (e < 0) {  // (the key: the raw value, as the message shows it)
+      r.status = st;
+      if (st == IE_E_INTERP) r.key = raw_text(T, cur_hit, r.key_len);
+      return r;
+    }
     cur_hit = nh;
   }
   r.status = IE_OK_VALUE;

@@ -1430,7 +1430,7 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
     uint64_t pbase = 0;
     if (lane == 0) pbase = atomicAdd((unsigned long long*)W.pool_used, (unsigned long long)(4 * rcap));
     pbase = __shfl(pbase, 0, 64);
-    LitOut r{IE_E_OVERFLOW, 0, 0, IE_VID_NONE, 0, false};
+    LitOut r{IE_E_OVERFLOW, 0, 0, IE_VID_NONE, 0, nullptr, 0};
 #ifndef IE_EXP_NOLIT
     if (rcap && pbase + 4 * rcap <= W.pool_bytes)
 #else
@@ -1440,11 +1440,11 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
                     W.lit_cap_max != 0);
     if (r.status == IE_OK_STR && (r.res_len > kLenMask || (r.res_off >> 4) > 0xFFFFFFFFull))
       r.status = IE_E_OVERFLOW;
-    if ((r.status == IE_NEEDS_HOST || (W.err_keys && r.status == IE_E_INTERP)) && W.host_keys && r.has_key) {
+    if ((r.status == IE_NEEDS_HOST || (W.err_keys && r.status == IE_E_INTERP)) && W.host_keys && r.key) {
       // the key the host must look up (get_interpdata's file fallback, py:452-461), or the missing
       // key an IE_E_INTERP message names (py:467): a record {string index, key length, key bytes}
       // in the exec's host-key list
-      const uint64_t need = 8 + ((r.res_len + 3) & ~3ull);
+      const uint64_t need = 8 + ((r.key_len + 3ull) & ~3ull);
       uint64_t at = 0;
       if (lane == 0) at = atomicAdd((unsigned long long*)W.host_keys_used, (unsigned long long)need);
       at = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(at >> 32), 0, 64) << 32) | (uint32_t)__shfl((int)(uint32_t)at, 0, 64);
@@ -1452,9 +1452,9 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
         if (lane == 0) {
           uint32_t* hdr = (uint32_t*)(W.host_keys + at);
           hdr[0] = B.out_index ? gld(B.out_index + gi) : (uint32_t)gi;
-          hdr[1] = (uint32_t)r.res_len;
+          hdr[1] = r.key_len;
         }
-        for (uint64_t k = lane; k < r.res_len; k += 64) W.host_keys[at + 8 + k] = W.pool[r.res_off + k];
+        for (uint32_t k = lane; k < r.key_len; k += 64) W.host_keys[at + 8 + k] = r.key[k];
       }
     }
 
