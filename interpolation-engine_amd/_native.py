@@ -286,14 +286,24 @@ def batch_to_python(res_ptr):
     vid = np.ctypeslib.as_array(r.value_id, shape=(n,)).copy() if n else np.zeros(0, np.uint32)
     blob = ctypes.string_at(r.bytes, r.bytes_len) if r.bytes_len else b""
     lib().ie_batch_free(res_ptr)
-    outs = [blob[int(offs[i]):int(offs[i + 1])] for i in range(n)]
+    o = offs.tolist()
+    outs = [blob[o[i]:o[i + 1]] for i in range(n)]
     return outs, st.tolist(), vid.tolist()
 
 
 def pack(strings):
     """list[str|bytes] -> (bytes blob, uint64 offsets array)"""
     import numpy as np
-    bs = [enc(s) if isinstance(s, str) else bytes(s) for s in strings]
+    memo = {}  # batches repeat strings (a task's texts once per state): each encoded once
+
+    def one(s):
+        if type(s) is str:
+            b = memo.get(s)
+            if b is None:
+                b = memo[s] = enc(s)
+            return b
+        return bytes(s)
+    bs = [one(s) for s in strings]
     offs = np.zeros(len(bs) + 1, dtype=np.uint64)
     if bs:
         offs[1:] = np.cumsum([len(b) for b in bs], dtype=np.uint64)

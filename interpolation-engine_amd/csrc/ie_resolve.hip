@@ -48,15 +48,22 @@
 #define IE_EARLY_TEXT 1
 #endif
 
-// chain jobs with wave-uniform skips (empty job slots, no template after the child, short keys)
+// chain jobs with wave-uniform skips (empty job slots, no template after the child, short keys):
+// config 3 0.856 -> 0.837 ms, VALU -7.4 % per wave (profiles/r04/ab/)
 #ifndef IE_JOBS_V2
-#define IE_JOBS_V2 0
+#define IE_JOBS_V2 1
 #endif
 
 // three workgroup barriers fewer per tile (the two scans' trailing barriers, the literal path's when
 // no string took it)
 #ifndef IE_FEWER_BARRIERS
 #define IE_FEWER_BARRIERS 0
+#endif
+
+// per-string offsets / lengths / statuses / value ids with plain (L2-merged) stores instead of
+// non-temporal ones
+#ifndef IE_DESC_TEMPORAL
+#define IE_DESC_TEMPORAL 0
 #endif
 
 // the tile's statuses as dword stores from the LDS copy (one 256-byte run per tile) instead of one
@@ -1623,9 +1630,15 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
     // (a deferred subset writes at its strings' places in the batch; a string the fused unescape
     // command deferred is written again by the deferred pass)
     const uint64_t o_i = B.out_index ? (uint64_t)gld(B.out_index + i_t) : i_t;
-    gsts(B.out_off + o_i, base + local);
-    if (VIEWS) gsts(B.out_len + o_i, s_st[tid_t] == IE_OK_STR ? s_olen[tid_t] : 0u);
-    if (!st_words) gsts(B.status + o_i, st);
+#if IE_DESC_TEMPORAL
+#define IE_DST gst
+#else
+#define IE_DST gsts
+#endif
+    IE_DST(B.out_off + o_i, base + local);
+    if (VIEWS) IE_DST(B.out_len + o_i, s_st[tid_t] == IE_OK_STR ? s_olen[tid_t] : 0u);
+    if (!st_words) IE_DST(B.status + o_i, st);
+#undef IE_DST
     if (st == IE_OK_VALUE || st == IE_RECURSE) gst(B.value_id + o_i, s_olen[tid_t]);
   }
   if (!VIEWS && last == B.n && tid == 0) {

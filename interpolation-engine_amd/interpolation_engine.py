@@ -244,12 +244,20 @@ class InsertsTableSet:
                                                      offs.ctypes.data, len(strings), ctypes.byref(res)),
                     "ie_interpolate_batch_ids")
         outs, sts, vids = N.batch_to_python(res)
-        return [(st, N.dec(o) if st == N.OK_STR else (vids[i] if st == N.OK_VALUE else None))
+        memo = {}  # (many states give the same text: each distinct output decoded once)
+
+        def text(o):
+            t = memo.get(o)
+            if t is None:
+                t = memo[o] = N.dec(o)
+            return t
+        return [(st, text(o) if st == N.OK_STR else (vids[i] if st == N.OK_VALUE else None))
                 for i, (o, st) in enumerate(zip(outs, sts))]
 
     def results(self, strings, table_ids=None):
         """Like interpolate_inserts on each string; failures come back as exception instances."""
-        ids = [0] * len(strings) if table_ids is None else list(table_ids)
+        ids = [0] * len(strings) if table_ids is None else (
+            table_ids.tolist() if hasattr(table_ids, "tolist") else list(table_ids))
         out = []
         got = self.run(strings, table_ids)
         # the keys the device could not look up (IE_NEEDS_HOST), also those built from values, and

@@ -59,7 +59,7 @@ def _pattern_range(pats, blocks, keys):
 
 def _str_results(tset, strings, ids):
     """interpolate_inserts on the device, then str() (py:1692, 1698-1699, 1722, 1738)."""
-    if not strings:
+    if not len(strings):
         return []
     return [r if isinstance(r, BaseException) else str(r) for r in tset.results(strings, ids)]
 
@@ -79,13 +79,9 @@ def goto_map_states(states, task, dialect="py", device=0, tables=None):
     tset = tables or IE.InsertsTableSet(states, dialect=dialect, device=device)
     try:
         # value text, then all keys, then all values, for every state in one batch
-        strings, ids = [], []
-        for s in range(n):
-            strings.append(task["text"])
-            strings.extend(_first_key(d) for d in maps)
-            strings.extend(_first_value(d) for d in maps)
-            ids.extend([s] * (1 + 2 * m))
-        res = _str_results(tset, strings, ids)
+        block = [task["text"]] + [_first_key(d) for d in maps] + [_first_value(d) for d in maps]
+        import numpy as np
+        res = _str_results(tset, block * n, np.repeat(np.arange(n, dtype=np.uint32), 1 + 2 * m))
     finally:
         if tables is None:
             tset.close()

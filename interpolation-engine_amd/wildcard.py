@@ -69,13 +69,17 @@ class Wildcards:
     def first_match(self, strings, ranges=None):
         """[(index of the first matching wildcard or -1, [captures as str])] per string."""
         match, ncap, caps = self.match_raw(strings, ranges)
+        match, ncap = match.tolist(), ncap.tolist()
         out = []
         for i, s in enumerate(strings):
-            b = N.enc(s) if isinstance(s, str) else bytes(s)
             if match[i] < 0:
                 out.append((-1, []))
                 continue
-            out.append((int(match[i]), [N.dec(b[int(a):int(a) + int(ln)]) for a, ln in caps[i, :int(ncap[i])]]))
+            if not ncap[i]:
+                out.append((match[i], []))
+                continue
+            b = N.enc(s) if isinstance(s, str) else bytes(s)
+            out.append((match[i], [N.dec(b[a:a + ln]) for a, ln in caps[i, :ncap[i]].tolist()]))
         return out
 
 
