@@ -68,3 +68,10 @@ if [ -n "${PMC_NOEVAL:-}" ]; then
   IE_DEBUG_NOEVAL=1 timeout -s KILL 90 rocprofv3 --pmc $PMC --output-format csv -d $O/pmc_main_noeval -o run -- \
     python3 bench.py --steps 3 --warmup 1 --no-cpu --reserve=32 > $O/pmc_main_noeval.log 2>&1 || exit $?
 fi
+# WRITE_SIZE per variant (WRITE_VARIANTS) for the configs in WRITE_CFGS
+for v in ${WRITE_VARIANTS:-}; do
+  if [ "$v" = main ]; then LIBP=""; else LIBP=interpolation-engine_amd/libie_amd_$v.so; fi
+  for c in ${WRITE_CFGS:-5 3}; do
+    IE_LIB_PATH=$LIBP timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/wv_${v}_c$c -o run -- python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu --replay 0 > $O/wv_${v}_c$c.log 2>&1 || exit $?
+  done
+done
