@@ -140,6 +140,7 @@ struct ie_exec {
   DevBuf host_keys;
   std::vector<uint8_t> hk;
   bool hk_host = false;
+  bool hk_dirty = true;  // the device list may hold records (a pass with host keys enabled ran since the reset)
   // the fused unescape command's deferred pass: list, views into the pool, table ids
   DevBuf u_list, u_off, u_len, u_tid;
   // host-API staging
@@ -347,7 +348,8 @@ Work make_work(ie_exec* x, uint64_t* total) {
 // d_out_len / d_in_len (k_resolve only): views output / views input (ie_interpolate_device_views)
 // a device pass starts a new host-key list
 int reset_host_keys(ie_exec* x) {
-  if (x->host_keys.p) IE_HIP(hipMemsetAsync(x->host_keys.p, 0, 16, x->stream));
+  if (x->host_keys.p && x->hk_dirty) IE_HIP(hipMemsetAsync(x->host_keys.p, 0, 16, x->stream));
+  x->hk_dirty = false;
   return IE_SUCCESS;
 }
 
@@ -409,6 +411,7 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
     W.host_keys = (uint8_t*)x->host_keys.p + 16;
     W.host_keys_used = (uint64_t*)x->host_keys.p;
     W.host_keys_cap = x->host_keys.bytes - 16;
+    x->hk_dirty = true;
   }
   W.err_keys = op == kOpInterp && x->opt_err_keys ? 1u : 0u;
   W.recurse = op == kOpInterp && x->in_cmd && t->dialect == IE_DIALECT_PY ? 1u : 0u;
@@ -673,7 +676,12 @@ int run_host(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, const 
   for (uint64_t i = 0; i < n; i++)
     if (b->status[i] != IE_OK_VALUE && b->status[i] != IE_RECURSE) b->value_id[i] = IE_VID_NONE;
   std::vector<uint8_t> recs;  // this batch's host-key records (the device pass above)
-  if (op == kOpInterp && t && ((t->dev.flags & TF_HAS_DIR) || x->opt_err_keys) && (rc = read_host_keys(x, recs))) {
+  // (records exist only for strings that ended IE_NEEDS_HOST or IE_E_INTERP: no read-back, and no
+  // reset before the next pass, when none did)
+  bool any_keys = false;
+  for (uint64_t i = 0; i < n && !any_keys; i++) any_keys = b->status[i] == IE_NEEDS_HOST || b->status[i] == IE_E_INTERP;
+  if (!any_keys) x->hk_dirty = false;
+  if (any_keys && op == kOpInterp && t && ((t->dev.flags & TF_HAS_DIR) || x->opt_err_keys) && (rc = read_host_keys(x, recs))) {
     ie_batch_free(b);
     return rc;
   }

@@ -60,18 +60,6 @@
 #define IE_FEWER_BARRIERS 0
 #endif
 
-// per-string offsets / lengths / statuses / value ids with plain (L2-merged) stores instead of
-// non-temporal ones
-#ifndef IE_DESC_TEMPORAL
-#define IE_DESC_TEMPORAL 0
-#endif
-
-// the tile's statuses as dword stores from the LDS copy (one 256-byte run per tile) instead of one
-// byte store per lane
-#ifndef IE_STATUS_WORDS
-#define IE_STATUS_WORDS 0
-#endif
-
 namespace ie {
 // everything of one tile size lives in its own namespace: ie_resolve512.hip compiles this file
 // again with 512-string tiles (IE_RBLOCK=512, IE_RNS=r512, IE_RESOLVE_WIDE)
@@ -1214,7 +1202,7 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
   __shared__ __attribute__((aligned(16))) uint8_t s_in[kRTileBytes + 48];
   __shared__ __attribute__((aligned(16))) uint8_t s_u[kUnionLds];
   __shared__ uint32_t s_olen[kRBlock];  // output length; the value id for IE_OK_VALUE strings
-  __shared__ __attribute__((aligned(4))) uint8_t s_st[kRBlock];
+  __shared__ uint8_t s_st[kRBlock];
   __shared__ uint16_t s_pend[kRBlock];
   __shared__ uint32_t s_misc[4];  // tile, pending count, defer slot
   __shared__ uint64_t s_red[kRBlock / 64 + 2];
@@ -1619,26 +1607,13 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
   uint32_t tid_t;
   asm volatile("v_mov_b32 %0, %1" : "=v"(tid_t) : "v"(tid));
   const uint64_t i_t = first + tid_t;
-  // (a whole tile's statuses in input order at a 4-aligned place: dword stores of the LDS copy)
-  const bool st_words = IE_STATUS_WORDS && !B.out_index && (((uintptr_t)(B.status + first)) & 3u) == 0u;
-  if (st_words && !(W.debug_noeval & 8u)) {
-    const uint32_t nst = (uint32_t)(last - first), nw = nst >> 2;
-    if (tid_t < nw) gsts((uint32_t*)(B.status + first) + tid_t, ((const lds_u32*)(const lds_u8*)s_st)[tid_t]);
-    else if (tid_t >= (nst & ~3u) && tid_t < nst) gsts(B.status + i_t, st);  // the last 1-3
-  }
   if (i_t < B.n && !(W.debug_noeval & 8u)) {  // (diagnostic bit 3: no per-string stores, a traffic split)
     // (a deferred subset writes at its strings' places in the batch; a string the fused unescape
     // command deferred is written again by the deferred pass)
     const uint64_t o_i = B.out_index ? (uint64_t)gld(B.out_index + i_t) : i_t;
-#if IE_DESC_TEMPORAL
-#define IE_DST gst
-#else
-#define IE_DST gsts
-#endif
-    IE_DST(B.out_off + o_i, base + local);
-    if (VIEWS) IE_DST(B.out_len + o_i, s_st[tid_t] == IE_OK_STR ? s_olen[tid_t] : 0u);
-    if (!st_words) IE_DST(B.status + o_i, st);
-#undef IE_DST
+    gsts(B.out_off + o_i, base + local);
+    if (VIEWS) gsts(B.out_len + o_i, s_st[tid_t] == IE_OK_STR ? s_olen[tid_t] : 0u);
+    gsts(B.status + o_i, st);
     if (st == IE_OK_VALUE || st == IE_RECURSE) gst(B.value_id + o_i, s_olen[tid_t]);
   }
   if (!VIEWS && last == B.n && tid == 0) {

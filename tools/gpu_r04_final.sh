@@ -40,6 +40,7 @@ for c in ${CONFIGS:-3 2 4 5}; do
   timeout -k 10 300 python -u bench.py --config $c > $O/bench_cfg$c.log 2>&1 || { tail -20 $O/bench_cfg$c.log; exit 1; }
   tail -1 $O/bench_cfg$c.log | cut -c1-300
 done
+[ -n "${NOHOST:-}" ] && exit 0
 timeout -k 10 300 python -u tools/mirror_latency.py > $O/mirror_latency.json 2> $O/mirror.err || { tail -20 $O/mirror.err; exit 1; }
 timeout -k 10 600 python -u tools/task_times.py > $O/task_times.json 2> $O/task_times.err || { tail -20 $O/task_times.err; exit 1; }
 timeout -k 10 300 python -u bench.py --gpus 2 --device 0 --steps 10 --warmup 2 --no-cpu > $O/bench_2ranks.log 2>&1 || { tail -20 $O/bench_2ranks.log; exit 1; }
