@@ -54,6 +54,13 @@
 #define IE_JOBS_V2 1
 #endif
 
+// the fused unescape command unescapes the staged tile string by string, in place, after the
+// classification (only the strings holding a '\\' do work; their chunks are classified again),
+// instead of compacting the whole stage before it (unescape_stage: a block scan and four barriers)
+#ifndef IE_UNESC_V2
+#define IE_UNESC_V2 1
+#endif
+
 // three workgroup barriers fewer per tile (the two scans' trailing barriers, the literal path's when
 // no string took it)
 #ifndef IE_FEWER_BARRIERS
@@ -1260,7 +1267,7 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
   {
     pre.commit((uint4*)s_in, tid);
     __syncthreads();
-    if (UNESC) unescape_stage<kStageV>(pre.v, (lds_u8*)s_in, s_u, s_red, nv, lane_staged, p0, sn, tid);
+    if (UNESC && !IE_UNESC_V2) unescape_stage<kStageV>(pre.v, (lds_u8*)s_in, s_u, s_red, nv, lane_staged, p0, sn, tid);
     for (uint32_t c0 = 0; c0 < nv; c0 += kRBlock) {  // uniform trip count: ballots below
       const uint32_t c = c0 + tid;
       bool odd = false, esc = false;
@@ -1276,6 +1283,42 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
     if (tid < 10) s_cm[nv + tid] = 0;  // the event windows read past the last chunk
   }
   __syncthreads();
+#if IE_UNESC_V2
+  if (UNESC) {
+    // recursive_unescape (py:1436-1440: '\{' -> '{', then '\}' -> '}'; a removed '\' never makes
+    // a new pair, so one left-to-right pass equals the two replaces) on this lane's staged string,
+    // in place: only strings whose chunks hold a '\' have anything to do
+    const uint32_t ca = p0 >> 4, cz = sn ? (p0 + (uint32_t)sn - 1u) >> 4 : ca;
+    bool esc_in = false;
+    if (lane_staged && sn)
+      for (uint32_t c = ca; c <= cz && !esc_in; c++) esc_in = ((s_esc[c >> 5] >> (c & 31u)) & 1u) != 0u;
+    uint32_t nsn = (uint32_t)sn;
+    if (esc_in) {
+      lds_u8* const b = (lds_u8*)s_in + p0;
+      uint32_t w = 0;
+      for (uint32_t k = 0; k < (uint32_t)sn; k++) {
+        const uint8_t ch = b[k];
+        const uint8_t nx = k + 1u < (uint32_t)sn ? b[k + 1u] : (uint8_t)0;
+        if (!(ch == '\\' && (nx == '{' || nx == '}'))) b[w++] = ch;  // w <= k: in place
+      }
+      nsn = w;
+    }
+    __syncthreads();  // every string's bytes are final
+    if (esc_in && nsn != (uint32_t)sn) {
+      // this string's chunks again (a chunk shared with a neighbour: the same value from the same
+      // final bytes); the odd / escape bits only ever gain bits (a moved '\' or 0xE3 byte)
+      const uint32_t cn = nsn ? (p0 + nsn - 1u) >> 4 : ca;
+      for (uint32_t c = ca; c <= cn; c++) {
+        bool odd = false, esc = false;
+        s_cm[c] = chunk_classify((const lds_u32*)(lds_u8*)s_in + 4 * c, odd, esc);
+        if (odd) atomicOr((uint32_t*)(s_odd + (c >> 5)), 1u << (c & 31u));
+        if (esc) atomicOr((uint32_t*)(s_esc + (c >> 5)), 1u << (c & 31u));
+      }
+    }
+    sn = nsn;
+    __syncthreads();
+  }
+#endif
   IE_STAMP(1);
 
   // ---- 2. evaluate ----
