@@ -1293,15 +1293,24 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
     if (lane_staged && sn)
       for (uint32_t c = ca; c <= cz && !esc_in; c++) esc_in = ((s_esc[c >> 5] >> (c & 31u)) & 1u) != 0u;
     uint32_t nsn = (uint32_t)sn;
-    if (esc_in) {
-      lds_u8* const b = (lds_u8*)s_in + p0;
+    // the wave takes such strings one at a time, 64 bytes per step: a byte is kept unless it is a
+    // '\' before a brace; the kept bytes move down to their rank (in place: a step writes only
+    // below its own block, which every lane has read)
+    for (uint64_t todo = __ballot(esc_in); todo; todo &= todo - 1ull) {
+      const uint32_t j = (uint32_t)__builtin_ctzll(todo);
+      const uint32_t jp0 = (uint32_t)__shfl((int)p0, (int)j, 64), jsn = (uint32_t)__shfl((int)(uint32_t)sn, (int)j, 64);
+      lds_u8* const b = (lds_u8*)s_in + jp0;
       uint32_t w = 0;
-      for (uint32_t k = 0; k < (uint32_t)sn; k++) {
-        const uint8_t ch = b[k];
-        const uint8_t nx = k + 1u < (uint32_t)sn ? b[k + 1u] : (uint8_t)0;
-        if (!(ch == '\\' && (nx == '{' || nx == '}'))) b[w++] = ch;  // w <= k: in place
+      for (uint32_t k0 = 0; k0 < jsn; k0 += 64) {
+        const uint32_t k = k0 + lane;
+        const uint8_t ch = k < jsn ? b[k] : (uint8_t)0;
+        const uint8_t nx = k + 1u < jsn ? b[k + 1u] : (uint8_t)0;
+        const bool keep = k < jsn && !(ch == '\\' && (nx == '{' || nx == '}'));
+        const uint64_t km = __ballot(keep);
+        if (keep) b[w + (uint32_t)__popcll(km & ((1ull << lane) - 1ull))] = ch;
+        w += (uint32_t)__popcll(km);
       }
-      nsn = w;
+      if (lane == j) nsn = w;
     }
     __syncthreads();  // every string's bytes are final
     if (esc_in && nsn != (uint32_t)sn) {
