@@ -54,13 +54,6 @@
 #define IE_JOBS_V2 1
 #endif
 
-// the fused unescape command unescapes the staged tile string by string, in place, after the
-// classification (only the strings holding a '\\' do work; their chunks are classified again),
-// instead of compacting the whole stage before it (unescape_stage: a block scan and four barriers)
-#ifndef IE_UNESC_V2
-#define IE_UNESC_V2 1
-#endif
-
 // three workgroup barriers fewer per tile (the two scans' trailing barriers, the literal path's when
 // no string took it)
 #ifndef IE_FEWER_BARRIERS
@@ -1008,102 +1001,6 @@ __device__ __forceinline__ bool maybe_simple(const uint8_t* s, uint32_t n) {
   return l < n && s[l] == '}';
 }
 
-// The unescape command's recursive_unescape (py:1665 / rust-project/src/runtime.rs:1046), done on
-// the staged tile before it is resolved. recursive_unescape is two str.replace passes ('\\{' -> '{',
-// then '\\}' -> '}'); neither can create a pair for the other (a removed '\\' leaves a brace
-// behind the byte before it), so together they drop exactly the '\\' bytes followed by a brace
-// within the same string. The drops are marked per 16-byte chunk (bit k: byte k is dropped), a
-// '\\' that ends its string is restored (the brace after it is the next string's), an exclusive scan
-// gives every chunk's shift, and the chunks, still in the prefetch registers, are written back to
-// the stage compacted. Each lane then moves its string's start and length to the compacted stage
-// (only staged strings: the others are the deferred pass's). Every lane calls it (barriers).
-template <int MAXV>
-__device__ __attribute__((always_inline)) void unescape_stage(const uint4 (&v)[MAXV], lds_u8* stage, uint8_t* s_u,
-                                                             uint64_t* s_red, uint32_t nv, bool staged, uint32_t& p0,
-                                                             uint64_t& sn, uint32_t tid) {
-  lds_u32* const drop = (lds_u32*)(lds_u8*)s_u;                 // kChunks + 1 words
-  lds_u32* const dpre = (lds_u32*)(lds_u8*)s_u + kChunks + 8;   // kChunks + 1 words
-  auto mask_of = [](uint32_t x, uint32_t c) {  // top bit of each byte set where the byte is c
-    const uint32_t y = x ^ (c * 0x01010101u);
-    return ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u;
-  };
-  // 1. drop masks
-#pragma unroll
-  for (int k = 0; k < MAXV; k++) {
-    const uint32_t c = tid + (uint32_t)k * kRBlock;
-    if (c < nv) {
-      const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
-      uint32_t bs = 0, br = 0;
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        bs |= nib(mask_of(w[q], '\\')) << (4 * q);
-        br |= nib(mask_of(w[q], '{') | mask_of(w[q], '}')) << (4 * q);
-      }
-      const uint8_t nx = c + 1 < nv ? stage[16 * (c + 1)] : (uint8_t)0;
-      br |= (nx == '{' || nx == '}') ? 0x10000u : 0u;
-      // the whole stage: a views batch stages strings past the tile's span too (the bytes of no
-      // string move with the rest, harmlessly)
-      drop[c] = bs & (br >> 1) & 0xFFFFu;
-    }
-  }
-  if (tid == 0) drop[nv] = 0;
-  __syncthreads();
-  // 2. a '\\' that ends its string precedes the next string's brace: kept
-  if (staged && sn) {
-    const uint32_t x = p0 + (uint32_t)sn - 1u;
-    if ((drop[x >> 4] >> (x & 15u)) & 1u) atomicAnd((uint32_t*)(drop + (x >> 4)), ~(1u << (x & 15u)));
-  }
-  __syncthreads();
-  // 3. drops before each chunk (each lane a contiguous run of chunks)
-  const uint32_t R = (nv + kRBlock - 1) / kRBlock, c_lo = min(tid * R, nv), c_hi = min(c_lo + R, nv);
-  uint32_t cnt = 0;
-  for (uint32_t c = c_lo; c < c_hi; c++) cnt += (uint32_t)__popc(drop[c]);
-  uint64_t total;
-  uint32_t run = (uint32_t)block_scan(cnt, s_red, &total);
-  for (uint32_t c = c_lo; c < c_hi; c++) {
-    dpre[c] = run;
-    run += (uint32_t)__popc(drop[c]);
-  }
-  if (tid == 0) dpre[nv] = (uint32_t)total;
-  __syncthreads();
-  // 4. the chunks back to the stage, compacted (sources in registers: in place is safe)
-  if (total) {
-#pragma unroll
-    for (int k = 0; k < MAXV; k++) {
-      const uint32_t c = tid + (uint32_t)k * kRBlock;
-      const uint32_t dm = c < nv ? drop[c] : 0u;
-      const uint32_t sh = c < nv ? dpre[c] : 0u;
-      if (c < nv && sh) {
-        const uint32_t w[8] = {v[k].x, v[k].y, v[k].z, v[k].w, 0u, 0u, 0u, 0u};
-        if (dm == 0) {
-          put_words(stage + 16 * c - sh, w, 16);
-        } else {
-          uint32_t o = 16 * c - sh;
-          for (uint32_t b = 0; b < 16; b++)
-            if (!((dm >> b) & 1u)) stage[o++] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
-        }
-      } else if (c < nv && dm) {  // no shift yet, but drops inside this chunk
-        const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
-        uint32_t o = 16 * c;
-        for (uint32_t b = 0; b < 16; b++)
-          if (!((dm >> b) & 1u)) stage[o++] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
-      }
-    }
-  }
-  __syncthreads();
-  // 5. this string in the compacted stage
-  if (staged && total) {
-    auto D = [&](uint32_t x) {
-      const uint32_t c = x >> 4;
-      return dpre[c] + (uint32_t)__popc(drop[c] & ((1u << (x & 15u)) - 1u));
-    };
-    const uint32_t e = p0 + (uint32_t)sn;
-    const uint32_t a = p0 - D(p0);
-    sn = (uint64_t)(e - D(e) - a);
-    p0 = a;
-  }
-}
-
 // The deferred tiles' bytes (see k_resolve): one workgroup per deferred tile at a time. Each
 // lane rebuilds its string's pieces from the stored descriptor (template runs from the input in
 // global memory, values from the table or the literal pool) and the tile's output goes through
@@ -1194,9 +1091,10 @@ __global__ __launch_bounds__(kRBlock) void k_emit_windows(Batch B0, Work W, DevT
 // give the reference's results; the host picks per batch stream (ie_host.cpp, "fail commit").
 // VIEWS: B.out_len set; each tile claims its output range with one atomic on W.cursor (no
 // global order, no look-back) and writes each string's start and length.
-// UNESC (with VIEWS): the unescape command's resolve, fused with its recursive_unescape: the tile
-// is unescaped in the LDS stage (unescape_stage) and then resolved; strings that cannot be finished
-// there (not staged, or needing the literal path) go to W.udefer_list for the deferred pass.
+// UNESC (with VIEWS): the unescape command's resolve, fused with its recursive_unescape: each
+// staged string is unescaped in place in the LDS stage (after the classification; its chunks are
+// classified again) and then resolved; strings that cannot be finished there (not staged, or
+// needing the literal path) go to W.udefer_list for the deferred pass.
 template <bool FAILC, bool MULTI, bool VIEWS, bool UNESC = false, bool LK = false>
 __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES_PER_EU))) void k_resolve(Batch B0, Work W, DevTable T, uint8_t* out,
                                                     uint64_t cap) {
@@ -1267,7 +1165,6 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
   {
     pre.commit((uint4*)s_in, tid);
     __syncthreads();
-    if (UNESC && !IE_UNESC_V2) unescape_stage<kStageV>(pre.v, (lds_u8*)s_in, s_u, s_red, nv, lane_staged, p0, sn, tid);
     for (uint32_t c0 = 0; c0 < nv; c0 += kRBlock) {  // uniform trip count: ballots below
       const uint32_t c = c0 + tid;
       bool odd = false, esc = false;
@@ -1283,11 +1180,12 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
     if (tid < 10) s_cm[nv + tid] = 0;  // the event windows read past the last chunk
   }
   __syncthreads();
-#if IE_UNESC_V2
   if (UNESC) {
-    // recursive_unescape (py:1436-1440: '\{' -> '{', then '\}' -> '}'; a removed '\' never makes
-    // a new pair, so one left-to-right pass equals the two replaces) on this lane's staged string,
-    // in place: only strings whose chunks hold a '\' have anything to do
+    // the fused unescape command: recursive_unescape (py:1436-1440, runtime.rs:1046: '\{' -> '{',
+    // then '\}' -> '}'; a removed '\' leaves a brace behind the byte before it, never a new pair,
+    // so one left-to-right pass equals the two replaces; a '\' that ends its string stays, the
+    // brace after it being the next string's) on this lane's staged string, in place: only strings
+    // whose chunks hold a '\' have anything to do
     const uint32_t ca = p0 >> 4, cz = sn ? (p0 + (uint32_t)sn - 1u) >> 4 : ca;
     bool esc_in = false;
     if (lane_staged && sn)
@@ -1327,7 +1225,6 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
     sn = nsn;
     __syncthreads();
   }
-#endif
   IE_STAMP(1);
 
   // ---- 2. evaluate ----
