@@ -1164,7 +1164,61 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
   const bool lane_staged = p0 + sn <= 16ull * nv;
   {
     pre.commit((uint4*)s_in, tid);
+    if (UNESC) {
+      // the fused unescape command: which staged chunks hold a '\\' (from the prefetch registers)
+#pragma unroll
+      for (int k = 0; k < kStageV; k++) {
+        const uint32_t c = tid + (uint32_t)k * kRBlock;
+        uint32_t hz = 0;
+        if (c < pre.nv) {
+          const uint32_t w4[4] = {pre.v[k].x, pre.v[k].y, pre.v[k].z, pre.v[k].w};
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            const uint32_t y = w4[q] ^ 0x5C5C5C5Cu;
+            hz |= (y - 0x01010101u) & ~y & 0x80808080u;
+          }
+        }
+        const uint64_t eb = __ballot(hz != 0u);
+        if (lane == 0 && (uint32_t)k * kRBlock < pre.nv) {
+          s_esc[(k * kRBlock + 64 * wave) >> 5] = (uint32_t)eb;
+          s_esc[((k * kRBlock + 64 * wave) >> 5) + 1] = (uint32_t)(eb >> 32);
+        }
+      }
+    }
     __syncthreads();
+    if (UNESC) {
+      // recursive_unescape (py:1436-1440, runtime.rs:1046: '\\{' -> '{', then '\\}' -> '}'; a
+      // removed '\\' leaves a brace behind the byte before it, never a new pair, so one
+      // left-to-right pass equals the two replaces; a '\\' that ends its string stays, the brace
+      // after it being the next string's) on this lane's staged string, in place, before the
+      // classification: only strings whose chunks hold a '\\' have anything to do
+      const uint32_t ca = p0 >> 4, cz = sn ? (p0 + (uint32_t)sn - 1u) >> 4 : ca;
+      bool esc_in = false;
+      if (lane_staged && sn)
+        for (uint32_t c = ca; c <= cz && !esc_in; c++) esc_in = ((s_esc[c >> 5] >> (c & 31u)) & 1u) != 0u;
+      uint32_t nsn = (uint32_t)sn;
+      // the wave takes such strings one at a time, 64 bytes per step: a byte is kept unless it is
+      // a '\\' before a brace; the kept bytes move down to their rank (in place: a step writes
+      // only below its own block, which every lane has read)
+      for (uint64_t todo = __ballot(esc_in); todo; todo &= todo - 1ull) {
+        const uint32_t j = (uint32_t)__builtin_ctzll(todo);
+        const uint32_t jp0 = (uint32_t)__shfl((int)p0, (int)j, 64), jsn = (uint32_t)__shfl((int)(uint32_t)sn, (int)j, 64);
+        lds_u8* const b = (lds_u8*)s_in + jp0;
+        uint32_t w = 0;
+        for (uint32_t k0 = 0; k0 < jsn; k0 += 64) {
+          const uint32_t k = k0 + lane;
+          const uint8_t ch = k < jsn ? b[k] : (uint8_t)0;
+          const uint8_t nx = k + 1u < jsn ? b[k + 1u] : (uint8_t)0;
+          const bool keep = k < jsn && !(ch == '\\' && (nx == '{' || nx == '}'));
+          const uint64_t km = __ballot(keep);
+          if (keep) b[w + (uint32_t)__popcll(km & ((1ull << lane) - 1ull))] = ch;
+          w += (uint32_t)__popcll(km);
+        }
+        if (lane == j) nsn = w;
+      }
+      sn = nsn;
+      __syncthreads();  // every string's bytes are final: the classification sees the unescaped stage
+    }
     for (uint32_t c0 = 0; c0 < nv; c0 += kRBlock) {  // uniform trip count: ballots below
       const uint32_t c = c0 + tid;
       bool odd = false, esc = false;
@@ -1180,51 +1234,6 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
     if (tid < 10) s_cm[nv + tid] = 0;  // the event windows read past the last chunk
   }
   __syncthreads();
-  if (UNESC) {
-    // the fused unescape command: recursive_unescape (py:1436-1440, runtime.rs:1046: '\{' -> '{',
-    // then '\}' -> '}'; a removed '\' leaves a brace behind the byte before it, never a new pair,
-    // so one left-to-right pass equals the two replaces; a '\' that ends its string stays, the
-    // brace after it being the next string's) on this lane's staged string, in place: only strings
-    // whose chunks hold a '\' have anything to do
-    const uint32_t ca = p0 >> 4, cz = sn ? (p0 + (uint32_t)sn - 1u) >> 4 : ca;
-    bool esc_in = false;
-    if (lane_staged && sn)
-      for (uint32_t c = ca; c <= cz && !esc_in; c++) esc_in = ((s_esc[c >> 5] >> (c & 31u)) & 1u) != 0u;
-    uint32_t nsn = (uint32_t)sn;
-    // the wave takes such strings one at a time, 64 bytes per step: a byte is kept unless it is a
-    // '\' before a brace; the kept bytes move down to their rank (in place: a step writes only
-    // below its own block, which every lane has read)
-    for (uint64_t todo = __ballot(esc_in); todo; todo &= todo - 1ull) {
-      const uint32_t j = (uint32_t)__builtin_ctzll(todo);
-      const uint32_t jp0 = (uint32_t)__shfl((int)p0, (int)j, 64), jsn = (uint32_t)__shfl((int)(uint32_t)sn, (int)j, 64);
-      lds_u8* const b = (lds_u8*)s_in + jp0;
-      uint32_t w = 0;
-      for (uint32_t k0 = 0; k0 < jsn; k0 += 64) {
-        const uint32_t k = k0 + lane;
-        const uint8_t ch = k < jsn ? b[k] : (uint8_t)0;
-        const uint8_t nx = k + 1u < jsn ? b[k + 1u] : (uint8_t)0;
-        const bool keep = k < jsn && !(ch == '\\' && (nx == '{' || nx == '}'));
-        const uint64_t km = __ballot(keep);
-        if (keep) b[w + (uint32_t)__popcll(km & ((1ull << lane) - 1ull))] = ch;
-        w += (uint32_t)__popcll(km);
-      }
-      if (lane == j) nsn = w;
-    }
-    __syncthreads();  // every string's bytes are final
-    if (esc_in && nsn != (uint32_t)sn) {
-      // this string's chunks again (a chunk shared with a neighbour: the same value from the same
-      // final bytes); the odd / escape bits only ever gain bits (a moved '\' or 0xE3 byte)
-      const uint32_t cn = nsn ? (p0 + nsn - 1u) >> 4 : ca;
-      for (uint32_t c = ca; c <= cn; c++) {
-        bool odd = false, esc = false;
-        s_cm[c] = chunk_classify((const lds_u32*)(lds_u8*)s_in + 4 * c, odd, esc);
-        if (odd) atomicOr((uint32_t*)(s_odd + (c >> 5)), 1u << (c & 31u));
-        if (esc) atomicOr((uint32_t*)(s_esc + (c >> 5)), 1u << (c & 31u));
-      }
-    }
-    sn = nsn;
-    __syncthreads();
-  }
   IE_STAMP(1);
 
   // ---- 2. evaluate ----
