@@ -188,21 +188,35 @@ class InsertsTableSet:
         n = len(changes)
         if n == 0:
             return True
-        kb, tb, kinds, tids, vids = [], [], np.zeros(n, np.int32), np.zeros(n, np.uint32), np.zeros(n, np.uint32)
-        for i, (t, k, v) in enumerate(changes):
+        kb, tb, kinds, tids, vids = [], [], [], [], []
+        nd, kmemo, values = len(self.dicts), {}, self.values
+        for t, k, v in changes:
             if type(k) is not str:
                 raise TypeError("insert keys must be str")
-            if t < 0 or t >= len(self.dicts):
+            if t < 0 or t >= nd:
                 raise IndexError("dict index beyond the table set")
-            tids[i] = t
-            kb.append(N.enc(k))
+            tids.append(t)
+            e = kmemo.get(k)
+            if e is None:
+                e = kmemo[k] = N.enc(k)
+            kb.append(e)
             if v is DELETE:
-                kinds[i], text = -1, ""
+                kinds.append(-1)
+                vids.append(0)
+                tb.append(b"")
+                continue
+            if type(v) is str:
+                kinds.append(N.KIND_STR)
+                tb.append(N.enc(v))
             else:
-                kinds[i], text = (N.KIND_STR, v) if type(v) is str else render(v, self.dialect)
-                vids[i] = len(self.values)
-                self.values.append(v)
-            tb.append(N.enc(text))
+                kd, text = render(v, self.dialect)
+                kinds.append(kd)
+                tb.append(N.enc(text))
+            vids.append(len(values))
+            values.append(v)
+        kinds = np.asarray(kinds, np.int32)
+        tids = np.asarray(tids, np.uint32)
+        vids = np.asarray(vids, np.uint32)
         kblob = np.frombuffer(b"".join(kb) + b"\0", np.uint8)
         tblob = np.frombuffer(b"".join(tb) + b"\0", np.uint8)
         klen = np.fromiter(map(len, kb), np.uint64, n)
