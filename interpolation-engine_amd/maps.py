@@ -46,6 +46,24 @@ def _first_value(d):
     return next(iter(d.values()))
 
 
+_WC_CACHE = {}  # compiled pattern lists by (patterns, device, dialect), most recent last
+_WC_CACHE_MAX = 64
+
+
+def _wildcards(pats, device, dialect):
+    """The compiled device form of an ordered wildcard list: a map task's keys are the same texts
+    call after call (as Python's re caches the reference's compiled regexes), so the last 64 lists
+    stay compiled instead of being built and freed for every step."""
+    key = (tuple(pats), device, dialect)
+    w = _WC_CACHE.pop(key, None)
+    if w is None:
+        w = Wildcards(pats, device=device, dialect=dialect)
+        if len(_WC_CACHE) >= _WC_CACHE_MAX:
+            _WC_CACHE.pop(next(iter(_WC_CACHE))).close()
+    _WC_CACHE[key] = w
+    return w
+
+
 def _pattern_range(pats, blocks, keys):
     """The [lo, hi) of `keys` in the pattern list `pats`, appended once per distinct key list (the
     map keys are usually the same text in every state)."""
@@ -114,11 +132,7 @@ def goto_map_states(states, task, dialect="py", device=0, tables=None):
         pending.append(s)
         ranges.append(_pattern_range(pats, blocks, keys[s]))
     if pending:
-        w = Wildcards(pats, device=device, dialect=dialect)
-        try:
-            found = w.first_match([texts[s] for s in pending], ranges)
-        finally:
-            w.close()
+        found = _wildcards(pats, device, dialect).first_match([texts[s] for s in pending], ranges)
         for s, (r, (p, _)) in zip(pending, zip(ranges, found)):
             if p < 0:  # py:1708
                 out[s] = AssertionError("Order Index %s: goto_map has no matches for '%s'."
@@ -299,11 +313,7 @@ def _replace_strings(tset, states, leaves, owner, keys, maps, m, repeat, dialect
             tried.append(i)
         hits = []
         if pats:
-            w = Wildcards(pats, device=device, dialect=dialect)
-            try:
-                found = w.first_match([cur[i] for i in tried], ranges)
-            finally:
-                w.close()
+            found = _wildcards(pats, device, dialect).first_match([cur[i] for i in tried], ranges)
         else:
             found = [(-1, [])] * len(tried)
         for i, r, (p, caps) in zip(tried, ranges, found):
