@@ -394,8 +394,9 @@ class DevResult:
 
 
 def assert_views_disjoint(starts, lens, total):
-    """A views output: every result inside [0, total) and no two overlapping (k_lean's stripes may
-    leave gaps, so total is the extent used, at least the sum of the lengths)."""
+    """A views output: every result inside [0, total) and no two overlapping (reserved ranges leave
+    gaps between tiles, so `total` here is the extent the caller read back, at least the sum of the
+    lengths)."""
     starts, lens = np.asarray(starts, np.int64), np.asarray(lens, np.int64)
     nz = lens > 0
     s, l = starts[nz], lens[nz]
