@@ -1165,25 +1165,28 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
   {
     pre.commit((uint4*)s_in, tid);
     if (UNESC) {
-      // the fused unescape command: which staged chunks hold a '\\' (from the prefetch registers)
+      // the fused unescape command: per staged chunk, the bytes that are '\\' (bits 0-15) and the
+      // braces (bits 16-31), from the prefetch registers, in the chunk-mask array (the
+      // classification below overwrites it)
 #pragma unroll
       for (int k = 0; k < kStageV; k++) {
         const uint32_t c = tid + (uint32_t)k * kRBlock;
-        uint32_t hz = 0;
         if (c < pre.nv) {
           const uint32_t w4[4] = {pre.v[k].x, pre.v[k].y, pre.v[k].z, pre.v[k].w};
+          uint32_t bs = 0, br = 0;
 #pragma unroll
           for (int q = 0; q < 4; q++) {
-            const uint32_t y = w4[q] ^ 0x5C5C5C5Cu;
-            hz |= (y - 0x01010101u) & ~y & 0x80808080u;
+            const uint32_t x = w4[q], x7 = x & 0x7F7F7F7Fu;
+            const uint32_t nb = ((x7 ^ 0x5C5C5C5Cu) + 0x7F7F7F7Fu) | x;
+            const uint32_t no = ((x7 ^ 0x7B7B7B7Bu) + 0x7F7F7F7Fu) | x;
+            const uint32_t nc = ((x7 ^ 0x7D7D7D7Du) + 0x7F7F7F7Fu) | x;
+            bs |= nib(~nb) << (4 * q);
+            br |= nib(~(no & nc)) << (4 * q);
           }
-        }
-        const uint64_t eb = __ballot(hz != 0u);
-        if (lane == 0 && (uint32_t)k * kRBlock < pre.nv) {
-          s_esc[(k * kRBlock + 64 * wave) >> 5] = (uint32_t)eb;
-          s_esc[((k * kRBlock + 64 * wave) >> 5) + 1] = (uint32_t)(eb >> 32);
+          s_cm[c] = bs | (br << 16);
         }
       }
+      if (tid < 2) s_cm[pre.nv + tid] = 0;  // (the chunk after the last: no brace)
     }
     __syncthreads();
     if (UNESC) {
@@ -1191,11 +1194,19 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
       // removed '\\' leaves a brace behind the byte before it, never a new pair, so one
       // left-to-right pass equals the two replaces; a '\\' that ends its string stays, the brace
       // after it being the next string's) on this lane's staged string, in place, before the
-      // classification: only strings whose chunks hold a '\\' have anything to do
-      const uint32_t ca = p0 >> 4, cz = sn ? (p0 + (uint32_t)sn - 1u) >> 4 : ca;
+      // classification: only strings with a '\\' before a brace inside them have anything to do
       bool esc_in = false;
-      if (lane_staged && sn)
-        for (uint32_t c = ca; c <= cz && !esc_in; c++) esc_in = ((s_esc[c >> 5] >> (c & 31u)) & 1u) != 0u;
+      if (lane_staged && sn > 1) {
+        const uint32_t a = p0, z = p0 + (uint32_t)sn - 2u;  // candidate positions: not the last byte
+        for (uint32_t c = a >> 4; c <= (z >> 4) && !esc_in; c++) {
+          const uint32_t m = s_cm[c], mn = s_cm[c + 1];
+          const uint32_t brn = (m >> 17) | ((mn >> 16) & 1u) << 15;  // brace at the next byte
+          uint32_t d = m & 0xFFFFu & brn;
+          if (c == (a >> 4)) d &= 0xFFFFu << (a & 15u);
+          if (c == (z >> 4)) d &= 0xFFFFu >> (15u - (z & 15u));
+          esc_in = d != 0u;
+        }
+      }
       uint32_t nsn = (uint32_t)sn;
       // the wave takes such strings one at a time, 64 bytes per step: a byte is kept unless it is
       // a '\\' before a brace; the kept bytes move down to their rank (in place: a step writes
