@@ -214,6 +214,16 @@ class InsertsTableSet:
                 tb.append(N.enc(text))
             vids.append(len(values))
             values.append(v)
+        if n <= 32:  # a scalar caller's few stores: ctypes arrays (numpy's per-call cost dominates)
+            arr = (N.KV * n)(*[N.KV(k, len(k), t, len(t), kd, 0) for k, t, kd in zip(kb, tb, kinds)])
+            ta, va = (ctypes.c_uint32 * n)(*tids), (ctypes.c_uint32 * n)(*vids)
+            t0 = time.perf_counter()
+            rc = N.lib().ie_table_set_update(self.h, ctypes.byref(arr), ta, va, n)
+            self.last_update_native_s = time.perf_counter() - t0
+            if rc == N.ERR_CAPACITY:
+                return False
+            N.check(rc, "ie_table_set_update")
+            return True
         kinds = np.asarray(kinds, np.int32)
         tids = np.asarray(tids, np.uint32)
         vids = np.asarray(vids, np.uint32)
