@@ -784,7 +784,8 @@ struct Ent {
 
 // Byte patches of device memory, applied by one upload and one kernel (k_patch): patch k writes
 // len[k] (<= 256) bytes of data (at soff[k]) to the device address dst[k]. Synchronous. The upload
-// goes through a grow-only staging buffer of the caller's (a table's).
+// goes through a grow-only staging buffer of the caller's (a table's); a set of at most
+// kPatchInlineN 16-byte pieces goes in the kernel's arguments instead (k_patch_inline).
 struct Patches {
   std::vector<uint8_t> data;
   std::vector<uint64_t> dst;
@@ -807,6 +808,21 @@ int apply_patches(DevBuf& staging, const Patches& P) {
   const uint64_t n = P.dst.size();
   if (!n) return IE_SUCCESS;
   if (P.data.size() >= (1ull << 32)) return fail(IE_ERR_INVALID, "patch set above 4 GiB");
+  uint64_t pieces = 0;
+  for (uint64_t k = 0; k < n; k++) pieces += (P.len[k] + 15) / 16;
+  if (pieces <= kPatchInlineN) {  // no upload: the launch carries the bytes
+    PatchInline a{};
+    for (uint64_t k = 0; k < n; k++)
+      for (uint32_t o = 0; o < P.len[k]; o += 16, a.n++) {
+        a.dst[a.n] = P.dst[k] + o;
+        a.len[a.n] = (uint8_t)std::min<uint32_t>(16, P.len[k] - o);
+        memcpy(a.data[a.n], P.data.data() + P.soff[k] + o, a.len[a.n]);
+      }
+    hipError_t e = launch_patch_inline(a, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) return fail(IE_ERR_HIP, std::string("table patch: ") + hipGetErrorString(e));
+    return IE_SUCCESS;
+  }
   const uint64_t o_dst = (P.data.size() + 15) & ~15ull, o_soff = o_dst + 8 * n, o_len = o_soff + 4 * n;
   std::vector<uint8_t> blob(o_len + 4 * n);
   memcpy(blob.data(), P.data.data(), P.data.size());

@@ -133,6 +133,17 @@ hipError_t launch_resolve_deferring(const Batch& B, const Work& W, const DevTabl
 // (ie_table_set_update / _set_clock)
 hipError_t launch_patch(const uint8_t* src, const uint64_t* dst, const uint32_t* soff, const uint32_t* len, uint32_t n,
                         hipStream_t st);
+// a small patch set carried in the kernel's arguments (no upload before the launch): a scalar
+// set_interpdata's few entries, pilot and text, as up to kPatchInlineN pieces of <= 16 bytes
+// (piece c: len[c] bytes of data[16c..] to dst[c]), one lane each
+constexpr uint32_t kPatchInlineN = 128;
+struct PatchInline {
+  uint32_t data[kPatchInlineN][4];
+  uint64_t dst[kPatchInlineN];
+  uint8_t len[kPatchInlineN];
+  uint32_t n;
+};
+hipError_t launch_patch_inline(const PatchInline& a, hipStream_t st);
 hipError_t launch_status_carry(const uint8_t* before, uint8_t* after, uint64_t n, hipStream_t st);
 hipError_t launch_debug_probe(const DevTable& T, const uint8_t* key, uint32_t klen, uint64_t* out,
                               hipStream_t st);

@@ -1789,6 +1789,26 @@ hipError_t launch_patch(const uint8_t* src, const uint64_t* dst, const uint32_t*
   return hipGetLastError();
 }
 
+__global__ void k_patch_inline(const PatchInline a) {
+  const uint32_t c = threadIdx.x;
+  if (c >= a.n) return;
+  const uint32_t w[4] = {a.data[c][0], a.data[c][1], a.data[c][2], a.data[c][3]}, l = a.len[c];
+  uint8_t* d = (uint8_t*)(uintptr_t)a.dst[c];
+  if (l == 16 && ((uintptr_t)d & 15u) == 0) {
+    gst4((uint4*)d, make_uint4(w[0], w[1], w[2], w[3]));
+    return;
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < 16; j++)
+    if (j < l) d[j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+}
+
+hipError_t launch_patch_inline(const PatchInline& a, hipStream_t st) {
+  if (!a.n || a.n > kPatchInlineN) return a.n ? hipErrorInvalidValue : hipSuccess;
+  hipLaunchKernelGGL(k_patch_inline, dim3(1), dim3(kPatchInlineN), 0, st, a);
+  return hipGetLastError();
+}
+
 // the listed strings (W.udefer_list) as a views subset of the batch (their bytes where they are)
 __global__ void k_gather_listed(Batch B, Work W, uint64_t* sub_off, uint32_t* sub_len, uint32_t* sub_tid) {
   const uint32_t count = __hip_atomic_load(W.udefer_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -375,6 +375,25 @@ class InsertsTable(InsertsTableSet):
         if self.dicts[0] is not inserts:  # (a merged inserts-directory snapshot, or another dict)
             return False
         snap, mutable = self._snapshot
+        logged = inserts.keys_since(self._version) if isinstance(inserts, VersionedInserts) else None
+        if logged is not None:  # only the keys stored since this snapshot (VersionedInserts' log)
+            changes = [(0, k, inserts[k] if k in inserts else DELETE) for k in logged
+                       if (k in inserts and (k not in snap or snap[k] is not inserts[k]
+                                             or isinstance(inserts[k], (list, dict)))) or (k not in inserts and k in snap)]
+            if not self.update(changes):
+                return False
+            for _, k, v in changes:
+                if v is DELETE:
+                    snap.pop(k, None)
+                    mutable.pop(k, None)
+                    continue
+                snap[k] = v
+                if isinstance(v, (list, dict)):
+                    mutable[k] = render(v, self.dialect)[1]
+                else:
+                    mutable.pop(k, None)
+            self._version = inserts.version
+            return True
         changes = [(0, k, v) for k, v in inserts.items()
                    if k not in snap or snap[k] is not v
                    or (k in mutable and render(v, self.dialect)[1] != mutable[k])]
@@ -443,26 +462,58 @@ def _missing_key_exception(key, keys, has_dir):
 class VersionedInserts(dict):
     """A dict that counts its mutations, so table_for() recognises an unchanged inserts dict in
     O(1) instead of comparing every value (use it as the runner's `state['inserts']`). Mutating a
-    list or dict value in place is not a mutation of this dict: bump() after doing that."""
-    __slots__ = ("version",)
+    list or dict value in place is not a mutation of this dict: bump() after doing that.
+    `d[k] = v` and `del d[k]` are also logged (version, key), so a table refreshes from the keys
+    stored since its version instead of comparing the whole dict; the log covers the versions after
+    log_base (other mutators, bump() and a full log start it again)."""
+    __slots__ = ("version", "log", "log_base")
+    _LOG_MAX = 64
 
     def __init__(self, *a, **k):
         super().__init__(*a, **k)
         self.version = 0
+        self.log = []
+        self.log_base = 0
 
     def bump(self):
         self.version += 1
+        self.log, self.log_base = [], self.version
+
+    def __setitem__(self, k, v):
+        self.version += 1
+        dict.__setitem__(self, k, v)
+        self._logged(k)
+
+    def __delitem__(self, k):
+        self.version += 1
+        dict.__delitem__(self, k)
+        self._logged(k)
+
+    def _logged(self, k):
+        if len(self.log) >= self._LOG_MAX:
+            self.log, self.log_base = [], self.version
+        else:
+            self.log.append((self.version, k))
+
+    def keys_since(self, version):
+        """The keys stored or deleted after `version`, or None when the log does not cover it."""
+        if version is None or version < self.log_base:
+            return None
+        return {k for v, k in self.log if v > version}
 
     def _mut(name):
         base = getattr(dict, name)
 
         def f(self, *a, **k):
             self.version += 1
-            return base(self, *a, **k)
+            try:
+                return base(self, *a, **k)
+            finally:
+                self.log, self.log_base = [], self.version
         f.__name__ = name
         return f
 
-    for _n in ("__setitem__", "__delitem__", "update", "pop", "popitem", "clear", "setdefault", "__ior__"):
+    for _n in ("update", "pop", "popitem", "clear", "setdefault", "__ior__"):
         locals()[_n] = _mut(_n)
     del _n, _mut
 

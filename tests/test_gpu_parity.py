@@ -899,6 +899,49 @@ def test_mirror_table_cache_versioned_and_bounded():
     assert len(PKG.interpolation_engine._cache) <= PKG.interpolation_engine._CACHE_SIZE
 
 
+def test_mirror_refresh_from_logged_keys_matches_oracle():
+    """A scalar caller's dict mutated between calls (py:470-471 stores and `del`, a bulk update,
+    an in-place list change announced with bump(), a store of the same object): each
+    interpolate_inserts refreshes the cached table from VersionedInserts' log of stored keys (or a
+    whole-dict comparison where the log does not reach) and must equal the oracle on the live dict."""
+    rng = random.Random(5)
+    keys = ["k%d" % j for j in range(24)]
+    ins = PKG.VersionedInserts({k: "v" + k for k in keys})
+    ins["L"] = ["a", 1]
+    ins["nest"] = "<{k3}>"
+    strings = ["{k0}|{k5}|{nest}", "x{k%d}y" % 7, "{{k1}}", "L={L}", "n{nest}{k23}"]
+    ie = PKG.interpolation_engine
+    for step in range(60):
+        r = rng.random()
+        if r < 0.45:
+            ins[rng.choice(keys)] = rng.choice(["s%d" % step, "{k2}", "", "tail {k4}.", "k1"])
+        elif r < 0.55:
+            k = rng.choice(keys[8:])
+            if k in ins:
+                del ins[k]
+        elif r < 0.65:
+            ins.update({rng.choice(keys): "u%d" % step, "new%d" % step: "n"})
+        elif r < 0.75:
+            ins["L"].append(step)
+            ins.bump()
+        elif r < 0.85:
+            k = rng.choice(keys[:8])
+            ins[k] = ins[k]  # the same object again
+        else:
+            ins["k%d" % rng.randrange(24)] = ["x", step]
+        ref = O.Oracle({k: v for k, v in ins.items()}, "py", clock=CLOCK)
+        for s in strings:
+            st, out, _ = ref.interpolate(s)
+            if st == "OK_STR":
+                assert ie.interpolate_inserts(ins, s) == out, (step, s)
+            elif st == "OK_VALUE":
+                assert ie.interpolate_inserts(ins, s) is ins[s[1:-1]], (step, s)
+            else:
+                with pytest.raises(Exception):
+                    ie.interpolate_inserts(ins, s)
+    ie.table_for(ins)  # (the cached table still follows the dict)
+
+
 def test_interpolate_states_batch():
     states = [{"scenario": "s%d" % j, "stage": "first", "L": [j]} for j in range(50)]
     items = [(j % 50, c) for j, c in enumerate(["{scenario}", "x{stage}|{scenario}", "{L}", "{nope}"] * 50)]
