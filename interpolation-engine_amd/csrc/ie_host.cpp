@@ -130,6 +130,7 @@ struct ie_exec {
   // back asynchronously (never a wait): > 0.1 % of a batch switches to it, a batch with none back
   bool fail_commit = false;
   bool stat_pending = false;
+  bool no_stats = false;  // run_host_small: no statistics copy (two stream operations of a scalar call)
   uint64_t stat_n = 0;
   uint32_t* stat_host = nullptr;  // pinned
   hipEvent_t stat_ev = nullptr;
@@ -469,7 +470,7 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
     } else {
       IE_HIP(wide ? launch_resolve512(B, W, t->dev, out->bytes, cap, st) : launch_resolve(B, W, t->dev, out->bytes, cap, st));
     }
-    if (!x->stat_pending) {
+    if (!x->stat_pending && !x->no_stats) {
       if (!x->stat_host) {
         IE_HIP(hipHostMalloc((void**)&x->stat_host, 64, hipHostMallocDefault));
         IE_HIP(hipEventCreateWithFlags(&x->stat_ev, hipEventDisableTiming));
@@ -539,8 +540,11 @@ int run_host_small(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, 
   uint8_t* const dout = dv + in_size;
   IE_HIP(hipMemcpyAsync(dv, h, i_bytes + in_bytes, hipMemcpyHostToDevice, x->stream));
   ie_dev_out o{dout + o_bytes, cap, (uint64_t*)(dout + o_off), dout + o_st, (uint32_t*)(dout + o_vid), (uint64_t*)dout};
+  // (the adaptive fail-commit / deferral statistics come from the larger batches)
+  x->no_stats = true;
   int rc = run_device(x, op, t, dv + i_bytes, (const uint64_t*)dv, n, &o,
                       table_id ? (const uint32_t*)(dv + i_tid) : nullptr, views ? (uint32_t*)(dout + o_len) : nullptr);
+  x->no_stats = false;
   if (rc) return rc;
   IE_HIP(hipMemcpyAsync(ho, dout, o_err, hipMemcpyDeviceToHost, x->stream));
   IE_HIP(hipMemcpyAsync(ho + o_err, (uint32_t*)x->counters.p + 1, 4, hipMemcpyDeviceToHost, x->stream));
