@@ -131,6 +131,7 @@ struct ie_exec {
   bool fail_commit = false;
   bool stat_pending = false;
   bool no_stats = false;  // run_host_small: no statistics copy (two stream operations of a scalar call)
+  uint8_t* ctr_override = nullptr;  // run_host_small: the counters in its own block, zeroed by its input copy
   uint64_t stat_n = 0;
   uint32_t* stat_host = nullptr;  // pinned
   hipEvent_t stat_ev = nullptr;
@@ -319,23 +320,24 @@ int ensure_work(ie_exec* x, int op, uint64_t n) {
 
 Work make_work(ie_exec* x, uint64_t* total) {
   Work W{};
+  void* const C = x->ctr_override ? (void*)x->ctr_override : x->counters.p;
   W.total = total;
-  W.tile_ticket = (uint32_t*)x->counters.p;
-  W.err = (uint32_t*)x->counters.p + 1;
-  W.stats = (uint32_t*)x->counters.p + 4;
+  W.tile_ticket = (uint32_t*)C;
+  W.err = (uint32_t*)C + 1;
+  W.stats = (uint32_t*)C + 4;
   W.stamps = x->stamp_tiles ? (uint64_t*)x->stamps.p : nullptr;
   W.debug_noeval = x->opt_noeval;  // diagnostic hooks, see DESIGN.md
   W.fast_mode = x->opt_fast;       // 0: exact evaluator only
-  W.pool_used = (uint64_t*)x->counters.p + 1;
-  W.defer_count = (uint32_t*)x->counters.p + 9;
+  W.pool_used = (uint64_t*)C + 1;
+  W.defer_count = (uint32_t*)C + 9;
   W.defer_tiles = (uint32_t*)x->defer_tiles.p;
   W.defer_desc = (uint4*)x->defer_desc.p;
-  W.tile_state = (uint64_t*)((uint8_t*)x->counters.p + kCounterBytes);
-  W.shards = (uint64_t*)((uint8_t*)x->counters.p + 64);
+  W.tile_state = (uint64_t*)((uint8_t*)C + kCounterBytes);
+  W.shards = (uint64_t*)((uint8_t*)C + 64);
   W.n_shards = kSumShards;
-  W.cursor = (uint64_t*)x->counters.p + 5;  // words 10-11
-  W.udefer_count = (uint32_t*)x->counters.p + 12;
-  W.res_ovf = (uint64_t*)x->counters.p + 7;  // words 14-15
+  W.cursor = (uint64_t*)C + 5;  // words 10-11
+  W.udefer_count = (uint32_t*)C + 12;
+  W.res_ovf = (uint64_t*)C + 7;  // words 14-15
   W.zero_on_overflow = x->cmd_first ? 1u : 0u;
   W.pool = (uint8_t*)x->pool.p;
   W.pool_bytes = x->pool.bytes;
@@ -423,7 +425,7 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
   if (x->timing) IE_HIP(hipEventRecord(x->ev[0], st));
   // the counters and, for a packed interpolation, the look-back words (one fill instead of two)
   const uint64_t zero_tiles = (op == kOpInterp && n && !d_out_len) ? (n + 127) / 128 : 0;  // (ensure_work)
-  IE_HIP(hipMemsetAsync(x->counters.p, 0, kCounterBytes + zero_tiles * sizeof(uint64_t), st));
+  if (!x->ctr_override) IE_HIP(hipMemsetAsync(x->counters.p, 0, kCounterBytes + zero_tiles * sizeof(uint64_t), st));
   if (n == 0) {
     if (!d_out_len) IE_HIP(hipMemsetAsync(out->offsets, 0, sizeof(uint64_t), st));
     IE_HIP(hipMemsetAsync(out->total, 0, sizeof(uint64_t), st));
@@ -516,11 +518,15 @@ int run_host_small(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, 
   // input block: offsets | table ids | bytes (the device block keeps room for the loads' over-read)
   const uint64_t i_tid = al256((n + 1) * 8), i_bytes = i_tid + al256(table_id ? n * 4 : 0);
   const uint64_t in_size = i_bytes + al256(in_bytes + 64);
+  // then the call's counters and look-back words (zeroed here, sent with the input, read back with
+  // the output: no fill, one read-back); the exec's own counters when timing asks for its telemetry
+  const bool own_ctr = !x->timing;
+  const uint64_t ctr_size = own_ctr ? al256(kCounterBytes + ((n + 127) / 128 + 1) * sizeof(uint64_t)) : 0;
   // output block: total | offsets | lengths (views) | statuses | value ids | bytes; then the
   // device error word, read with a copy of its own
   const uint64_t o_off = 256, o_len = o_off + al256((n + 1) * 8), o_st = o_len + al256(views ? n * 4 : 0),
                  o_vid = o_st + al256(n + 1), o_bytes = o_vid + al256((n + 1) * 4), o_err = o_bytes + al256(cap);
-  const uint64_t need = in_size + o_err + 256;
+  const uint64_t need = in_size + ctr_size + o_err + 256;
   IE_HIP(x->sm_dev.ensure(std::max<uint64_t>(need, 1ull << 19)));
   if (x->sm_host_bytes < need) {
     if (x->sm_host) (void)hipHostFree(x->sm_host);
@@ -531,25 +537,32 @@ int run_host_small(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, 
     x->sm_host_bytes = want;
   }
   uint8_t* const h = x->sm_host;
-  uint8_t* const ho = h + in_size;
+  uint8_t* const ho = h + in_size + ctr_size;
   uint64_t* const hoff = (uint64_t*)h;
   for (uint64_t i = 0; i <= n; i++) hoff[i] = offsets[i] - base;
   if (table_id) memcpy(h + i_tid, table_id, n * 4);
   if (in_bytes) memcpy(h + i_bytes, bytes + base, in_bytes);
+  if (ctr_size) memset(h + in_size, 0, ctr_size);
   uint8_t* const dv = (uint8_t*)x->sm_dev.p;
-  uint8_t* const dout = dv + in_size;
-  IE_HIP(hipMemcpyAsync(dv, h, i_bytes + in_bytes, hipMemcpyHostToDevice, x->stream));
+  uint8_t* const dout = dv + in_size + ctr_size;
+  IE_HIP(hipMemcpyAsync(dv, h, ctr_size ? in_size + ctr_size : i_bytes + in_bytes, hipMemcpyHostToDevice, x->stream));
   ie_dev_out o{dout + o_bytes, cap, (uint64_t*)(dout + o_off), dout + o_st, (uint32_t*)(dout + o_vid), (uint64_t*)dout};
   // (the adaptive fail-commit / deferral statistics come from the larger batches)
   x->no_stats = true;
+  x->ctr_override = ctr_size ? dv + in_size : nullptr;
   int rc = run_device(x, op, t, dv + i_bytes, (const uint64_t*)dv, n, &o,
                       table_id ? (const uint32_t*)(dv + i_tid) : nullptr, views ? (uint32_t*)(dout + o_len) : nullptr);
   x->no_stats = false;
+  x->ctr_override = nullptr;
   if (rc) return rc;
-  IE_HIP(hipMemcpyAsync(ho, dout, o_err, hipMemcpyDeviceToHost, x->stream));
-  IE_HIP(hipMemcpyAsync(ho + o_err, (uint32_t*)x->counters.p + 1, 4, hipMemcpyDeviceToHost, x->stream));
+  if (ctr_size) {
+    IE_HIP(hipMemcpyAsync(h + in_size, dv + in_size, ctr_size + o_err, hipMemcpyDeviceToHost, x->stream));
+  } else {
+    IE_HIP(hipMemcpyAsync(ho, dout, o_err, hipMemcpyDeviceToHost, x->stream));
+    IE_HIP(hipMemcpyAsync(ho + o_err, (uint32_t*)x->counters.p + 1, 4, hipMemcpyDeviceToHost, x->stream));
+  }
   IE_HIP(hipStreamSynchronize(x->stream));
-  const uint32_t err = *(const uint32_t*)(ho + o_err);  // (check_device_error's rules)
+  const uint32_t err = ctr_size ? ((const uint32_t*)(h + in_size))[1] : *(const uint32_t*)(ho + o_err);  // (check_device_error's rules)
   if (err & 2u) return fail(IE_ERR_CAPACITY, "a step's output did not fit its caller-sized buffer");
   if (err) return fail(IE_ERR_TIMEOUT, "look-back spin timed out (a predecessor tile never published)");
   total = *(const uint64_t*)ho;
