@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <mutex>
 #include <string>
 #include <string_view>
 #include <unordered_map>
@@ -1085,8 +1086,22 @@ int preresolve(ie_table* t0, std::vector<Ent>& ents, uint32_t n_tables, int32_t 
     offs.push_back(bytes.size());
     tids.push_back(ents[i].tid);  // a value resolves against its own table of the set
   }
+  // one exec per device kept for these passes (a table set built per map step would otherwise pay
+  // an exec's stream and buffers each time); IE_PRE_EXEC_CACHE=0: a fresh exec per build
+  static std::mutex mu;
+  static ie_exec* kept[64] = {};
+  static const bool keep = !(getenv("IE_PRE_EXEC_CACHE") && atoi(getenv("IE_PRE_EXEC_CACHE")) == 0);
+  std::unique_lock<std::mutex> lk(mu, std::defer_lock);
+  const bool use_kept = keep && device >= 0 && device < 64;
   ie_exec* x = nullptr;
-  int rc = ie_exec_create(device, nullptr, &x);
+  int rc = IE_SUCCESS;
+  if (use_kept) {
+    lk.lock();
+    if (!kept[device]) rc = ie_exec_create(device, nullptr, &kept[device]);
+    x = kept[device];
+  } else {
+    rc = ie_exec_create(device, nullptr, &x);
+  }
   if (rc) return rc;
   ie_batch* b = nullptr;
   ie_batch* b2 = nullptr;
@@ -1095,7 +1110,7 @@ int preresolve(ie_table* t0, std::vector<Ent>& ents, uint32_t n_tables, int32_t 
   if (!rc) rc = ie_table_set_clock(t0, &other);
   if (!rc) rc = run_host(x, kOpInterp, t0, bytes.data(), offs.data(), cand.size(), &b2, tids.data());
   if (!rc) rc = ie_table_set_clock(t0, &clock);
-  ie_exec_destroy(x);
+  if (!use_kept) ie_exec_destroy(x);
   if (rc) {
     ie_batch_free(b);
     ie_batch_free(b2);

@@ -45,7 +45,9 @@ def main():
         for rep in range(2):
             st = [dict(s) for s in states]
             prof = None
-            if rep and n == 10_000 and os.environ.get("IE_TASK_PROFILE"):  # where the host time goes
+            # where the host time goes: IE_TASK_PROFILE (10k states) or IE_TASK_PROFILE_N=<states>
+            pn = int(os.environ.get("IE_TASK_PROFILE_N") or (10_000 if os.environ.get("IE_TASK_PROFILE") else 0))
+            if rep and n == pn:
                 import cProfile
                 prof = cProfile.Profile()
                 prof.enable()
@@ -57,7 +59,7 @@ def main():
                 import io
                 import pstats
                 buf = io.StringIO()
-                pstats.Stats(prof, stream=buf).sort_stats("tottime").print_stats(25)
+                pstats.Stats(prof, stream=buf).sort_stats("tottime").print_stats(40)
                 sys.stderr.write(buf.getvalue())
             best = dt if best is None else min(best, dt)
         out["states_%d" % n] = {"us_per_state_task": [round(1e6 * x / n, 2) for x in per_task],
