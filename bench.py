@@ -612,7 +612,7 @@ def replay_states(args, W, x, resolve, res):
     states."""
     from interpolation_engine_amd import workloads as Wk
     from oracle import oracle as O
-    upd, nat, rsv, nch = [], [], [], 0
+    upd, nat, rsv, nch, arena = [], [], [], 0, []
     for it in range(args.replay):
         changes = []
         for j, ins in enumerate(W.states):
@@ -636,6 +636,7 @@ def replay_states(args, W, x, resolve, res):
         upd.append(t1 - t0)
         nat.append(W.tset.last_update_native_s)
         rsv.append(t3 - t2)
+        arena.append(W.tset.arena_stats())
     threads, _ = cpu_share()
     oracles = [O.Oracle(ins, "py", clock=CLOCK) for ins in W.states]
     buf = np.frombuffer(W.blob + bytes(1), np.uint8)
@@ -645,6 +646,9 @@ def replay_states(args, W, x, resolve, res):
     return {"iterations": args.replay, "stores_per_iteration": nch,
             "store_ms": [round(1e3 * v, 3) for v in upd], "store_library_ms": [round(1e3 * v, 3) for v in nat],
             "resolve_ms": [round(1e3 * v, 3) for v in rsv],
+            "arena_bytes": [a[0] for a in arena], "arena_live_bytes": [a[1] for a in arena],
+            "arena_compactions": arena[-1][2] if arena else 0,
+            "values_held": len(W.tset.values),
             "identical_to_oracle_after_replay": same,
             "note": "store_ms = InsertsTableSet.update (Python packing + ie_table_set_update); resolve_ms = wall "
                     "time of one batch (launch + sync)"}

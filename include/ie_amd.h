@@ -80,7 +80,7 @@ enum ie_status {
 #define IE_ERR_NOMEM (-3)
 #define IE_ERR_NO_DEVICE (-4)
 #define IE_ERR_TIMEOUT (-5)
-#define IE_ERR_CAPACITY (-6) /* caller-owned output buffer too small: see *total */
+#define IE_ERR_CAPACITY (-6) /* caller-owned output buffer too small (see *total), or a table full (rebuild) */
 
 /* Divergence caps. The reference loops forever on self-referential inserts (py:516 has no bound)
  * or grows without limit; both the oracle and the device path stop a string once its working
@@ -117,7 +117,11 @@ typedef struct ie_clock {
 #define IE_TABLE_HAS_INSERTS_DIR 1u /* missing keys report IE_NEEDS_HOST instead of IE_E_INTERP */
 #define IE_TABLE_MUTABLE 2u         /* room for ie_table_set_update's new keys (entries at load 0.5, not 0.8) */
 
-typedef struct ie_table ie_table; /* immutable after build; read-only on device; thread-safe */
+/* A table is read-only on the device. It may be used by several execs / host threads at once, EXCEPT
+ * while ie_table_set_update or ie_table_set_clock rewrites it: those two patch the device copy in
+ * place (after waiting for the device), so the caller must not run a batch on the table from
+ * another thread while they run (they are not synchronised with other threads' launches). */
+typedef struct ie_table ie_table;
 typedef struct ie_exec ie_exec;   /* one per host thread: device, stream, workspace           */
 
 /* Device-resident output of a batch call. All pointers are DEVICE pointers owned by the caller.
@@ -195,8 +199,17 @@ int ie_table_set_clock(ie_table* t, const ie_clock* now);
  * text (both then resolve through the exact evaluator, in the reference's order). IE_ERR_CAPACITY:
  * a new key found no placement (the entries before it were applied, it and the rest were not:
  * rebuild the table; a table built with IE_TABLE_MUTABLE keeps room for about as many new keys as it
- * was built with). */
+ * was built with). Every change is validated before any is applied (IE_ERR_INVALID leaves the table
+ * unchanged). Texts: a rewrite whose new text fits the old one's room is written in place, any other
+ * text is appended to the table's arena; the replaced bytes are counted dead, and the arena is
+ * compacted (host mirror + one upload) when the dead bytes outnumber the live ones. A change that
+ * would take an arena offset past the table's limit (2^32 - 16, or ie_table_set_arena_limit's) even
+ * after a compaction returns IE_ERR_CAPACITY (the changes before it applied): rebuild the table. */
 int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, const uint32_t* vid, uint64_t n);
+/* Arena bookkeeping: bytes in use, bytes of live entries, compactions so far (any may be NULL). */
+int ie_table_arena_stats(const ie_table* t, uint64_t* bytes, uint64_t* live, uint64_t* compactions);
+/* Lower the arena limit of ie_table_set_update (tests: force compaction and IE_ERR_CAPACITY early). */
+int ie_table_set_arena_limit(ie_table* t, uint64_t bytes);
 uint64_t ie_table_entries(const ie_table* t);
 uint32_t ie_table_tables(const ie_table* t);
 int32_t ie_table_dialect(const ie_table* t);

@@ -39,7 +39,7 @@ EXPORTS = [
     "ie_synth_create", "ie_synth_free", "ie_synth_kv", "ie_synth_strings_host",
     "ie_synth_strings_device", "ie_debug_probe",
     "ie_wildcards_build", "ie_wildcards_free", "ie_wildcard_match_device", "ie_wildcard_match_batch",
-    "ie_table_replicate", "ie_shard_bounds",
+    "ie_table_replicate", "ie_shard_bounds", "ie_table_arena_stats", "ie_table_set_arena_limit",
 ]
 WC_MAX_CAP = 16
 
@@ -97,6 +97,8 @@ def signatures():
         "ie_table_free": (None, [vp]),
         "ie_table_set_clock": (ctypes.c_int, [vp, ctypes.POINTER(Clock)]),
         "ie_table_set_update": (ctypes.c_int, [vp, vp, vp, vp, u64]),
+        "ie_table_arena_stats": (ctypes.c_int, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]),
+        "ie_table_set_arena_limit": (ctypes.c_int, [vp, u64]),
         "ie_table_tables": (u32, [vp]),
         "ie_table_entries": (u64, [vp]),
         "ie_table_dialect": (i32, [vp]),

@@ -88,6 +88,12 @@ struct ie_table {
   std::vector<uint16_t> h_pilots;
   std::vector<uint8_t> h_arena;
   uint64_t arena_cap = 0;
+  // arena bookkeeping (ie_table_set_update): bytes the live entries occupy (the rest of h_arena is
+  // dead: replaced texts), the largest arena the table may have (an offset must stay below 2^32;
+  // ie_table_set_arena_limit lowers it), and how often it was compacted
+  uint64_t arena_live = 0;
+  uint64_t arena_limit = 0xFFFFFFF0ull;
+  uint64_t n_compactions = 0;
   std::vector<std::vector<uint32_t>> groups;
   std::unordered_map<uint32_t, std::vector<uint32_t>> rawalt;
   DevBuf patch_staging;  // ie_table_set_update / _set_clock uploads
@@ -886,7 +892,69 @@ Entry make_entry(ie_table* t, std::string_view key, std::string_view text, uint3
   b.text_off = arena_append(t, text, key);
   memcpy(b.key, key.data(), std::min<size_t>(key.size(), kInlineKey));
   memcpy(b.text, text.data(), std::min<size_t>(text.size(), kInlineText));
+  t->arena_live += ((key_off_of(b.text_off, b.text_len) + b.key_len + 3ull) & ~3ull) - b.text_off;
   return b;
+}
+
+// [first, end) of an entry's bytes in the arena: [raw text, pad, u32 raw length] (EF_RAWALT),
+// [splice text, pad, key], padded to 4
+void arena_span(const ie_table* t, const Entry& e, uint64_t& first, uint64_t& end) {
+  first = e.text_off;
+  if (e.flags & EF_RAWALT) {
+    uint32_t rl;
+    memcpy(&rl, t->h_arena.data() + e.text_off - 4, 4);
+    first -= 4 + ((rl + 3ull) & ~3ull);
+  }
+  end = (key_off_of(e.text_off, e.text_len) + e.key_len + 3ull) & ~3ull;
+}
+
+// an entry leaves the table or its texts are replaced: its arena bytes are dead
+void arena_release(ie_table* t, const Entry& e) {
+  if (!(e.flags & EF_OCCUPIED)) return;
+  uint64_t a, b;
+  arena_span(t, e, a, b);
+  t->arena_live -= std::min<uint64_t>(t->arena_live, b - a);
+}
+
+// Rewrite of a present key (set_interpdata of a key the table has): the new text goes where the old
+// one was when it fits there (the key moves up behind it; the freed tail is dead), else it is
+// appended. False: no room in place (the caller appends).
+bool rewrite_in_place(ie_table* t, Entry& e, std::string_view text, uint32_t flags, uint32_t vid) {
+  if ((e.flags & EF_RAWALT) || ((text.size() + 3ull) & ~3ull) > ((e.text_len + 3ull) & ~3ull)) return false;
+  uint64_t a, b;
+  arena_span(t, e, a, b);
+  uint8_t* base = t->h_arena.data();
+  const std::string key(mirror_key(t, e));
+  memset(base + a, 0, b - a);
+  memcpy(base + e.text_off, text.data(), text.size());
+  const uint32_t ko = key_off_of(e.text_off, (uint32_t)text.size());
+  memcpy(base + ko, key.data(), key.size());
+  t->arena_live -= (b - a) - ((((uint64_t)ko + key.size() + 3ull) & ~3ull) - e.text_off);
+  e.text_len = (uint32_t)text.size();
+  e.vid = vid;
+  e.flags = flags | EF_OCCUPIED | (e.flags & ~((1u << kTidShift) - 1u));
+  memset(e.text, 0, kInlineText);
+  memcpy(e.text, text.data(), std::min<size_t>(text.size(), kInlineText));
+  return true;
+}
+
+// Compaction: every live entry's bytes copied into a fresh arena, in slot order, offsets rewritten
+// (the caller uploads the entries and the arena whole)
+void compact_arena(ie_table* t) {
+  std::vector<uint8_t> na;
+  na.reserve(t->arena_live + 64);
+  for (Entry& e : t->h_entries) {
+    if (!(e.flags & EF_OCCUPIED)) continue;
+    uint64_t a, b;
+    arena_span(t, e, a, b);
+    while (na.size() & 3) na.push_back(0);
+    const uint64_t at = na.size();
+    na.insert(na.end(), t->h_arena.begin() + a, t->h_arena.begin() + b);
+    e.text_off = (uint32_t)(at + (e.text_off - a));
+  }
+  t->h_arena = std::move(na);
+  t->arena_live = t->h_arena.size();
+  t->n_compactions++;
 }
 
 // Whole-table re-placement at the same capacity (ie_table_set_update, when a group found no pilot
@@ -1037,6 +1105,7 @@ int upload_table(const std::vector<Ent>& ents, uint32_t n_tables, int32_t dialec
   t->dev.maxtext = maxtext;
   t->h_entries = std::move(entries);
   t->h_pilots = std::move(pilots);
+  t->arena_live = arena.size();
   t->h_arena = std::move(arena);
   *out = t;
   return IE_SUCCESS;
@@ -1240,6 +1309,9 @@ int ie_table_replicate(const ie_table* t, int32_t device, ie_table** out) {
   c->h_pilots = t->h_pilots;
   c->h_arena = t->h_arena;
   c->arena_cap = t->arena_cap;
+  c->arena_live = t->arena_live;
+  c->arena_limit = t->arena_limit;
+  c->n_compactions = t->n_compactions;
   c->groups = t->groups;
   c->rawalt = t->rawalt;
   c->dev = t->dev;
@@ -1316,25 +1388,42 @@ int ie_table_set_clock(ie_table* t, const ie_clock* now) {
 // table that changed go back to their raw text, since they were resolved against the old dict.
 int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, const uint32_t* vid, uint64_t n) {
   if (!t || (n && (!kv || !table_id || !vid))) return fail(IE_ERR_INVALID, "null argument");
+  // every change is checked before any is applied: a rejected call leaves the table as it was
+  for (uint64_t i = 0; i < n; i++) {
+    if (table_id[i] >= t->n_tables) return fail(IE_ERR_INVALID, "table id beyond the table set");
+    if (kv[i].key_len && !kv[i].key) return fail(IE_ERR_INVALID, "null key");
+    if (kv[i].kind < 0) continue;
+    if (kv[i].kind > IE_KIND_DICT) return fail(IE_ERR_INVALID, "bad kind");
+    if (vid[i] >= IE_VID_CLOCK_HHMMSS) return fail(IE_ERR_INVALID, "value id out of range");
+    if (kv[i].text_len && !kv[i].text) return fail(IE_ERR_INVALID, "null text");
+    if (kv[i].key_len >= 0xFFFFFFF0ull || kv[i].text_len >= 0xFFFFFFF0ull) return fail(IE_ERR_INVALID, "key or text above 4 GiB");
+  }
   int rc = set_device(t->device);
   if (rc) return rc;
   IE_HIP(hipDeviceSynchronize());  // no batch may still read the table
-  const uint64_t arena0 = t->h_arena.size();
+  uint64_t arena0 = t->h_arena.size();
   uint64_t seed = t->dev.seed;
   const uint32_t nb = t->dev.nb, m = t->dev.m;
   bool whole = false;                      // entries and pilots re-placed: upload them whole
+  bool whole_arena = false;                // the arena was compacted: upload it whole
   std::vector<uint32_t> dirty;             // entry slots to upload
   std::vector<uint32_t> dirty_groups;      // pilots to upload
+  std::vector<uint32_t> rewritten;         // slots whose arena bytes were rewritten in place
   std::vector<uint32_t> touched;           // tables whose pre-resolved values must go raw
   int status = IE_SUCCESS;
-  auto is_clock = [](uint32_t v) { return v == IE_VID_CLOCK_HHMM || v == IE_VID_CLOCK_HHMMSS; };
+  // room for an append of `need` bytes below the table's arena limit (offsets stay below 2^32):
+  // compacted first when dead bytes would make the room; false: IE_ERR_CAPACITY
+  auto room = [&](uint64_t need) -> bool {
+    if (t->h_arena.size() + need + 8 <= t->arena_limit) return true;
+    if (t->arena_live + need + 8 > t->arena_limit) return false;
+    compact_arena(t);
+    whole = whole_arena = true;
+    return t->h_arena.size() + need + 8 <= t->arena_limit;
+  };
   for (uint64_t i = 0; i < n; i++) {
     const uint32_t tb = table_id[i];
-    if (tb >= t->n_tables) return fail(IE_ERR_INVALID, "table id beyond the table set");
     std::string_view key(kv[i].key ? kv[i].key : "", kv[i].key_len);
     if (key.empty() || key == "HH:MM" || key == "HH:MM:SS") continue;  // never looked up (py:433-446)
-    if (kv[i].kind > IE_KIND_DICT) return fail(IE_ERR_INVALID, "bad kind");
-    if (vid[i] >= IE_VID_CLOCK_HHMMSS && kv[i].kind >= 0) return fail(IE_ERR_INVALID, "value id out of range");
     const uint64_t h = key_hash(key, seed, tb);
     const uint32_t g = ph_group(h, nb), slot = ph_slot(h, t->h_pilots[g], m);
     Entry& cur = t->h_entries[slot];
@@ -1343,6 +1432,7 @@ int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
       if (!present) continue;
       auto& gs = t->groups[g];
       gs.erase(std::remove(gs.begin(), gs.end(), slot), gs.end());
+      arena_release(t, cur);
       cur = Entry{};
       dirty.push_back(slot);
       t->n_entries--;
@@ -1350,13 +1440,28 @@ int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
       continue;
     }
     std::string_view text(kv[i].text ? kv[i].text : "", kv[i].text_len);
-    if (key.size() >= 0xFFFFFFF0ull || text.size() >= 0xFFFFFFF0ull) return fail(IE_ERR_INVALID, "key or text above 4 GiB");
     const uint32_t flags = kind_flags(kv[i].kind, t->dialect) | text_flags(text);
-    touched.push_back(tb);
+    const uint64_t need = ((text.size() + 3ull) & ~3ull) + key.size() + 4;
     if (present) {
-      cur = make_entry(t, key, text, flags, vid[i], tb);
+      // the new text where the old one was when it fits, else appended
+      if (rewrite_in_place(t, cur, text, flags, vid[i])) {
+        rewritten.push_back(slot);
+      } else {
+        if (!room(need)) {
+          status = fail(IE_ERR_CAPACITY, "table arena full (limit reached even after compaction): rebuild the table");
+          break;
+        }
+        arena_release(t, t->h_entries[slot]);
+        t->h_entries[slot] = make_entry(t, key, text, flags, vid[i], tb);
+      }
       dirty.push_back(slot);
+      touched.push_back(tb);
     } else {
+      if (!room(need)) {
+        status = fail(IE_ERR_CAPACITY, "table arena full (limit reached even after compaction): rebuild the table");
+        break;
+      }
+      touched.push_back(tb);
       // re-place the group with the new key: a pilot that sends every member to a distinct slot
       // that is free or one of the group's own
       std::vector<uint32_t>& gs = t->groups[g];
@@ -1381,18 +1486,23 @@ int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
       }
       if (!found) {
         // every entry placed again under a new seed, at the same capacity
-        if (!replace_all(t, make_entry(t, key, text, flags, vid[i], tb))) {
+        const Entry extra = make_entry(t, key, text, flags, vid[i], tb);
+        if (!replace_all(t, extra)) {
+          arena_release(t, extra);
           status = fail(IE_ERR_CAPACITY, "no free placement for a new key: rebuild the table with more room");
-          n = i;  // apply (upload) what came before, stop here
-          break;
+          break;  // apply (upload) what came before, stop here
         }
         seed = t->dev.seed;
-        whole = true;
+        whole = whole_arena = true;  // (the slots rewritten in place so far moved with the rest)
         t->n_entries++;
         if (key.size() > kInlineKey && key.size() <= 2 * kInlineKey) t->dev.flags |= TF_LONG_KEYS;
         t->dev.maxtext = std::max<uint64_t>(t->dev.maxtext, text.size());
         continue;
       }
+      // the group's members move together: one from -> to map, applied once to the slot lists (a
+      // member may move into the old slot of another, so remapping member by member could move an
+      // already remapped slot again)
+      std::unordered_map<uint32_t, uint32_t> moved_to;
       std::vector<Entry> moved;
       for (uint32_t s2 : gs) moved.push_back(t->h_entries[s2]);
       for (uint32_t s2 : gs) {
@@ -1403,13 +1513,29 @@ int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
         const uint32_t from = gs[k], to = cand[k];
         t->h_entries[to] = moved[k];
         dirty.push_back(to);
-        if (from != to) {
-          for (uint32_t& cs : t->clock_slots)
-            if (cs == from && is_clock(moved[k].vid)) cs = to;
-          auto it = t->rawalt.find(moved[k].flags >> kTidShift);
-          if (it != t->rawalt.end())
-            for (uint32_t& rs : it->second)
-              if (rs == from) rs = to;
+        if (from != to) moved_to[from] = to;
+      }
+      if (!moved_to.empty()) {
+        for (uint32_t& cs : t->clock_slots) {
+          auto it = moved_to.find(cs);
+          if (it != moved_to.end()) cs = it->second;
+        }
+        std::vector<uint32_t> tabs;  // the tables whose pre-resolved entries moved
+        for (const Entry& e : moved)
+          if (e.flags & EF_RAWALT) tabs.push_back(e.flags >> kTidShift);
+        std::sort(tabs.begin(), tabs.end());
+        tabs.erase(std::unique(tabs.begin(), tabs.end()), tabs.end());
+        for (uint32_t tt : tabs) {
+          auto it = t->rawalt.find(tt);
+          if (it == t->rawalt.end()) continue;
+          for (uint32_t& rs : it->second) {
+            auto jt = moved_to.find(rs);
+            if (jt != moved_to.end()) rs = jt->second;
+          }
+        }
+        for (uint32_t& rs : rewritten) {
+          auto it = moved_to.find(rs);
+          if (it != moved_to.end()) rs = it->second;
         }
       }
       t->h_entries[cand.back()] = make_entry(t, key, text, flags, vid[i], tb);
@@ -1437,31 +1563,58 @@ int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
       const uint32_t roff = e.text_off - 4 - ((rl + 3u) & ~3u);
       const std::string raw((const char*)a + roff, rl), key(mirror_key(t, e));
       const uint32_t kflags = e.flags & (EF_KIND_MASK | EF_SPLICE_OK | EF_KEY_STR | EF_KEY_UNHASHABLE);
+      if (!room(((raw.size() + 3ull) & ~3ull) + key.size() + 4)) {
+        status = fail(IE_ERR_CAPACITY, "table arena full (limit reached even after compaction): rebuild the table");
+        continue;
+      }
+      arena_release(t, e);
       e = make_entry(t, key, raw, kflags | text_flags(raw), e.vid, tb);
       t->dev.maxtext = std::max<uint64_t>(t->dev.maxtext, raw.size());
       dirty.push_back(s2);
     }
     t->rawalt.erase(it);
   }
+  // dead bytes beyond the live ones (and beyond 64 KB): compact (one whole upload)
+  const uint64_t dead = t->h_arena.size() - std::min<uint64_t>(t->h_arena.size(), t->arena_live);
+  if (dead > t->arena_live && dead > (64u << 10)) {
+    compact_arena(t);
+    whole = whole_arena = true;
+  }
   // upload: the appended arena bytes, the changed entries, the changed pilots
   const bool grown = t->h_arena.size() > t->arena_cap;
-  if (grown) {  // grow the device arena (the whole mirror goes up again)
-    DevBuf na;
-    const uint64_t cap = t->h_arena.size() + std::max<uint64_t>(t->h_arena.size() / 4, 1ull << 16);
-    IE_HIP(na.ensure(cap + 16));
-    IE_HIP(hipMemset(na.p, 0, cap + 16));
-    IE_HIP(hipMemcpy(na.p, t->h_arena.data(), t->h_arena.size(), hipMemcpyHostToDevice));
-    t->arena.release();
-    t->arena = na;
-    na.p = nullptr;
-    t->arena_cap = cap;
-    t->dev.arena = (const uint8_t*)t->arena.p;
+  if (grown || whole_arena) {  // (re)allocate when grown; the whole mirror goes up
+    if (grown) {
+      DevBuf na;
+      const uint64_t cap = std::min<uint64_t>(t->arena_limit, t->h_arena.size() + std::max<uint64_t>(t->h_arena.size() / 4, 1ull << 16));
+      IE_HIP(na.ensure(cap + 16));
+      t->arena.release();
+      t->arena = na;
+      na.p = nullptr;
+      t->arena_cap = cap;
+      t->dev.arena = (const uint8_t*)t->arena.p;
+    }
+    IE_HIP(hipMemset(t->arena.p, 0, t->arena_cap + 16));
+    IE_HIP(hipMemcpy(t->arena.p, t->h_arena.data(), t->h_arena.size(), hipMemcpyHostToDevice));
+    arena0 = t->h_arena.size();
   }
-  // one upload and one kernel for the appended texts, the changed entries and pilots (the whole
-  // entry array in one copy when many changed)
+  // one upload and one kernel for the appended texts, the texts rewritten in place, the changed
+  // entries and pilots (the whole entry array in one copy when many changed)
   Patches pe;
-  if (t->h_arena.size() > arena0 && !grown)
+  if (t->h_arena.size() > arena0)
     pe.add((uint8_t*)t->arena.p + arena0, t->h_arena.data() + arena0, t->h_arena.size() - arena0);
+  if (!whole_arena) {
+    std::sort(rewritten.begin(), rewritten.end());
+    rewritten.erase(std::unique(rewritten.begin(), rewritten.end()), rewritten.end());
+    for (uint32_t s2 : rewritten) {
+      const Entry& e = t->h_entries[s2];
+      if (!(e.flags & EF_OCCUPIED)) continue;
+      uint64_t a, b2;
+      arena_span(t, e, a, b2);
+      if (a >= arena0) continue;  // inside the appended tail, sent whole above
+      b2 = std::min<uint64_t>(b2, arena0);
+      pe.add((uint8_t*)t->arena.p + a, t->h_arena.data() + a, b2 - a);
+    }
+  }
   std::sort(dirty.begin(), dirty.end());
   dirty.erase(std::unique(dirty.begin(), dirty.end()), dirty.end());
   if (whole || dirty.size() * 8 > t->h_entries.size()) {
@@ -1479,6 +1632,23 @@ int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
   if ((rc = apply_patches(t->patch_staging, pe))) return rc;
   t->dev.n_entries = (uint32_t)t->n_entries;
   return status;
+}
+
+// arena bookkeeping of a table (ie_table_set_update): bytes in use, bytes of live entries, compactions
+int ie_table_arena_stats(const ie_table* t, uint64_t* bytes, uint64_t* live, uint64_t* compactions) {
+  if (!t) return fail(IE_ERR_INVALID, "null argument");
+  if (bytes) *bytes = t->h_arena.size();
+  if (live) *live = t->arena_live;
+  if (compactions) *compactions = t->n_compactions;
+  return IE_SUCCESS;
+}
+
+// the largest arena ie_table_set_update may grow the table to (default and maximum 2^32 - 16:
+// every arena offset is a 32-bit word); a smaller limit makes IE_ERR_CAPACITY come earlier
+int ie_table_set_arena_limit(ie_table* t, uint64_t bytes) {
+  if (!t) return fail(IE_ERR_INVALID, "null argument");
+  t->arena_limit = std::min<uint64_t>(bytes, 0xFFFFFFF0ull);
+  return IE_SUCCESS;
 }
 
 int ie_exec_host_keys(ie_exec* x, uint8_t* buf, uint64_t cap, uint64_t* used) {

@@ -100,7 +100,7 @@ class InsertsTableSet:
     include/ie_amd.h ie_table_set_build): every string names the dict it resolves against.
     This is the batch form of get_interpdata for many forked interpreter states (config 5)."""
 
-    def __init__(self, dicts, dialect="py", clock=None, device=0, has_inserts_dir=False, mutable=True):
+    def __init__(self, dicts, dialect="py", clock=None, device=0, has_inserts_dir=False, mutable=False):
         self.clock_pinned = clock is not None  # else the wall clock at build (set_clock re-reads it)
         if clock is None:
             now = _dt.datetime.now()
@@ -190,6 +190,7 @@ class InsertsTableSet:
             return True
         kb, tb, kinds, tids, vids = [], [], [], [], []
         nd, kmemo, values = len(self.dicts), {}, self.values
+        vid_of, free = self._vids()
         for t, k, v in changes:
             if type(k) is not str:
                 raise TypeError("insert keys must be str")
@@ -200,10 +201,20 @@ class InsertsTableSet:
             if e is None:
                 e = kmemo[k] = N.enc(k)
             kb.append(e)
+            # the value id of (t, k): a rewrite keeps the key's id (its old value is dropped), a
+            # new key takes a freed id or a new one, a delete frees the key's id
+            tk = (t, k)
+            old = vid_of.get(tk)
+            if old is None and tk not in vid_of:
+                old = self._build_vid(t, k)
             if v is DELETE:
                 kinds.append(-1)
                 vids.append(0)
                 tb.append(b"")
+                if old is not None:
+                    values[old] = None
+                    free.append(old)
+                    vid_of[tk] = None
                 continue
             if type(v) is str:
                 kinds.append(N.KIND_STR)
@@ -212,8 +223,15 @@ class InsertsTableSet:
                 kd, text = render(v, self.dialect)
                 kinds.append(kd)
                 tb.append(N.enc(text))
-            vids.append(len(values))
-            values.append(v)
+            if old is None:
+                if free:
+                    old = free.pop()
+                else:
+                    old = len(values)
+                    values.append(None)
+                vid_of[tk] = old
+            values[old] = v
+            vids.append(old)
         if n <= 32:  # a scalar caller's few stores: ctypes arrays (numpy's per-call cost dominates)
             arr = (N.KV * n)(*[N.KV(k, len(k), t, len(t), kd, 0) for k, t, kd in zip(kb, tb, kinds)])
             ta, va = (ctypes.c_uint32 * n)(*tids), (ctypes.c_uint32 * n)(*vids)
@@ -245,6 +263,31 @@ class InsertsTableSet:
             return False
         N.check(rc, "ie_table_set_update")
         return True
+
+    def _vids(self):
+        """(t, key) -> value id of the keys stored since the build (None: deleted), and the freed ids."""
+        if not hasattr(self, "_vid_of"):
+            self._vid_of, self._free, self._tkeys = {}, [], {}
+        return self._vid_of, self._free
+
+    def _build_vid(self, t, k):
+        """The value id key k of dict t had at the build (its kv index), or None."""
+        m = self._tkeys.get(t)
+        if m is None:
+            a = self.starts[t]
+            m = self._tkeys[t] = {kk: a + i for i, kk in enumerate(self.keys[a:self.starts[t + 1]])}
+        return m.get(k)
+
+    def set_arena_limit(self, nbytes):
+        """Lower the text arena's limit (update then reports False, a rebuild, once it is reached)."""
+        N.check(N.lib().ie_table_set_arena_limit(self.h, nbytes), "ie_table_set_arena_limit")
+
+    def arena_stats(self):
+        """(bytes in use, live bytes, compactions) of the table set's text arena."""
+        b, l, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        N.check(N.lib().ie_table_arena_stats(self.h, ctypes.byref(b), ctypes.byref(l), ctypes.byref(c)),
+                "ie_table_arena_stats")
+        return b.value, l.value, c.value
 
     # --------------------------------------------------------------------------------------
     def run(self, strings, table_ids=None, exec_=None):
@@ -364,7 +407,8 @@ class InsertsTable(InsertsTableSet):
 
     def __init__(self, inserts, dialect="py", clock=None, device=0, has_inserts_dir=False, extra=None):
         merged = inserts if not extra else {**extra, **inserts}  # the inserts win (py:450 before 452)
-        super().__init__([merged], dialect=dialect, clock=clock, device=device, has_inserts_dir=has_inserts_dir)
+        super().__init__([merged], dialect=dialect, clock=clock, device=device, has_inserts_dir=has_inserts_dir,
+                         mutable=True)
         self._snapshot = (dict(inserts), {k: render(v, dialect)[1] for k, v in inserts.items()
                                           if isinstance(v, (list, dict))})
         self._version = getattr(inserts, "version", None)
@@ -521,6 +565,8 @@ class VersionedInserts(dict):
 _CACHE_SIZE = 8
 _cache = {}  # (id(inserts), dialect, device) -> (inserts, InsertsTable), least recently used first
 _dir_snap = {}  # path -> (stat signature, version, {key: value})
+_dir_checked = {}  # path -> time.monotonic() of its last signature check
+inserts_dir_ttl = 0.0  # seconds a directory signature stays trusted (0: checked on every call)
 _dir_bad = {}   # file path -> the error reading it raised (left out of the snapshot)
 
 
@@ -619,9 +665,17 @@ def inserts_dir_snapshot(path):
     """(version, {key: recursive_escape(value)}) for read_inserts_dir(path), the escape on the
     device. The reference reads the files at every lookup; here the directory is re-read when its
     stat signature (every entry's path, type, size and modification time) changed since the last
-    call, which sees every write that changes a file's mtime or size."""
-    sig = _dir_signature(path)
+    call, which sees every write that changes a file's mtime or size. Known deviation: a rewrite
+    that keeps a file's size AND lands within one mtime tick of the previous write is not seen
+    (the reference, which opens the file at every lookup, sees it). The signature costs one stat
+    per entry per call; `inserts_dir_ttl` (seconds, default 0: every call) lets a caller with a
+    large, rarely written directory skip it for that long after the last check."""
     hit = _dir_snap.get(path)
+    now = time.monotonic()
+    if hit is not None and inserts_dir_ttl > 0 and now - _dir_checked.get(path, -1e18) < inserts_dir_ttl:
+        return hit[1], hit[2]
+    sig = _dir_signature(path)
+    _dir_checked[path] = now
     if hit is not None and hit[0] == sig:
         return hit[1], hit[2]
     raw = read_inserts_dir(path)

@@ -414,7 +414,7 @@ def run_map_tasks(states, tasks, dialect="py", device=0):
     try:
         for task in tasks:
             if tset is None:
-                tset = IE.InsertsTableSet(states, dialect=dialect, device=device)
+                tset = IE.InsertsTableSet(states, dialect=dialect, device=device, mutable=True)
             if task["cmd"] == "goto_map":
                 outs.append(goto_map_states(states, task, dialect, device, tables=tset))
                 continue

@@ -4,7 +4,9 @@ between two batches (values rewritten, keys added, including 17-32 byte keys, ke
 brace-bearing values, typed values), the device copy is updated in place, and every string of the
 second batch is compared with the oracle resolving it against its state's mutated dict. Also: the
 pre-resolved values of a changed state go back to raw (they were resolved against the old dict),
-and the clock entries follow their slots when a new key re-places their pilot group."""
+the clock entries and pre-resolved values follow their slots when new keys re-place their pilot
+groups, the text arena is compacted and stays bounded under config 5's rewrite pattern, and a
+small forced arena limit gives IE_ERR_CAPACITY (a rebuild) instead of a wrapped offset."""
 import random
 
 import pytest
@@ -57,7 +59,7 @@ def test_updates_match_the_oracle_on_mutated_states():
         for j in range(t % 5):
             d["k%d" % j] = "v%d-%d" % (t, j)
         states.append(d)
-    tset = IE.InsertsTableSet(states, clock=CLOCK)
+    tset = IE.InsertsTableSet(states, clock=CLOCK, mutable=True)
     try:
         strings, ids = _strings(rng, states, 12)
         assert not _check(tset, states, strings, ids)
@@ -94,7 +96,7 @@ def test_preresolved_values_go_raw_when_their_state_changes():
     # 'a' holds braces: pre-resolved at build against b = 'B'; after b changes the device must not
     # keep the old resolution
     states = [{"a": "<{b}>", "b": "B"}, {"a": "<{b}>", "b": "C"}]
-    tset = IE.InsertsTableSet(states, clock=CLOCK)
+    tset = IE.InsertsTableSet(states, clock=CLOCK, mutable=True)
     try:
         assert [r for r in tset.results(["x{a}", "x{a}"], [0, 1])] == ["x<B>", "x<C>"]
         states[0]["b"] = "Z"
@@ -108,7 +110,7 @@ def test_clock_entries_follow_replaced_groups():
     # many new keys re-place pilot groups (some holding a clock entry); set_clock must still find
     # every table's clock entries
     states = [{"k": "v"} for _ in range(64)]
-    tset = IE.InsertsTableSet(states, clock=CLOCK)
+    tset = IE.InsertsTableSet(states, clock=CLOCK, mutable=True)
     try:
         # within the headroom IE_TABLE_MUTABLE leaves (slots for twice the built keys)
         changes = [(t, "new%d_%d" % (t, j), "x") for t in range(64) for j in range(2)]
@@ -126,7 +128,7 @@ def test_updates_beyond_the_headroom_ask_for_a_rebuild():
     # more new keys than the table set has free slots: update says so (False), and a rebuilt table
     # set answers for the grown dicts
     states = [{"k": "v"} for _ in range(64)]
-    tset = IE.InsertsTableSet(states, clock=CLOCK)
+    tset = IE.InsertsTableSet(states, clock=CLOCK, mutable=True)
     try:
         changes = [(t, "new%d_%d" % (t, j), "x") for t in range(64) for j in range(8)]
         for t, k, v in changes:
@@ -134,9 +136,93 @@ def test_updates_beyond_the_headroom_ask_for_a_rebuild():
         assert not tset.update(changes)
     finally:
         tset.close()
-    tset = IE.InsertsTableSet(states, clock=CLOCK)
+    tset = IE.InsertsTableSet(states, clock=CLOCK, mutable=True)
     try:
         got = tset.results(["{k}{new%d_7}" % t for t in range(64)], list(range(64)))
         assert got == ["vx"] * 64
+    finally:
+        tset.close()
+
+
+def test_clock_and_preresolved_slots_survive_many_group_moves():
+    # tables whose keys are mostly clock entries and pre-resolved values: every new key re-places its
+    # pilot group, whose members often move into each other's old slots; after each round the clock
+    # is re-set (every table's two clock entries must still be found) and a pre-resolved value's
+    # dependency changes (its slot must still be listed, so that it goes back to raw)
+    states = [{"a": "<{b}>", "b": "B%d" % t} for t in range(1500)]
+    tset = IE.InsertsTableSet(states, clock=CLOCK, mutable=True)
+    try:
+        for rnd in range(2):
+            changes = [(t, "n%d_%d" % (rnd, t), "x%d" % t) for t in range(len(states))]
+            for t, k, v in changes:
+                states[t][k] = v
+            assert tset.update(changes)
+            clk = (rnd + 1, 10 + rnd, 20 + rnd)
+            assert tset.set_clock(clk)
+            got = tset.results(["{HH:MM}|{HH:MM:SS}" for _ in states], list(range(len(states))))
+            assert got == ["%02d:%02d|%02d:%02d:%02d" % (clk[0], clk[1], *clk)] * len(states)
+        changes = [(t, "b", "Z%d" % t) for t in range(0, len(states), 2)]
+        for t, k, v in changes:
+            states[t][k] = v
+        assert tset.update(changes)
+        got = tset.results(["x{a}" for _ in states], list(range(len(states))))
+        assert got == ["x<%s>" % st["b"] for st in states]
+    finally:
+        tset.close()
+
+
+def test_arena_is_compacted_and_stays_bounded():
+    # config 5's loop rewrites a long history text in every state every iteration: replaced texts
+    # are counted dead and the arena is compacted once they outnumber the live bytes; every string
+    # matches the oracle on the mutated states after every round
+    rng = random.Random(5)
+    states = [{"hist": "h%d" % t, "name": "n%d" % t, "short": "s"} for t in range(200)]
+    tset = IE.InsertsTableSet(states, clock=CLOCK, mutable=True)
+    try:
+        for rnd in range(12):
+            changes = []
+            for t, d in enumerate(states):
+                # growing histories (appended), and short rewrites that fit in place
+                d["hist"] = d["hist"] + (" turn %d:%d " % (rnd, t)) * rng.randrange(1, 40)
+                d["short"] = "s%d" % (rnd % 3)
+                changes += [(t, "hist", d["hist"]), (t, "short", d["short"])]
+            assert tset.update(changes)
+            strings = ["{hist}|{short}|{name}" for _ in states] + ["x{short}y" for _ in states]
+            bad = _check(tset, states, strings, list(range(len(states))) * 2)
+            assert not bad, (rnd, bad[:3])
+            size, live, comp = tset.arena_stats()
+            # after every call the dead bytes are at most the live ones (or 64 KB)
+            assert size <= 2 * live + (64 << 10) + 64, (rnd, size, live)
+        size, live, comp = tset.arena_stats()
+        assert comp >= 1, (size, live, comp)
+        assert len(tset.values) <= sum(len(d) for d in states) + 2 * len(states)  # value ids reused
+    finally:
+        tset.close()
+
+
+def test_arena_limit_reports_capacity_not_a_wrap():
+    # a small forced limit: updates fit until the live texts exceed it, then update reports False
+    # (IE_ERR_CAPACITY, rebuild) instead of wrapping an offset; what came before stays correct
+    states = [{"v": "x", "w": "y"} for _ in range(64)]
+    tset = IE.InsertsTableSet(states, clock=CLOCK, mutable=True)
+    try:
+        size0, live0, _ = tset.arena_stats()
+        tset.set_arena_limit(size0 + 24 * 1024)
+        ok_rounds = 0
+        for rnd in range(40):
+            changes = [(t, "v", "%d:" % rnd + "z" * (40 * rnd)) for t in range(64)]
+            for t, k, v in changes:
+                states[t][k] = v
+            if not tset.update(changes):
+                break
+            ok_rounds += 1
+            bad = _check(tset, states, ["{v}{w}" for _ in states], list(range(64)))
+            assert not bad, (rnd, bad[:2])
+        assert 0 < ok_rounds < 40
+    finally:
+        tset.close()
+    tset = IE.InsertsTableSet(states, clock=CLOCK, mutable=True)
+    try:
+        assert not _check(tset, states, ["{v}{w}" for _ in states], list(range(64)))
     finally:
         tset.close()

@@ -53,7 +53,7 @@ def main():
     defaults = json.load(open(os.path.join(ROOT, "tests", "golden", "config5_stream.json"), encoding="utf-8"))["defaults"]
     states = [Wk.state_inserts(defaults, j) for j in range(10_000)]
     t0 = time.perf_counter()
-    tset = pkg.InsertsTableSet(states, clock=(12, 34, 56))
+    tset = pkg.InsertsTableSet(states, clock=(12, 34, 56), mutable=True)
     out["states_10k_build_ms"] = round(1e3 * (time.perf_counter() - t0), 2)
     times, lib_times = [], []
     for it in range(3):
