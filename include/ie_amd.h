@@ -232,10 +232,11 @@ int ie_exec_timing(ie_exec* x, ie_timing* out); /* syncs */
 #define IE_OPT_TILE 4
 #define IE_OPT_VIEWS 5 /* 1 (default): the host batch APIs resolve into a views layout (no look-back) and
                           pack the results in input order on the host; 0: packed on the device */
-#define IE_OPT_DEFER 7 /* views batches: 1: strings the chain jobs cannot finish go to a second pass in
-                          tiles of their own (the exact evaluator and the literal path then run on
-                          full tiles of such strings); -1 adaptive (above 0.4 % of a batch); 0
-                          (default): in their tiles (config 5 measured 2.5x slower deferred) */
+#define IE_OPT_DEFER 7 /* views batches in two passes: a first pass without the exact evaluator and
+                          the literal path (leaner registers and schedule), then the strings it could
+                          not finish in tiles of their own. 2 (default): batches of >= 2^21 strings,
+                          and any batch after one with > 0.4 % such strings; 1: always; -1: only the
+                          latter; 0: never (one pass, every string in its tile) */
 #define IE_OPT_RESERVE 8 /* views output of a packed batch: 0 (default): each tile claims its range on one
                           cursor (the bytes packed without gaps, *total = sum of lengths); F in 16..1024:
                           tile t writes at F/16 x its input span's offset from the batch's first byte

@@ -62,6 +62,14 @@ IE_HD uint32_t fmix32(uint32_t x) {
   return x;
 }
 
+// Two-choice (cuckoo) placement, the one-trip table experiment (IE_CUCKOO builds; host env
+// IE_CUCKOO=1): a key sits in one of its two candidate entries, both read in the same round.
+IE_HD void ck_slots(uint64_t h, uint32_t m, uint32_t& s1, uint32_t& s2) {
+  s1 = (uint32_t)(((uint64_t)fmix32((uint32_t)h) * m) >> 32);
+  s2 = (uint32_t)(((uint64_t)fmix32((uint32_t)(h >> 32) ^ 0x5BD1E995u) * m) >> 32);
+  if (s2 == s1) s2 = s1 + 1 == m ? 0u : s1 + 1;
+}
+
 // pilot group of a key hash (multiply-shift range reduction of the high word)
 IE_HD uint32_t ph_group(uint64_t h, uint32_t nb) {
   return (uint32_t)(((uint64_t)(uint32_t)(h >> 32) * (uint64_t)nb) >> 32);
@@ -124,6 +132,7 @@ constexpr uint32_t kMaxTables = 1u << (32 - kTidShift);
 enum : uint32_t {
   TF_HAS_DIR = 1u,
   TF_LONG_KEYS = 2u,  // some key is 17-32 bytes long: k_resolve's chain jobs compare key tails (LK)
+  TF_CUCKOO = 4u,     // two-choice placement (the IE_CUCKOO experiment), no pilots
 };
 
 constexpr uint32_t kInlineKey = 16;   // bytes of key kept inline in an entry

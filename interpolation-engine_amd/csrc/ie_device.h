@@ -115,8 +115,14 @@ struct Hit {
 };
 
 __device__ __forceinline__ uint32_t ph_lookup_slot(const DevTable& T, uint64_t h) {
+#ifdef IE_CUCKOO
+  uint32_t s1, s2;
+  ck_slots(h, T.m, s1, s2);
+  return s1;
+#else
   const uint32_t pilot = gld(T.pilots + ph_group(h, T.nb));
   return ph_slot(h, pilot, T.m);
+#endif
 }
 
 // the rest of a long key (bytes 16..klen) against the arena copy; b in any address space
@@ -135,16 +141,26 @@ __device__ __forceinline__ bool entry_head_ok(uint4 q0, uint32_t klen, uint32_t 
 // set. Returns the entry index or -1.
 __device__ int32_t find_bytes(const DevTable& T, uint32_t tid, const uint8_t* key, uint32_t klen, Hit& h) {
   const uint64_t hash = hash_key(klen, [&](uint32_t j) { return key[j]; }, T.seed, tid);
-  const uint32_t slot = ph_lookup_slot(T, hash);
-  const Entry* e = T.entries + slot;
-  const uint4 q0 = gld4((const uint4*)e), q1 = gld4((const uint4*)e + 1);
-  const uint32_t kw[4] = {q1.x, q1.y, q1.z, q1.w};
-  bool eq = entry_head_ok(q0, klen, tid);
-  const uint32_t ni = klen < kInlineKey ? klen : kInlineKey;
-  for (uint32_t j = 0; j < ni; j++) eq &= (uint8_t)(kw[j >> 2] >> (8 * (j & 3))) == key[j];
-  if (eq && klen > kInlineKey) eq = long_key_eq(T, q0, key, klen);
-  h = Hit{q0.y, q0.w, gld(&e->vid), q0.z};
-  return eq ? (int32_t)slot : -1;
+#ifdef IE_CUCKOO
+  uint32_t cs[2];
+  ck_slots(hash, T.m, cs[0], cs[1]);
+  for (int c = 0; c < 2; c++) {
+    const uint32_t slot = cs[c];
+#else
+  {
+    const uint32_t slot = ph_lookup_slot(T, hash);
+#endif
+    const Entry* e = T.entries + slot;
+    const uint4 q0 = gld4((const uint4*)e), q1 = gld4((const uint4*)e + 1);
+    const uint32_t kw[4] = {q1.x, q1.y, q1.z, q1.w};
+    bool eq = entry_head_ok(q0, klen, tid);
+    const uint32_t ni = klen < kInlineKey ? klen : kInlineKey;
+    for (uint32_t j = 0; j < ni; j++) eq &= (uint8_t)(kw[j >> 2] >> (8 * (j & 3))) == key[j];
+    if (eq && klen > kInlineKey) eq = long_key_eq(T, q0, key, klen);
+    h = Hit{q0.y, q0.w, gld(&e->vid), q0.z};
+    if (eq) return (int32_t)slot;
+  }
+  return -1;
 }
 
 // Lookup of a key held as dwords at a 4-byte aligned address (generic pointer),
@@ -163,9 +179,22 @@ __device__ __forceinline__ int32_t find_small(const DevTable& T, uint32_t tid, c
       hash = hash_word(hash, kw[d]);
     }
   }
+#ifdef IE_CUCKOO
+  uint32_t s1, s2;
+  ck_slots(hash, T.m, s1, s2);
+  const Entry* e = T.entries + s1;
+  const Entry* e2 = T.entries + s2;
+  const uint4 a0 = gld4((const uint4*)e), a1 = gld4((const uint4*)e + 1);
+  const uint4 b0 = gld4((const uint4*)e2), b1 = gld4((const uint4*)e2 + 1);
+  const bool eqb = entry_head_ok(b0, klen, tid) & (b1.x == kw[0]) & (b1.y == kw[1]) & (b1.z == kw[2]) & (b1.w == kw[3]);
+  const uint4 q0 = eqb ? b0 : a0, q1 = eqb ? b1 : a1;
+  const uint32_t slot = eqb ? s2 : s1;
+  e = eqb ? e2 : e;
+#else
   const uint32_t slot = ph_lookup_slot(T, hash);
   const Entry* e = T.entries + slot;
   const uint4 q0 = gld4((const uint4*)e), q1 = gld4((const uint4*)e + 1);
+#endif
   const bool eq = entry_head_ok(q0, klen, tid) & (q1.x == kw[0]) & (q1.y == kw[1]) & (q1.z == kw[2]) & (q1.w == kw[3]);
   h = Hit{q0.y, q0.w, gld(&e->vid), q0.z};
   return eq ? (int32_t)slot : -1;

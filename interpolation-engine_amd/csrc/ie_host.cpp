@@ -121,8 +121,9 @@ struct ie_exec {
   uint32_t opt_fast = 1;          // 0: exact evaluator only (IE_FAST)
   int32_t opt_tile = 0;           // k_resolve tile: 0 by call site, 256 or 512 forced (IE_TILE)
   int32_t opt_views = 1;          // host batch APIs resolve into a views layout (IE_VIEWS; 0: packed on the device)
-  int32_t opt_defer = 0;          // views batches: heavy strings to a second pass: -1 adaptive, 0 (default:
-                                  // measured slower on config 5) / 1 (IE_DEFER)
+  int32_t opt_defer = 2;          // views batches in two passes (a LEAN first pass, the strings it cannot
+                                  // finish in a second): 2 (default) batches of >= kLeanMinN strings or
+                                  // with many heavy strings, -1 the latter only, 0 never, 1 always (IE_DEFER)
   bool defer_slow = false;        // the adaptive choice (from an earlier batch's counts)
   int32_t opt_small = 1;          // host batches of <= 1024 strings / 64 KB: one pinned copy each way (IE_SMALL_HOST)
   int32_t opt_err_keys = 0;       // IE_OPT_ERROR_KEYS: record the missing key of every IE_E_INTERP string
@@ -304,6 +305,10 @@ int set_device(int32_t dev) {
 // [2..3] pool bytes used (u64), [4..8] telemetry (literal strings, deferred tiles, look-back polls,
 // exact-path strings, chain failures), [9] deferred-tile count, [10..11] views output cursor (u64),
 // [12] the fused unescape command's deferred-string count; zeroed on every call.
+// a views batch this large takes the two-pass path by default (IE_OPT_DEFER 2): the LEAN first pass
+// saves more than the second pass's fixed cost (config 3 0.844 -> 0.815 ms, config 2 0.108 -> 0.106 ms,
+// profiles/r05/ab/lean_two_pass.txt)
+constexpr uint64_t kLeanMinN = 1ull << 19;
 constexpr uint32_t kSumShards = 16;  // reserved-range tile sums (IE_OPT_RESERVE), 128 B apart after the counters
 constexpr uint64_t kCounterBytes = 64 + kSumShards * 128;
 int ensure_work(ie_exec* x, int op, uint64_t n) {
@@ -467,7 +472,7 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
       IE_HIP(launch_unescape_cmd(B, W, t->dev, out->bytes, cap, (uint64_t*)x->u_off.p, (uint32_t*)x->u_len.p,
                                  d_tid ? (uint32_t*)x->u_tid.p : nullptr, st));
     } else if (d_out_len && !x->in_cmd && !x->opt_noeval &&
-               (x->opt_defer == 1 || (x->opt_defer < 0 && x->defer_slow))) {
+               (x->opt_defer == 1 || (x->opt_defer != 0 && x->defer_slow) || (x->opt_defer == 2 && n >= kLeanMinN))) {
       // a views batch with heavy strings: two passes (launch_resolve_deferring)
       IE_HIP(x->u_list.ensure(n * 4 + 4));
       IE_HIP(x->u_off.ensure(n * 8 + 8));
@@ -1052,7 +1057,45 @@ int upload_table(const std::vector<Ent>& ents, uint32_t n_tables, int32_t dialec
   uint64_t seed = 0xA0761D6478BD642Full;
   std::vector<uint16_t> pilots;
   std::vector<uint32_t> slot_of;
-  for (int attempt = 0;; attempt++) {
+  // the one-trip table experiment (IE_CUCKOO=1 with a k_resolve built -DIE_CUCKOO): two-choice
+  // placement at load 0.4, no pilots; such a table takes no ie_table_set_update
+  static const bool cuckoo = getenv("IE_CUCKOO") && atoi(getenv("IE_CUCKOO")) == 1;
+  if (cuckoo) {
+    m = std::max<uint64_t>(16, (5 * nk) / 2 + 16);
+    pilots.assign(nb, 0);
+    for (int attempt = 0;; attempt++) {
+      if (attempt > 64) return fail(IE_ERR_INVALID, "cuckoo placement failed");
+      std::vector<uint64_t> hs(items.size());
+      for (size_t i = 0; i < items.size(); i++) hs[i] = key_hash(ents[i].key, seed, ents[i].tid);
+      std::vector<int64_t> occ(m, -1);
+      bool ok = true;
+      for (size_t i = 0; i < items.size() && ok; i++) {
+        int64_t cur = (int64_t)i;
+        uint32_t a, b;
+        ck_slots(hs[cur], (uint32_t)m, a, b);
+        uint32_t pos = a;
+        int kick = 0;
+        for (; kick < 1000; kick++) {
+          if (occ[pos] < 0) {
+            occ[pos] = cur;
+            break;
+          }
+          std::swap(cur, occ[pos]);
+          ck_slots(hs[cur], (uint32_t)m, a, b);
+          pos = pos == a ? b : a;
+        }
+        ok = kick < 1000;
+      }
+      if (ok) {
+        slot_of.assign(items.size(), 0);
+        for (uint64_t s2 = 0; s2 < m; s2++)
+          if (occ[s2] >= 0) slot_of[occ[s2]] = (uint32_t)s2;
+        break;
+      }
+      seed = fmix64_host(seed + 0x9E3779B97F4A7C15ull);
+    }
+  }
+  for (int attempt = 0; !cuckoo; attempt++) {
     if (m > (1ull << 31)) return fail(IE_ERR_INVALID, "table too large");
     std::vector<uint64_t> hs(items.size());
     for (size_t i = 0; i < items.size(); i++) hs[i] = key_hash(ents[i].key, seed, ents[i].tid);
@@ -1101,7 +1144,8 @@ int upload_table(const std::vector<Ent>& ents, uint32_t n_tables, int32_t dialec
   t->dev.n_entries = (uint32_t)ents.size();
   t->dev.n_tables = n_tables;
   t->dev.dialect = (uint32_t)dialect;
-  t->dev.flags = ((flags & IE_TABLE_HAS_INSERTS_DIR) ? TF_HAS_DIR : 0u) | (long_keys ? TF_LONG_KEYS : 0u);
+  t->dev.flags = ((flags & IE_TABLE_HAS_INSERTS_DIR) ? TF_HAS_DIR : 0u) | (long_keys ? TF_LONG_KEYS : 0u) |
+                 (cuckoo ? TF_CUCKOO : 0u);
   t->dev.maxtext = maxtext;
   t->h_entries = std::move(entries);
   t->h_pilots = std::move(pilots);
@@ -1398,6 +1442,7 @@ int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
     if (kv[i].text_len && !kv[i].text) return fail(IE_ERR_INVALID, "null text");
     if (kv[i].key_len >= 0xFFFFFFF0ull || kv[i].text_len >= 0xFFFFFFF0ull) return fail(IE_ERR_INVALID, "key or text above 4 GiB");
   }
+  if (t->dev.flags & TF_CUCKOO) return fail(IE_ERR_INVALID, "a two-choice (IE_CUCKOO) table takes no updates");
   int rc = set_device(t->device);
   if (rc) return rc;
   IE_HIP(hipDeviceSynchronize());  // no batch may still read the table
@@ -1686,7 +1731,7 @@ int ie_exec_create(int32_t device, void* hip_stream, ie_exec** out) {
     x->opt_reserve = v >= 16 && v <= 1024 ? (uint32_t)v : 0u;
   }
   if (const char* e = getenv("IE_SMALL_HOST")) x->opt_small = atoi(e) != 0;
-  if (const char* e = getenv("IE_DEFER")) x->opt_defer = atoi(e) < 0 ? -1 : atoi(e) != 0 ? 1 : 0;
+  if (const char* e = getenv("IE_DEFER")) x->opt_defer = atoi(e) < 0 ? -1 : atoi(e) >= 2 ? 2 : atoi(e) != 0 ? 1 : 0;
   if (const char* e = getenv("IE_DEBUG_STAMPS")) x->stamps_path = e;
   if (hip_stream) {
     x->stream = (hipStream_t)hip_stream;
@@ -1820,7 +1865,7 @@ int ie_exec_set_option(ie_exec* x, int32_t option, int64_t value) {
       x->opt_reserve = (uint32_t)value;
       return IE_SUCCESS;
     case IE_OPT_DEFER:
-      if (value < -1 || value > 1) return fail(IE_ERR_INVALID, "defer must be -1, 0 or 1");
+      if (value < -1 || value > 2) return fail(IE_ERR_INVALID, "defer must be -1, 0, 1 or 2");
       x->opt_defer = (int32_t)value;
       return IE_SUCCESS;
     case IE_OPT_ERROR_KEYS:

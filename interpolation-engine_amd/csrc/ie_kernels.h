@@ -72,6 +72,11 @@ struct Work {
   // staged, or needing the literal path) are listed here for the deferred pass
   uint32_t* udefer_list;  // n
   uint32_t* udefer_count; // 1
+  // a LEAN first pass (launch_resolve_deferring) writes each deferred string's view for the second
+  // pass itself: its input offset, length and table id at the string's place in udefer_list
+  uint64_t* sub_off;
+  uint32_t* sub_len;
+  uint32_t* sub_tid;
   uint64_t* shards;      // 16 u64 words 16 apart (reserved ranges' tile sums), zeroed per call
   uint32_t n_shards;
   uint32_t defer_slow;   // k_resolve on a views batch: strings the chain jobs cannot finish are listed

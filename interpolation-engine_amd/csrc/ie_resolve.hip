@@ -561,12 +561,24 @@ __device__ void resolve_jobs(const DevTable& T, const lds_u8* tile, const ChainJ
       asm volatile("" ::"v"(h[0]), "v"(h[1]));
       stamp[6] = __builtin_amdgcn_s_memrealtime();
     }
+#ifdef IE_CUCKOO
+    // two-choice table: both candidate entries in one round (one memory latency per level)
+    uint32_t slot2[NJ];
+#pragma unroll
+    for (int q = 0; q < NJ; q++) {
+      uint32_t a = 0, b = 0;
+      if (on[q]) ck_slots(h[q], T.m, a, b);
+      slot[q] = a;
+      slot2[q] = b;
+    }
+#else
     // pilots, then entries: two memory latencies per round, every job's in flight together
 #pragma unroll
     for (int q = 0; q < NJ; q++) {
       const uint32_t pilot = on[q] ? (uint32_t)gld(T.pilots + ph_group(h[q], T.nb)) : 0u;
       slot[q] = on[q] ? ph_slot(h[q], pilot, T.m) : 0u;
     }
+#endif
     if (stamp && threadIdx.x == 0 && r == 0) {  // diagnostic: pilots arrived
       asm volatile("" ::"v"(slot[0]), "v"(slot[1]));
       stamp[13] = __builtin_amdgcn_s_memrealtime();
@@ -581,6 +593,17 @@ __device__ void resolve_jobs(const DevTable& T, const lds_u8* tile, const ChainJ
         P[q].q0 = gld4(e);
         P[q].q1 = gld4(e + 1);
         P[q].q2 = gld4(e + 2);
+#ifdef IE_CUCKOO
+        const uint4* e2 = (const uint4*)(T.entries + slot2[q]);
+        const uint4 b0 = gld4(e2), b1 = gld4(e2 + 1), b2 = gld4(e2 + 2);
+        // the second candidate holds the key: take it (its slot, its words)
+        const bool sb = on[q] && entry_head_ok(b0, klen[q], tb[q]) & (b1.x == kw[q].x) & (b1.y == kw[q].y) &
+                        (b1.z == kw[q].z) & (b1.w == kw[q].w);
+        if (sb) {
+          P[q].q0 = b0, P[q].q1 = b1, P[q].q2 = b2;
+          slot[q] = slot2[q];
+        }
+#endif
         if (__any(on[q] && wh[q])) wvid[q] = on[q] && wh[q] ? gld(&T.entries[slot[q]].vid) : IE_VID_NONE;
       }
     }
@@ -1095,7 +1118,7 @@ __global__ __launch_bounds__(kRBlock) void k_emit_windows(Batch B0, Work W, DevT
 // staged string is unescaped in place in the LDS stage (after the classification; its chunks are
 // classified again) and then resolved; strings that cannot be finished there (not staged, or
 // needing the literal path) go to W.udefer_list for the deferred pass.
-template <bool FAILC, bool MULTI, bool VIEWS, bool UNESC = false, bool LK = false>
+template <bool FAILC, bool MULTI, bool VIEWS, bool UNESC = false, bool LK = false, bool LEAN = false>
 __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES_PER_EU))) void k_resolve(Batch B0, Work W, DevTable T, uint8_t* out,
                                                     uint64_t cap) {
   // a deferred subset counts its strings on the device (the grid is sized for B0.n)
@@ -1324,7 +1347,10 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
     // a views batch with heavy strings (W.defer_slow, chosen per batch by the host): the strings the
     // chain jobs could not finish go to a second pass, in tiles of their own, instead of holding up
     // this tile (and its 255 other strings) in the exact evaluator or the literal path
-    const bool dslow = VIEWS && !UNESC && W.defer_slow != 0u;
+    // LEAN (a views first pass, launch_resolve_deferring): this instance has no exact evaluator and
+    // no literal path at all, so its registers and schedule are the chain evaluator's alone (config 3
+    // 0.840 -> 0.804 ms, profiles/r05/ab/); every string they would take is deferred
+    const bool dslow = VIEWS && !UNESC && (LEAN || W.defer_slow != 0u);
     if (dslow) {
       const uint64_t dm = __ballot(slow);
       if (dm && lane == 0) atomicAdd(W.stats + 3, (uint32_t)__popcll(dm));
@@ -1332,8 +1358,8 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
       slow = false;
     }
     // the rest: the exact evaluator (scratch: the lane's own chain-evaluator columns)
-    const uint64_t slow_m = __ballot(slow);
-    if (slow_m) {
+    const uint64_t slow_m = LEAN ? 0ull : __ballot(slow);
+    if (!LEAN && slow_m) {
       if (lane == 0 && W.fast_mode) atomicAdd(W.stats + 3, (uint32_t)__popcll(slow_m));  // rare
       lds_u8* const kb = (lds_u8*)(s_u + tid * kKeyCap);
       lds_u32* const stk = (lds_u32*)(lds_u8*)(s_u + kKbufLds) + tid;
@@ -1358,7 +1384,13 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
         uint32_t base = 0;
         if (lane == 0) base = atomicAdd(W.udefer_count, (uint32_t)__popcll(m));
         base = __shfl(base, 0, 64);
-        if (dfr) W.udefer_list[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)i;
+        const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        if (dfr) W.udefer_list[pos] = (uint32_t)i;
+        if (LEAN && dfr) {  // (the second pass's view of the string: no gather kernel)
+          W.sub_off[pos] = so;
+          W.sub_len[pos] = (uint32_t)min(sn, (uint64_t)0xFFFFFFFFu);
+          if (MULTI) W.sub_tid[pos] = tid_s;
+        }
       }
     }
     pend = i < B.n && st == kStatusPending;
@@ -1370,8 +1402,8 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
   IE_STAMP(2);
 
   // ---- 3. literal path for the pending strings, one wave each; results in the union ----
-  const uint32_t npend = s_misc[1];
-  if (npend) {  // uniform
+  const uint32_t npend = LEAN ? 0u : s_misc[1];
+  if (!LEAN && npend) {  // uniform
   if (tid == 0) atomicAdd(W.stats, npend);
   // the descriptors wait in the free part of the union while the waves run the literal path (its
   // registers are what the wave then needs; s_lit uses the union's first 4 * kRBlock bytes)
@@ -1700,7 +1732,7 @@ __global__ __launch_bounds__(kRBlock) void k_unesc_deferred(Batch B, Work W, uin
 }
 
 hipError_t launch_resolve_impl(const Batch& B, const Work& W, const DevTable& T, uint8_t* out, uint64_t cap,
-                               hipStream_t st, bool unesc = false) {
+                               hipStream_t st, bool unesc = false, bool lean = false) {
   const uint64_t tiles = (B.n + kRBlock - 1) / kRBlock;
   if (!tiles) return hipSuccess;
   if (tiles > 0xFFFFFFFFull) return hipErrorInvalidValue;
@@ -1719,6 +1751,25 @@ hipError_t launch_resolve_impl(const Batch& B, const Work& W, const DevTable& T,
   // LK: a table with 17-32 byte keys gets the instances whose chain jobs take such keys (they cost
   // config 3 3 %: their registers; config 5 -32 %: its long keys leave the exact evaluator)
   const int variant = ((T.flags & TF_LONG_KEYS) ? 8 : 0) | (W.fail_commit ? 4 : 0) | (multi ? 2 : 0) | (B.out_len ? 1 : 0);
+#if !defined(IE_RESOLVE_WIDE)
+  if (lean && B.out_len) {  // the views first pass without the exact evaluator and literal path
+    switch (variant >> 1) {
+#define IE_LAUNCH_LEAN(V, F, M, L) \
+  case V: hipLaunchKernelGGL((k_resolve<F, M, true, false, L, true>), dim3(grid), dim3(kRBlock), 0, st, B, W, T, out, cap); break;
+      IE_LAUNCH_LEAN(0, false, false, false)
+      IE_LAUNCH_LEAN(1, false, true, false)
+      IE_LAUNCH_LEAN(2, true, false, false)
+      IE_LAUNCH_LEAN(3, true, true, false)
+      IE_LAUNCH_LEAN(4, false, false, true)
+      IE_LAUNCH_LEAN(5, false, true, true)
+      IE_LAUNCH_LEAN(6, true, false, true)
+      IE_LAUNCH_LEAN(7, true, true, true)
+#undef IE_LAUNCH_LEAN
+    }
+    hipLaunchKernelGGL(k_emit_windows, dim3(grid < 512u ? grid : 512u), dim3(kRBlock), 0, st, B, W, T, out);
+    return hipGetLastError();
+  }
+#endif
   switch (variant) {
 #define IE_LAUNCH(V, F, M, S, L) \
   case V: hipLaunchKernelGGL((k_resolve<F, M, S, false, L>), dim3(grid), dim3(kRBlock), 0, st, B, W, T, out, cap); break;
@@ -1809,37 +1860,28 @@ hipError_t launch_patch_inline(const PatchInline& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-// the listed strings (W.udefer_list) as a views subset of the batch (their bytes where they are)
-__global__ void k_gather_listed(Batch B, Work W, uint64_t* sub_off, uint32_t* sub_len, uint32_t* sub_tid) {
-  const uint32_t count = __hip_atomic_load(W.udefer_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < count; j += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t idx = W.udefer_list[j];
-    const uint64_t so = gld(B.in_off + idx);
-    sub_off[j] = so;
-    sub_len[j] = B.in_len ? gld(B.in_len + idx) : (uint32_t)min(gld(B.in_off + idx + 1) - so, (uint64_t)0xFFFFFFFFu);
-    if (sub_tid) sub_tid[j] = B.table_id ? gld(B.table_id + idx) : 0u;
-  }
-}
-
 // k_resolve on a views batch in two passes (IE_OPT_DEFER): the strings the chain jobs could not
-// finish are listed by the first (W.defer_slow) and resolved by the second as a subset
+// finish are listed by the first (the LEAN instances) and resolved by the second (the full ones) as
+// a subset
 hipError_t launch_resolve_deferring(const Batch& B, const Work& W, const DevTable& T, uint8_t* out, uint64_t cap,
                                     uint64_t* sub_off, uint32_t* sub_len, uint32_t* sub_tid, hipStream_t st) {
   if (!B.out_len || !B.n) return hipErrorInvalidValue;
+  // first pass: the LEAN instances (no exact evaluator, no literal path), which also write the
+  // deferred strings' views (sub_off / sub_len / sub_tid) for the second pass
+  const bool multi = B.table_id != nullptr;
   Work W1 = W;
   W1.defer_slow = 1;
-  hipError_t e = IE_RNS::launch_resolve_impl(B, W1, T, out, cap, st);
+  W1.sub_off = sub_off;
+  W1.sub_len = sub_len;
+  W1.sub_tid = multi ? sub_tid : nullptr;
+  hipError_t e = IE_RNS::launch_resolve_impl(B, W1, T, out, cap, st, false, true);
   if (e != hipSuccess) return e;
-  // the windowed-tile list is the second pass's again
-  e = hipMemsetAsync(W.defer_count, 0, sizeof(uint32_t), st);
-  if (e != hipSuccess) return e;
-  const bool multi = B.table_id != nullptr;
-  const uint32_t gb = (uint32_t)((B.n + 255) / 256 < 1024 ? (B.n + 255) / 256 : 1024);
-  hipLaunchKernelGGL(k_gather_listed, dim3(gb), dim3(256), 0, st, B, W, sub_off, sub_len, multi ? sub_tid : nullptr);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  // the second pass's windowed-tile list restarts at 0: its own counter word (counters word 13,
+  // zeroed with the rest at the call's start; the first pass's list was consumed by its
+  // k_emit_windows)
   Work W2 = W;
   W2.defer_slow = 0;
+  W2.defer_count = W.defer_count + 4;
   const Batch D{B.bytes, sub_off, B.n, B.out_off, B.status, B.value_id, multi ? sub_tid : nullptr, sub_len, B.out_len,
                 W.udefer_list, W.udefer_count};
   return IE_RNS::launch_resolve_impl(D, W2, T, out, cap, st);
