@@ -157,6 +157,10 @@ def parse(argv=None):
                          "(ie_table_set_update) and resolving the batch again (0: none)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="",
                     help="weak: --n units per GPU; strong: --n units over all GPUs (default per config: DEFAULT_SCALING)")
+    ap.add_argument("--check-shard", type=int, default=-1,
+                    help="strings of every rank's own shard checked against the oracle after the timed steps "
+                         "(status, length, FNV-1a per string; config 5: the rank's whole batch); -1: 20000 "
+                         "when there are several ranks, 0 otherwise")
     ap.add_argument("--dry-run", action="store_true",
                     help="control plane only (launcher, rank/device assignment, barrier, max over ranks): no library, "
                          "no GPU; --dry-devices devices are taken as visible")
@@ -473,6 +477,19 @@ def main(argv=None):
         res = Result(N, n, d_out, d_ooff, d_st, d_olen, d_tot)
         replay = replay_states(args, W, x, resolve, res)
 
+    # every rank checks its own shard (the 1 -> 8 GPU runs verify every GPU's results, not rank 0's)
+    nchk = args.check_shard if args.check_shard >= 0 else (20000 if world > 1 else 0)
+    mine = None
+    if nchk:
+        res = Result(N, n, d_out2 if cmd else d_out, d_ooff2 if cmd else d_ooff, d_st2 if cmd else d_st,
+                     d_olen2 if cmd else d_olen, d_tot2 if cmd else d_tot)
+        mine = shard_check(args, W, res, nchk, rank, first)
+    checks, launch = [mine], [round(gpu_ms, 4)]
+    if dist:
+        checks, launch = [None] * world, [None] * world
+        dist.all_gather_object(checks, mine)
+        dist.all_gather_object(launch, round(gpu_ms, 4))
+
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic_cfg%d.json" % cfg)
     if os.path.exists(pmc_path):
@@ -515,11 +532,14 @@ def main(argv=None):
                          "kernel": "k_resolve (single pass: stage, evaluate, %s, emit) + k_emit_windows"
                                    % ("claim the tile's output range" if views else "look-back"),
                          "launch_ms": round(gpu_ms, 4), "alg_bytes_per_launch": alg_bytes,
+                         "launch_ms_ranks": launch, "launch_ms_max": max(launch), "launch_ms_min": min(launch),
                          "telemetry": {"kernel_ms": round(tm.resolve_ms, 4), "literal_strings": int(tm.n_complex),
                                        "windowed_tiles": int(tm.n_direct), "exact_strings": int(tm.n_exact),
                                        "chain_failures": int(tm.n_chain_fail), "deferred": int(tm.n_deferred)}},
             "cpu_baseline": cpu,
         }
+        if nchk:
+            line["shard_checks"] = checks
         if cfg == 5:
             line["config"]["states_per_gpu"] = n_units
             line["replay"] = replay
@@ -599,6 +619,27 @@ def cpu_baseline(args, W, N, res):
                       "single-thread on the first %d (%.2f s)%s; GPU results identical on all %d: %s"
                       % (m, int(offs[m]), threads, wall, m1, wall1,
                          "; each OK result then through the unescape command" if cmd else "", m, same)}
+
+
+def shard_check(args, W, res, m, rank, first):
+    """This rank's own results against the oracle: the first m strings of its shard (config 4: each
+    OK result then through the unescape command; config 5: every string of the rank's states, each
+    against its own state's dict), per string status, length and FNV-1a of the bytes."""
+    from oracle import oracle as O
+    threads, _ = cpu_share()
+    if args.config == 5:
+        oracles = [O.Oracle(ins, "py", clock=CLOCK) for ins in W.states]
+        buf = np.frombuffer(W.blob + bytes(1), np.uint8)
+        st, ln, hs = np.zeros(W.n, np.uint8), np.zeros(W.n, np.uint64), np.zeros(W.n, np.uint64)
+        O.run_batch_sets(oracles, W.ids, buf, W.offs, threads, st, ln, hs)
+        return {"rank": rank, "first_state": first, "states": len(W.states), "strings": W.n,
+                "identical": res.compare(W.n, st, ln, hs, threads)}
+    m = int(min(m, W.n))
+    ref = O.Oracle.from_kv(ctypes.cast(W.kvp, ctypes.c_void_p), W.nkv, "py", clock=CLOCK)
+    buf, offs = W.host_sample(m)
+    st, ln, hs = np.zeros(m, np.uint8), np.zeros(m, np.uint64), np.zeros(m, np.uint64)
+    ref.run_batch(buf, offs, m, threads, st, ln, hs, None, unescape_cmd=args.config == 4)
+    return {"rank": rank, "first_string": first, "strings": m, "identical": res.compare(m, st, ln, hs, threads)}
 
 
 def replay_states(args, W, x, resolve, res):

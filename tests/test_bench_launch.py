@@ -65,3 +65,24 @@ def test_two_ranks_on_one_card_report_one_gpu():
     assert p.returncode == 0, p.stderr[-3000:]
     assert line["n_gpus"] == 1 and line["ranks"] == 2 and line["devices"] == [0, 0]
     assert line["config"]["statuses"] == {"OK_STR": 200000} and line["value"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config,n,scaling", [(4, 400000, "weak"), (5, 600, "strong")], ids=["cfg4-weak", "cfg5-strong"])
+def test_two_ranks_check_their_own_shards(config, n, scaling):
+    """The multi-rank path of the configs the 8-GPU run scales differently: config 4 weak (every rank
+    its own 12.5M-string shape, the fused unescape command), config 5 strong (the states split over
+    the ranks). Every rank checks its own shard against the oracle and the line carries every
+    rank's kernel time."""
+    p, line = _run("--gpus", "2", "--device", "0", "--config", str(config), "--n", str(n), "--steps", "3",
+                   "--warmup", "1", "--no-cpu", "--replay", "0", "--check-shard", "20000", timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert line["ranks"] == 2 and line["scaling"] == scaling
+    checks = line["shard_checks"]
+    assert [c["rank"] for c in checks] == [0, 1] and all(c["identical"] for c in checks), checks
+    if scaling == "weak":
+        assert [c["first_string"] for c in checks] == [0, n]
+    else:
+        assert [c["first_state"] for c in checks] == [0, n // 2] and sum(c["states"] for c in checks) == n
+    r = line["roofline"]
+    assert len(r["launch_ms_ranks"]) == 2 and r["launch_ms_max"] >= r["launch_ms_min"] > 0
