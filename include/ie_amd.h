@@ -66,6 +66,9 @@ enum ie_status {
   IE_NEEDS_HOST = 7,      /* key missing and an --inserts-dir is configured (py:452-461)   */
   IE_DIVERGED = 8,        /* iteration cap hit: the reference would loop forever           */
   IE_E_OVERFLOW = 9,      /* string over its single-pass scratch budget (host APIs retry)  */
+  IE_E_NO_MATCH = 11,     /* ie_goto_map: no key matches the text (py:1708's AssertionError)   */
+  IE_E_NO_NULL = 12,      /* ie_goto_map: the text failed to interpolate and no key is 'NULL'
+                             (py:1703's AssertionError)                                        */
   IE_RECURSE = 10         /* ie_unescape_cmd_device, py dialect: the unescaped item is a whole-string
                              '{key}' as written, so recursive_interpolate walks its result again
                              (py:1463-1464); the result (a str, list or dict; value_id = the insert
@@ -369,6 +372,59 @@ int ie_wildcard_match_device(ie_exec* x, const ie_wildcards* w, const uint8_t* d
                              uint64_t n, const uint32_t* d_range, int32_t* d_match, uint8_t* d_ncap, uint32_t* d_caps);
 int ie_wildcard_match_batch(ie_exec* x, const ie_wildcards* w, const uint8_t* bytes, const uint64_t* offsets,
                             uint64_t n, const uint32_t* range, int32_t* match, uint8_t* ncap, uint32_t* caps);
+
+/* ---- the map commands over the states of a table set (py:1689-1773, 1843-1868;
+ * rust-project/src/runtime.rs:1085-1169, 1649-1731, 1754-1775). State s is table s of the set;
+ * every interpolation runs in the resolve kernels and every wildcard test in k_wildcard: a command
+ * over any number of states is a few device batches (synchronous; results owned by the library
+ * until ie_map_result_free). A map is one {key: value} pair of the task's target_maps /
+ * wildcard_maps, raw (the task pre-pass skips them, py:1471-1477).
+ *
+ * Per item: status IE_OK_STR (the result in bytes/offsets), or why it failed. `where` names the
+ * string whose failure the reference raises: 0 = the item itself (goto_map: its text; replace:
+ * the leaf, bytes = the string that failed), 1 + j = map j's key, 1 + n_maps + j = map j's value
+ * (replace: bytes = the text the key matched; its captures are that key's wildcard groups).
+ * `chosen`: the map taken (-1 none). value_id: a typed whole-string result's insert (names). ---- */
+typedef struct ie_map_pair {
+  const char* key;
+  uint64_t key_len;
+  const char* value;
+  uint64_t value_len;
+} ie_map_pair;
+typedef struct ie_map_result {
+  uint8_t* bytes;
+  uint64_t bytes_len;
+  uint64_t* offsets;  /* n + 1 */
+  uint8_t* status;    /* n     */
+  uint32_t* where;    /* n     */
+  int32_t* chosen;    /* n     */
+  uint32_t* value_id; /* n     */
+  uint64_t n;
+} ie_map_result;
+void ie_map_result_free(ie_map_result* r);
+/* goto_map (py:1689-1711) in every state: text, keys and values interpolated and str()-ed; the text's
+ * InterpolationException (IE_E_INTERP only) takes the 'NULL' key's value (IE_E_NO_NULL without
+ * one), any other failure of the text, then the first failing key, then the first failing value
+ * propagates; else the value of the first key that wildcard-matches the text (IE_E_NO_MATCH: none).
+ * n = the number of tables; bytes: the target (the caller treats 'CONTINUE'). */
+int ie_goto_map(ie_exec* x, const ie_table* t, const char* text, uint64_t text_len, const ie_map_pair* maps,
+                uint32_t n_maps, ie_map_result** out);
+/* replace_map (py:1713-1773): replace_str on n leaves (leaf i: a string of state table_id[i], the
+ * caller's walk of the item, py:1748-1759): each pass interpolates the leaf, takes the first map whose
+ * interpolated key matches (a key that fails before a match fails the leaf), interpolates its value
+ * against inserts | {'1': capture 1, ...}; repeat_until_done repeats until nothing changes (the
+ * reference's unbounded loop stops at 100000 passes: IE_DIVERGED). name (nullable): output_name,
+ * interpolated per state (py:1715, no str(): typed results keep their value id) into *names. The
+ * clock the keys read is the table's (ie_table_set_clock before the call). */
+int ie_replace_map(ie_exec* x, const ie_table* t, const char* name, uint64_t name_len, const uint8_t* bytes,
+                   const uint64_t* offsets, const uint32_t* table_id, uint64_t n, const ie_map_pair* maps,
+                   uint32_t n_maps, int32_t repeat_until_done, ie_map_result** names, ie_map_result** out);
+/* delete (except_matching = 0: the keys some wildcard matches, py:1843-1855) / delete_except (1: the
+ * keys no wildcard matches, py:1857-1868) in the given states (NULL: every state): wildcards packed
+ * (offsets[n + 1]), as the task pre-pass left them; the keys are removed from the table set
+ * (ie_table_set_update) and listed in out (bytes = the key, where = its state). */
+int ie_delete_keys(ie_exec* x, ie_table* t, const uint32_t* states, uint32_t n_states, const uint8_t* wbytes,
+                   const uint64_t* woffsets, uint32_t n_wildcards, int32_t except_matching, ie_map_result** out);
 
 /* ---- get_simple_insertkey (py:477-495 / interp.rs:11-29), host-side classifier used by the
  * callers' control flow (recursive_interpolate, validate_program). Returns 1 when the reference

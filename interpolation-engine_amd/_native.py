@@ -13,9 +13,10 @@ LIB_PATH = os.environ.get("IE_LIB_PATH") or os.path.join(PKG_DIR, "libie_amd.so"
 IE_DIALECT = {"py": 0, "rs": 1}
 KIND_STR, KIND_INT, KIND_LIST, KIND_FLOAT, KIND_BOOL, KIND_NULL, KIND_DICT = range(7)
 (OK_STR, OK_VALUE, E_INTERP, E_ASSERT_BRACES, E_ASSERT_TYPE, E_UNHASHABLE, E_RS_PANIC, NEEDS_HOST,
- DIVERGED, E_OVERFLOW, RECURSE) = range(11)
+ DIVERGED, E_OVERFLOW, RECURSE, E_NO_MATCH, E_NO_NULL) = range(13)
 STATUS_NAMES = ["OK_STR", "OK_VALUE", "E_INTERP", "E_ASSERT_BRACES", "E_ASSERT_TYPE",
-                "E_UNHASHABLE", "E_RS_PANIC", "NEEDS_HOST", "DIVERGED", "E_OVERFLOW", "RECURSE"]
+                "E_UNHASHABLE", "E_RS_PANIC", "NEEDS_HOST", "DIVERGED", "E_OVERFLOW", "RECURSE",
+                "E_NO_MATCH", "E_NO_NULL"]
 VID_NONE, VID_HHMM, VID_HHMMSS = 0xFFFFFFFF, 0xFFFFFFFE, 0xFFFFFFFD
 TABLE_HAS_INSERTS_DIR = 1
 TABLE_MUTABLE = 2
@@ -40,6 +41,7 @@ EXPORTS = [
     "ie_synth_strings_device", "ie_debug_probe",
     "ie_wildcards_build", "ie_wildcards_free", "ie_wildcard_match_device", "ie_wildcard_match_batch",
     "ie_table_replicate", "ie_shard_bounds", "ie_table_arena_stats", "ie_table_set_arena_limit",
+    "ie_goto_map", "ie_replace_map", "ie_delete_keys", "ie_map_result_free",
 ]
 WC_MAX_CAP = 16
 
@@ -72,6 +74,36 @@ class BatchRes(ctypes.Structure):
                 ("value_id", ctypes.POINTER(ctypes.c_uint32)), ("n", ctypes.c_uint64)]
 
 
+class MapPair(ctypes.Structure):
+    _fields_ = [("key", ctypes.c_char_p), ("key_len", ctypes.c_uint64),
+                ("value", ctypes.c_char_p), ("value_len", ctypes.c_uint64)]
+
+
+class MapResult(ctypes.Structure):
+    _fields_ = [("bytes", ctypes.POINTER(ctypes.c_uint8)), ("bytes_len", ctypes.c_uint64),
+                ("offsets", ctypes.POINTER(ctypes.c_uint64)), ("status", ctypes.POINTER(ctypes.c_uint8)),
+                ("where", ctypes.POINTER(ctypes.c_uint32)), ("chosen", ctypes.POINTER(ctypes.c_int32)),
+                ("value_id", ctypes.POINTER(ctypes.c_uint32)), ("n", ctypes.c_uint64)]
+
+
+def map_result_to_python(res_ptr):
+    """Copy an ie_map_result into Python and free it: a list of (bytes, status, where, chosen, value id)."""
+    r = res_ptr.contents
+    n = r.n
+    blob = ctypes.string_at(r.bytes, r.bytes_len) if r.bytes_len else b""
+    o = [r.offsets[i] for i in range(n + 1)]
+    out = [(blob[o[i]:o[i + 1]], r.status[i], r.where[i], r.chosen[i], r.value_id[i]) for i in range(n)]
+    lib().ie_map_result_free(res_ptr)
+    return out
+
+
+def map_pairs(pairs):
+    """[(key str, value str)] -> (ctypes array of MapPair, the encoded bytes kept alive)"""
+    keep = [(enc(k), enc(v)) for k, v in pairs]
+    arr = (MapPair * max(1, len(keep)))(*[MapPair(k, len(k), v, len(v)) for k, v in keep])
+    return arr, keep
+
+
 class Timing(ctypes.Structure):
     _fields_ = [("resolve_ms", ctypes.c_float), ("complex_ms", ctypes.c_float),
                 ("total_ms", ctypes.c_float), ("n_complex", ctypes.c_uint64), ("n_direct", ctypes.c_uint64),
@@ -99,6 +131,12 @@ def signatures():
         "ie_table_set_update": (ctypes.c_int, [vp, vp, vp, vp, u64]),
         "ie_table_arena_stats": (ctypes.c_int, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "ie_table_set_arena_limit": (ctypes.c_int, [vp, u64]),
+        "ie_goto_map": (ctypes.c_int, [vp, vp, ctypes.c_char_p, u64, vp, u32, ctypes.POINTER(ctypes.POINTER(MapResult))]),
+        "ie_replace_map": (ctypes.c_int, [vp, vp, ctypes.c_char_p, u64, vp, vp, vp, u64, vp, u32, i32,
+                                          ctypes.POINTER(ctypes.POINTER(MapResult)),
+                                          ctypes.POINTER(ctypes.POINTER(MapResult))]),
+        "ie_delete_keys": (ctypes.c_int, [vp, vp, vp, u32, vp, vp, u32, i32, ctypes.POINTER(ctypes.POINTER(MapResult))]),
+        "ie_map_result_free": (None, [ctypes.POINTER(MapResult)]),
         "ie_table_tables": (u32, [vp]),
         "ie_table_entries": (u64, [vp]),
         "ie_table_dialect": (i32, [vp]),

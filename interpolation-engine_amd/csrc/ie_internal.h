@@ -1,0 +1,195 @@
+// ie_internal.h — the host library's internal types, shared by its translation units (ie_host.cpp:
+// tables, execs, batches; ie_maps.cpp: the map commands). Not part of the C ABI (include/ie_amd.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <string>
+#include <string_view>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/ie_amd.h"
+#include "ie_common.h"
+#include "ie_kernels.h"
+
+using namespace ie;
+
+// the calling thread's last error text (ie_last_error); returns code
+int fail(int code, const std::string& msg);
+
+#define IE_HIP(call)                                                                   \
+  do {                                                                                 \
+    hipError_t e_ = (call);                                                            \
+    if (e_ != hipSuccess)                                                              \
+      return fail(IE_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_));     \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  uint64_t bytes = 0;
+  hipError_t ensure(uint64_t need) {
+    if (need <= bytes && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    uint64_t n = std::max<uint64_t>(need, 256);
+    hipError_t e = hipMalloc(&p, n);
+    if (e == hipSuccess) bytes = n;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+};
+
+
+bool have_device();
+
+struct ie_table {
+  int32_t device = 0;
+  int32_t dialect = 0;
+  uint32_t flags = 0;
+  uint64_t n_entries = 0;
+  uint32_t n_tables = 1;  // inserts dicts in the set
+  DevTable dev{};
+  // the clock entries ('HH:MM', 'HH:MM:SS' of every table): their slots (ie_table_set_clock)
+  std::vector<uint32_t> clock_slots;
+  DevBuf entries, pilots, arena;
+  // host mirror of the device table (ie_table_set_update, ie_table_set_clock): entries, pilots,
+  // the arena (device capacity arena_cap), the slots of each pilot group, and per table of the set
+  // the slots of its pre-resolved (EF_RAWALT) entries
+  std::vector<Entry> h_entries;
+  std::vector<uint16_t> h_pilots;
+  std::vector<uint8_t> h_arena;
+  uint64_t arena_cap = 0;
+  // arena bookkeeping (ie_table_set_update): bytes the live entries occupy (the rest of h_arena is
+  // dead: replaced texts), the largest arena the table may have (an offset must stay below 2^32;
+  // ie_table_set_arena_limit lowers it), and how often it was compacted
+  uint64_t arena_live = 0;
+  uint64_t arena_limit = 0xFFFFFFF0ull;
+  uint64_t n_compactions = 0;
+  std::vector<std::vector<uint32_t>> groups;
+  // (table id << 32 | value id) -> slot, built on demand (ie_maps.cpp: str() of a typed result),
+  // dropped by every update
+  mutable std::unordered_map<uint64_t, uint32_t> vid_slot;
+  mutable bool vid_ok = false;
+  std::unordered_map<uint32_t, std::vector<uint32_t>> rawalt;
+  DevBuf patch_staging;  // ie_table_set_update / _set_clock uploads
+  ~ie_table() {
+    entries.release();
+    pilots.release();
+    arena.release();
+    patch_staging.release();
+  }
+};
+
+struct ie_exec {
+  // compiled wildcard lists of the map commands (ie_maps.cpp), most recent last: a map task's keys
+  // are the same texts call after call, so their device copies are kept instead of re-uploaded
+  std::vector<std::pair<std::string, struct ie_wildcards*>> wc_cache;
+  int32_t device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  bool timing = false;
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  std::vector<hipEvent_t> marks;  // ie_exec_mark slots
+  bool ev_recorded = false;
+  uint32_t lit_cap_max = 0;
+  uint64_t pool_request = 256ull << 20;
+  bool pool_fixed = false;  // set by ie_exec_set_scratch: the caller sized the pool, no wait/re-run
+  // options (ie_exec_set_option); defaults read once from the environment at ie_exec_create
+  int32_t opt_fail_commit = -1;   // -1 adaptive, 0 / 1 forced (IE_FAIL_COMMIT)
+  uint32_t opt_fast = 1;          // 0: exact evaluator only (IE_FAST)
+  int32_t opt_tile = 0;           // k_resolve tile: 0 by call site, 256 or 512 forced (IE_TILE)
+  int32_t opt_views = 1;          // host batch APIs resolve into a views layout (IE_VIEWS; 0: packed on the device)
+  int32_t opt_defer = 2;          // views batches in two passes (a LEAN first pass, the strings it cannot
+                                  // finish in a second): 2 (default) batches of >= kLeanMinN strings or
+                                  // with many heavy strings, -1 the latter only, 0 never, 1 always (IE_DEFER)
+  bool defer_slow = false;        // the adaptive choice (from an earlier batch's counts)
+  int32_t opt_small = 1;          // host batches of <= 1024 strings / 64 KB: one pinned copy each way (IE_SMALL_HOST)
+  int32_t opt_err_keys = 0;       // IE_OPT_ERROR_KEYS: record the missing key of every IE_E_INTERP string
+  uint32_t opt_reserve = 0;       // views output of a packed batch: reserved ranges at opt_reserve / 16 x the
+                                  // input offsets (IE_OPT_RESERVE; 0: one claim per tile on one cursor)
+  bool in_cmd = false;            // inside the unescape command's second resolve
+  bool cmd_first = false;         // the unescape command's unescape step (offsets zeroed on overflow)
+  bool cmd_fused = false;         // the fused unescape command (views): launch_unescape_cmd
+  uint32_t opt_noeval = 0;        // diagnostic verbatim copy (IE_DEBUG_NOEVAL)
+  std::string stamps_path;        // diagnostic phase stamps (IE_DEBUG_STAMPS)
+  // fail commit (k_resolve<true>): chosen from the chain-failure count of an earlier batch, read
+  // back asynchronously (never a wait): > 0.1 % of a batch switches to it, a batch with none back
+  bool fail_commit = false;
+  bool stat_pending = false;
+  bool no_stats = false;  // run_host_small: no statistics copy (two stream operations of a scalar call)
+  uint8_t* ctr_override = nullptr;  // run_host_small: the counters in its own block, zeroed by its input copy
+  uint64_t stat_n = 0;
+  uint32_t* stat_host = nullptr;  // pinned
+  hipEvent_t stat_ev = nullptr;
+  // workspace
+  DevBuf counters, pool, out_len, tile_sum, tile_base, defer_tiles, defer_desc;
+  // keys only the host can look up (IE_NEEDS_HOST): [u64 bytes used | pad][records] (ie_exec_host_keys);
+  // a host batch call keeps its records (all its device passes, indices of its own batch) in hk
+  DevBuf host_keys;
+  std::vector<uint8_t> hk;
+  bool hk_host = false;
+  bool hk_dirty = true;  // the device list may hold records (a pass with host keys enabled ran since the reset)
+  // the fused unescape command's deferred pass: list, views into the pool, table ids
+  DevBuf u_list, u_off, u_len, u_tid;
+  // host-API staging
+  DevBuf in_bytes, in_off, in_tid, o_bytes, o_off, o_len, o_status, o_vid, o_total, wc_range, wc_match, wc_ncap, wc_caps;
+  // synth scratch
+  DevBuf s_lens, s_part;
+  DevBuf stamps;        // diagnostic phase stamps (env IE_DEBUG_STAMPS=<file>)
+  uint64_t stamp_tiles = 0;
+  // small host batches: one device block and one pinned host block (inputs, then outputs)
+  DevBuf sm_dev;
+  uint8_t* sm_host = nullptr;
+  uint64_t sm_host_bytes = 0;
+  ~ie_exec() {
+    for (auto& kv : wc_cache) ie_wildcards_free(kv.second);
+    sm_dev.release();
+    if (sm_host) (void)hipHostFree(sm_host);
+    for (DevBuf* b : {&u_list, &u_off, &u_len, &u_tid, &host_keys}) b->release();
+    for (DevBuf* b : {&counters, &pool, &out_len, &tile_sum, &tile_base, &defer_tiles, &defer_desc, &in_bytes,
+                      &in_off, &in_tid, &o_bytes, &o_off, &o_len, &o_status, &o_vid, &o_total, &wc_range, &wc_match, &wc_ncap, &wc_caps,
+                      &s_lens, &s_part, &stamps})
+      b->release();
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
+    for (auto& e : marks)
+      if (e) (void)hipEventDestroy(e);
+    if (stat_ev) (void)hipEventDestroy(stat_ev);
+    if (stat_host) (void)hipHostFree(stat_host);
+    if (own_stream && stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+struct ie_wildcards {
+  int32_t device = 0;
+  uint32_t n_pat = 0;
+  DevBuf bytes, lit_off, lit_len, pat_lit;
+  WcSet dev{};
+  ~ie_wildcards() {
+    for (DevBuf* b : {&bytes, &lit_off, &lit_len, &pat_lit}) b->release();
+  }
+};
+
+struct ie_synth {
+  SynthParams P{};
+  std::vector<std::string> keys, texts;
+  std::vector<ie_kv> kv;
+};
+
+// helpers of ie_host.cpp used by the other translation units
+int set_device(int32_t dev);
+uint32_t text_flags(const std::string_view t);
+uint32_t kind_flags(int32_t kind, int32_t dialect);
+uint64_t key_hash(const std::string_view k, uint64_t seed, uint32_t tid);
+// the key stored at a slot of a table's host mirror
+std::string_view mirror_key(const ie_table* t, const ie::Entry& e);
+// a batch through the device from host memory (H2D, kernels, D2H): op kOpInterp / kOpUnescape / kOpEscape
+int run_host(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, const uint64_t* offsets,
+             uint64_t n, ie_batch** outp, const uint32_t* table_id = nullptr);

@@ -85,8 +85,10 @@ def _str_results(tset, strings, ids):
 # ------------------------------------------------------------------------------------------
 # goto_map (py:1689-1711)
 # ------------------------------------------------------------------------------------------
-def goto_map_states(states, task, dialect="py", device=0, tables=None):
-    """goto_map for each state: [{'goto_target': t} | None | exception instance]. tables: an
+def _goto_map_states_host(states, task, dialect="py", device=0, tables=None):
+    """goto_map for each state, driven from Python around one device batch per step (the
+    inserts-directory path: its keys may need host completion). [{'goto_target': t} | None |
+    exception instance]. tables: an
     InsertsTableSet of exactly these states' dicts, to share between tasks that do not change them
     (run_map_tasks does); else one is built for this task."""
     maps = task["target_maps"]
@@ -190,8 +192,9 @@ def _rebuild(skel, done):
     return skel
 
 
-def replace_map_states(states, task, dialect="py", device=0, tables=None):
-    """replace_map for each state: [(output_name, value) | exception instance]. The caller
+def _replace_map_states_host(states, task, dialect="py", device=0, tables=None):
+    """replace_map for each state, driven from Python (the inserts-directory path). [(output_name,
+    value) | exception instance]. The caller
     stores value under output_name (set_interpdata, py:1771-1773); nothing is mutated here.
     tables: as goto_map_states."""
     maps = task["wildcard_maps"]
@@ -405,11 +408,250 @@ def _value_dict(state, value, caps, dialect):
     return out
 
 
+# ------------------------------------------------------------------------------------------
+# the map commands behind the C ABI (csrc/ie_maps.cpp: ie_goto_map, ie_replace_map, ie_delete_keys)
+# ------------------------------------------------------------------------------------------
+def _pairs(maps):
+    """[(key, value)] of a task's maps, or None when one is not a str (the host-driven path then
+    raises where the reference raises)."""
+    out = [(_first_key(d), _first_value(d)) for d in maps]
+    return out if all(type(k) is str and type(v) is str for k, v in out) else None
+
+
+def _errors_of(tset, wanted):
+    """{(state, string): the exception the reference raises for it}, one device batch."""
+    keys = list(dict.fromkeys(wanted))
+    got = tset.results([s for _, s in keys], [t for t, _ in keys]) if keys else []
+    return {k: (g if isinstance(g, BaseException) else RuntimeError("expected a failure of %r" % (k[1],)))
+            for k, g in zip(keys, got)}
+
+
+def goto_map_states(states, task, dialect="py", device=0, tables=None):
+    """goto_map (py:1689-1711) for each state: [{'goto_target': t} | None | exception instance], by
+    ONE library call over every state (ie_goto_map: text, keys and values interpolated in one device
+    batch, the first match in one k_wildcard launch). tables: an InsertsTableSet of exactly these
+    states' dicts, to share between tasks that do not change them (run_map_tasks does); else one is
+    built for this task."""
+    n = len(states)
+    if n == 0:
+        return []
+    pairs = _pairs(task["target_maps"])
+    tset = tables or IE.InsertsTableSet(states, dialect=dialect, device=device)
+    try:
+        if tset.has_dir or pairs is None or type(task["text"]) is not str:
+            return _goto_map_states_host(states, task, dialect, device, tables=tset)
+        import ctypes
+        arr, keep = IE.N.map_pairs(pairs)
+        text = IE.N.enc(task["text"])
+        res = ctypes.POINTER(IE.N.MapResult)()
+        x = IE.get_exec(tset.device)
+        IE.N.check(IE.N.lib().ie_goto_map(x.h, tset.h, text, len(text), arr, len(pairs), ctypes.byref(res)),
+                   "ie_goto_map")
+        rows = IE.N.map_result_to_python(res)
+        m = len(pairs)
+        src = lambda w: task["text"] if w == 0 else pairs[w - 1][0] if w <= m else pairs[w - 1 - m][1]  # noqa: E731
+        errs = _errors_of(tset, [(s, src(w)) for s, (_, st, w, _, _) in enumerate(rows)
+                                 if st not in (IE.N.OK_STR, IE.N.E_NO_MATCH, IE.N.E_NO_NULL)])
+    finally:
+        if tables is None:
+            tset.close()
+    out = []
+    label = task.get("traceback_label")
+    for s, (b, st, w, _, _) in enumerate(rows):
+        if st == IE.N.OK_STR:
+            target = IE.N.dec(b)
+            out.append({"goto_target": target} if target != "CONTINUE" else None)
+        elif st == IE.N.E_NO_MATCH:  # py:1708
+            out.append(AssertionError("Order Index %s: goto_map has no matches for '%s'." % (label, IE.N.dec(b))))
+        elif st == IE.N.E_NO_NULL:  # py:1703
+            out.append(AssertionError("Order Index %s: value text '%s' could not be resolved but 'NULL' is not a "
+                                      "key in target_maps." % (label, task["text"])))
+        else:
+            out.append(errs[(s, src(w))])
+    return out
+
+
+def replace_map_states(states, task, dialect="py", device=0, tables=None):
+    """replace_map (py:1713-1773) for each state: [(output_name, value) | exception instance]; the
+    caller stores value under output_name (set_interpdata, py:1771-1773). The item's walk
+    (recursive_replace, py:1748-1759: whole-string keys through get_interpdata) is done here on the
+    states' dicts; output_name and every leaf's replace_str loop (interpolate, first matching map,
+    the value against inserts | captures, repeat_until_done) are ONE library call over every state
+    (ie_replace_map). tables: as goto_map_states."""
+    maps = task["wildcard_maps"]
+    n, m = len(states), len(maps)
+    if n == 0:
+        return []
+    pairs = _pairs(maps)
+    name = task["output_name"]
+    tset = tables or IE.InsertsTableSet(states, dialect=dialect, device=device)
+    try:
+        if tset.has_dir or pairs is None or type(name) is not str:
+            return _replace_map_states_host(states, task, dialect, device, tables=tset)
+        out = [None] * n
+        skels, leaves, owner = [None] * n, [], []
+        for s in range(n):
+            mine = []
+            try:
+                skels[s] = (_leaves(states[s], task["item"], mine), len(leaves))
+            except (IE.InterpolationException, AssertionError, TypeError) as e:
+                out[s] = e
+                continue
+            leaves.extend(mine)
+            owner.extend([s] * len(mine))
+        import ctypes
+        import numpy as np
+        arr, keep = IE.N.map_pairs(pairs)
+        blob, offs = IE.N.pack(leaves)
+        ids = np.asarray(owner, np.uint32)
+        nb = IE.N.enc(name)
+        res, nres = ctypes.POINTER(IE.N.MapResult)(), ctypes.POINTER(IE.N.MapResult)()
+        x = IE.get_exec(tset.device)
+        IE.N.check(IE.N.lib().ie_replace_map(x.h, tset.h, nb, len(nb), ctypes.cast(ctypes.c_char_p(blob), ctypes.c_void_p),
+                                             offs.ctypes.data, ids.ctypes.data, len(leaves), arr, m,
+                                             1 if task.get("repeat_until_done", False) else 0, ctypes.byref(nres),
+                                             ctypes.byref(res)), "ie_replace_map")
+        names = IE.N.map_result_to_python(nres)
+        rows = IE.N.map_result_to_python(res) if leaves else []
+        # the exceptions of the failed strings (rare): names, leaves, keys; a failed value with the
+        # captures its key took (its message lists inserts | extra_inserts, py:467)
+        want, vfail = [], []
+        for s, (b, st, _, _, _) in enumerate(names):
+            if st not in (IE.N.OK_STR, IE.N.OK_VALUE):
+                want.append((s, name))
+        for i, (b, st, w, ch, _) in enumerate(rows):
+            if st == IE.N.OK_STR:
+                continue
+            if w == 0:
+                want.append((owner[i], IE.N.dec(b)))
+            elif w <= m:
+                want.append((owner[i], pairs[w - 1][0]))
+            else:
+                vfail.append(i)
+        errs = _errors_of(tset, want)
+        # the interpolated keys whose captures a failed value took
+        kwant = list(dict.fromkeys((owner[i], pairs[rows[i][2] - 1 - m][0]) for i in vfail))
+        kgot = dict(zip(kwant, _str_results(tset, [k for _, k in kwant], [t for t, _ in kwant])))
+    finally:
+        if tables is None:
+            tset.close()
+    verr = {}
+    for i in vfail:
+        b, st, w, ch, _ = rows[i]
+        s = owner[i]
+        key = kgot[(s, pairs[w - 1 - m][0])]
+        caps = []
+        if not isinstance(key, BaseException):
+            from .wildcard import get_wildcard_matches
+            caps = get_wildcard_matches(key, IE.N.dec(b))
+        full = dict(states[s], **{str(k + 1): c for k, c in enumerate(caps)})
+        xs = IE.InsertsTableSet([full], dialect=dialect, device=device)
+        try:
+            verr[i] = xs.results([pairs[w - 1 - m][1]], [0])[0]
+        finally:
+            xs.close()
+    no_value = object()
+    value_if_error = ([v for k, v in pairs if k == "NULL"] + [no_value])[0]  # py:1761
+    label = task.get("traceback_label")
+    count = [0] * n
+    for o in owner:
+        count[o] += 1
+    for s in range(n):
+        b, st, _, _, vid = names[s]
+        if st not in (IE.N.OK_STR, IE.N.OK_VALUE):
+            # output_name is interpolated before the reference's try (py:1715, 1762): its error
+            # reaches the caller as it is, whatever 'NULL' says
+            out[s] = errs[(s, name)]
+            continue
+        nm = IE.N.dec(b) if st == IE.N.OK_STR else tset.value(vid)  # (a typed output_name, py:1715)
+        if out[s] is not None:
+            e = out[s]
+        else:
+            skel, base = skels[s]
+            e, done = None, []
+            for k in range(base, base + count[s]):
+                bb, lst, w, _, _ = rows[k]
+                if lst == IE.N.OK_STR:
+                    done.append(IE.N.dec(bb))
+                    continue
+                e = verr[k] if k in verr else errs[(s, IE.N.dec(bb) if w == 0 else pairs[w - 1][0])]
+                break
+        if e is None:
+            out[s] = (nm, _rebuild(skel, done))
+        elif isinstance(e, IE.InterpolationException):
+            if value_if_error is no_value:  # py:1765-1766
+                out[s] = AssertionError("%s: replace_map encountered an interpolation error without 'NULL' key: %r"
+                                        % (label, e))
+            else:
+                out[s] = (nm, copy.deepcopy(value_if_error))
+        else:
+            out[s] = e
+    return out
+
+
+def delete_states(states, task, dialect="py", device=0, tables=None):
+    """delete / delete_except (py:1843-1868) in each state: the keys some wildcard matches (delete)
+    or no wildcard matches (delete_except) are removed from the state dicts and from `tables` (the
+    device copy, ie_delete_keys: every key of every state in one k_wildcard launch). The wildcards
+    are the task's after its pre-pass (recursive_interpolate, py:1501): interpolated per state.
+    Returns the deleted keys per state."""
+    n = len(states)
+    if n == 0:
+        return []
+    except_ = task["cmd"] == "delete_except"
+    tset = tables or IE.InsertsTableSet(states, dialect=dialect, device=device, mutable=True)
+    out = [[] for _ in range(n)]
+    try:
+        # the pre-pass on the wildcards (py:1501); states with the same list share one call
+        groups = {}
+        wl = task["wildcards"]
+        if any(IE.get_simple_insertkey(w) or (type(w) is str and "{" in w) for w in wl):
+            got = tset.results([w if type(w) is str else str(w) for w in wl] * n,
+                               [s for s in range(n) for _ in wl])
+            for s in range(n):
+                r = got[s * len(wl):(s + 1) * len(wl)]
+                bad = next((e for e in r if isinstance(e, BaseException)), None)
+                if bad is not None:
+                    out[s] = bad
+                    continue
+                groups.setdefault(tuple(str(v) for v in r), []).append(s)
+        else:
+            groups[tuple(str(w) for w in wl)] = list(range(n))
+        import ctypes
+        import numpy as np
+        x = IE.get_exec(tset.device)
+        for wild, members in groups.items():
+            blob, offs = IE.N.pack(list(wild))
+            ids = np.asarray(members, np.uint32)
+            res = ctypes.POINTER(IE.N.MapResult)()
+            IE.N.check(IE.N.lib().ie_delete_keys(x.h, tset.h, ids.ctypes.data, len(members),
+                                                 ctypes.cast(ctypes.c_char_p(blob), ctypes.c_void_p), offs.ctypes.data,
+                                                 len(wild), 1 if except_ else 0, ctypes.byref(res)), "ie_delete_keys")
+            for b, _, s, _, _ in IE.N.map_result_to_python(res):
+                k = IE.N.dec(b)
+                states[s].pop(k, None)
+                out[s].append(k)
+            # keys a dict holds but the table never does (the clock names, ''): the same test
+            odd = [(s, k) for s in members for k in states[s] if k in ("", "HH:MM", "HH:MM:SS")]
+            if odd:
+                from .wildcard import Wildcards
+                found = Wildcards(list(wild), device=device, dialect=dialect).first_match([k for _, k in odd])
+                for (s, k), (p, _) in zip(odd, found):
+                    if (p >= 0) != except_:
+                        del states[s][k]
+                        out[s].append(k)
+    finally:
+        if tables is None:
+            tset.close()
+    return out
+
+
 def run_map_tasks(states, tasks, dialect="py", device=0):
-    """goto_map / replace_map tasks in order over many states (the reference's loop applies them
-    one state at a time): one table set per stretch of tasks that leaves the states unchanged, a
-    replace_map's results stored into each state before the next task (set_interpdata,
-    py:470-471). Returns one list of per-state outcomes per task."""
+    """goto_map / replace_map / delete / delete_except tasks in order over many states (the
+    reference's loop applies them one state at a time): one table set for the whole run, a
+    replace_map's results stored into each state (set_interpdata, py:470-471) and a delete's keys
+    removed (py:1843-1868) in place on its device copy (ie_table_set_update) before the next task.
+    Returns one list of per-state outcomes per task."""
     outs, tset = [], None
     try:
         for task in tasks:
@@ -417,6 +659,10 @@ def run_map_tasks(states, tasks, dialect="py", device=0):
                 tset = IE.InsertsTableSet(states, dialect=dialect, device=device, mutable=True)
             if task["cmd"] == "goto_map":
                 outs.append(goto_map_states(states, task, dialect, device, tables=tset))
+                continue
+            if task["cmd"] in ("delete", "delete_except"):
+                # (the device copy is updated in place by the library call)
+                outs.append(delete_states(states, task, dialect, device, tables=tset))
                 continue
             got = replace_map_states(states, task, dialect, device, tables=tset)
             outs.append(got)

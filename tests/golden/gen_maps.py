@@ -15,7 +15,9 @@ tasks run in program order on each state, replace_map's results carried to the l
   maps_py.json  {"tasks": [...], "defaults": {...}, "states": N, "results": [[outcome per task]
                  per state]}; an outcome is {"goto": target|null} | {"set": [name, value]} for
                  values up to 256 characters, else {"set": [name, null], "len": L, "fnv": H}
-                 (FNV-1a of the UTF-8 bytes) | {"err": class name}
+                 (FNV-1a of the UTF-8 bytes) | {"err": class name}; "delete": the program's
+                 delete_except tasks on every state and delete edge cases on one state, each
+                 outcome {"keys": the remaining keys, sorted} | {"err": class name}
 
 Usage:  python tests/golden/gen_maps.py [--ref /root/reference/src] [--states 240]
 """
@@ -110,6 +112,44 @@ EDGE_TASKS = [
 ]
 
 
+# delete / delete_except (py:1843-1868) after the task pre-pass (py:1501 interpolates the wildcards)
+DELETE_STATE = {"a": "apple", "ab": "x", "b": "banana", "n": 3, "who": "guard", "guard": "g",
+                "enable_x": "1", "enable_y": "0", "multi\nline": "m", "k*": "star"}
+DELETE_TASKS = [
+    {"cmd": "delete", "wildcards": ["a*"], "traceback_label": "D1"},
+    {"cmd": "delete_except", "wildcards": ["a*", "enable_*"], "traceback_label": "D2"},
+    {"cmd": "delete", "wildcards": ["{who}", "n"], "traceback_label": "D3"},
+    {"cmd": "delete_except", "wildcards": [], "traceback_label": "D4"},
+    {"cmd": "delete", "wildcards": [], "traceback_label": "D5"},
+    {"cmd": "delete", "wildcards": ["*line", "k\\*"], "traceback_label": "D6"},
+    {"cmd": "delete", "wildcards": ["{missing}"], "traceback_label": "D7"},
+    {"cmd": "delete_except", "wildcards": ["*"], "traceback_label": "D8"},
+]
+
+
+def delete_tasks(program):
+    out = []
+
+    def walk(ts):
+        for t in ts:
+            if isinstance(t, dict) and t.get("cmd") in ("delete", "delete_except"):
+                out.append(t)
+            if isinstance(t, dict) and isinstance(t.get("tasks"), list):
+                walk(t["tasks"])
+    walk(program["order"])
+    return out
+
+
+def run_delete(ie, inserts, t):
+    """One delete task through the reference's execute_task: the remaining keys (sorted) or the error."""
+    state = {"order_index": 1, "inserts": copy.deepcopy(inserts), "output": ""}
+    try:
+        asyncio.run(ie.execute_task(state, copy.deepcopy(t), {}, {}, "x"))
+        return {"keys": sorted(state["inserts"])}
+    except Exception as e:  # noqa: BLE001 — the class is the outcome
+        return {"err": type(e).__name__}
+
+
 def run_task(ie, state, t):
     """One task through the reference's execute_task: an outcome record (see the module doc)."""
     try:
@@ -173,8 +213,15 @@ def main():
                 row.append({"err": type(e).__name__})
         results.append(row)
     edge = [run_task(ie, {"order_index": 1, "inserts": copy.deepcopy(EDGE_STATE), "output": ""}, t) for t in EDGE_TASKS]
+    # the program's delete_except tasks on every state as the loop reaches them (make_state's keys
+    # plus what its replace_maps stored), and the delete edge cases on one state
+    dtasks = delete_tasks(program)
+    dres = [[run_delete(ie, make_state(defaults, j), t) for t in dtasks] for j in range(args.states)]
+    dedge = [run_delete(ie, DELETE_STATE, t) for t in DELETE_TASKS]
     out = {"tasks": tasks, "defaults": defaults, "states": args.states, "results": results,
-           "edge": {"state": EDGE_STATE, "tasks": EDGE_TASKS, "results": edge}}
+           "edge": {"state": EDGE_STATE, "tasks": EDGE_TASKS, "results": edge},
+           "delete": {"tasks": dtasks, "results": dres, "edge_state": DELETE_STATE, "edge_tasks": DELETE_TASKS,
+                      "edge_results": dedge}}
     with open(os.path.join(HERE, "maps_py.json"), "w", encoding="utf-8") as f:
         json.dump(out, f, ensure_ascii=False, indent=0)
     from collections import Counter

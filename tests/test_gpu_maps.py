@@ -121,3 +121,49 @@ def test_error_order_edges_match_reference():
         if not _check(want, got) or ("msg" in want and str(got) != want["msg"]):
             bad.append((task["traceback_label"], want, repr(got)[:300]))
     assert not bad, bad
+
+
+def test_delete_except_of_the_program_matches_reference():
+    """text_adventure.json5's delete_except tasks (:29, :63) on every state, one library call per task
+    over all states (ie_delete_keys: every key of every state in one k_wildcard launch, the keys
+    removed from the device table set in place), against the reference's execute_task."""
+    g = load_golden("maps_py.json")
+    d = g["delete"]
+    bad = []
+    for k, task in enumerate(d["tasks"]):
+        states = [make_state(g["defaults"], j) for j in range(g["states"])]
+        tset = M.IE.InsertsTableSet(states, mutable=True)
+        try:
+            gone = M.delete_states(states, task, tables=tset)
+            # the device copy agrees with the dicts: every remaining key resolves, no deleted one does
+            probe = [("{%s}" % kk, j) for j, st in enumerate(states) for kk in list(st)[:3]]
+            probe += [("{%s}" % kk, j) for j, ks in enumerate(gone) for kk in ks[:2]]
+            res = tset.results([p for p, _ in probe], [j for _, j in probe])
+        finally:
+            tset.close()
+        for j, st in enumerate(states):
+            if sorted(st) != d["results"][j][k]["keys"]:
+                bad.append((k, j, sorted(st), d["results"][j][k]))
+        for (p, j), r in zip(probe, res):
+            key = p[1:-1]
+            if (key in states[j]) == isinstance(r, BaseException):
+                bad.append(("device", j, key, repr(r)[:80]))
+    assert not bad, (len(bad), bad[:6])
+
+
+def test_delete_edges_match_reference():
+    """delete / delete_except edge cases (tests/golden/gen_maps.py DELETE_TASKS): interpolated
+    wildcards, empty lists, DOTALL groups across a newline, a wildcard that fails to interpolate."""
+    import copy
+    d = load_golden("maps_py.json")["delete"]
+    bad = []
+    for task, want in zip(d["edge_tasks"], d["edge_results"]):
+        st = copy.deepcopy(d["edge_state"])
+        got = M.delete_states([st], task)[0]
+        if "err" in want:
+            ok = isinstance(got, BaseException) and type(got).__name__ == want["err"]
+        else:
+            ok = not isinstance(got, BaseException) and sorted(st) == want["keys"]
+        if not ok:
+            bad.append((task["traceback_label"], want, repr(got)[:200], sorted(st)))
+    assert not bad, bad

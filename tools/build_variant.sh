@@ -16,5 +16,5 @@ cp $C/*.h $tmp/
 H="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-result -I$C -I$tmp"
 /opt/rocm/bin/hipcc $H -mllvm -amdgpu-sched-strategy=max-ilp "$@" -c $tmp/ie_resolve.hip -o $tmp/r.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $tmp/r.o $O/ie_resolve512.hip.o $O/ie_escape.hip.o \
-  $O/ie_wildcard.hip.o $O/ie_host.cpp.o -o interpolation-engine_amd/libie_amd_$name.so
+  $O/ie_wildcard.hip.o $O/ie_host.cpp.o $O/ie_maps.cpp.o -o interpolation-engine_amd/libie_amd_$name.so
 rm -rf $tmp
