@@ -653,7 +653,7 @@ def replay_states(args, W, x, resolve, res):
     states."""
     from interpolation_engine_amd import workloads as Wk
     from oracle import oracle as O
-    upd, nat, rsv, nch, arena = [], [], [], 0, []
+    upd, nat, rsv, nch, arena, split = [], [], [], 0, [], []
     for it in range(args.replay):
         changes = []
         for j, ins in enumerate(W.states):
@@ -676,6 +676,7 @@ def replay_states(args, W, x, resolve, res):
         t3 = time.perf_counter()
         upd.append(t1 - t0)
         nat.append(W.tset.last_update_native_s)
+        split.append(W.tset.last_update_split_s)
         rsv.append(t3 - t2)
         arena.append(W.tset.arena_stats())
     threads, _ = cpu_share()
@@ -686,13 +687,16 @@ def replay_states(args, W, x, resolve, res):
     same = res.compare(W.n, st, ln, hs, threads)
     return {"iterations": args.replay, "stores_per_iteration": nch,
             "store_ms": [round(1e3 * v, 3) for v in upd], "store_library_ms": [round(1e3 * v, 3) for v in nat],
+            "store_pack_ms": [round(1e3 * v[0], 3) for v in split],
+            "store_values_ms": [round(1e3 * v[2], 3) for v in split],
             "resolve_ms": [round(1e3 * v, 3) for v in rsv],
             "arena_bytes": [a[0] for a in arena], "arena_live_bytes": [a[1] for a in arena],
             "arena_compactions": arena[-1][2] if arena else 0,
             "values_held": len(W.tset.values),
             "identical_to_oracle_after_replay": same,
-            "note": "store_ms = InsertsTableSet.update (Python packing + ie_table_set_update); resolve_ms = wall "
-                    "time of one batch (launch + sync)"}
+            "note": "store_ms = InsertsTableSet.update: store_pack_ms (csrc/ie_pack.c: the changes -> ie_kv "
+                    "records, texts transcoded across host threads) + store_library_ms (ie_table_set_store) + "
+                    "store_values_ms (the value list); resolve_ms = wall time of one batch (launch + sync)"}
 
 
 def cpu_baseline_states(args, W, N, res, model, budget, threads):

@@ -209,6 +209,13 @@ int ie_table_set_clock(ie_table* t, const ie_clock* now);
  * would take an arena offset past the table's limit (2^32 - 16, or ie_table_set_arena_limit's) even
  * after a compaction returns IE_ERR_CAPACITY (the changes before it applied): rebuild the table. */
 int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, const uint32_t* vid, uint64_t n);
+/* ie_table_set_update with the value ids handed out by the table (the caller keeps no (table, key) ->
+ * id map): a rewrite keeps its key's id, a new key takes an id a delete freed or the next unused one
+ * (a table set's build gives kv i the id i), a delete frees its key's id. vid_out[i] = the id change
+ * i stored under (for a delete: the id it freed), IE_VID_NONE for a change that stored nothing (an
+ * absent key deleted, the keys '', 'HH:MM', 'HH:MM:SS', or a change after an IE_ERR_CAPACITY stop).
+ * Ids exhausted (2^32 - 3): IE_ERR_CAPACITY. */
+int ie_table_set_store(ie_table* t, const ie_kv* kv, const uint32_t* table_id, uint64_t n, uint32_t* vid_out);
 /* Arena bookkeeping: bytes in use, bytes of live entries, compactions so far (any may be NULL). */
 int ie_table_arena_stats(const ie_table* t, uint64_t* bytes, uint64_t* live, uint64_t* compactions);
 /* Lower the arena limit of ie_table_set_update (tests: force compaction and IE_ERR_CAPACITY early). */

@@ -26,7 +26,7 @@ OPT_ERROR_KEYS = 9
 # every symbol include/ie_amd.h declares (tests check the .so exports exactly these)
 EXPORTS = [
     "ie_abi_version", "ie_build_id", "ie_last_error", "ie_device_count",
-    "ie_table_build", "ie_table_set_build", "ie_table_set_clock", "ie_table_set_update", "ie_table_free", "ie_table_entries", "ie_table_tables",
+    "ie_table_build", "ie_table_set_build", "ie_table_set_clock", "ie_table_set_update", "ie_table_set_store", "ie_table_free", "ie_table_entries", "ie_table_tables",
     "ie_table_dialect",
     "ie_exec_create", "ie_exec_destroy", "ie_exec_sync", "ie_exec_set_timing", "ie_exec_timing",
     "ie_exec_set_scratch", "ie_exec_set_option", "ie_exec_host_keys",
@@ -129,6 +129,7 @@ def signatures():
         "ie_table_free": (None, [vp]),
         "ie_table_set_clock": (ctypes.c_int, [vp, ctypes.POINTER(Clock)]),
         "ie_table_set_update": (ctypes.c_int, [vp, vp, vp, vp, u64]),
+        "ie_table_set_store": (ctypes.c_int, [vp, vp, vp, u64, vp]),
         "ie_table_arena_stats": (ctypes.c_int, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "ie_table_set_arena_limit": (ctypes.c_int, [vp, u64]),
         "ie_goto_map": (ctypes.c_int, [vp, vp, ctypes.c_char_p, u64, vp, u32, ctypes.POINTER(ctypes.POINTER(MapResult))]),
@@ -209,6 +210,27 @@ def check(rc, what):
     if rc != 0:
         msg = lib().ie_last_error()
         raise RuntimeError("%s failed (%d): %s" % (what, rc, msg.decode("utf-8", "replace") if msg else ""))
+
+
+_pack = None
+
+
+def host_threads():
+    """Threads for the host-side byte work (IE_HOST_THREADS, else the cores, at most 8)."""
+    v = int(os.environ.get("IE_HOST_THREADS", "0") or 0)
+    return v if v > 0 else max(1, min(8, os.cpu_count() or 1))
+
+
+def pack_module():
+    """The store packer (csrc/ie_pack.c, built in-tree by __graft_entry__.build next to the library)."""
+    global _pack
+    if _pack is None:
+        try:
+            from . import _ie_pack
+        except ImportError as e:
+            raise RuntimeError("the store packer _ie_pack is not built (run __graft_entry__.build()): %s" % e)
+        _pack = _ie_pack
+    return _pack
 
 
 def enc(s):

@@ -9,6 +9,7 @@
 //                  convenience ie_interpolate_batch (H2D, kernels, D2H, capacity/overflow retry).
 // There is no CPU execution path for the resolver: every string is resolved by the kernels in
 // ie_kernels.hip; when no device is present the entry points fail with IE_ERR_NO_DEVICE.
+#include <emmintrin.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -25,7 +26,6 @@
 #include "../../include/ie_amd.h"
 #include "ie_common.h"
 #include "ie_kernels.h"
-
 #include "ie_internal.h"
 
 thread_local std::string g_err;
@@ -42,21 +42,34 @@ bool have_device() {
 
 
 // ---- splice-text analysis for the fast path (see DESIGN.md "inert values") ----
+// The rules look at the bytes around a brace, a backslash or U+3020's lead byte only: 16 bytes at a
+// time are tested for those four bytes (SSE2), and the rules run at the hits (a store's history text
+// is kilobytes without one).
 uint32_t text_flags(const std::string_view t) {
-  bool inert = true;
+  const uint8_t* p = (const uint8_t*)t.data();
   const size_t n = t.size();
-  for (size_t i = 0; i < n && inert; i++) {
-    const uint8_t c = (uint8_t)t[i];
-    if ((c == '{' || c == '}') && (i == 0 || t[i - 1] != '\\')) inert = false;  // re-resolves
-    if (c == 0xE3 && i + 2 < n && (uint8_t)t[i + 1] == 0x80 && (uint8_t)t[i + 2] == 0xA0)
-      inert = false;  // U+3020 collides with the placeholders
-    if (c == '\\' && i + 1 < n && t[i + 1] == '}') {
-      if (i == 0) inert = false;                                   // '.' + '\}' across the seam
-      else if (t[i - 1] == '.' || t[i - 1] == '}') inert = false;  // '.\}' restores as '\{.'
-    }
+  auto breaks = [&](size_t i) -> bool {  // does the byte at i make the text non-inert?
+    const uint8_t c = p[i];
+    if (c == '{' || c == '}') return i == 0 || p[i - 1] != '\\';  // re-resolves
+    if (c == 0xE3) return i + 2 < n && p[i + 1] == 0x80 && p[i + 2] == 0xA0;  // U+3020 collides with the placeholders
+    if (c == '\\' && i + 1 < n && p[i + 1] == '}')
+      return i == 0 || p[i - 1] == '.' || p[i - 1] == '}';  // '.' + '\}' across the seam; '.\}' restores as '\{.'
+    return false;
+  };
+  size_t i = 0;
+  const __m128i lb = _mm_set1_epi8('{'), rb = _mm_set1_epi8('}'), bs = _mm_set1_epi8('\\'),
+                e3 = _mm_set1_epi8((char)0xE3);
+  for (; i + 16 <= n; i += 16) {
+    const __m128i v = _mm_loadu_si128((const __m128i*)(p + i));
+    uint32_t hit = (uint32_t)_mm_movemask_epi8(_mm_or_si128(_mm_or_si128(_mm_cmpeq_epi8(v, lb), _mm_cmpeq_epi8(v, rb)),
+                                                            _mm_or_si128(_mm_cmpeq_epi8(v, bs), _mm_cmpeq_epi8(v, e3))));
+    for (; hit; hit &= hit - 1)
+      if (breaks(i + __builtin_ctz(hit))) return 0u;
   }
-  if (n && t[n - 1] == '\\') inert = false;  // escapes a following brace (trailing backslash)
-  return inert ? EF_INERT : 0u;
+  for (; i < n; i++)
+    if (breaks(i)) return 0u;
+  if (n && p[n - 1] == '\\') return 0u;  // escapes a following brace (trailing backslash)
+  return EF_INERT;
 }
 
 uint32_t kind_flags(int32_t kind, int32_t dialect) {
@@ -672,6 +685,43 @@ struct Patches {
     }
   }
   bool empty() const { return dst.empty(); }
+  // many ranges at once: pieces and places counted serially, the bytes copied across the host
+  // threads (the ranges sit all over a mirror of tens of MB: the reads are cache misses)
+  void add_many(const std::vector<CopyJob>& r) {
+    const size_t nr = r.size();
+    if (!nr) return;
+    std::vector<uint64_t> pf(nr + 1), df(nr + 1);
+    pf[0] = dst.size();
+    df[0] = data.size();
+    for (size_t k = 0; k < nr; k++) {
+      const uint64_t np = (r[k].len + 255) / 256;
+      pf[k + 1] = pf[k] + np;
+      df[k + 1] = df[k] + (np ? (np - 1) * 256 + ((r[k].len - (np - 1) * 256 + 15) & ~15ull) : 0);
+    }
+    dst.resize(pf[nr]);
+    soff.resize(pf[nr]);
+    len.resize(pf[nr]);
+    data.resize(df[nr]);
+    parallel_for(nr, [&](uint64_t lo, uint64_t hi) {
+      for (uint64_t k = lo; k < hi; k++) {
+        uint64_t p = pf[k], d = df[k];
+        for (uint64_t o = 0; o < r[k].len; o += 256, p++) {
+          const uint32_t l = (uint32_t)std::min<uint64_t>(256, r[k].len - o);
+          dst[p] = r[k].dst + o;
+          soff[p] = (uint32_t)d;
+          len[p] = l;
+          memcpy(data.data() + d, r[k].src + o, l);
+          d += (l + 15) & ~15u;
+        }
+      }
+    });
+  }
+  void reserve(uint64_t pieces, uint64_t bytes) {
+    dst.reserve(pieces);
+    soff.reserve(pieces);
+    len.reserve(pieces);
+    data.reserve(bytes + 16 * pieces);
+  }
 };
 
 int apply_patches(DevBuf& staging, const Patches& P) {
@@ -720,13 +770,29 @@ std::string_view mirror_key(const ie_table* t, const Entry& e) {
 // [text][pad to 4][key] appended to the mirror's arena: the new text's offset (kernels read a long
 // key at key_off_of(text_off, text_len))
 uint32_t arena_append(ie_table* t, std::string_view text, std::string_view key) {
-  std::vector<uint8_t>& a = t->h_arena;
+  HostArena& a = t->h_arena;
   while (a.size() & 3) a.push_back(0);
   const uint32_t off = (uint32_t)a.size();
-  a.insert(a.end(), text.begin(), text.end());
+  if (t->defer && text.size() >= 256) {  // (placed now, copied with the others in parallel)
+    t->defer->push_back(CopyJob{off, (const uint8_t*)text.data(), text.size()});
+    a.grow(text.size());
+  } else {
+    a.insert(a.end(), text.begin(), text.end());
+  }
   while (a.size() & 3) a.push_back(0);
   a.insert(a.end(), key.begin(), key.end());
   return off;
+}
+
+// the deferred text copies of ie_table_set_update, across the host threads
+void flush_copies(ie_table* t) {
+  if (!t->defer || t->defer->empty()) return;
+  std::vector<CopyJob>& jobs = *t->defer;
+  uint8_t* const a = t->h_arena.data();
+  parallel_for(jobs.size(), [&](uint64_t lo, uint64_t hi) {
+    for (uint64_t k = lo; k < hi; k++) memcpy(a + jobs[k].dst, jobs[k].src, jobs[k].len);
+  });
+  jobs.clear();
 }
 
 Entry make_entry(ie_table* t, std::string_view key, std::string_view text, uint32_t flags, uint32_t vid, uint32_t tb) {
@@ -787,18 +853,30 @@ bool rewrite_in_place(ie_table* t, Entry& e, std::string_view text, uint32_t fla
 // Compaction: every live entry's bytes copied into a fresh arena, in slot order, offsets rewritten
 // (the caller uploads the entries and the arena whole)
 void compact_arena(ie_table* t) {
-  std::vector<uint8_t> na;
-  na.reserve(t->arena_live + 64);
+  flush_copies(t);
+  HostArena na;
+  na.swap(t->h_arena_spare);
+  na.clear();
+  na.reserve(t->arena_live + t->arena_live / 2 + 64);  // (room for the appends that follow)
+  // the new places in slot order, then the bytes copied across the host threads
+  std::vector<CopyJob> jobs;
+  jobs.reserve(t->n_entries);
+  uint64_t at = 0;
   for (Entry& e : t->h_entries) {
     if (!(e.flags & EF_OCCUPIED)) continue;
     uint64_t a, b;
-    arena_span(t, e, a, b);
-    while (na.size() & 3) na.push_back(0);
-    const uint64_t at = na.size();
-    na.insert(na.end(), t->h_arena.begin() + a, t->h_arena.begin() + b);
+    arena_span(t, e, a, b);  // (starts and ends 4-aligned)
+    jobs.push_back(CopyJob{at, t->h_arena.data() + a, b - a});
     e.text_off = (uint32_t)(at + (e.text_off - a));
+    at += b - a;
   }
-  t->h_arena = std::move(na);
+  na.grow(at);
+  uint8_t* const dst = na.data();
+  parallel_for(jobs.size(), [&](uint64_t lo, uint64_t hi) {
+    for (uint64_t k = lo; k < hi; k++) memcpy(dst + jobs[k].dst, jobs[k].src, jobs[k].len);
+  });
+  t->h_arena.swap(na);
+  t->h_arena_spare.swap(na);
   t->arena_live = t->h_arena.size();
   t->n_compactions++;
 }
@@ -854,7 +932,7 @@ bool replace_all(ie_table* t, const Entry& extra) {
 // Entries -> perfect-hash table on the device.
 int upload_table(const std::vector<Ent>& ents, uint32_t n_tables, int32_t dialect, uint32_t flags,
                  int32_t device, ie_table** out) {
-  std::vector<uint8_t> arena;
+  HostArena arena;
   std::vector<Entry> items;
   items.reserve(ents.size());
   uint64_t maxtext = 8;
@@ -1156,6 +1234,7 @@ int ie_table_set_build(const ie_kv* kv, const uint64_t* kv_start, uint32_t n_tab
   rc = upload_table(ents, n_tables, dialect, flags, device, &t0);
   if (rc || getenv("IE_NO_PRERESOLVE")) {  // diagnostic switch: raw splice texts only
     *out = t0;
+    if (t0) t0->next_vid = (uint32_t)std::min<uint64_t>(kv_start[n_tables], IE_VID_CLOCK_HHMMSS);
     return rc;
   }
   *out = t0;
@@ -1164,7 +1243,9 @@ int ie_table_set_build(const ie_kv* kv, const uint64_t* kv_start, uint32_t n_tab
   if (rc) {
     ie_table_free(*out);
     *out = nullptr;
+    return rc;
   }
+  (*out)->next_vid = (uint32_t)std::min<uint64_t>(kv_start[n_tables], IE_VID_CLOCK_HHMMSS);  // (a kv's index is its id)
   return rc;
 }
 
@@ -1197,6 +1278,8 @@ int ie_table_replicate(const ie_table* t, int32_t device, ie_table** out) {
   c->arena_live = t->arena_live;
   c->arena_limit = t->arena_limit;
   c->n_compactions = t->n_compactions;
+  c->next_vid = t->next_vid;
+  c->free_vids = t->free_vids;
   c->groups = t->groups;
   c->rawalt = t->rawalt;
   c->dev = t->dev;
@@ -1271,77 +1354,178 @@ int ie_table_set_clock(ie_table* t, const ie_clock* now) {
 // applied (the caller rebuilds). Values are taken as given: a brace-bearing value is not pre-resolved (the
 // exact evaluator resolves it in the reference's order), and the pre-resolved values of every
 // table that changed go back to their raw text, since they were resolved against the old dict.
-int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, const uint32_t* vid, uint64_t n) {
-  if (!t || (n && (!kv || !table_id || !vid))) return fail(IE_ERR_INVALID, "null argument");
+// a set of entry slots (bitmap): marked in any order, listed in slot order without a sort
+struct SlotSet {
+  std::vector<uint64_t> w;
+  explicit SlotSet(uint32_t m) : w((m + 63) / 64, 0) {}
+  void set(uint32_t s) { w[s >> 6] |= 1ull << (s & 63); }
+  void clear(uint32_t s) { w[s >> 6] &= ~(1ull << (s & 63)); }
+  bool has(uint32_t s) const { return (w[s >> 6] >> (s & 63)) & 1; }
+  uint64_t count() const {
+    uint64_t c = 0;
+    for (uint64_t x : w) c += (uint64_t)__builtin_popcountll(x);
+    return c;
+  }
+  std::vector<uint32_t> slots() const {
+    std::vector<uint32_t> out;
+    for (size_t k = 0; k < w.size(); k++)
+      for (uint64_t x = w[k]; x; x &= x - 1) out.push_back((uint32_t)(k * 64 + __builtin_ctzll(x)));
+    return out;
+  }
+};
+
+// ie_table_set_update (value ids given: vid_in) and ie_table_set_store (value ids handed out by the
+// table: a rewrite keeps its key's id, a new key takes a freed id or the next one, a delete frees
+// its key's id; vid_out[i] = the id, IE_VID_NONE for a key never stored)
+static int table_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, const uint32_t* vid_in,
+                        uint32_t* vid_out, uint64_t n) {
+  const bool autov = vid_in == nullptr;
+  if (!t || (n && (!kv || !table_id || (autov && !vid_out)))) return fail(IE_ERR_INVALID, "null argument");
+  const uint32_t* const vid = vid_in;
   // every change is checked before any is applied: a rejected call leaves the table as it was
   for (uint64_t i = 0; i < n; i++) {
     if (table_id[i] >= t->n_tables) return fail(IE_ERR_INVALID, "table id beyond the table set");
     if (kv[i].key_len && !kv[i].key) return fail(IE_ERR_INVALID, "null key");
     if (kv[i].kind < 0) continue;
     if (kv[i].kind > IE_KIND_DICT) return fail(IE_ERR_INVALID, "bad kind");
-    if (vid[i] >= IE_VID_CLOCK_HHMMSS) return fail(IE_ERR_INVALID, "value id out of range");
+    if (!autov && vid[i] >= IE_VID_CLOCK_HHMMSS) return fail(IE_ERR_INVALID, "value id out of range");
     if (kv[i].text_len && !kv[i].text) return fail(IE_ERR_INVALID, "null text");
     if (kv[i].key_len >= 0xFFFFFFF0ull || kv[i].text_len >= 0xFFFFFFF0ull) return fail(IE_ERR_INVALID, "key or text above 4 GiB");
   }
   if (t->dev.flags & TF_CUCKOO) return fail(IE_ERR_INVALID, "a two-choice (IE_CUCKOO) table takes no updates");
   t->vid_ok = false;
+  Trace tr("update");
   int rc = set_device(t->device);
   if (rc) return rc;
   IE_HIP(hipDeviceSynchronize());  // no batch may still read the table
+  tr.mark("sync", n);
   uint64_t arena0 = t->h_arena.size();
   uint64_t seed = t->dev.seed;
   const uint32_t nb = t->dev.nb, m = t->dev.m;
   bool whole = false;                      // entries and pilots re-placed: upload them whole
   bool whole_arena = false;                // the arena was compacted: upload it whole
-  std::vector<uint32_t> dirty;             // entry slots to upload
+  SlotSet dirty(m);                        // entry slots to upload
   std::vector<uint32_t> dirty_groups;      // pilots to upload
-  std::vector<uint32_t> rewritten;         // slots whose arena bytes were rewritten in place
+  SlotSet rewritten(m);                    // slots whose arena bytes were rewritten in place
   std::vector<uint32_t> touched;           // tables whose pre-resolved values must go raw
   int status = IE_SUCCESS;
+  uint64_t call_start = t->h_arena.size();  // (the texts placed since: maybe not copied yet)
   // room for an append of `need` bytes below the table's arena limit (offsets stay below 2^32):
   // compacted first when dead bytes would make the room; false: IE_ERR_CAPACITY
   auto room = [&](uint64_t need) -> bool {
     if (t->h_arena.size() + need + 8 <= t->arena_limit) return true;
     if (t->arena_live + need + 8 > t->arena_limit) return false;
-    compact_arena(t);
+    compact_arena(t);  // (flushes the deferred copies first)
+    call_start = t->h_arena.size();
     whole = whole_arena = true;
     return t->h_arena.size() + need + 8 <= t->arena_limit;
   };
+  // the texts' inert flags and the keys' hashes (under the current seed), across the host threads
+  // before the (serial) placement
+  std::vector<uint32_t> tflags(n, 0);
+  std::vector<uint64_t> khash(n);
+  const uint64_t seed0 = seed;
+  parallel_for(n, [&](uint64_t lo, uint64_t hi) {
+    for (uint64_t i = lo; i < hi; i++) {
+      if (kv[i].kind >= 0) tflags[i] = text_flags(std::string_view(kv[i].text ? kv[i].text : "", kv[i].text_len));
+      khash[i] = key_hash(std::string_view(kv[i].key ? kv[i].key : "", kv[i].key_len), seed0, table_id[i]);
+    }
+  });
+  tr.mark("flags, hashes", n);
+  // long texts are placed now and copied later, in parallel (flush_copies: before a compaction, a
+  // rewrite of a text placed in this call, and the upload)
+  std::vector<CopyJob> jobs;
+  struct DeferScope {
+    ie_table* t;
+    ~DeferScope() { t->defer = nullptr; }
+  } defer_scope{t};
+  t->defer = &jobs;
+  {  // room for the appends ahead in one reallocation (not a doubling copy in the middle of them)
+    uint64_t est = 0;
+    for (uint64_t i = 0; i < n; i++)
+      if (kv[i].kind >= 0) est += kv[i].text_len + kv[i].key_len + 8;
+    const uint64_t sz = t->h_arena.size();
+    if (t->h_arena.capacity() < sz + est)
+      t->h_arena.reserve(std::min<uint64_t>(std::max<uint64_t>(sz + est, sz + sz / 2), t->arena_limit + 64));
+  }
+  // (an applied store's id: reported, and taken from the free list or the counter)
+  auto take = [&](uint64_t i, uint32_t v, bool kept) {
+    if (!autov) return;
+    vid_out[i] = v;
+    if (kept) return;
+    if (!t->free_vids.empty() && t->free_vids.back() == v) t->free_vids.pop_back();
+    else if (v == t->next_vid) t->next_vid++;
+  };
+  if (autov)
+    for (uint64_t i = 0; i < n; i++) vid_out[i] = IE_VID_NONE;
+  else
+    for (uint64_t i = 0; i < n; i++)
+      if (kv[i].kind >= 0) t->next_vid = std::max(t->next_vid, vid[i] + 1);
   for (uint64_t i = 0; i < n; i++) {
     const uint32_t tb = table_id[i];
     std::string_view key(kv[i].key ? kv[i].key : "", kv[i].key_len);
     if (key.empty() || key == "HH:MM" || key == "HH:MM:SS") continue;  // never looked up (py:433-446)
-    const uint64_t h = key_hash(key, seed, tb);
+    // (the pilot a few changes ahead and the entry one step nearer pulled into the cache: the
+    // mirror's entries are tens of MB and every change lands somewhere else in them)
+    if (seed == seed0) {
+      if (i + 16 < n) __builtin_prefetch(&t->h_pilots[ph_group(khash[i + 16], nb)]);
+      if (i + 8 < n) {
+        const uint64_t h8 = khash[i + 8];
+        __builtin_prefetch(&t->h_entries[ph_slot(h8, t->h_pilots[ph_group(h8, nb)], m)]);
+      }
+    }
+    const uint64_t h = seed == seed0 ? khash[i] : key_hash(key, seed, tb);
     const uint32_t g = ph_group(h, nb), slot = ph_slot(h, t->h_pilots[g], m);
     Entry& cur = t->h_entries[slot];
     const bool present = (cur.flags & EF_OCCUPIED) && (cur.flags >> kTidShift) == tb && mirror_key(t, cur) == key;
+    // the change's value id
+    uint32_t v = 0;
+    if (!autov) {
+      v = vid[i];
+    } else if (kv[i].kind >= 0 && present) {
+      v = cur.vid;
+    } else if (kv[i].kind >= 0) {
+      if (!t->free_vids.empty()) {
+        v = t->free_vids.back();
+      } else if (t->next_vid >= IE_VID_CLOCK_HHMMSS) {
+        status = fail(IE_ERR_CAPACITY, "value ids exhausted: rebuild the table");
+        break;
+      } else {
+        v = t->next_vid;
+      }
+    }
     if (kv[i].kind < 0) {  // del inserts[key]
       if (!present) continue;
+      if (autov) {
+        t->free_vids.push_back(cur.vid);
+        vid_out[i] = cur.vid;
+      }
       auto& gs = t->groups[g];
       gs.erase(std::remove(gs.begin(), gs.end(), slot), gs.end());
       arena_release(t, cur);
       cur = Entry{};
-      dirty.push_back(slot);
+      dirty.set(slot);
       t->n_entries--;
       touched.push_back(tb);
       continue;
     }
     std::string_view text(kv[i].text ? kv[i].text : "", kv[i].text_len);
-    const uint32_t flags = kind_flags(kv[i].kind, t->dialect) | text_flags(text);
+    const uint32_t flags = kind_flags(kv[i].kind, t->dialect) | tflags[i];
+    if (present && cur.text_off >= call_start && !jobs.empty()) flush_copies(t);  // (placed in this call)
     const uint64_t need = ((text.size() + 3ull) & ~3ull) + key.size() + 4;
     if (present) {
       // the new text where the old one was when it fits, else appended
-      if (rewrite_in_place(t, cur, text, flags, vid[i])) {
-        rewritten.push_back(slot);
+      if (rewrite_in_place(t, cur, text, flags, v)) {
+        rewritten.set(slot);
       } else {
         if (!room(need)) {
           status = fail(IE_ERR_CAPACITY, "table arena full (limit reached even after compaction): rebuild the table");
           break;
         }
         arena_release(t, t->h_entries[slot]);
-        t->h_entries[slot] = make_entry(t, key, text, flags, vid[i], tb);
+        t->h_entries[slot] = make_entry(t, key, text, flags, v, tb);
       }
-      dirty.push_back(slot);
+      dirty.set(slot);
       touched.push_back(tb);
     } else {
       if (!room(need)) {
@@ -1373,7 +1557,7 @@ int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
       }
       if (!found) {
         // every entry placed again under a new seed, at the same capacity
-        const Entry extra = make_entry(t, key, text, flags, vid[i], tb);
+        const Entry extra = make_entry(t, key, text, flags, v, tb);
         if (!replace_all(t, extra)) {
           arena_release(t, extra);
           status = fail(IE_ERR_CAPACITY, "no free placement for a new key: rebuild the table with more room");
@@ -1384,6 +1568,7 @@ int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
         t->n_entries++;
         if (key.size() > kInlineKey && key.size() <= 2 * kInlineKey) t->dev.flags |= TF_LONG_KEYS;
         t->dev.maxtext = std::max<uint64_t>(t->dev.maxtext, text.size());
+        take(i, v, false);
         continue;
       }
       // the group's members move together: one from -> to map, applied once to the slot lists (a
@@ -1394,12 +1579,12 @@ int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
       for (uint32_t s2 : gs) moved.push_back(t->h_entries[s2]);
       for (uint32_t s2 : gs) {
         t->h_entries[s2] = Entry{};
-        dirty.push_back(s2);
+        dirty.set(s2);
       }
       for (size_t k = 0; k < moved.size(); k++) {
         const uint32_t from = gs[k], to = cand[k];
         t->h_entries[to] = moved[k];
-        dirty.push_back(to);
+        dirty.set(to);
         if (from != to) moved_to[from] = to;
       }
       if (!moved_to.empty()) {
@@ -1420,13 +1605,13 @@ int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
             if (jt != moved_to.end()) rs = jt->second;
           }
         }
-        for (uint32_t& rs : rewritten) {
-          auto it = moved_to.find(rs);
-          if (it != moved_to.end()) rs = it->second;
-        }
+        std::vector<uint32_t> rw;  // (all cleared first, then set at their new slots: see above)
+        for (const auto& ft : moved_to)
+          if (rewritten.has(ft.first)) rw.push_back(ft.second), rewritten.clear(ft.first);
+        for (uint32_t to : rw) rewritten.set(to);
       }
-      t->h_entries[cand.back()] = make_entry(t, key, text, flags, vid[i], tb);
-      dirty.push_back(cand.back());
+      t->h_entries[cand.back()] = make_entry(t, key, text, flags, v, tb);
+      dirty.set(cand.back());
       gs.assign(cand.begin(), cand.end());
       t->h_pilots[g] = (uint16_t)pilot;
       dirty_groups.push_back(g);
@@ -1434,7 +1619,12 @@ int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
     }
     if (key.size() > kInlineKey && key.size() <= 2 * kInlineKey) t->dev.flags |= TF_LONG_KEYS;
     t->dev.maxtext = std::max<uint64_t>(t->dev.maxtext, text.size());
+    take(i, v, present);
   }
+  tr.mark("apply", n);
+  flush_copies(t);
+  t->defer = nullptr;  // (the pre-resolved values below copy out of temporaries: no deferral)
+  tr.mark("copies", t->h_arena.size() - call_start);
   // values pre-resolved against the old dict of a changed table: back to their raw text
   std::sort(touched.begin(), touched.end());
   touched.erase(std::unique(touched.begin(), touched.end()), touched.end());
@@ -1457,22 +1647,25 @@ int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
       arena_release(t, e);
       e = make_entry(t, key, raw, kflags | text_flags(raw), e.vid, tb);
       t->dev.maxtext = std::max<uint64_t>(t->dev.maxtext, raw.size());
-      dirty.push_back(s2);
+      dirty.set(s2);
     }
     t->rawalt.erase(it);
   }
+  tr.mark("rawalt", touched.size());
   // dead bytes beyond the live ones (and beyond 64 KB): compact (one whole upload)
   const uint64_t dead = t->h_arena.size() - std::min<uint64_t>(t->h_arena.size(), t->arena_live);
   if (dead > t->arena_live && dead > (64u << 10)) {
     compact_arena(t);
     whole = whole_arena = true;
   }
+  tr.mark("compact?", t->h_arena.size());
   // upload: the appended arena bytes, the changed entries, the changed pilots
   const bool grown = t->h_arena.size() > t->arena_cap;
   if (grown || whole_arena) {  // (re)allocate when grown; the whole mirror goes up
     if (grown) {
       DevBuf na;
-      const uint64_t cap = std::min<uint64_t>(t->arena_limit, t->h_arena.size() + std::max<uint64_t>(t->h_arena.size() / 4, 1ull << 16));
+      // (twice the mirror: a store loop appending tens of MB per call reallocates rarely)
+      const uint64_t cap = std::min<uint64_t>(t->arena_limit, t->h_arena.size() + std::max<uint64_t>(t->h_arena.size(), 1ull << 16));
       IE_HIP(na.ensure(cap + 16));
       t->arena.release();
       t->arena = na;
@@ -1480,34 +1673,51 @@ int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
       t->arena_cap = cap;
       t->dev.arena = (const uint8_t*)t->arena.p;
     }
-    IE_HIP(hipMemset(t->arena.p, 0, t->arena_cap + 16));
     IE_HIP(hipMemcpy(t->arena.p, t->h_arena.data(), t->h_arena.size(), hipMemcpyHostToDevice));
+    IE_HIP(hipMemset((uint8_t*)t->arena.p + t->h_arena.size(), 0, t->arena_cap + 16 - t->h_arena.size()));
     arena0 = t->h_arena.size();
+    tr.mark("arena upload", arena0);
   }
-  // one upload and one kernel for the appended texts, the texts rewritten in place, the changed
-  // entries and pilots (the whole entry array in one copy when many changed)
+  // the appended texts in one copy; one upload and one kernel for the texts rewritten in place, the
+  // changed entries and pilots (the whole entry array in one copy when many changed)
   Patches pe;
-  if (t->h_arena.size() > arena0)
-    pe.add((uint8_t*)t->arena.p + arena0, t->h_arena.data() + arena0, t->h_arena.size() - arena0);
-  if (!whole_arena) {
-    std::sort(rewritten.begin(), rewritten.end());
-    rewritten.erase(std::unique(rewritten.begin(), rewritten.end()), rewritten.end());
-    for (uint32_t s2 : rewritten) {
-      const Entry& e = t->h_entries[s2];
-      if (!(e.flags & EF_OCCUPIED)) continue;
-      uint64_t a, b2;
-      arena_span(t, e, a, b2);
-      if (a >= arena0) continue;  // inside the appended tail, sent whole above
-      b2 = std::min<uint64_t>(b2, arena0);
-      pe.add((uint8_t*)t->arena.p + a, t->h_arena.data() + a, b2 - a);
-    }
+  if (t->h_arena.size() > arena0) {  // the appended texts: one contiguous copy
+    IE_HIP(hipMemcpy((uint8_t*)t->arena.p + arena0, t->h_arena.data() + arena0, t->h_arena.size() - arena0,
+                     hipMemcpyHostToDevice));
+    tr.mark("tail upload", t->h_arena.size() - arena0);
   }
-  std::sort(dirty.begin(), dirty.end());
-  dirty.erase(std::unique(dirty.begin(), dirty.end()), dirty.end());
-  if (whole || dirty.size() * 8 > t->h_entries.size()) {
+  {
+    const uint64_t nd = dirty.count();
+    pe.reserve(nd + dirty_groups.size() + 16, nd * sizeof(Entry));
+  }
+  if (!whole_arena) {
+    const std::vector<uint32_t> rs = rewritten.slots();
+    std::vector<CopyJob> rr(rs.size());
+    parallel_for(rs.size(), [&](uint64_t lo, uint64_t hi) {
+      for (uint64_t k = lo; k < hi; k++) {
+        const Entry& e = t->h_entries[rs[k]];
+        rr[k] = CopyJob{0, nullptr, 0};
+        if (!(e.flags & EF_OCCUPIED)) continue;
+        uint64_t a, b2;
+        arena_span(t, e, a, b2);
+        if (a >= arena0) continue;  // inside the appended tail, sent whole above
+        b2 = std::min<uint64_t>(b2, arena0);
+        rr[k] = CopyJob{(uint64_t)(uintptr_t)((uint8_t*)t->arena.p + a), t->h_arena.data() + a, b2 - a};
+      }
+    });
+    pe.add_many(rr);
+  }
+  // (the whole entry array in one copy when that is cheaper than a patch per entry: a copy moves
+  // ~20 GB/s, a patch costs ~100 ns of host work)
+  if (whole || dirty.count() * 32 > t->h_entries.size()) {
     IE_HIP(hipMemcpy(t->entries.p, t->h_entries.data(), t->h_entries.size() * sizeof(Entry), hipMemcpyHostToDevice));
   } else {
-    for (uint32_t s2 : dirty) pe.add((Entry*)t->entries.p + s2, &t->h_entries[s2], sizeof(Entry));
+    const std::vector<uint32_t> ds = dirty.slots();
+    std::vector<CopyJob> er(ds.size());
+    for (size_t k = 0; k < ds.size(); k++)
+      er[k] = CopyJob{(uint64_t)(uintptr_t)((Entry*)t->entries.p + ds[k]), (const uint8_t*)&t->h_entries[ds[k]],
+                      sizeof(Entry)};
+    pe.add_many(er);
   }
   if (whole) {
     IE_HIP(hipMemcpy(t->pilots.p, t->h_pilots.data(), t->h_pilots.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
@@ -1516,9 +1726,20 @@ int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
     dirty_groups.erase(std::unique(dirty_groups.begin(), dirty_groups.end()), dirty_groups.end());
     for (uint32_t g : dirty_groups) pe.add((uint16_t*)t->pilots.p + g, &t->h_pilots[g], sizeof(uint16_t));
   }
+  tr.mark("patch build", pe.data.size());
   if ((rc = apply_patches(t->patch_staging, pe))) return rc;
+  tr.mark("patch apply", pe.dst.size());
   t->dev.n_entries = (uint32_t)t->n_entries;
   return status;
+}
+
+int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, const uint32_t* vid, uint64_t n) {
+  if (n && !vid) return fail(IE_ERR_INVALID, "null argument");
+  return table_update(t, kv, table_id, vid, nullptr, n);
+}
+
+int ie_table_set_store(ie_table* t, const ie_kv* kv, const uint32_t* table_id, uint64_t n, uint32_t* vid_out) {
+  return table_update(t, kv, table_id, nullptr, vid_out, n);
 }
 
 // arena bookkeeping of a table (ie_table_set_update): bytes in use, bytes of live entries, compactions

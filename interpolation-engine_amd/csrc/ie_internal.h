@@ -3,10 +3,19 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
+
+#include <sys/mman.h>
+
+#include <algorithm>
+#include <chrono>
+#include <new>
 
 #include <string>
 #include <string_view>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -49,6 +58,125 @@ struct DevBuf {
 
 bool have_device();
 
+// IE_HOST_TRACE=1: each phase's host wall time to stderr (where a map command's or an update's
+// time goes); off: one branch per mark
+struct Trace {
+  const bool on = getenv("IE_HOST_TRACE") != nullptr;
+  const char* cmd;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  explicit Trace(const char* c) : cmd(c) {}
+  void mark(const char* what, uint64_t n = 0) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "[ie_host] %-8s %-14s n=%-9llu %10.1f us\n", cmd, what, (unsigned long long)n,
+            std::chrono::duration<double, std::micro>(now - t).count());
+    t = now;
+  }
+};
+
+// fn(lo, hi) over [0, n) split across up to IE_HOST_THREADS host threads (default: the cores, at
+// most 8): the table mirror's bulk byte work (text scans, text copies, compaction)
+inline unsigned host_threads() {
+  static const unsigned n = [] {
+    const char* e = getenv("IE_HOST_THREADS");
+    const long v = e ? atol(e) : 0;
+    return v > 0 ? (unsigned)v : std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+  }();
+  return n;
+}
+template <class F>
+void parallel_for(uint64_t n, F&& fn) {
+  const unsigned T = (unsigned)std::min<uint64_t>(host_threads(), n);
+  if (T <= 1) {
+    fn((uint64_t)0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(T - 1);
+  for (unsigned k = 1; k < T; k++) th.emplace_back([&fn, n, k, T] { fn(n * k / T, n * (k + 1) / T); });
+  fn((uint64_t)0, n / T);
+  for (std::thread& x : th) x.join();
+}
+
+// a text copy ie_table_set_update defers until the appends are placed (then done in parallel)
+struct CopyJob {
+  uint64_t dst;
+  const uint8_t* src;
+  uint64_t len;
+};
+
+// The host mirror of a table's text arena: a growable byte buffer over an anonymous mapping, grown
+// by mremap (the kernel moves page tables, not bytes: a 200 MB arena grows without a copy) and
+// backed by transparent huge pages where the kernel gives them (a store appends tens of MB of
+// history text per iteration: 2 MB faults, not 4 KB ones). Appends only; the subset of
+// std::vector's interface the table code uses.
+class HostArena {
+ public:
+  HostArena() = default;
+  HostArena(const HostArena& o) { insert(end(), o.begin(), o.end()); }
+  HostArena& operator=(const HostArena& o) {
+    if (this != &o) {
+      n_ = 0;
+      insert(end(), o.begin(), o.end());
+    }
+    return *this;
+  }
+  HostArena(HostArena&& o) noexcept { swap(o); }
+  HostArena& operator=(HostArena&& o) noexcept {
+    swap(o);  // (o takes ours and frees it)
+    return *this;
+  }
+  ~HostArena() {
+    if (p_) munmap(p_, cap_);
+  }
+  void swap(HostArena& o) noexcept {
+    std::swap(p_, o.p_);
+    std::swap(n_, o.n_);
+    std::swap(cap_, o.cap_);
+  }
+  uint8_t* data() { return p_; }
+  const uint8_t* data() const { return p_; }
+  uint8_t* begin() { return p_; }
+  uint8_t* end() { return p_ + n_; }
+  const uint8_t* begin() const { return p_; }
+  const uint8_t* end() const { return p_ + n_; }
+  uint64_t size() const { return n_; }
+  uint64_t capacity() const { return cap_; }
+  bool empty() const { return n_ == 0; }
+  void clear() { n_ = 0; }
+  void reserve(uint64_t want) {
+    if (want <= cap_) return;
+    const uint64_t kStep = 2ull << 20;
+    const uint64_t cap = (std::max<uint64_t>(want, cap_ * 2) + kStep - 1) & ~(kStep - 1);
+    void* q = p_ ? mremap(p_, cap_, cap, MREMAP_MAYMOVE)
+                 : mmap(nullptr, cap, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (q == MAP_FAILED) throw std::bad_alloc();
+    madvise((uint8_t*)q + cap_, cap - cap_, MADV_HUGEPAGE);
+    p_ = (uint8_t*)q;
+    cap_ = cap;
+  }
+  void grow(uint64_t k) {  // k more bytes, written later (ie_table_set_update's deferred copies)
+    reserve(n_ + k);
+    n_ += k;
+  }
+  void push_back(uint8_t b) {
+    if (n_ == cap_) reserve(n_ + 1);
+    p_[n_++] = b;
+  }
+  template <class It>
+  void insert(uint8_t* /* end() only */, It first, It last) {
+    const uint64_t k = (uint64_t)(last - first);
+    if (!k) return;
+    reserve(n_ + k);
+    memcpy(p_ + n_, &*first, k);
+    n_ += k;
+  }
+
+ private:
+  uint8_t* p_ = nullptr;
+  uint64_t n_ = 0, cap_ = 0;
+};
+
 struct ie_table {
   int32_t device = 0;
   int32_t dialect = 0;
@@ -64,7 +192,9 @@ struct ie_table {
   // the slots of its pre-resolved (EF_RAWALT) entries
   std::vector<Entry> h_entries;
   std::vector<uint16_t> h_pilots;
-  std::vector<uint8_t> h_arena;
+  HostArena h_arena;
+  HostArena h_arena_spare;
+  std::vector<CopyJob>* defer = nullptr;  // set inside ie_table_set_update: long texts copied later  // the buffer the next compaction copies into (pages already touched)
   uint64_t arena_cap = 0;
   // arena bookkeeping (ie_table_set_update): bytes the live entries occupy (the rest of h_arena is
   // dead: replaced texts), the largest arena the table may have (an offset must stay below 2^32;
@@ -72,6 +202,10 @@ struct ie_table {
   uint64_t arena_live = 0;
   uint64_t arena_limit = 0xFFFFFFF0ull;
   uint64_t n_compactions = 0;
+  // value ids ie_table_set_store hands out: the next unused one (the build's kv count), and those
+  // deleted keys gave back
+  uint32_t next_vid = 0;
+  std::vector<uint32_t> free_vids;
   std::vector<std::vector<uint32_t>> groups;
   // (table id << 32 | value id) -> slot, built on demand (ie_maps.cpp: str() of a typed result),
   // dropped by every update

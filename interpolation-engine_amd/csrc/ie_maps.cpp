@@ -28,6 +28,7 @@ namespace {
 
 constexpr uint32_t kMaxPasses = 100000;  // repeat_until_done without a fixed point: IE_DIVERGED
 
+
 struct MapOut {
   std::vector<uint8_t> bytes;
   std::vector<uint64_t> off{0};
@@ -170,7 +171,9 @@ int match_first(ie_exec* x, const ie_table* t, const std::vector<std::string>& p
     w = cache[k].second;
     std::rotate(cache.begin() + k, cache.begin() + k + 1, cache.end());  // (to the back: most recent)
   }
+  Trace tr("match");
   if (!w) {
+    tr.mark("wc lookup", cache.size());
     int rc = ie_wildcards_build(pb.data(), po.data(), (uint32_t)pats.size(), t->dialect, x->device, &w);
     if (rc) return rc;
     if (cache.size() >= 64) {
@@ -178,9 +181,13 @@ int match_first(ie_exec* x, const ie_table* t, const std::vector<std::string>& p
       cache.erase(cache.begin());
     }
     cache.emplace_back(std::move(sig), w);
+    tr.mark("wc build", pats.size());
   }
-  return ie_wildcard_match_batch(x, w, strs.bytes.data(), strs.off.data(), n, range.empty() ? nullptr : range.data(),
-                                 m.match.data(), m.ncap.data(), m.caps.data());
+  const int rc = ie_wildcard_match_batch(x, w, strs.bytes.data(), strs.off.data(), n,
+                                         range.empty() ? nullptr : range.data(), m.match.data(), m.ncap.data(),
+                                         m.caps.data());
+  tr.mark("wc batch", n);
+  return rc;
 }
 
 // the pattern range of a key list in `pats`, appended once per distinct list (states whose map
@@ -326,9 +333,12 @@ int ie_goto_map(ie_exec* x, const ie_table* t, const char* text, uint64_t text_l
     for (uint32_t j = 0; j < m; j++) in.add(std::string_view(maps[j].key, maps[j].key_len), s);
     for (uint32_t j = 0; j < m; j++) in.add(std::string_view(maps[j].value, maps[j].value_len), s);
   }
+  Trace tr("goto");
+  tr.mark("pack", in.size());
   Res r;
   int rc = interp(x, t, in, r);
   if (rc) return rc;
+  tr.mark("interp", in.size());
   MapOut o;
   o.status.reserve(n);
   Blocks blocks;
@@ -394,8 +404,10 @@ int ie_goto_map(ie_exec* x, const ie_table* t, const char* text, uint64_t text_l
     pend.push_back(s);
     fail_at.push_back(m);
   }
+  tr.mark("blocks", blocks.pats.size());
   Match mt;
   if ((rc = match_first(x, t, blocks.pats, texts, range, mt))) return rc;
+  tr.mark("match", texts.size());
   for (size_t k = 0; k < pend.size(); k++) {  // py:1707-1709: the first key matching the text
     const uint32_t s = pend[k];
     const uint64_t b = (uint64_t)s * (1 + 2 * m);
@@ -415,7 +427,9 @@ int ie_goto_map(ie_exec* x, const ie_table* t, const char* text, uint64_t text_l
     if (st[s] == IE_OK_STR) o.push(r.text[b + 1 + m + ch[s]], IE_OK_STR, 0, ch[s]);
     else o.push(st[s] == IE_E_NO_MATCH ? std::string_view(r.text[b]) : std::string_view(), st[s], wh[s], -1);  // (py:1708 names the text)
   }
-  return emit(o, out);
+  rc = emit(o, out);
+  tr.mark("emit", n);
+  return rc;
 }
 
 int ie_replace_map(ie_exec* x, const ie_table* t, const char* name, uint64_t name_len, const uint8_t* bytes,
@@ -447,6 +461,7 @@ int ie_replace_map(ie_exec* x, const ie_table* t, const char* name, uint64_t nam
   std::vector<uint64_t> active(n);
   for (uint64_t i = 0; i < n; i++) active[i] = i;
   MapOut nm;
+  Trace tr("replace");
   int rc = IE_SUCCESS;
   if (name && n == 0) {  // output_name alone (no leaves to run)
     Strs in;
@@ -476,8 +491,10 @@ int ie_replace_map(ie_exec* x, const ie_table* t, const char* name, uint64_t nam
     const uint64_t name0 = in.size();
     if (pass == 1 && name)
       for (uint32_t s = 0; s < nt; s++) in.add(std::string_view(name, name_len), s);
+    tr.mark("pack", in.size());
     Res r;
     if ((rc = interp(x, t, in, r))) return rc;
+    tr.mark("interp", in.size());
     if (pass == 1 && name) {  // no str(): a typed output_name stays typed (py:1715)
       for (uint32_t s = 0; s < nt; s++) {
         const uint64_t k = name0 + s;
@@ -518,8 +535,10 @@ int ie_replace_map(ie_exec* x, const ie_table* t, const char* name, uint64_t nam
       range.push_back(rg.second);
       mstr.add(cur[i], table_id[i]);
     }
+    tr.mark("blocks", blocks.pats.size());
     Match mt;
     if ((rc = match_first(x, t, blocks.pats, mstr, range, mt))) return rc;
+    tr.mark("match", mstr.size());
     // 3. the matched maps' values against inserts | {'1': capture, ...} (py:1732-1738)
     Strs vin;                                // captures spliced in, on the states' own tables
     std::vector<uint64_t> vleaf;
@@ -558,8 +577,10 @@ int ie_replace_map(ie_exec* x, const ie_table* t, const char* name, uint64_t nam
         slow_leaf.push_back(i);
       }
     }
+    tr.mark("captures", vin.size());
     Res vr;
     if ((rc = interp(x, t, vin, vr))) return rc;
+    tr.mark("values", vin.size());
     for (size_t q = 0; q < vleaf.size(); q++) {
       const uint64_t i = vleaf[q];
       if (!ok(vr.st[q])) st[i] = vr.st[q], wh[i] = 1 + m + (uint32_t)ch[i];  // (cur[i]: the matched text)
@@ -577,6 +598,7 @@ int ie_replace_map(ie_exec* x, const ie_table* t, const char* name, uint64_t nam
         if (!ok(sr.st[q])) st[i] = sr.st[q], wh[i] = 1 + m + (uint32_t)ch[i];
         else cur[i] = sr.text[q];
       }
+      tr.mark("slow values", sin.size());
     }
     // 4. a fixed point, or one pass without repeat_until_done (py:1742-1745)
     std::vector<uint64_t> next;
@@ -590,7 +612,9 @@ int ie_replace_map(ie_exec* x, const ie_table* t, const char* name, uint64_t nam
   MapOut o;
   for (uint64_t i = 0; i < n; i++) o.push(cur[i], st[i], st[i] == IE_OK_STR ? 0u : wh[i], ch[i]);
   if (name) emit(nm, names);
-  return emit(o, out);
+  rc = emit(o, out);
+  tr.mark("emit", n);
+  return rc;
 }
 
 int ie_delete_keys(ie_exec* x, ie_table* t, const uint32_t* states, uint32_t n_states, const uint8_t* wbytes,

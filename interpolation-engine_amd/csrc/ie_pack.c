@@ -1,0 +1,371 @@
+// ie_pack.c — the host side's store packing as a CPython module (_ie_pack): InsertsTableSet.update's
+// changes [(dict index, key, value)] -> the ie_kv records and table ids ie_table_set_store takes,
+// pointing straight into an ASCII str's own bytes (no copy) or into one buffer the other texts are
+// transcoded into across host threads (no per-object UTF-8 cache left behind on the caller's
+// strings), and the
+// stored values written back into the table set's value list by the ids the library handed out.
+// Host-only code (gcc), no device calls: the library keeps the C ABI, this only feeds it.
+//
+// Rendering (the splice text, py:531 / interp.rs:314): a str is its own text, an int (not a bool)
+// is str(int) in both dialects; anything else goes through the caller's render(v, dialect).
+#define PY_SSIZE_T_CLEAN
+#include <Python.h>
+#include <emmintrin.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <string.h>
+
+typedef struct {
+  const char* key;
+  uint64_t key_len;
+  const char* text;
+  uint64_t text_len;
+  int32_t kind;
+  uint32_t reserved;
+} kv_rec;  // = ie_kv (include/ie_amd.h)
+
+enum { KIND_STR = 0, KIND_INT = 1 };
+
+#ifndef IE_PACK_ID
+#define IE_PACK_ID "unstamped"
+#endif
+__attribute__((used)) static const char kPackId[] = "IE_BUILD_ID:" IE_PACK_ID;  // (__graft_entry__.built_id)
+
+// A text that is not ASCII: transcoded into the call's buffer (its offset there found by a count
+// pass), both passes across the threads with the GIL released (the strs are immutable and the
+// changes list keeps them alive)
+typedef struct {
+  const void* src;
+  uint64_t len;  // code units
+  int kind;      // 1, 2, 4 bytes per unit
+  uint64_t rec;  // record index * 2 + (0: key, 1: text)
+  uint64_t off, out;
+} job_t;
+
+static inline uint8_t* put_cp(uint8_t* o, uint32_t c) {  // one code point (surrogates: 3 bytes, as 'surrogatepass')
+  if (c < 0x80) {
+    *o++ = (uint8_t)c;
+  } else if (c < 0x800) {
+    *o++ = (uint8_t)(0xC0 | (c >> 6));
+    *o++ = (uint8_t)(0x80 | (c & 0x3F));
+  } else if (c < 0x10000) {
+    *o++ = (uint8_t)(0xE0 | (c >> 12));
+    *o++ = (uint8_t)(0x80 | ((c >> 6) & 0x3F));
+    *o++ = (uint8_t)(0x80 | (c & 0x3F));
+  } else {
+    *o++ = (uint8_t)(0xF0 | (c >> 18));
+    *o++ = (uint8_t)(0x80 | ((c >> 12) & 0x3F));
+    *o++ = (uint8_t)(0x80 | ((c >> 6) & 0x3F));
+    *o++ = (uint8_t)(0x80 | (c & 0x3F));
+  }
+  return o;
+}
+
+static uint64_t utf8_len(const job_t* j) {
+  uint64_t n = j->len;
+  if (j->kind == 1) {
+    const uint8_t* d = (const uint8_t*)j->src;
+    for (uint64_t i = 0; i < j->len; i++) n += d[i] >> 7;
+  } else if (j->kind == 2) {
+    const uint16_t* d = (const uint16_t*)j->src;
+    for (uint64_t i = 0; i < j->len; i++) n += (d[i] >= 0x80) + (d[i] >= 0x800);
+  } else {
+    const uint32_t* d = (const uint32_t*)j->src;
+    for (uint64_t i = 0; i < j->len; i++) n += (d[i] >= 0x80) + (d[i] >= 0x800) + (d[i] >= 0x10000);
+  }
+  return n;
+}
+
+static void transcode(const job_t* j, uint8_t* o) {  // (runs of ASCII 8-16 units at a time)
+  const uint64_t len = j->len;
+  uint64_t i = 0;
+  if (j->kind == 1) {
+    const uint8_t* d = (const uint8_t*)j->src;
+    while (i < len) {
+      if (i + 16 <= len) {
+        const __m128i v = _mm_loadu_si128((const __m128i*)(d + i));
+        if (!_mm_movemask_epi8(v)) {
+          _mm_storeu_si128((__m128i*)o, v);
+          o += 16;
+          i += 16;
+          continue;
+        }
+      }
+      o = put_cp(o, d[i++]);
+    }
+  } else if (j->kind == 2) {
+    const uint16_t* d = (const uint16_t*)j->src;
+    const __m128i hi = _mm_set1_epi16((short)0xFF80);
+    while (i < len) {
+      if (i + 8 <= len) {
+        const __m128i v = _mm_loadu_si128((const __m128i*)(d + i));
+        if (_mm_movemask_epi8(_mm_cmpeq_epi16(_mm_and_si128(v, hi), _mm_setzero_si128())) == 0xFFFF) {
+          _mm_storel_epi64((__m128i*)o, _mm_packus_epi16(v, v));
+          o += 8;
+          i += 8;
+          continue;
+        }
+      }
+      o = put_cp(o, d[i++]);
+    }
+  } else {
+    const uint32_t* d = (const uint32_t*)j->src;
+    const __m128i hi = _mm_set1_epi32((int)0xFFFFFF80u);
+    while (i < len) {
+      if (i + 8 <= len) {
+        const __m128i v0 = _mm_loadu_si128((const __m128i*)(d + i)), v1 = _mm_loadu_si128((const __m128i*)(d + i + 4));
+        const __m128i z = _mm_cmpeq_epi32(_mm_and_si128(_mm_or_si128(v0, v1), hi), _mm_setzero_si128());
+        if (_mm_movemask_epi8(z) == 0xFFFF) {
+          const __m128i w = _mm_packs_epi32(v0, v1);  // (all < 0x80: no saturation)
+          _mm_storel_epi64((__m128i*)o, _mm_packus_epi16(w, w));
+          o += 8;
+          i += 8;
+          continue;
+        }
+      }
+      o = put_cp(o, d[i++]);
+    }
+  }
+}
+
+typedef struct {
+  job_t* jobs;
+  uint64_t lo, hi;
+  uint8_t* buf;  // NULL: the count pass
+} span_t;
+
+static void* run_span(void* arg) {
+  span_t* sp = (span_t*)arg;
+  for (uint64_t k = sp->lo; k < sp->hi; k++) {
+    if (sp->buf) transcode(&sp->jobs[k], sp->buf + sp->jobs[k].off);
+    else sp->jobs[k].out = utf8_len(&sp->jobs[k]);
+  }
+  return NULL;
+}
+
+// one pass over the jobs across up to `threads` threads (split by code units, not by count)
+static void run_jobs(job_t* jobs, uint64_t n, uint8_t* buf, int threads) {
+  uint64_t units = 0;
+  for (uint64_t k = 0; k < n; k++) units += jobs[k].len * (uint64_t)jobs[k].kind;
+  if (threads > 16) threads = 16;
+  if (threads < 1 || units < (1u << 20)) threads = 1;
+  span_t sp[16];
+  pthread_t th[16];
+  uint64_t k = 0, acc = 0;
+  for (int w = 0; w < threads; w++) {
+    sp[w].jobs = jobs;
+    sp[w].buf = buf;
+    sp[w].lo = k;
+    const uint64_t want = units * (uint64_t)(w + 1) / (uint64_t)threads;
+    while (k < n && (acc < want || w == threads - 1)) acc += jobs[k].len * (uint64_t)jobs[k].kind, k++;
+    sp[w].hi = k;
+  }
+  int started[16] = {0};
+  for (int w = 1; w < threads; w++) started[w] = pthread_create(&th[w], NULL, run_span, &sp[w]) == 0;
+  run_span(&sp[0]);
+  for (int w = 1; w < threads; w++) {
+    if (started[w]) pthread_join(th[w], NULL);
+    else run_span(&sp[w]);
+  }
+}
+
+typedef struct {
+  job_t* p;
+  uint64_t n, cap;
+} jobs_t;
+
+// the record's UTF-8 ('surrogatepass', as _native.enc): an ASCII str is its own UTF-8 (a pointer
+// into it); any other becomes a job
+static int utf8_of(PyObject* s, jobs_t* J, uint64_t rec, const char** p, uint64_t* n) {
+  if (PyUnicode_READY(s) < 0) return -1;
+  if (PyUnicode_IS_ASCII(s)) {
+    *p = (const char*)PyUnicode_DATA(s);
+    *n = (uint64_t)PyUnicode_GET_LENGTH(s);
+    return 0;
+  }
+  if (J->n == J->cap) {
+    const uint64_t cap = J->cap ? 2 * J->cap : 1024;
+    job_t* q = (job_t*)PyMem_RawRealloc(J->p, cap * sizeof(job_t));
+    if (!q) {
+      PyErr_NoMemory();
+      return -1;
+    }
+    J->p = q;
+    J->cap = cap;
+  }
+  job_t* j = &J->p[J->n++];
+  j->src = PyUnicode_DATA(s);
+  j->len = (uint64_t)PyUnicode_GET_LENGTH(s);
+  j->kind = PyUnicode_KIND(s);
+  j->rec = rec;
+  *p = NULL;
+  *n = 0;
+  return 0;
+}
+
+static void free_buf(PyObject* cap) { PyMem_RawFree(PyCapsule_GetPointer(cap, "ie_pack.buf")); }
+
+// pack(changes, n_tables, delete, render, dialect, threads) -> (kv: bytearray, table_ids: bytearray,
+// keep) (keep: what the records point into besides the changes' own strs; alive until the call)
+static PyObject* pack(PyObject* self, PyObject* args) {
+  (void)self;
+  PyObject *changes, *del, *render, *dialect;
+  long long n_tables;
+  int threads = 1;
+  if (!PyArg_ParseTuple(args, "OLOOO|i", &changes, &n_tables, &del, &render, &dialect, &threads)) return NULL;
+  PyObject* seq = PySequence_Fast(changes, "changes must be a sequence");
+  if (!seq) return NULL;
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+  PyObject* kvb = PyByteArray_FromStringAndSize(NULL, (Py_ssize_t)(n * sizeof(kv_rec)));
+  PyObject* tidb = PyByteArray_FromStringAndSize(NULL, (Py_ssize_t)(n * 4));
+  PyObject* keep = PyList_New(0);
+  jobs_t J = {NULL, 0, 0};
+  uint8_t* buf = NULL;
+  if (!kvb || !tidb || !keep) goto fail;
+  kv_rec* kv = (kv_rec*)PyByteArray_AS_STRING(kvb);
+  uint32_t* tid = (uint32_t*)PyByteArray_AS_STRING(tidb);
+  for (Py_ssize_t i = 0; i < n; i++) {
+    PyObject* c = PySequence_Fast_GET_ITEM(seq, i);
+    if (!PyTuple_Check(c) || PyTuple_GET_SIZE(c) != 3) {
+      PyErr_SetString(PyExc_TypeError, "a change is a (dict index, key, value) tuple");
+      goto fail;
+    }
+    PyObject *t = PyTuple_GET_ITEM(c, 0), *k = PyTuple_GET_ITEM(c, 1), *v = PyTuple_GET_ITEM(c, 2);
+    const long long tb = PyLong_AsLongLong(t);
+    if (tb == -1 && PyErr_Occurred()) goto fail;
+    if (!PyUnicode_Check(k)) {
+      PyErr_SetString(PyExc_TypeError, "insert keys must be str");
+      goto fail;
+    }
+    if (tb < 0 || tb >= n_tables) {
+      PyErr_SetString(PyExc_IndexError, "dict index beyond the table set");
+      goto fail;
+    }
+    tid[i] = (uint32_t)tb;
+    kv_rec* r = &kv[i];
+    memset(r, 0, sizeof *r);
+    if (utf8_of(k, &J, 2 * (uint64_t)i, &r->key, &r->key_len) < 0) goto fail;
+    if (v == del) {
+      r->kind = -1;
+      continue;
+    }
+    PyObject* text = NULL;
+    if (PyUnicode_CheckExact(v)) {
+      r->kind = KIND_STR;
+      text = v;
+    } else if (PyLong_CheckExact(v)) {
+      r->kind = KIND_INT;
+      text = PyObject_Str(v);
+      if (!text || PyList_Append(keep, text) < 0) {
+        Py_XDECREF(text);
+        goto fail;
+      }
+      Py_DECREF(text);
+    } else {
+      PyObject* kt = PyObject_CallFunctionObjArgs(render, v, dialect, NULL);  // (kind, text)
+      if (!kt) goto fail;
+      if (PyList_Append(keep, kt) < 0) {
+        Py_DECREF(kt);
+        goto fail;
+      }
+      Py_DECREF(kt);
+      if (!PyTuple_Check(kt) || PyTuple_GET_SIZE(kt) != 2 || !PyUnicode_Check(PyTuple_GET_ITEM(kt, 1))) {
+        PyErr_SetString(PyExc_TypeError, "render must return (kind, str)");
+        goto fail;
+      }
+      r->kind = (int32_t)PyLong_AsLong(PyTuple_GET_ITEM(kt, 0));
+      if (r->kind == -1 && PyErr_Occurred()) goto fail;
+      text = PyTuple_GET_ITEM(kt, 1);
+    }
+    if (utf8_of(text, &J, 2 * (uint64_t)i + 1, &r->text, &r->text_len) < 0) goto fail;
+  }
+  if (J.n) {  // the texts that are not ASCII: count, place, transcode; then the records point there
+    uint64_t total = 0;
+    Py_BEGIN_ALLOW_THREADS
+    run_jobs(J.p, J.n, NULL, threads);
+    Py_END_ALLOW_THREADS
+    for (uint64_t k = 0; k < J.n; k++) {
+      J.p[k].off = total;
+      total += J.p[k].out;
+    }
+    buf = (uint8_t*)PyMem_RawMalloc(total + 16);
+    if (!buf) {
+      PyErr_NoMemory();
+      goto fail;
+    }
+    Py_BEGIN_ALLOW_THREADS
+    run_jobs(J.p, J.n, buf, threads);
+    Py_END_ALLOW_THREADS
+    for (uint64_t k = 0; k < J.n; k++) {
+      kv_rec* r = &kv[J.p[k].rec / 2];
+      if (J.p[k].rec & 1) r->text = (const char*)buf + J.p[k].off, r->text_len = J.p[k].out;
+      else r->key = (const char*)buf + J.p[k].off, r->key_len = J.p[k].out;
+    }
+    PyObject* cap = PyCapsule_New(buf, "ie_pack.buf", free_buf);
+    if (!cap) goto fail;
+    buf = NULL;  // (the capsule owns it)
+    if (PyList_Append(keep, cap) < 0) {
+      Py_DECREF(cap);
+      goto fail;
+    }
+    Py_DECREF(cap);
+  }
+  PyMem_RawFree(J.p);
+  Py_DECREF(seq);
+  return Py_BuildValue("(NNN)", kvb, tidb, keep);
+fail:
+  PyMem_RawFree(J.p);
+  PyMem_RawFree(buf);
+  Py_DECREF(seq);
+  Py_XDECREF(kvb);
+  Py_XDECREF(tidb);
+  Py_XDECREF(keep);
+  return NULL;
+}
+
+// assign(values, changes, vids, delete) -> None: values[vids[i]] = the stored value (None for a
+// delete), the list grown with None as the ids need; ids 0xFFFFFFFF are skipped
+static PyObject* assign(PyObject* self, PyObject* args) {
+  (void)self;
+  PyObject *values, *changes, *vids, *del;
+  if (!PyArg_ParseTuple(args, "O!OOO", &PyList_Type, &values, &changes, &vids, &del)) return NULL;
+  Py_buffer vb;
+  if (PyObject_GetBuffer(vids, &vb, PyBUF_SIMPLE) < 0) return NULL;
+  PyObject* seq = PySequence_Fast(changes, "changes must be a sequence");
+  if (!seq) {
+    PyBuffer_Release(&vb);
+    return NULL;
+  }
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+  if (vb.len < (Py_ssize_t)(n * 4)) {
+    PyErr_SetString(PyExc_ValueError, "fewer ids than changes");
+    goto fail;
+  }
+  const uint32_t* id = (const uint32_t*)vb.buf;
+  for (Py_ssize_t i = 0; i < n; i++) {
+    if (id[i] == 0xFFFFFFFFu) continue;
+    while (PyList_GET_SIZE(values) <= (Py_ssize_t)id[i])
+      if (PyList_Append(values, Py_None) < 0) goto fail;
+    PyObject* v = PyTuple_GET_ITEM(PySequence_Fast_GET_ITEM(seq, i), 2);
+    if (v == del) v = Py_None;
+    Py_INCREF(v);
+    if (PyList_SetItem(values, (Py_ssize_t)id[i], v) < 0) goto fail;  // (steals v, drops the old value)
+  }
+  Py_DECREF(seq);
+  PyBuffer_Release(&vb);
+  Py_RETURN_NONE;
+fail:
+  Py_DECREF(seq);
+  PyBuffer_Release(&vb);
+  return NULL;
+}
+
+static PyMethodDef methods[] = {
+    {"pack", pack, METH_VARARGS, "changes -> (ie_kv records, table ids, keep-alive list)"},
+    {"assign", assign, METH_VARARGS, "store the values under the ids the library handed out"},
+    {NULL, NULL, 0, NULL},
+};
+
+static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_ie_pack", NULL, -1, methods, NULL, NULL, NULL, NULL};
+
+PyMODINIT_FUNC PyInit__ie_pack(void) { return PyModule_Create(&module); }

@@ -180,103 +180,33 @@ class InsertsTableSet:
 
     def update(self, changes):
         """set_interpdata on the device copy (py:470-471 `inserts[key] = value`, or DELETE for
-        `del`), without a rebuild (ie_table_set_update): changes = [(dict index, key, value)].
+        `del`), without a rebuild (ie_table_set_store): changes = [(dict index, key, value)].
         The caller's dicts are not touched (the states the table set was built from are usually the
         caller's own, already updated). False when the library found no placement for a new key:
-        then rebuild the table set."""
-        import numpy as np
+        then rebuild the table set. The packing is native (csrc/ie_pack.c: ie_kv records over the
+        str objects' own UTF-8) and the library hands out the value ids (a rewrite keeps its key's,
+        a delete frees it); the stored values land in self.values under those ids."""
         n = len(changes)
         if n == 0:
             return True
-        kb, tb, kinds, tids, vids = [], [], [], [], []
-        nd, kmemo, values = len(self.dicts), {}, self.values
-        vid_of, free = self._vids()
-        for t, k, v in changes:
-            if type(k) is not str:
-                raise TypeError("insert keys must be str")
-            if t < 0 or t >= nd:
-                raise IndexError("dict index beyond the table set")
-            tids.append(t)
-            e = kmemo.get(k)
-            if e is None:
-                e = kmemo[k] = N.enc(k)
-            kb.append(e)
-            # the value id of (t, k): a rewrite keeps the key's id (its old value is dropped), a
-            # new key takes a freed id or a new one, a delete frees the key's id
-            tk = (t, k)
-            old = vid_of.get(tk)
-            if old is None and tk not in vid_of:
-                old = self._build_vid(t, k)
-            if v is DELETE:
-                kinds.append(-1)
-                vids.append(0)
-                tb.append(b"")
-                if old is not None:
-                    values[old] = None
-                    free.append(old)
-                    vid_of[tk] = None
-                continue
-            if type(v) is str:
-                kinds.append(N.KIND_STR)
-                tb.append(N.enc(v))
-            else:
-                kd, text = render(v, self.dialect)
-                kinds.append(kd)
-                tb.append(N.enc(text))
-            if old is None:
-                if free:
-                    old = free.pop()
-                else:
-                    old = len(values)
-                    values.append(None)
-                vid_of[tk] = old
-            values[old] = v
-            vids.append(old)
-        if n <= 32:  # a scalar caller's few stores: ctypes arrays (numpy's per-call cost dominates)
-            arr = (N.KV * n)(*[N.KV(k, len(k), t, len(t), kd, 0) for k, t, kd in zip(kb, tb, kinds)])
-            ta, va = (ctypes.c_uint32 * n)(*tids), (ctypes.c_uint32 * n)(*vids)
-            t0 = time.perf_counter()
-            rc = N.lib().ie_table_set_update(self.h, ctypes.byref(arr), ta, va, n)
-            self.last_update_native_s = time.perf_counter() - t0
-            if rc == N.ERR_CAPACITY:
-                return False
-            N.check(rc, "ie_table_set_update")
-            return True
-        kinds = np.asarray(kinds, np.int32)
-        tids = np.asarray(tids, np.uint32)
-        vids = np.asarray(vids, np.uint32)
-        kblob = np.frombuffer(b"".join(kb) + b"\0", np.uint8)
-        tblob = np.frombuffer(b"".join(tb) + b"\0", np.uint8)
-        klen = np.fromiter(map(len, kb), np.uint64, n)
-        tlen = np.fromiter(map(len, tb), np.uint64, n)
-        arr = np.zeros(n, dtype=[("key", "<u8"), ("key_len", "<u8"), ("text", "<u8"), ("text_len", "<u8"),
-                                 ("kind", "<i4"), ("reserved", "<u4")])
-        arr["key"] = kblob.ctypes.data + np.concatenate(([0], np.cumsum(klen)[:-1])).astype(np.uint64)
-        arr["key_len"] = klen
-        arr["text"] = tblob.ctypes.data + np.concatenate(([0], np.cumsum(tlen)[:-1])).astype(np.uint64)
-        arr["text_len"] = tlen
-        arr["kind"] = kinds
+        P = N.pack_module()
+        tp = time.perf_counter()
+        kv, tids, keep = P.pack(changes, len(self.dicts), DELETE, render, self.dialect, N.host_threads())
+        vids = bytearray(4 * n)
+        cv = ctypes.c_char * (4 * n)
         t0 = time.perf_counter()
-        rc = N.lib().ie_table_set_update(self.h, ctypes.c_void_p(arr.ctypes.data), tids.ctypes.data, vids.ctypes.data, n)
-        self.last_update_native_s = time.perf_counter() - t0
+        rc = N.lib().ie_table_set_store(self.h, (ctypes.c_char * len(kv)).from_buffer(kv), cv.from_buffer(tids), n,
+                                        cv.from_buffer(vids))
+        t1 = time.perf_counter()
+        del keep  # (the records point into these texts until the call returns)
         if rc == N.ERR_CAPACITY:
             return False
-        N.check(rc, "ie_table_set_update")
+        N.check(rc, "ie_table_set_store")
+        P.assign(self.values, changes, vids, DELETE)
+        # (where a store call's time goes: packing, the library, the value list)
+        self.last_update_native_s = t1 - t0
+        self.last_update_split_s = (t0 - tp, t1 - t0, time.perf_counter() - t1)
         return True
-
-    def _vids(self):
-        """(t, key) -> value id of the keys stored since the build (None: deleted), and the freed ids."""
-        if not hasattr(self, "_vid_of"):
-            self._vid_of, self._free, self._tkeys = {}, [], {}
-        return self._vid_of, self._free
-
-    def _build_vid(self, t, k):
-        """The value id key k of dict t had at the build (its kv index), or None."""
-        m = self._tkeys.get(t)
-        if m is None:
-            a = self.starts[t]
-            m = self._tkeys[t] = {kk: a + i for i, kk in enumerate(self.keys[a:self.starts[t + 1]])}
-        return m.get(k)
 
     def set_arena_limit(self, nbytes):
         """Lower the text arena's limit (update then reports False, a rebuild, once it is reached)."""
