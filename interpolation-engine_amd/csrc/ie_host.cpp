@@ -836,7 +836,17 @@ bool rewrite_in_place(ie_table* t, Entry& e, std::string_view text, uint32_t fla
   uint64_t a, b;
   arena_span(t, e, a, b);
   uint8_t* base = t->h_arena.data();
-  const std::string key(mirror_key(t, e));
+  const std::string_view k0 = mirror_key(t, e);
+  char kbuf[256];  // (the key moves: copied out first; a long key on the heap)
+  std::string klong;
+  std::string_view key;
+  if (k0.size() <= sizeof kbuf) {
+    memcpy(kbuf, k0.data(), k0.size());
+    key = std::string_view(kbuf, k0.size());
+  } else {
+    klong.assign(k0);
+    key = klong;
+  }
   memset(base + a, 0, b - a);
   memcpy(base + e.text_off, text.data(), text.size());
   const uint32_t ko = key_off_of(e.text_off, (uint32_t)text.size());
@@ -1026,8 +1036,10 @@ int upload_table(const std::vector<Ent>& ents, uint32_t n_tables, int32_t dialec
   for (size_t i = 0; i < items.size(); i++) entries[slot_of[i]] = items[i];
   ie_table* t = new ie_table();
   t->groups.assign(nb, {});
+  t->clock_slots.assign(2ull * n_tables, UINT32_MAX);
   for (size_t i = 0; i < items.size(); i++) {
-    if (items[i].vid == IE_VID_CLOCK_HHMM || items[i].vid == IE_VID_CLOCK_HHMMSS) t->clock_slots.push_back(slot_of[i]);
+    if (items[i].vid == IE_VID_CLOCK_HHMM || items[i].vid == IE_VID_CLOCK_HHMMSS)
+      t->clock_slots[2ull * ents[i].tid + (items[i].vid == IE_VID_CLOCK_HHMMSS)] = slot_of[i];
     if (items[i].flags & EF_RAWALT) t->rawalt[ents[i].tid].push_back(slot_of[i]);
     t->groups[ph_group(key_hash(ents[i].key, seed, ents[i].tid), nb)].push_back(slot_of[i]);
   }
@@ -1335,6 +1347,7 @@ int ie_table_set_clock(ie_table* t, const ie_clock* now) {
   snprintf(hhmmss, sizeof hhmmss, "%02d:%02d:%02d", now->hour, now->minute, now->second);
   Patches pe;  // every table's two clock entries and their arena texts: one upload
   for (uint32_t slot : t->clock_slots) {
+    if (slot == UINT32_MAX) continue;
     Entry& e = t->h_entries[slot];
     const char* txt = e.vid == IE_VID_CLOCK_HHMM ? hhmm : hhmmss;
     if (strlen(txt) != e.text_len) return fail(IE_ERR_INVALID, "clock field out of range");
@@ -1393,12 +1406,21 @@ static int table_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
     if (kv[i].key_len >= 0xFFFFFFF0ull || kv[i].text_len >= 0xFFFFFFF0ull) return fail(IE_ERR_INVALID, "key or text above 4 GiB");
   }
   if (t->dev.flags & TF_CUCKOO) return fail(IE_ERR_INVALID, "a two-choice (IE_CUCKOO) table takes no updates");
-  t->vid_ok = false;
   Trace tr("update");
   int rc = set_device(t->device);
   if (rc) return rc;
   IE_HIP(hipDeviceSynchronize());  // no batch may still read the table
   tr.mark("sync", n);
+  if (!t->occ_ok) {
+    t->occ.assign((t->h_entries.size() + 63) / 64, 0);
+    for (size_t s2 = 0; s2 < t->h_entries.size(); s2++)
+      if (t->h_entries[s2].flags & EF_OCCUPIED) t->occ[s2 >> 6] |= 1ull << (s2 & 63);
+    t->occ_ok = true;
+  }
+  auto occupy = [t](uint32_t s2, bool on) {
+    if (on) t->occ[s2 >> 6] |= 1ull << (s2 & 63);
+    else t->occ[s2 >> 6] &= ~(1ull << (s2 & 63));
+  };
   uint64_t arena0 = t->h_arena.size();
   uint64_t seed = t->dev.seed;
   const uint32_t nb = t->dev.nb, m = t->dev.m;
@@ -1410,6 +1432,7 @@ static int table_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
   std::vector<uint32_t> touched;           // tables whose pre-resolved values must go raw
   int status = IE_SUCCESS;
   uint64_t call_start = t->h_arena.size();  // (the texts placed since: maybe not copied yet)
+  uint64_t n_tries = 0, n_replace_all = 0;  // (IE_HOST_TRACE)
   // room for an append of `need` bytes below the table's arena limit (offsets stay below 2^32):
   // compacted first when dead bytes would make the room; false: IE_ERR_CAPACITY
   auto room = [&](uint64_t need) -> bool {
@@ -1473,6 +1496,11 @@ static int table_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
         const uint64_t h8 = khash[i + 8];
         __builtin_prefetch(&t->h_entries[ph_slot(h8, t->h_pilots[ph_group(h8, nb)], m)]);
       }
+      if (i + 4 < n) {  // (and the text a rewrite in place will overwrite)
+        const uint64_t h4 = khash[i + 4];
+        const Entry& e4 = t->h_entries[ph_slot(h4, t->h_pilots[ph_group(h4, nb)], m)];
+        if (e4.text_off < t->h_arena.size()) __builtin_prefetch(t->h_arena.data() + e4.text_off, 1);
+      }
     }
     const uint64_t h = seed == seed0 ? khash[i] : key_hash(key, seed, tb);
     const uint32_t g = ph_group(h, nb), slot = ph_slot(h, t->h_pilots[g], m);
@@ -1504,6 +1532,7 @@ static int table_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
       gs.erase(std::remove(gs.begin(), gs.end(), slot), gs.end());
       arena_release(t, cur);
       cur = Entry{};
+      occupy(slot, false);
       dirty.set(slot);
       t->n_entries--;
       touched.push_back(tb);
@@ -1546,10 +1575,11 @@ static int table_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
       bool found = false;
       uint32_t pilot = 0;
       for (uint32_t p = 0; p < 65536 && !found; p++) {
+        n_tries++;
         bool ok = true;
         for (size_t k = 0; k < hs.size() && ok; k++) {
           const uint32_t c = ph_slot(hs[k], p, m);
-          ok = !(t->h_entries[c].flags & EF_OCCUPIED) || std::find(gs.begin(), gs.end(), c) != gs.end();
+          ok = !((t->occ[c >> 6] >> (c & 63)) & 1) || std::find(gs.begin(), gs.end(), c) != gs.end();
           for (size_t j = 0; j < k && ok; j++) ok = cand[j] != c;
           cand[k] = c;
         }
@@ -1558,6 +1588,7 @@ static int table_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
       if (!found) {
         // every entry placed again under a new seed, at the same capacity
         const Entry extra = make_entry(t, key, text, flags, v, tb);
+        n_replace_all++;
         if (!replace_all(t, extra)) {
           arena_release(t, extra);
           status = fail(IE_ERR_CAPACITY, "no free placement for a new key: rebuild the table with more room");
@@ -1565,6 +1596,10 @@ static int table_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
         }
         seed = t->dev.seed;
         whole = whole_arena = true;  // (the slots rewritten in place so far moved with the rest)
+        std::fill(t->occ.begin(), t->occ.end(), 0ull);
+        for (size_t s2 = 0; s2 < t->h_entries.size(); s2++)
+          if (t->h_entries[s2].flags & EF_OCCUPIED) occupy((uint32_t)s2, true);
+        t->vid_ok = false;
         t->n_entries++;
         if (key.size() > kInlineKey && key.size() <= 2 * kInlineKey) t->dev.flags |= TF_LONG_KEYS;
         t->dev.maxtext = std::max<uint64_t>(t->dev.maxtext, text.size());
@@ -1579,19 +1614,20 @@ static int table_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
       for (uint32_t s2 : gs) moved.push_back(t->h_entries[s2]);
       for (uint32_t s2 : gs) {
         t->h_entries[s2] = Entry{};
+        occupy(s2, false);
         dirty.set(s2);
       }
       for (size_t k = 0; k < moved.size(); k++) {
         const uint32_t from = gs[k], to = cand[k];
         t->h_entries[to] = moved[k];
+        occupy(to, true);
         dirty.set(to);
         if (from != to) moved_to[from] = to;
       }
       if (!moved_to.empty()) {
-        for (uint32_t& cs : t->clock_slots) {
-          auto it = moved_to.find(cs);
-          if (it != moved_to.end()) cs = it->second;
-        }
+        for (size_t k = 0; k < moved.size(); k++)  // (a clock entry's place in clock_slots: 2 * table + which)
+          if (moved[k].vid == IE_VID_CLOCK_HHMM || moved[k].vid == IE_VID_CLOCK_HHMMSS)
+            t->clock_slots[2ull * (moved[k].flags >> kTidShift) + (moved[k].vid == IE_VID_CLOCK_HHMMSS)] = cand[k];
         std::vector<uint32_t> tabs;  // the tables whose pre-resolved entries moved
         for (const Entry& e : moved)
           if (e.flags & EF_RAWALT) tabs.push_back(e.flags >> kTidShift);
@@ -1611,6 +1647,7 @@ static int table_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
         for (uint32_t to : rw) rewritten.set(to);
       }
       t->h_entries[cand.back()] = make_entry(t, key, text, flags, v, tb);
+      occupy(cand.back(), true);
       dirty.set(cand.back());
       gs.assign(cand.begin(), cand.end());
       t->h_pilots[g] = (uint16_t)pilot;
@@ -1622,6 +1659,8 @@ static int table_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
     take(i, v, present);
   }
   tr.mark("apply", n);
+  tr.mark("(pilot tries)", n_tries);
+  tr.mark("(re-placements)", n_replace_all);
   flush_copies(t);
   t->defer = nullptr;  // (the pre-resolved values below copy out of temporaries: no deferral)
   tr.mark("copies", t->h_arena.size() - call_start);
@@ -1730,6 +1769,14 @@ static int table_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
   if ((rc = apply_patches(t->patch_staging, pe))) return rc;
   tr.mark("patch apply", pe.dst.size());
   t->dev.n_entries = (uint32_t)t->n_entries;
+  if (t->vid_ok) {  // the value ids of the changed slots (a stale one is caught on use)
+    for (uint32_t s2 : dirty.slots()) {
+      const Entry& e = t->h_entries[s2];
+      if (!(e.flags & EF_OCCUPIED) || e.vid >= IE_VID_CLOCK_HHMMSS) continue;
+      if (e.vid >= t->vid_slot.size()) t->vid_slot.resize(e.vid + 1, UINT32_MAX);
+      t->vid_slot[e.vid] = s2;
+    }
+  }
   return status;
 }
 

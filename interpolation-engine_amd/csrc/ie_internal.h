@@ -185,7 +185,7 @@ struct ie_table {
   uint32_t n_tables = 1;  // inserts dicts in the set
   DevTable dev{};
   // the clock entries ('HH:MM', 'HH:MM:SS' of every table): their slots (ie_table_set_clock)
-  std::vector<uint32_t> clock_slots;
+  std::vector<uint32_t> clock_slots;  // [2 * table + 0/1]: 'HH:MM' / 'HH:MM:SS' (UINT32_MAX: none)
   DevBuf entries, pilots, arena;
   // host mirror of the device table (ie_table_set_update, ie_table_set_clock): entries, pilots,
   // the arena (device capacity arena_cap), the slots of each pilot group, and per table of the set
@@ -207,10 +207,13 @@ struct ie_table {
   uint32_t next_vid = 0;
   std::vector<uint32_t> free_vids;
   std::vector<std::vector<uint32_t>> groups;
-  // (table id << 32 | value id) -> slot, built on demand (ie_maps.cpp: str() of a typed result),
-  // dropped by every update
-  mutable std::unordered_map<uint64_t, uint32_t> vid_slot;
+  // value id -> slot, built on demand (ie_maps.cpp: str() of a typed result), kept by the updates
+  mutable std::vector<uint32_t> vid_slot;  // value id -> slot (UINT32_MAX: none); checked on use
   mutable bool vid_ok = false;
+  // occupied slots (bitmap) for ie_table_set_update's pilot searches: cache-resident where the
+  // entries are tens of MB; built on the first update, kept by the updates, dropped by a re-placement
+  std::vector<uint64_t> occ;
+  bool occ_ok = false;
   std::unordered_map<uint32_t, std::vector<uint32_t>> rawalt;
   DevBuf patch_staging;  // ie_table_set_update / _set_clock uploads
   ~ie_table() {

@@ -20,6 +20,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <deque>
 #include <unordered_map>
 
 #include "ie_internal.h"
@@ -84,25 +85,51 @@ struct Strs {
 // the results of a batch: str() of each (py:1692, 1698-1699, 1722, 1738: a whole-string key's
 // typed result is str()-ed), the status (IE_OK_VALUE kept, with its value id)
 struct Res {
-  std::vector<std::string> text;
+  std::vector<std::string_view> text;  // into the batch's bytes, or into `owned` (a typed result's str())
   std::vector<uint8_t> st;
   std::vector<uint32_t> vid;
+  std::deque<std::string> owned;
+  ie_batch* b = nullptr;
+  Res() = default;
+  Res(const Res&) = delete;
+  Res& operator=(const Res&) = delete;
+  ~Res() { ie_batch_free(b); }
 };
 
 // str() of the raw insert behind a whole-string result (py:510-514): the entry's rendering (the
 // raw text of a pre-resolved one), or the clock's text for the clock ids
+ie_clock table_clock(const ie_table* t);
+
 bool value_str(const ie_table* t, uint32_t tb, uint32_t vid, std::string& out) {
+  if (vid == IE_VID_CLOCK_HHMM || vid == IE_VID_CLOCK_HHMMSS) {  // (one clock for every table of a set)
+    const ie_clock c = table_clock(t);
+    char buf[16];
+    snprintf(buf, sizeof buf, vid == IE_VID_CLOCK_HHMM ? "%02d:%02d" : "%02d:%02d:%02d", c.hour, c.minute, c.second);
+    out = buf;
+    return true;
+  }
   if (!t->vid_ok) {
-    t->vid_slot.clear();
+    t->vid_slot.assign(t->next_vid, UINT32_MAX);
     for (uint32_t s = 0; s < (uint32_t)t->h_entries.size(); s++) {
       const Entry& e = t->h_entries[s];
-      if (e.flags & EF_OCCUPIED) t->vid_slot[((uint64_t)(e.flags >> kTidShift) << 32) | e.vid] = s;
+      if (!(e.flags & EF_OCCUPIED) || e.vid >= IE_VID_CLOCK_HHMMSS) continue;
+      if (e.vid >= t->vid_slot.size()) t->vid_slot.resize(e.vid + 1, UINT32_MAX);
+      t->vid_slot[e.vid] = s;
     }
     t->vid_ok = true;
   }
-  auto it = t->vid_slot.find(((uint64_t)tb << 32) | vid);
-  if (it == t->vid_slot.end()) return false;
-  const Entry& e = t->h_entries[it->second];
+  auto holds = [&](uint32_t s) {
+    const Entry& e = t->h_entries[s];
+    return (e.flags & EF_OCCUPIED) && e.vid == vid && (e.flags >> kTidShift) == tb;
+  };
+  uint32_t s = vid < t->vid_slot.size() ? t->vid_slot[vid] : UINT32_MAX;
+  if (s == UINT32_MAX || !holds(s)) {  // (a caller's ids shared between tables: the slow way)
+    s = UINT32_MAX;
+    for (uint32_t k = 0; k < (uint32_t)t->h_entries.size() && s == UINT32_MAX; k++)
+      if (holds(k)) s = k;
+    if (s == UINT32_MAX) return false;
+  }
+  const Entry& e = t->h_entries[s];
   const uint8_t* a = t->h_arena.data();
   if (e.flags & EF_RAWALT) {
     uint32_t rl;
@@ -116,26 +143,27 @@ bool value_str(const ie_table* t, uint32_t tb, uint32_t vid, std::string& out) {
 
 int interp(ie_exec* x, const ie_table* t, const Strs& in, Res& r) {
   const uint64_t n = in.size();
-  r.text.assign(n, std::string());
+  r.text.assign(n, std::string_view());
   r.st.assign(n, IE_OK_STR);
   r.vid.assign(n, IE_VID_NONE);
   if (!n) return IE_SUCCESS;
-  ie_batch* b = nullptr;
-  int rc = run_host(x, kOpInterp, t, in.bytes.data(), in.off.data(), n, &b, in.tid.data());
+  ie_batch_free(r.b);
+  r.b = nullptr;
+  int rc = run_host(x, kOpInterp, t, in.bytes.data(), in.off.data(), n, &r.b, in.tid.data());
   if (rc) return rc;
+  const ie_batch* b = r.b;
   for (uint64_t i = 0; i < n; i++) {
     r.st[i] = b->status[i];
     if (b->status[i] == IE_OK_STR) {
-      r.text[i].assign((const char*)b->bytes + b->offsets[i], b->offsets[i + 1] - b->offsets[i]);
+      r.text[i] = std::string_view((const char*)b->bytes + b->offsets[i], b->offsets[i + 1] - b->offsets[i]);
     } else if (b->status[i] == IE_OK_VALUE) {
       r.vid[i] = b->value_id[i];
-      if (!value_str(t, in.tid[i], b->value_id[i], r.text[i])) {
-        ie_batch_free(b);
+      r.owned.emplace_back();
+      if (!value_str(t, in.tid[i], b->value_id[i], r.owned.back()))
         return fail(IE_ERR_INVALID, "a typed result's value id is not in the table");
-      }
+      r.text[i] = r.owned.back();
     }
   }
-  ie_batch_free(b);
   return IE_SUCCESS;
 }
 
@@ -194,20 +222,26 @@ int match_first(ie_exec* x, const ie_table* t, const std::vector<std::string>& p
 // keys interpolate to the same texts share one block)
 struct Blocks {
   std::vector<std::string> pats;
-  std::unordered_map<std::string, std::pair<uint32_t, uint32_t>> seen;
+  std::unordered_multimap<uint64_t, std::pair<uint32_t, uint32_t>> seen;  // (hash of the list -> its block)
   std::pair<uint32_t, uint32_t> range(const std::vector<std::string>& keys, uint32_t upto) {
-    std::string sig;
+    uint64_t h = 0xcbf29ce484222325ull ^ upto;
     for (uint32_t j = 0; j < upto; j++) {
-      sig += keys[j];
-      sig.push_back('\0');
-      sig += std::to_string(keys[j].size());
-      sig.push_back('\1');
+      for (const char c : keys[j]) h = (h ^ (uint8_t)c) * 0x100000001b3ull;
+      h = (h ^ keys[j].size()) * 0x9E3779B97F4A7C15ull;
     }
-    auto it = seen.find(sig);
-    if (it != seen.end()) return it->second;
+    auto eq = seen.equal_range(h);
+    for (auto it = eq.first; it != eq.second; ++it) {
+      const auto rg = it->second;
+      if (rg.second - rg.first != upto) continue;
+      bool same = true;
+      for (uint32_t j = 0; j < upto && same; j++) same = pats[rg.first + j] == keys[j];
+      if (same) return rg;
+    }
     const uint32_t lo = (uint32_t)pats.size();
     for (uint32_t j = 0; j < upto; j++) pats.push_back(keys[j]);
-    return seen[sig] = {lo, (uint32_t)pats.size()};
+    const std::pair<uint32_t, uint32_t> rg{lo, (uint32_t)pats.size()};
+    seen.emplace(h, rg);
+    return rg;
   }
 };
 
@@ -252,6 +286,7 @@ std::string substitute(std::string_view v, const std::vector<std::string_view>& 
 ie_clock table_clock(const ie_table* t) {
   ie_clock c{0, 0, 0};
   for (uint32_t s : t->clock_slots) {
+    if (s == UINT32_MAX) continue;
     const Entry& e = t->h_entries[s];
     if (e.vid == IE_VID_CLOCK_HHMMSS && e.text_len == 8) {
       const char* p = (const char*)t->h_arena.data() + e.text_off;
@@ -369,7 +404,7 @@ int ie_goto_map(ie_exec* x, const ie_table* t, const char* text, uint64_t text_l
       uint32_t f = m;  // the first map whose key or value fails: the maps before it can match
       for (uint32_t j = 0; j < m && f == m; j++)
         if (!ok(r.st[b + 1 + j]) || !ok(r.st[b + 1 + m + j])) f = j;
-      for (uint32_t j = 0; j < f; j++) keys[j] = r.text[b + 1 + j];
+      for (uint32_t j = 0; j < f; j++) keys[j].assign(r.text[b + 1 + j]);
       const auto rg = blocks.range(keys, f);
       range.push_back(rg.first);
       range.push_back(rg.second);
@@ -396,7 +431,7 @@ int ie_goto_map(ie_exec* x, const ie_table* t, const char* text, uint64_t text_l
       if (ch[s] < 0) st[s] = IE_E_NO_NULL;
       continue;
     }
-    for (uint32_t j = 0; j < m; j++) keys[j] = r.text[b + 1 + j];
+    for (uint32_t j = 0; j < m; j++) keys[j].assign(r.text[b + 1 + j]);
     const auto rg = blocks.range(keys, m);
     range.push_back(rg.first);
     range.push_back(rg.second);
@@ -512,7 +547,7 @@ int ie_replace_map(ie_exec* x, const ie_table* t, const char* name, uint64_t nam
           key_st[s] = r.st[k];
           break;
         }
-        keys[s][j] = r.text[k];
+        keys[s][j].assign(r.text[k]);
       }
     }
     std::vector<uint64_t> alive;
@@ -522,15 +557,19 @@ int ie_replace_map(ie_exec* x, const ie_table* t, const char* name, uint64_t nam
         st[i] = r.st[q];  // (cur[i]: the string that failed)
         continue;
       }
-      cur[i] = r.text[q];
+      cur[i].assign(r.text[q]);
       alive.push_back(i);
     }
     // 2. the first map whose key matches (py:1725-1735), every leaf in one launch
     Blocks blocks;
     Strs mstr;
     std::vector<uint32_t> range;
+    std::unordered_map<uint32_t, std::pair<uint32_t, uint32_t>> rg_of;  // (a state's leaves share its block)
     for (uint64_t i : alive) {
-      const auto rg = blocks.range(keys[table_id[i]], key_ok[table_id[i]]);
+      const uint32_t s = table_id[i];
+      auto it = rg_of.find(s);
+      if (it == rg_of.end()) it = rg_of.emplace(s, blocks.range(keys[s], key_ok[s])).first;
+      const auto rg = it->second;
       range.push_back(rg.first);
       range.push_back(rg.second);
       mstr.add(cur[i], table_id[i]);
@@ -584,7 +623,7 @@ int ie_replace_map(ie_exec* x, const ie_table* t, const char* name, uint64_t nam
     for (size_t q = 0; q < vleaf.size(); q++) {
       const uint64_t i = vleaf[q];
       if (!ok(vr.st[q])) st[i] = vr.st[q], wh[i] = 1 + m + (uint32_t)ch[i];  // (cur[i]: the matched text)
-      else cur[i] = vr.text[q];
+      else cur[i].assign(vr.text[q]);
     }
     if (!slow_owner.empty()) {
       ie_table* xt = nullptr;
@@ -596,7 +635,7 @@ int ie_replace_map(ie_exec* x, const ie_table* t, const char* name, uint64_t nam
       for (size_t q = 0; q < slow_leaf.size(); q++) {
         const uint64_t i = slow_leaf[q];
         if (!ok(sr.st[q])) st[i] = sr.st[q], wh[i] = 1 + m + (uint32_t)ch[i];
-        else cur[i] = sr.text[q];
+        else cur[i].assign(sr.text[q]);
       }
       tr.mark("slow values", sin.size());
     }
@@ -610,6 +649,11 @@ int ie_replace_map(ie_exec* x, const ie_table* t, const char* name, uint64_t nam
     active.swap(next);
   }
   MapOut o;
+  {
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < n; i++) total += cur[i].size();
+    o.bytes.reserve(total);
+  }
   for (uint64_t i = 0; i < n; i++) o.push(cur[i], st[i], st[i] == IE_OK_STR ? 0u : wh[i], ch[i]);
   if (name) emit(nm, names);
   rc = emit(o, out);
