@@ -702,7 +702,7 @@ struct Patches {
     soff.resize(pf[nr]);
     len.resize(pf[nr]);
     data.resize(df[nr]);
-    parallel_for(nr, [&](uint64_t lo, uint64_t hi) {
+    parallel_for(nr, df[nr] - df[0], [&](uint64_t lo, uint64_t hi) {
       for (uint64_t k = lo; k < hi; k++) {
         uint64_t p = pf[k], d = df[k];
         for (uint64_t o = 0; o < r[k].len; o += 256, p++) {
@@ -789,7 +789,9 @@ void flush_copies(ie_table* t) {
   if (!t->defer || t->defer->empty()) return;
   std::vector<CopyJob>& jobs = *t->defer;
   uint8_t* const a = t->h_arena.data();
-  parallel_for(jobs.size(), [&](uint64_t lo, uint64_t hi) {
+  uint64_t bytes = 0;
+  for (const CopyJob& j : jobs) bytes += j.len;
+  parallel_for(jobs.size(), bytes, [&](uint64_t lo, uint64_t hi) {
     for (uint64_t k = lo; k < hi; k++) memcpy(a + jobs[k].dst, jobs[k].src, jobs[k].len);
   });
   jobs.clear();
@@ -882,7 +884,7 @@ void compact_arena(ie_table* t) {
   }
   na.grow(at);
   uint8_t* const dst = na.data();
-  parallel_for(jobs.size(), [&](uint64_t lo, uint64_t hi) {
+  parallel_for(jobs.size(), at, [&](uint64_t lo, uint64_t hi) {
     for (uint64_t k = lo; k < hi; k++) memcpy(dst + jobs[k].dst, jobs[k].src, jobs[k].len);
   });
   t->h_arena.swap(na);
@@ -1448,7 +1450,9 @@ static int table_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
   std::vector<uint32_t> tflags(n, 0);
   std::vector<uint64_t> khash(n);
   const uint64_t seed0 = seed;
-  parallel_for(n, [&](uint64_t lo, uint64_t hi) {
+  uint64_t in_bytes = 0;
+  for (uint64_t i = 0; i < n; i++) in_bytes += kv[i].key_len + (kv[i].kind >= 0 ? kv[i].text_len : 0) + 16;
+  parallel_for(n, in_bytes, [&](uint64_t lo, uint64_t hi) {
     for (uint64_t i = lo; i < hi; i++) {
       if (kv[i].kind >= 0) tflags[i] = text_flags(std::string_view(kv[i].text ? kv[i].text : "", kv[i].text_len));
       khash[i] = key_hash(std::string_view(kv[i].key ? kv[i].key : "", kv[i].key_len), seed0, table_id[i]);
@@ -1732,7 +1736,7 @@ static int table_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
   if (!whole_arena) {
     const std::vector<uint32_t> rs = rewritten.slots();
     std::vector<CopyJob> rr(rs.size());
-    parallel_for(rs.size(), [&](uint64_t lo, uint64_t hi) {
+    parallel_for(rs.size(), rs.size() * 256, [&](uint64_t lo, uint64_t hi) {
       for (uint64_t k = lo; k < hi; k++) {
         const Entry& e = t->h_entries[rs[k]];
         rr[k] = CopyJob{0, nullptr, 0};
@@ -2255,6 +2259,41 @@ int ie_wildcard_match_batch(ie_exec* x, const ie_wildcards* w, const uint8_t* by
   if (rc) return rc;
   if (n == 0) return IE_SUCCESS;
   const uint64_t base = offsets[0], nb = offsets[n] - base;
+  // a small batch (a map task over a few states): one pinned block each way, one synchronisation
+  // (as run_host_small): [offsets | ranges | bytes] in, [match | ncap | caps] out
+  const uint64_t i_rng = al256((n + 1) * 8), i_bytes = i_rng + al256(range ? n * 8 : 0),
+                 in_size = i_bytes + al256(nb + 64);
+  const uint64_t o_ncap = al256(n * 4), o_caps = o_ncap + al256(n), out_size = o_caps + al256(n * 8 * IE_WC_MAX_CAP);
+  if (in_size + out_size <= (4ull << 20)) {
+    const uint64_t need = in_size + out_size;
+    IE_HIP(x->sm_dev.ensure(std::max<uint64_t>(need, 1ull << 19)));
+    if (x->sm_host_bytes < need) {
+      if (x->sm_host) (void)hipHostFree(x->sm_host);
+      x->sm_host = nullptr;
+      x->sm_host_bytes = 0;
+      const uint64_t want = std::max<uint64_t>(need, 1ull << 19);
+      IE_HIP(hipHostMalloc((void**)&x->sm_host, want, hipHostMallocDefault));
+      x->sm_host_bytes = want;
+    }
+    uint8_t* const h = x->sm_host;
+    uint8_t* const dv = (uint8_t*)x->sm_dev.p;
+    uint64_t* const hoff = (uint64_t*)h;
+    for (uint64_t i = 0; i <= n; i++) hoff[i] = offsets[i] - base;
+    if (range) memcpy(h + i_rng, range, n * 8);
+    if (nb) memcpy(h + i_bytes, bytes + base, nb);
+    memset(h + i_bytes + nb, 0, 64);
+    IE_HIP(hipMemcpyAsync(dv, h, in_size, hipMemcpyHostToDevice, x->stream));
+    uint8_t* const dout = dv + in_size;
+    rc = ie_wildcard_match_device(x, w, dv + i_bytes, (const uint64_t*)dv, n, range ? (const uint32_t*)(dv + i_rng) : nullptr,
+                                  (int32_t*)dout, dout + o_ncap, (uint32_t*)(dout + o_caps));
+    if (rc) return rc;
+    IE_HIP(hipMemcpyAsync(h + in_size, dout, out_size, hipMemcpyDeviceToHost, x->stream));
+    IE_HIP(hipStreamSynchronize(x->stream));
+    memcpy(match, h + in_size, n * 4);
+    memcpy(ncap, h + in_size + o_ncap, n);
+    memcpy(caps, h + in_size + o_caps, n * 8 * IE_WC_MAX_CAP);
+    return IE_SUCCESS;
+  }
   std::vector<uint64_t> off(offsets, offsets + n + 1);
   for (auto& o : off) o -= base;
   IE_HIP(x->in_bytes.ensure(nb + 16));

@@ -75,7 +75,7 @@ struct Trace {
 };
 
 // fn(lo, hi) over [0, n) split across up to IE_HOST_THREADS host threads (default: the cores, at
-// most 8): the table mirror's bulk byte work (text scans, text copies, compaction)
+// most 8): the table mirror's bulk byte work (text scans, text copies, compaction, patches)
 inline unsigned host_threads() {
   static const unsigned n = [] {
     const char* e = getenv("IE_HOST_THREADS");
@@ -84,9 +84,11 @@ inline unsigned host_threads() {
   }();
   return n;
 }
+// (`bytes`: about how much memory the whole loop touches; a thread per 256 KB at most, so a scalar
+// caller's few stores never pay a thread start)
 template <class F>
-void parallel_for(uint64_t n, F&& fn) {
-  const unsigned T = (unsigned)std::min<uint64_t>(host_threads(), n);
+void parallel_for(uint64_t n, uint64_t bytes, F&& fn) {
+  const unsigned T = (unsigned)std::min<uint64_t>(std::min<uint64_t>(host_threads(), n), bytes >> 18);
   if (T <= 1) {
     fn((uint64_t)0, n);
     return;

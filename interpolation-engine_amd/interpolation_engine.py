@@ -728,6 +728,8 @@ def get_simple_insertkey(content):
             if c == insert_start:
                 depth += 1
         return content[1:-1]
+    if content[0] != insert_start or content[-1] != insert_stop:  # (the loop fails at once, py:487-492)
+        return None
     b = N.enc(content)
     o, l = ctypes.c_uint64(), ctypes.c_uint64()
     if N.lib().ie_simple_insertkey(b, len(b), 0, ctypes.byref(o), ctypes.byref(l)):

@@ -535,21 +535,33 @@ def replace_map_states(states, task, dialect="py", device=0, tables=None):
     finally:
         if tables is None:
             tset.close()
+    # the failed values' exceptions: each value against its state | its captures, all in one table
+    # set and one batch (the captures: every failed leaf's text against its interpolated key, one
+    # k_wildcard launch)
     verr = {}
-    for i in vfail:
-        b, st, w, ch, _ = rows[i]
-        s = owner[i]
-        key = kgot[(s, pairs[w - 1 - m][0])]
-        caps = []
-        if not isinstance(key, BaseException):
-            from .wildcard import get_wildcard_matches
-            caps = get_wildcard_matches(key, IE.N.dec(b))
-        full = dict(states[s], **{str(k + 1): c for k, c in enumerate(caps)})
-        xs = IE.InsertsTableSet([full], dialect=dialect, device=device)
+    if vfail:
+        from .wildcard import Wildcards
+        keys_v = [kgot[(owner[i], pairs[rows[i][2] - 1 - m][0])] for i in vfail]
+        texts_v = [IE.N.dec(rows[i][0]) for i in vfail]
+        ok_q = [q for q, k in enumerate(keys_v) if not isinstance(k, BaseException)]
+        caps_v = [[] for _ in vfail]
+        if ok_q:
+            pats = list(dict.fromkeys(keys_v[q] for q in ok_q))
+            at = {p: j for j, p in enumerate(pats)}
+            wl = Wildcards(pats, device=device, dialect=dialect)
+            try:
+                got = wl.first_match([texts_v[q] for q in ok_q], [(at[keys_v[q]], at[keys_v[q]] + 1) for q in ok_q])
+            finally:
+                wl.close()
+            for q, (mi, cs) in zip(ok_q, got):
+                caps_v[q] = cs if mi >= 0 else []
+        fulls = [dict(states[owner[i]], **{str(k + 1): c for k, c in enumerate(caps_v[q])}) for q, i in enumerate(vfail)]
+        xs = IE.InsertsTableSet(fulls, dialect=dialect, device=device)
         try:
-            verr[i] = xs.results([pairs[w - 1 - m][1]], [0])[0]
+            got = xs.results([pairs[rows[i][2] - 1 - m][1] for i in vfail], list(range(len(vfail))))
         finally:
             xs.close()
+        verr = dict(zip(vfail, got))
     no_value = object()
     value_if_error = ([v for k, v in pairs if k == "NULL"] + [no_value])[0]  # py:1761
     label = task.get("traceback_label")
