@@ -205,6 +205,85 @@ static int utf8_of(PyObject* s, jobs_t* J, uint64_t rec, const char** p, uint64_
 
 static void free_buf(PyObject* cap) { PyMem_RawFree(PyCapsule_GetPointer(cap, "ie_pack.buf")); }
 
+// one record: key k, value v (the delete marker: kind -1); 0, or -1 with the Python error set
+static int pack_kv(PyObject* k, PyObject* v, kv_rec* r, uint64_t i, jobs_t* J, PyObject* keep, PyObject* del,
+                   PyObject* render, PyObject* dialect) {
+  if (!PyUnicode_Check(k)) {
+    PyErr_SetString(PyExc_TypeError, "insert keys must be str");
+    return -1;
+  }
+  memset(r, 0, sizeof *r);
+  if (utf8_of(k, J, 2 * i, &r->key, &r->key_len) < 0) return -1;
+  if (v == del) {
+    r->kind = -1;
+    return 0;
+  }
+  PyObject* text = NULL;
+  if (PyUnicode_CheckExact(v)) {
+    r->kind = KIND_STR;
+    text = v;
+  } else if (PyLong_CheckExact(v)) {
+    r->kind = KIND_INT;
+    text = PyObject_Str(v);
+    if (!text || PyList_Append(keep, text) < 0) {
+      Py_XDECREF(text);
+      return -1;
+    }
+    Py_DECREF(text);
+  } else {
+    PyObject* kt = PyObject_CallFunctionObjArgs(render, v, dialect, NULL);  // (kind, text)
+    if (!kt) return -1;
+    if (PyList_Append(keep, kt) < 0) {
+      Py_DECREF(kt);
+      return -1;
+    }
+    Py_DECREF(kt);
+    if (!PyTuple_Check(kt) || PyTuple_GET_SIZE(kt) != 2 || !PyUnicode_Check(PyTuple_GET_ITEM(kt, 1))) {
+      PyErr_SetString(PyExc_TypeError, "render must return (kind, str)");
+      return -1;
+    }
+    r->kind = (int32_t)PyLong_AsLong(PyTuple_GET_ITEM(kt, 0));
+    if (r->kind == -1 && PyErr_Occurred()) return -1;
+    text = PyTuple_GET_ITEM(kt, 1);
+  }
+  return utf8_of(text, J, 2 * i + 1, &r->text, &r->text_len);
+}
+
+// the texts that are not ASCII: counted, placed, transcoded (across the threads, the GIL released);
+// then the records point there and `keep` holds the buffer
+static int finish(kv_rec* kv, jobs_t* J, PyObject* keep, int threads) {
+  if (!J->n) return 0;
+  uint64_t total = 0;
+  Py_BEGIN_ALLOW_THREADS
+  run_jobs(J->p, J->n, NULL, threads);
+  Py_END_ALLOW_THREADS
+  for (uint64_t k = 0; k < J->n; k++) {
+    J->p[k].off = total;
+    total += J->p[k].out;
+  }
+  uint8_t* buf = (uint8_t*)PyMem_RawMalloc(total + 16);
+  if (!buf) {
+    PyErr_NoMemory();
+    return -1;
+  }
+  Py_BEGIN_ALLOW_THREADS
+  run_jobs(J->p, J->n, buf, threads);
+  Py_END_ALLOW_THREADS
+  for (uint64_t k = 0; k < J->n; k++) {
+    kv_rec* r = &kv[J->p[k].rec / 2];
+    if (J->p[k].rec & 1) r->text = (const char*)buf + J->p[k].off, r->text_len = J->p[k].out;
+    else r->key = (const char*)buf + J->p[k].off, r->key_len = J->p[k].out;
+  }
+  PyObject* cap = PyCapsule_New(buf, "ie_pack.buf", free_buf);
+  if (!cap) {
+    PyMem_RawFree(buf);
+    return -1;
+  }
+  const int rc = PyList_Append(keep, cap);
+  Py_DECREF(cap);
+  return rc;
+}
+
 // pack(changes, n_tables, delete, render, dialect, threads) -> (kv: bytearray, table_ids: bytearray,
 // keep) (keep: what the records point into besides the changes' own strs; alive until the call)
 static PyObject* pack(PyObject* self, PyObject* args) {
@@ -220,7 +299,6 @@ static PyObject* pack(PyObject* self, PyObject* args) {
   PyObject* tidb = PyByteArray_FromStringAndSize(NULL, (Py_ssize_t)(n * 4));
   PyObject* keep = PyList_New(0);
   jobs_t J = {NULL, 0, 0};
-  uint8_t* buf = NULL;
   if (!kvb || !tidb || !keep) goto fail;
   kv_rec* kv = (kv_rec*)PyByteArray_AS_STRING(kvb);
   uint32_t* tid = (uint32_t*)PyByteArray_AS_STRING(tidb);
@@ -230,10 +308,9 @@ static PyObject* pack(PyObject* self, PyObject* args) {
       PyErr_SetString(PyExc_TypeError, "a change is a (dict index, key, value) tuple");
       goto fail;
     }
-    PyObject *t = PyTuple_GET_ITEM(c, 0), *k = PyTuple_GET_ITEM(c, 1), *v = PyTuple_GET_ITEM(c, 2);
-    const long long tb = PyLong_AsLongLong(t);
+    const long long tb = PyLong_AsLongLong(PyTuple_GET_ITEM(c, 0));
     if (tb == -1 && PyErr_Occurred()) goto fail;
-    if (!PyUnicode_Check(k)) {
+    if (!PyUnicode_Check(PyTuple_GET_ITEM(c, 1))) {
       PyErr_SetString(PyExc_TypeError, "insert keys must be str");
       goto fail;
     }
@@ -242,83 +319,74 @@ static PyObject* pack(PyObject* self, PyObject* args) {
       goto fail;
     }
     tid[i] = (uint32_t)tb;
-    kv_rec* r = &kv[i];
-    memset(r, 0, sizeof *r);
-    if (utf8_of(k, &J, 2 * (uint64_t)i, &r->key, &r->key_len) < 0) goto fail;
-    if (v == del) {
-      r->kind = -1;
-      continue;
-    }
-    PyObject* text = NULL;
-    if (PyUnicode_CheckExact(v)) {
-      r->kind = KIND_STR;
-      text = v;
-    } else if (PyLong_CheckExact(v)) {
-      r->kind = KIND_INT;
-      text = PyObject_Str(v);
-      if (!text || PyList_Append(keep, text) < 0) {
-        Py_XDECREF(text);
-        goto fail;
-      }
-      Py_DECREF(text);
-    } else {
-      PyObject* kt = PyObject_CallFunctionObjArgs(render, v, dialect, NULL);  // (kind, text)
-      if (!kt) goto fail;
-      if (PyList_Append(keep, kt) < 0) {
-        Py_DECREF(kt);
-        goto fail;
-      }
-      Py_DECREF(kt);
-      if (!PyTuple_Check(kt) || PyTuple_GET_SIZE(kt) != 2 || !PyUnicode_Check(PyTuple_GET_ITEM(kt, 1))) {
-        PyErr_SetString(PyExc_TypeError, "render must return (kind, str)");
-        goto fail;
-      }
-      r->kind = (int32_t)PyLong_AsLong(PyTuple_GET_ITEM(kt, 0));
-      if (r->kind == -1 && PyErr_Occurred()) goto fail;
-      text = PyTuple_GET_ITEM(kt, 1);
-    }
-    if (utf8_of(text, &J, 2 * (uint64_t)i + 1, &r->text, &r->text_len) < 0) goto fail;
-  }
-  if (J.n) {  // the texts that are not ASCII: count, place, transcode; then the records point there
-    uint64_t total = 0;
-    Py_BEGIN_ALLOW_THREADS
-    run_jobs(J.p, J.n, NULL, threads);
-    Py_END_ALLOW_THREADS
-    for (uint64_t k = 0; k < J.n; k++) {
-      J.p[k].off = total;
-      total += J.p[k].out;
-    }
-    buf = (uint8_t*)PyMem_RawMalloc(total + 16);
-    if (!buf) {
-      PyErr_NoMemory();
+    if (pack_kv(PyTuple_GET_ITEM(c, 1), PyTuple_GET_ITEM(c, 2), &kv[i], (uint64_t)i, &J, keep, del, render, dialect) < 0)
       goto fail;
-    }
-    Py_BEGIN_ALLOW_THREADS
-    run_jobs(J.p, J.n, buf, threads);
-    Py_END_ALLOW_THREADS
-    for (uint64_t k = 0; k < J.n; k++) {
-      kv_rec* r = &kv[J.p[k].rec / 2];
-      if (J.p[k].rec & 1) r->text = (const char*)buf + J.p[k].off, r->text_len = J.p[k].out;
-      else r->key = (const char*)buf + J.p[k].off, r->key_len = J.p[k].out;
-    }
-    PyObject* cap = PyCapsule_New(buf, "ie_pack.buf", free_buf);
-    if (!cap) goto fail;
-    buf = NULL;  // (the capsule owns it)
-    if (PyList_Append(keep, cap) < 0) {
-      Py_DECREF(cap);
-      goto fail;
-    }
-    Py_DECREF(cap);
   }
+  if (finish(kv, &J, keep, threads) < 0) goto fail;
   PyMem_RawFree(J.p);
   Py_DECREF(seq);
   return Py_BuildValue("(NNN)", kvb, tidb, keep);
 fail:
   PyMem_RawFree(J.p);
-  PyMem_RawFree(buf);
   Py_DECREF(seq);
   Py_XDECREF(kvb);
   Py_XDECREF(tidb);
+  Py_XDECREF(keep);
+  return NULL;
+}
+
+// pack_dicts(dicts, render, dialect, threads) -> (kv: bytearray, kv_start: bytearray (n+1 u64), keep):
+// every dict's items in order (a table set's build, ie_table_set_build; kv i gets value id i)
+static PyObject* pack_dicts(PyObject* self, PyObject* args) {
+  (void)self;
+  PyObject *dicts, *render, *dialect;
+  int threads = 1;
+  if (!PyArg_ParseTuple(args, "OOO|i", &dicts, &render, &dialect, &threads)) return NULL;
+  PyObject* seq = PySequence_Fast(dicts, "dicts must be a sequence");
+  if (!seq) return NULL;
+  const Py_ssize_t nd = PySequence_Fast_GET_SIZE(seq);
+  Py_ssize_t n = 0;
+  for (Py_ssize_t t = 0; t < nd; t++) {
+    PyObject* d = PySequence_Fast_GET_ITEM(seq, t);
+    if (!PyDict_Check(d)) {
+      Py_DECREF(seq);
+      PyErr_SetString(PyExc_TypeError, "a table set is built from dicts");
+      return NULL;
+    }
+    n += PyDict_GET_SIZE(d);
+  }
+  PyObject* kvb = PyByteArray_FromStringAndSize(NULL, (Py_ssize_t)((n ? n : 1) * sizeof(kv_rec)));
+  PyObject* stb = PyByteArray_FromStringAndSize(NULL, (Py_ssize_t)((nd + 1) * 8));
+  PyObject* keep = PyList_New(0);
+  jobs_t J = {NULL, 0, 0};
+  if (!kvb || !stb || !keep) goto fail;
+  kv_rec* kv = (kv_rec*)PyByteArray_AS_STRING(kvb);
+  uint64_t* st = (uint64_t*)PyByteArray_AS_STRING(stb);
+  Py_ssize_t i = 0;
+  st[0] = 0;
+  for (Py_ssize_t t = 0; t < nd; t++) {
+    PyObject* d = PySequence_Fast_GET_ITEM(seq, t);
+    Py_ssize_t pos = 0;
+    PyObject *k, *v;
+    while (PyDict_Next(d, &pos, &k, &v)) {
+      if (i >= n) {
+        PyErr_SetString(PyExc_RuntimeError, "a dict changed size while packing");
+        goto fail;
+      }
+      if (pack_kv(k, v, &kv[i], (uint64_t)i, &J, keep, NULL, render, dialect) < 0) goto fail;
+      i++;
+    }
+    st[t + 1] = (uint64_t)i;
+  }
+  if (finish(kv, &J, keep, threads) < 0) goto fail;
+  PyMem_RawFree(J.p);
+  Py_DECREF(seq);
+  return Py_BuildValue("(NNN)", kvb, stb, keep);
+fail:
+  PyMem_RawFree(J.p);
+  Py_DECREF(seq);
+  Py_XDECREF(kvb);
+  Py_XDECREF(stb);
   Py_XDECREF(keep);
   return NULL;
 }
@@ -363,6 +431,7 @@ fail:
 static PyMethodDef methods[] = {
     {"pack", pack, METH_VARARGS, "changes -> (ie_kv records, table ids, keep-alive list)"},
     {"assign", assign, METH_VARARGS, "store the values under the ids the library handed out"},
+    {"pack_dicts", pack_dicts, METH_VARARGS, "dicts -> (ie_kv records, kv_start, keep-alive list)"},
     {NULL, NULL, 0, NULL},
 };
 

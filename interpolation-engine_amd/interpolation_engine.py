@@ -116,41 +116,21 @@ class InsertsTableSet:
             self.values.extend(d.values())
             starts.append(len(self.keys))
         self.starts = starts
-        n = len(self.keys)
-        # the ie_kv array as one numpy record array over two byte blobs (keys, splice texts): a
-        # table set of many states holds ~10^5 entries, and one ctypes struct per entry costs more
-        # than the device build
-        import numpy as np
-        texts, kinds = [None] * n, np.empty(max(1, n), np.int32)
-        for i, v in enumerate(self.values):
-            if type(v) is str:
-                texts[i], kinds[i] = v, N.KIND_STR
-            else:
-                kinds[i], texts[i] = render(v, dialect)
-        for k in self.keys:
-            if type(k) is not str:
-                raise TypeError("insert keys must be str")
-        kb = [N.enc(k) for k in self.keys]
-        tb = [N.enc(t) for t in texts]
-        kblob, tblob = np.frombuffer(b"".join(kb) + b"\0", np.uint8), np.frombuffer(b"".join(tb) + b"\0", np.uint8)
-        klen = np.fromiter(map(len, kb), np.uint64, n)
-        tlen = np.fromiter(map(len, tb), np.uint64, n)
-        arr = np.zeros(max(1, n), dtype=[("key", "<u8"), ("key_len", "<u8"), ("text", "<u8"), ("text_len", "<u8"),
-                                         ("kind", "<i4"), ("reserved", "<u4")])
-        if n:
-            arr["key"][:n] = kblob.ctypes.data + np.concatenate(([0], np.cumsum(klen)[:-1])).astype(np.uint64)
-            arr["key_len"][:n] = klen
-            arr["text"][:n] = tblob.ctypes.data + np.concatenate(([0], np.cumsum(tlen)[:-1])).astype(np.uint64)
-            arr["text_len"][:n] = tlen
-            arr["kind"][:n] = kinds[:n]
+        # the ie_kv records of every dict in one native pass (csrc/ie_pack.c: pointers into the
+        # str objects, the texts that are not ASCII transcoded across host threads): a table set of
+        # many states holds ~10^5 entries
+        kvb, stb, keep = N.pack_module().pack_dicts([d if isinstance(d, dict) else dict(d) for d in self.dicts],
+                                                     render, dialect, N.host_threads())
+        cb = ctypes.c_char * len(kvb)
         h = ctypes.c_void_p()
         clk = N.Clock(*self.clock)
-        st = (ctypes.c_uint64 * len(starts))(*starts)
-        N.check(N.lib().ie_table_set_build(ctypes.c_void_p(arr.ctypes.data), st, len(self.dicts),
+        st = (ctypes.c_char * len(stb)).from_buffer(stb)
+        N.check(N.lib().ie_table_set_build(cb.from_buffer(kvb), st, len(self.dicts),
                                            N.IE_DIALECT[dialect], ctypes.byref(clk),
                                            (N.TABLE_HAS_INSERTS_DIR if has_inserts_dir else 0) |
                                            (N.TABLE_MUTABLE if mutable else 0), device,
                                            ctypes.byref(h)), "ie_table_set_build")
+        del keep  # (the records pointed into these until the build returned)
         self.h = h
 
     def close(self):
