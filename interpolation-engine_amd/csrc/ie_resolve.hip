@@ -37,6 +37,11 @@
 #ifndef IE_WAVES_PER_EU
 #define IE_WAVES_PER_EU 4
 #endif
+// the long-key instances (17-32 byte keys, TF_LONG_KEYS; config 5): their key assembly does not fit
+// 128 VGPRs (7 dwords spilled per lane at 4 waves: ~40 MB of scratch writes per config-5 launch)
+#ifndef IE_WAVES_PER_EU_LK
+#define IE_WAVES_PER_EU_LK 4
+#endif
 
 #ifndef IE_RNS
 #define IE_RNS r256
@@ -437,10 +442,21 @@ constexpr uint32_t kResWhole = 1u << 27;  // a whole-string '{key}' (res_s: the 
 // inserts-dir or an unspliceable hit, recorded with its pair's opening offset) or at anything the
 // exact evaluator must decide (kResReject: a long key or text, a non-inert value, a failure when
 // !FAILC, a miss an inserts-dir might resolve).
+// chain jobs per lane and round: two (their lookups overlap); the long-key instances one: their
+// 32-byte key assembly does not fit two jobs in 128 VGPRs (two spilled 7 dwords per lane, 45-76 MB
+// of scratch writes per config-5 launch, WRITE_SIZE 1.57-1.95x algorithmic; one job: 1.02x and
+// 0.226 -> 0.218 ms, profiles/r05/ab/lk_jobs.txt); at 3 waves per SIMD two jobs fit without a spill
+// but run 0.278 ms
+#ifndef IE_LK_JOBS
+#define IE_LK_JOBS 1
+#endif
+template <bool LK>
+constexpr int kJobsPerLane = LK ? IE_LK_JOBS : 2;
+
 template <bool FAILC, bool LK>
 __device__ void resolve_jobs(const DevTable& T, const lds_u8* tile, const ChainJobs J, uint32_t j0, uint32_t njobs,
                              bool& chain_fail, uint64_t* stamp) {
-  constexpr int NJ = 2;
+  constexpr int NJ = kJobsPerLane<LK>;
   const uint32_t tid = threadIdx.x;
   bool on[NJ], done[NJ], wh[NJ];
   uint32_t job[NJ], cr[NJ], dep[NJ], ls[NJ], tb[NJ], res_k[NJ], res_s[NJ];
@@ -1119,7 +1135,7 @@ __global__ __launch_bounds__(kRBlock) void k_emit_windows(Batch B0, Work W, DevT
 // classified again) and then resolved; strings that cannot be finished there (not staged, or
 // needing the literal path) go to W.udefer_list for the deferred pass.
 template <bool FAILC, bool MULTI, bool VIEWS, bool UNESC = false, bool LK = false, bool LEAN = false>
-__global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVES_PER_EU))) void k_resolve(Batch B0, Work W, DevTable T, uint8_t* out,
+__global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(LK ? IE_WAVES_PER_EU_LK : IE_WAVES_PER_EU))) void k_resolve(Batch B0, Work W, DevTable T, uint8_t* out,
                                                     uint64_t cap) {
   // a deferred subset counts its strings on the device (the grid is sized for B0.n)
   Batch B = B0;
@@ -1333,7 +1349,7 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(IE_WAVE
       J.tbl[tid] = tid_s;
       __syncthreads();
       IE_STAMP(9);
-      for (uint32_t j0 = 0; j0 < njobs; j0 += 2 * kRBlock) resolve_jobs<FAILC, LK>(T, (const lds_u8*)s_in, J, j0, njobs, chain_fail, j0 == 0 ? stamp_row : nullptr);
+      for (uint32_t j0 = 0; j0 < njobs; j0 += kJobsPerLane<LK> * kRBlock) resolve_jobs<FAILC, LK>(T, (const lds_u8*)s_in, J, j0, njobs, chain_fail, j0 == 0 ? stamp_row : nullptr);
       IE_STAMP(10);
       __syncthreads();
       IE_STAMP(11);

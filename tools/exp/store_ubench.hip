@@ -3,7 +3,8 @@
 // counterpart is gather_ubench.hip):
 //   k_st<W>         coalesced W-byte stores, lane i at dst + i*W (W = 16, 8, 4, 2, 1): the per-string
 //                   offset (8), length / value id (4) and status (1) arrays, the 16-B stream-out
-//   k_st_nt<16>     the same 16-B stores, non-temporal
+//   k_st_nt<W>      the same stores, non-temporal (k_resolve's gst4s / gsts)
+//   k_st_half<4>    every other lane stores (a predicated per-string store)
 //   k_st_line<W>    one W-byte store per 64-B line (lane i at dst + i*64): partial-line writes
 //   k_st_run<W,R>   each lane writes R consecutive W-byte elements of its own (a per-string record
 //                   laid out lane-major: lanes write 64 R W apart)
@@ -70,6 +71,20 @@ __global__ __launch_bounds__(256) void k_st_nt16(uint8_t* dst, uint64_t n) {
 }
 
 template <int W>
+__global__ __launch_bounds__(256) void k_st_nt(uint8_t* dst, uint64_t n) {  // narrow non-temporal (gsts)
+  typedef typename Elem<W>::T T;
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+    __builtin_nontemporal_store(val<W>(i), (T*)dst + i);
+}
+
+template <int W>
+__global__ __launch_bounds__(256) void k_st_half(uint8_t* dst, uint64_t n) {  // every other lane stores
+  typedef typename Elem<W>::T T;
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+    if (i & 1) ((T*)dst)[i] = val<W>(i);
+}
+
+template <int W>
 __global__ __launch_bounds__(256) void k_st_line(uint8_t* dst, uint64_t n) {
   typedef typename Elem<W>::T T;
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
@@ -118,6 +133,10 @@ int main() {
     if (run("k_st_line<8>", [&] { k_st_line<8><<<grid, block>>>(dst, nl); }, nl * 8, nl * 64)) return 1;
     if (run("k_st_line<4>", [&] { k_st_line<4><<<grid, block>>>(dst, nl); }, nl * 4, nl * 64)) return 1;
     if (run("k_st_line<1>", [&] { k_st_line<1><<<grid, block>>>(dst, nl); }, nl, nl * 64)) return 1;
+    if (run("k_st_nt<8>", [&] { k_st_nt<8><<<grid, block>>>(dst, bytes / 8); }, bytes, bytes)) return 1;
+    if (run("k_st_nt<4>", [&] { k_st_nt<4><<<grid, block>>>(dst, bytes / 4); }, bytes, bytes)) return 1;
+    if (run("k_st_nt<1>", [&] { k_st_nt<1><<<grid, block>>>(dst, bytes); }, bytes, bytes)) return 1;
+    if (run("k_st_half<4>", [&] { k_st_half<4><<<grid, block>>>(dst, bytes / 4); }, bytes / 2, bytes)) return 1;
     if (run("k_st_run<8,2>", [&] { k_st_run<8, 2><<<grid, block>>>(dst, bytes / 16); }, bytes, bytes)) return 1;
     if (run("k_st_run<4,4>", [&] { k_st_run<4, 4><<<grid, block>>>(dst, bytes / 16); }, bytes, bytes)) return 1;
   }
