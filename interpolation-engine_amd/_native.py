@@ -215,10 +215,16 @@ def check(rc, what):
 _pack = None
 
 
+_host_threads = None
+
+
 def host_threads():
-    """Threads for the host-side byte work (IE_HOST_THREADS, else the cores, at most 8)."""
-    v = int(os.environ.get("IE_HOST_THREADS", "0") or 0)
-    return v if v > 0 else max(1, min(8, os.cpu_count() or 1))
+    """Threads for the host-side byte work (IE_HOST_THREADS, else the cores, at most 8; read once)."""
+    global _host_threads
+    if _host_threads is None:
+        v = int(os.environ.get("IE_HOST_THREADS", "0") or 0)
+        _host_threads = v if v > 0 else max(1, min(8, os.cpu_count() or 1))
+    return _host_threads
 
 
 def pack_module():
@@ -342,6 +348,13 @@ def batch_to_python(res_ptr):
     """Copy an ie_batch into Python: (list[bytes], list[int status], list[int vid])."""
     r = res_ptr.contents
     n = r.n
+    if n <= 16:  # (a scalar call: no numpy views, a few ctypes reads)
+        o = [r.offsets[i] for i in range(n + 1)] if n else [0]
+        blob = ctypes.string_at(r.bytes, r.bytes_len) if r.bytes_len else b""
+        st = [r.status[i] for i in range(n)]
+        vid = [r.value_id[i] for i in range(n)]
+        lib().ie_batch_free(res_ptr)
+        return [blob[o[i]:o[i + 1]] for i in range(n)], st, vid
     import numpy as np
     offs = np.ctypeslib.as_array(r.offsets, shape=(n + 1,)).copy() if n else np.zeros(1, np.uint64)
     st = np.ctypeslib.as_array(r.status, shape=(n,)).copy() if n else np.zeros(0, np.uint8)

@@ -260,6 +260,11 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
   int rc = set_device(x->device);
   if (rc) return rc;
   if (n > 0xFFFFFFF0ull) return fail(IE_ERR_INVALID, "batch larger than 2^32 strings");
+  if (op == kOpInterp && t->patch_pending.load(std::memory_order_acquire)) {  // (an update's patch kernel)
+    ie_table* tm = const_cast<ie_table*>(t);
+    if (hipEventQuery(t->patched) == hipSuccess) tm->patch_pending.store(false, std::memory_order_relaxed);
+    else IE_HIP(hipStreamWaitEvent(x->stream, t->patched, 0));
+  }
   rc = ensure_work(x, op, n);
   if (rc) return rc;
   x->stamp_tiles = 0;
@@ -724,7 +729,17 @@ struct Patches {
   }
 };
 
-int apply_patches(DevBuf& staging, const Patches& P) {
+// after the patch kernel: an event the table's next batches wait on (run_device), no device-wide
+// synchronisation (the next update or clock set synchronises the device first anyway)
+int patched_event(ie_table* t) {
+  if (!t->patched) IE_HIP(hipEventCreateWithFlags(&t->patched, hipEventDisableTiming));
+  IE_HIP(hipEventRecord(t->patched, nullptr));
+  t->patch_pending.store(true, std::memory_order_release);
+  return IE_SUCCESS;
+}
+
+int apply_patches(ie_table* t, const Patches& P) {
+  DevBuf& staging = t->patch_staging;
   const uint64_t n = P.dst.size();
   if (!n) return IE_SUCCESS;
   if (P.data.size() >= (1ull << 32)) return fail(IE_ERR_INVALID, "patch set above 4 GiB");
@@ -739,9 +754,8 @@ int apply_patches(DevBuf& staging, const Patches& P) {
         memcpy(a.data[a.n], P.data.data() + P.soff[k] + o, a.len[a.n]);
       }
     hipError_t e = launch_patch_inline(a, nullptr);
-    if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) return fail(IE_ERR_HIP, std::string("table patch: ") + hipGetErrorString(e));
-    return IE_SUCCESS;
+    return patched_event(t);
   }
   const uint64_t o_dst = (P.data.size() + 15) & ~15ull, o_soff = o_dst + 8 * n, o_len = o_soff + 4 * n;
   std::vector<uint8_t> blob(o_len + 4 * n);
@@ -755,9 +769,8 @@ int apply_patches(DevBuf& staging, const Patches& P) {
   if (e == hipSuccess)
     e = launch_patch(base, (const uint64_t*)(base + o_dst), (const uint32_t*)(base + o_soff),
                      (const uint32_t*)(base + o_len), (uint32_t)n, nullptr);
-  if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) return fail(IE_ERR_HIP, std::string("table patch: ") + hipGetErrorString(e));
-  return IE_SUCCESS;
+  return patched_event(t);
 }
 
 extern "C++" {
@@ -1358,7 +1371,7 @@ int ie_table_set_clock(ie_table* t, const ie_clock* now) {
     pe.add((Entry*)t->entries.p + slot, &e, sizeof(Entry));
     pe.add((uint8_t*)t->arena.p + e.text_off, txt, e.text_len);
   }
-  return apply_patches(t->patch_staging, pe);
+  return apply_patches(t, pe);
 }
 
 // set_interpdata on a built table (set): py:470-471 `inserts[key] = value` (and `del`) on state
@@ -1770,7 +1783,7 @@ static int table_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
     for (uint32_t g : dirty_groups) pe.add((uint16_t*)t->pilots.p + g, &t->h_pilots[g], sizeof(uint16_t));
   }
   tr.mark("patch build", pe.data.size());
-  if ((rc = apply_patches(t->patch_staging, pe))) return rc;
+  if ((rc = apply_patches(t, pe))) return rc;
   tr.mark("patch apply", pe.dst.size());
   t->dev.n_entries = (uint32_t)t->n_entries;
   if (t->vid_ok) {  // the value ids of the changed slots (a stale one is caught on use)

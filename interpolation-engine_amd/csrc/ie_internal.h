@@ -10,6 +10,7 @@
 #include <sys/mman.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <new>
 
@@ -218,7 +219,12 @@ struct ie_table {
   bool occ_ok = false;
   std::unordered_map<uint32_t, std::vector<uint32_t>> rawalt;
   DevBuf patch_staging;  // ie_table_set_update / _set_clock uploads
+  // the last patch kernel (null stream) of an update: batches wait for it on their own stream
+  // (run_device) instead of the update synchronising the device after it
+  hipEvent_t patched = nullptr;
+  std::atomic<bool> patch_pending{false};
   ~ie_table() {
+    if (patched) (void)hipEventDestroy(patched);
     entries.release();
     pilots.release();
     arena.release();

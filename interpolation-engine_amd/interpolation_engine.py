@@ -204,9 +204,16 @@ class InsertsTableSet:
         """Resolve a list of str on the device -> list of (status, payload); string i against dict
         table_ids[i] (all against dict 0 when table_ids is None); exec_: the caller's ie_exec
         (one per host thread), else this device's shared one."""
-        blob, offs = N.pack(strings)
         x = exec_ or get_exec(self.device)
         res = ctypes.POINTER(N.BatchRes)()
+        if table_ids is None and len(strings) == 1 and type(strings[0]) is str:
+            # a scalar call (interpolate_inserts): the string's bytes and two offsets, no numpy
+            b = N.enc(strings[0])
+            offs1 = (ctypes.c_uint64 * 2)(0, len(b))
+            N.check(N.lib().ie_interpolate_batch(x.h, self.h, b, offs1, 1, ctypes.byref(res)), "ie_interpolate_batch")
+            outs, sts, vids = N.batch_to_python(res)
+            return [(sts[0], N.dec(outs[0]) if sts[0] == N.OK_STR else (vids[0] if sts[0] == N.OK_VALUE else None))]
+        blob, offs = N.pack(strings)
         bp = ctypes.c_char_p(blob)
         if table_ids is None:
             N.check(N.lib().ie_interpolate_batch(x.h, self.h, ctypes.cast(bp, ctypes.c_void_p),
