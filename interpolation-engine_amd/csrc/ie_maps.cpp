@@ -149,17 +149,39 @@ int interp(ie_exec* x, const ie_table* t, const Strs& in, Res& r) {
   if (!n) return IE_SUCCESS;
   ie_batch_free(r.b);
   r.b = nullptr;
-  int rc = run_host(x, kOpInterp, t, in.bytes.data(), in.off.data(), n, &r.b, in.tid.data());
+  // A py string with no '{' and no U+3020 lead byte is its own interpolation (py:505-541: no
+  // simple key, the loop never starts, the escapes' protection is undone): such strings (a map's
+  // literal keys, a value's plain output going round repeat_until_done again) skip the device;
+  // every other string goes to k_resolve.
+  std::vector<uint64_t> dev;
+  Strs sub;
+  for (uint64_t i = 0; i < n; i++) {
+    const uint8_t* p = in.bytes.data() + in.off[i];
+    const uint64_t len = in.off[i + 1] - in.off[i];
+    if (t->dialect == IE_DIALECT_PY && !memchr(p, '{', len) && !memchr(p, 0xE3, len)) {
+      r.text[i] = std::string_view((const char*)p, len);
+      continue;
+    }
+    dev.push_back(i);
+  }
+  if (dev.empty()) return IE_SUCCESS;
+  const bool all = dev.size() == n;
+  if (!all)
+    for (uint64_t i : dev)
+      sub.add(std::string_view((const char*)in.bytes.data() + in.off[i], in.off[i + 1] - in.off[i]), in.tid[i]);
+  const Strs& q = all ? in : sub;
+  int rc = run_host(x, kOpInterp, t, q.bytes.data(), q.off.data(), q.size(), &r.b, q.tid.data());
   if (rc) return rc;
   const ie_batch* b = r.b;
-  for (uint64_t i = 0; i < n; i++) {
-    r.st[i] = b->status[i];
-    if (b->status[i] == IE_OK_STR) {
-      r.text[i] = std::string_view((const char*)b->bytes + b->offsets[i], b->offsets[i + 1] - b->offsets[i]);
-    } else if (b->status[i] == IE_OK_VALUE) {
-      r.vid[i] = b->value_id[i];
+  for (uint64_t k = 0; k < dev.size(); k++) {
+    const uint64_t i = dev[k];
+    r.st[i] = b->status[k];
+    if (b->status[k] == IE_OK_STR) {
+      r.text[i] = std::string_view((const char*)b->bytes + b->offsets[k], b->offsets[k + 1] - b->offsets[k]);
+    } else if (b->status[k] == IE_OK_VALUE) {
+      r.vid[i] = b->value_id[k];
       r.owned.emplace_back();
-      if (!value_str(t, in.tid[i], b->value_id[i], r.owned.back()))
+      if (!value_str(t, in.tid[i], b->value_id[k], r.owned.back()))
         return fail(IE_ERR_INVALID, "a typed result's value id is not in the table");
       r.text[i] = r.owned.back();
     }
