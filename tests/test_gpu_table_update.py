@@ -226,3 +226,59 @@ def test_arena_limit_reports_capacity_not_a_wrap():
         assert not _check(tset, states, ["{v}{w}" for _ in states], list(range(64)))
     finally:
         tset.close()
+
+
+def test_store_hands_out_value_ids():
+    # ie_table_set_store: a rewrite keeps its key's id, a new key takes the next id (a set's build
+    # gives kv i the id i), a delete frees its key's id and the next new key takes it; a typed
+    # whole-string result names the id the store reported
+    import ctypes
+    states = [{"a": "x", "b": 1}, {"c": "y"}]
+    tset = IE.InsertsTableSet(states, clock=CLOCK, mutable=True)
+    P = N.pack_module()
+    try:
+        def store(changes):
+            kv, tids, keep = P.pack(changes, len(states), IE.DELETE, IE.render, "py")
+            out = (ctypes.c_uint32 * len(changes))()
+            rc = N.lib().ie_table_set_store(tset.h, (ctypes.c_char * len(kv)).from_buffer(kv),
+                                            (ctypes.c_char * len(tids)).from_buffer(tids), len(changes), out)
+            assert rc == 0, N.STATUS_NAMES[rc] if rc < len(N.STATUS_NAMES) else rc
+            return list(out)
+        assert store([(0, "a", "x2"), (1, "d", 5), (0, "b", IE.DELETE), (1, "zz", IE.DELETE), (0, "", "e")]) == \
+            [0, 3, 1, 0xFFFFFFFF, 0xFFFFFFFF]
+        assert store([(1, "e", 7), (1, "f", [1, 2])]) == [1, 4]
+        got = tset.run(["{a}", "{d}", "{e}", "{f}", "{b}"], [0, 1, 1, 1, 0])
+        assert got[0] == (N.OK_VALUE, 0) and got[1] == (N.OK_VALUE, 3) and got[2] == (N.OK_VALUE, 1)
+        assert got[3] == (N.OK_VALUE, 4) and got[4][0] == N.E_INTERP
+    finally:
+        tset.close()
+
+
+def test_update_keeps_values_by_store_ids():
+    # the mirror's update goes through ie_table_set_store: typed whole-string results after rewrites,
+    # deletes and re-adds come back as the stored objects
+    states = [{"n": 1, "s": "x"} for _ in range(50)]
+    tset = IE.InsertsTableSet(states, clock=CLOCK, mutable=True)
+    try:
+        for rnd in range(4):
+            changes = []
+            for t in range(50):
+                if (t + rnd) % 3 == 0:
+                    changes.append((t, "n", IE.DELETE))
+                    states[t].pop("n", None)
+                else:
+                    changes.append((t, "n", [rnd, t]))
+                    states[t]["n"] = [rnd, t]
+                changes.append((t, "k%d" % rnd, {"r": rnd}))
+                states[t]["k%d" % rnd] = {"r": rnd}
+            assert tset.update(changes)
+            res = tset.results(["{n}" for _ in range(50)] + ["{k%d}" % rnd for _ in range(50)], list(range(50)) * 2)
+            for t in range(50):
+                want = states[t].get("n")
+                if want is None:
+                    assert isinstance(res[t], IE.InterpolationException)
+                else:
+                    assert res[t] == want
+                assert res[50 + t] == {"r": rnd}
+    finally:
+        tset.close()
