@@ -216,6 +216,10 @@ int ie_table_set_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
  * absent key deleted, the keys '', 'HH:MM', 'HH:MM:SS', or a change after an IE_ERR_CAPACITY stop).
  * Ids exhausted (2^32 - 3): IE_ERR_CAPACITY. */
 int ie_table_set_store(ie_table* t, const ie_kv* kv, const uint32_t* table_id, uint64_t n, uint32_t* vid_out);
+/* The stored value behind a value id (any table of a set: a set's ids are unique): its kind
+ * (IE_KIND_*) and text (ie_kv.text as stored; a pre-resolved value's raw text), read from the table's
+ * host mirror; the pointer is valid until the next update of the table. The clock ids have none. */
+int ie_table_value(const ie_table* t, uint32_t vid, int32_t* kind, const char** text, uint64_t* len);
 /* Arena bookkeeping: bytes in use, bytes of live entries, compactions so far (any may be NULL). */
 int ie_table_arena_stats(const ie_table* t, uint64_t* bytes, uint64_t* live, uint64_t* compactions);
 /* Lower the arena limit of ie_table_set_update (tests: force compaction and IE_ERR_CAPACITY early). */

@@ -26,7 +26,7 @@ OPT_ERROR_KEYS = 9
 # every symbol include/ie_amd.h declares (tests check the .so exports exactly these)
 EXPORTS = [
     "ie_abi_version", "ie_build_id", "ie_last_error", "ie_device_count",
-    "ie_table_build", "ie_table_set_build", "ie_table_set_clock", "ie_table_set_update", "ie_table_set_store", "ie_table_free", "ie_table_entries", "ie_table_tables",
+    "ie_table_build", "ie_table_set_build", "ie_table_set_clock", "ie_table_set_update", "ie_table_set_store", "ie_table_value", "ie_table_free", "ie_table_entries", "ie_table_tables",
     "ie_table_dialect",
     "ie_exec_create", "ie_exec_destroy", "ie_exec_sync", "ie_exec_set_timing", "ie_exec_timing",
     "ie_exec_set_scratch", "ie_exec_set_option", "ie_exec_host_keys",
@@ -130,6 +130,8 @@ def signatures():
         "ie_table_set_clock": (ctypes.c_int, [vp, ctypes.POINTER(Clock)]),
         "ie_table_set_update": (ctypes.c_int, [vp, vp, vp, vp, u64]),
         "ie_table_set_store": (ctypes.c_int, [vp, vp, vp, u64, vp]),
+        "ie_table_value": (ctypes.c_int, [vp, u32, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_void_p),
+                                          ctypes.POINTER(ctypes.c_uint64)]),
         "ie_table_arena_stats": (ctypes.c_int, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "ie_table_set_arena_limit": (ctypes.c_int, [vp, u64]),
         "ie_goto_map": (ctypes.c_int, [vp, vp, ctypes.c_char_p, u64, vp, u32, ctypes.POINTER(ctypes.POINTER(MapResult))]),

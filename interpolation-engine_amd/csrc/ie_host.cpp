@@ -1387,6 +1387,7 @@ struct SlotSet {
   std::vector<uint64_t> w;
   explicit SlotSet(uint32_t m) : w((m + 63) / 64, 0) {}
   void set(uint32_t s) { w[s >> 6] |= 1ull << (s & 63); }
+  void set_atomic(uint32_t s) { __atomic_fetch_or(&w[s >> 6], 1ull << (s & 63), __ATOMIC_RELAXED); }
   void clear(uint32_t s) { w[s >> 6] &= ~(1ull << (s & 63)); }
   bool has(uint32_t s) const { return (w[s >> 6] >> (s & 63)) & 1; }
   uint64_t count() const {
@@ -1501,7 +1502,112 @@ static int table_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
   else
     for (uint64_t i = 0; i < n; i++)
       if (kv[i].kind >= 0) t->next_vid = std::max(t->next_vid, vid[i] + 1);
-  for (uint64_t i = 0; i < n; i++) {
+  // A large call that only rewrites keys the tables have (a loop iteration's stores): the changes
+  // split by table over the host threads (a key's changes stay in order on one thread), each thread
+  // rewriting its entries in place or appending into an arena region of its own; anything else (a
+  // new key, a delete, a pre-resolved entry) takes the serial placement below.
+  bool parallel_done = false;
+  if (n >= 4096 && host_threads() > 1) {
+    std::vector<uint32_t> slot_of(n, UINT32_MAX);
+    std::atomic<bool> all_present{true};
+    parallel_for(n, in_bytes, [&](uint64_t lo, uint64_t hi) {
+      for (uint64_t i = lo; i < hi && all_present.load(std::memory_order_relaxed); i++) {
+        const std::string_view key(kv[i].key ? kv[i].key : "", kv[i].key_len);
+        if (key.empty() || key == "HH:MM" || key == "HH:MM:SS") continue;
+        const uint64_t h = khash[i];
+        const uint32_t slot = ph_slot(h, t->h_pilots[ph_group(h, nb)], m);
+        const Entry& e = t->h_entries[slot];
+        if (kv[i].kind < 0 || !(e.flags & EF_OCCUPIED) || (e.flags >> kTidShift) != table_id[i] ||
+            (e.flags & EF_RAWALT) || mirror_key(t, e) != key) {
+          all_present.store(false, std::memory_order_relaxed);
+          break;
+        }
+        slot_of[i] = slot;
+      }
+    });
+    const unsigned T = host_threads();
+    std::vector<std::vector<uint64_t>> mine(T);
+    std::vector<uint64_t> region(T + 1, 0);
+    if (all_present.load()) {
+      for (uint64_t i = 0; i < n; i++) {
+        if (slot_of[i] == UINT32_MAX) continue;
+        const unsigned k = table_id[i] % T;
+        mine[k].push_back(i);
+        region[k + 1] += ((kv[i].text_len + 3ull) & ~3ull) + ((kv[i].key_len + 3ull) & ~3ull);
+      }
+      for (unsigned k = 0; k < T; k++) region[k + 1] += region[k];
+    }
+    const uint64_t start = (t->h_arena.size() + 3ull) & ~3ull;
+    if (all_present.load() && start + region[T] + 8 <= t->arena_limit) {
+      while (t->h_arena.size() & 3) t->h_arena.push_back(0);
+      t->h_arena.grow(region[T]);
+      uint8_t* const base = t->h_arena.data();
+      std::vector<int64_t> live_delta(T, 0);
+      std::vector<uint64_t> maxtext(T, 0);
+      std::vector<std::vector<uint32_t>> touched_k(T);
+      parallel_for(T, ~0ull, [&](uint64_t lo, uint64_t hi) {
+        for (uint64_t k = lo; k < hi; k++) {
+          uint64_t cursor = start + region[k];
+          int64_t dl = 0;
+          for (uint64_t i : mine[k]) {
+            const uint32_t slot = slot_of[i], tb = table_id[i];
+            Entry& e = t->h_entries[slot];
+            const std::string_view key(kv[i].key, kv[i].key_len);
+            const std::string_view text(kv[i].text ? kv[i].text : "", kv[i].text_len);
+            const uint32_t flags = kind_flags(kv[i].kind, t->dialect) | tflags[i];
+            const uint32_t v = autov ? e.vid : vid[i];
+            const uint64_t a = e.text_off, b = (key_off_of(e.text_off, e.text_len) + e.key_len + 3ull) & ~3ull;
+            if (((text.size() + 3ull) & ~3ull) <= ((e.text_len + 3ull) & ~3ull)) {  // in place
+              memset(base + a, 0, b - a);
+              memcpy(base + a, text.data(), text.size());
+              const uint32_t ko = key_off_of(e.text_off, (uint32_t)text.size());
+              memcpy(base + ko, key.data(), key.size());
+              dl -= (int64_t)(b - a) - (int64_t)((((uint64_t)ko + key.size() + 3ull) & ~3ull) - a);
+              e.text_len = (uint32_t)text.size();
+              e.vid = v;
+              e.flags = flags | EF_OCCUPIED | (e.flags & ~((1u << kTidShift) - 1u));
+              memset(e.text, 0, kInlineText);
+              memcpy(e.text, text.data(), std::min<size_t>(text.size(), kInlineText));
+              rewritten.set_atomic(slot);
+            } else {  // appended in this thread's region: [text][pad][key][pad]
+              dl -= (int64_t)(b - a);
+              const uint64_t off = cursor;
+              memcpy(base + off, text.data(), text.size());
+              memset(base + off + text.size(), 0, ((text.size() + 3ull) & ~3ull) - text.size());
+              const uint32_t ko = key_off_of((uint32_t)off, (uint32_t)text.size());
+              memcpy(base + ko, key.data(), key.size());
+              cursor = ((uint64_t)ko + key.size() + 3ull) & ~3ull;
+              memset(base + ko + key.size(), 0, cursor - ko - key.size());
+              dl += (int64_t)(cursor - off);
+              Entry nb{};
+              nb.key_len = (uint32_t)key.size();
+              nb.text_len = (uint32_t)text.size();
+              nb.vid = v;
+              nb.flags = flags | EF_OCCUPIED | (tb << kTidShift);
+              nb.text_off = (uint32_t)off;
+              memcpy(nb.key, key.data(), std::min<size_t>(key.size(), kInlineKey));
+              memcpy(nb.text, text.data(), std::min<size_t>(text.size(), kInlineText));
+              e = nb;
+            }
+            dirty.set_atomic(slot);
+            touched_k[k].push_back(tb);
+            maxtext[k] = std::max<uint64_t>(maxtext[k], text.size());
+            if (autov) vid_out[i] = v;
+          }
+          memset(base + cursor, 0, start + region[k + 1] - cursor);  // (the region's unused tail: dead)
+          live_delta[k] = dl;
+        }
+      });
+      for (unsigned k = 0; k < T; k++) {
+        t->arena_live = (uint64_t)((int64_t)t->arena_live + live_delta[k]);
+        t->dev.maxtext = std::max<uint64_t>(t->dev.maxtext, maxtext[k]);
+        touched.insert(touched.end(), touched_k[k].begin(), touched_k[k].end());
+      }
+      parallel_done = true;
+      tr.mark("parallel rewrites", n);
+    }
+  }
+  for (uint64_t i = 0; i < n && !parallel_done; i++) {
     const uint32_t tb = table_id[i];
     std::string_view key(kv[i].key ? kv[i].key : "", kv[i].key_len);
     if (key.empty() || key == "HH:MM" || key == "HH:MM:SS") continue;  // never looked up (py:433-446)

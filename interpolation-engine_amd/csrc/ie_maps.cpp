@@ -100,14 +100,8 @@ struct Res {
 // raw text of a pre-resolved one), or the clock's text for the clock ids
 ie_clock table_clock(const ie_table* t);
 
-bool value_str(const ie_table* t, uint32_t tb, uint32_t vid, std::string& out) {
-  if (vid == IE_VID_CLOCK_HHMM || vid == IE_VID_CLOCK_HHMMSS) {  // (one clock for every table of a set)
-    const ie_clock c = table_clock(t);
-    char buf[16];
-    snprintf(buf, sizeof buf, vid == IE_VID_CLOCK_HHMM ? "%02d:%02d" : "%02d:%02d:%02d", c.hour, c.minute, c.second);
-    out = buf;
-    return true;
-  }
+// the slot holding value id vid (table tb, or any table when tb is UINT32_MAX), UINT32_MAX: none
+uint32_t slot_of_vid(const ie_table* t, uint32_t vid, uint32_t tb = UINT32_MAX) {
   if (!t->vid_ok) {
     t->vid_slot.assign(t->next_vid, UINT32_MAX);
     for (uint32_t s = 0; s < (uint32_t)t->h_entries.size(); s++) {
@@ -120,24 +114,39 @@ bool value_str(const ie_table* t, uint32_t tb, uint32_t vid, std::string& out) {
   }
   auto holds = [&](uint32_t s) {
     const Entry& e = t->h_entries[s];
-    return (e.flags & EF_OCCUPIED) && e.vid == vid && (e.flags >> kTidShift) == tb;
+    return (e.flags & EF_OCCUPIED) && e.vid == vid && (tb == UINT32_MAX || (e.flags >> kTidShift) == tb);
   };
   uint32_t s = vid < t->vid_slot.size() ? t->vid_slot[vid] : UINT32_MAX;
   if (s == UINT32_MAX || !holds(s)) {  // (a caller's ids shared between tables: the slow way)
     s = UINT32_MAX;
     for (uint32_t k = 0; k < (uint32_t)t->h_entries.size() && s == UINT32_MAX; k++)
       if (holds(k)) s = k;
-    if (s == UINT32_MAX) return false;
   }
-  const Entry& e = t->h_entries[s];
+  return s;
+}
+
+// an entry's stored text: the raw text of a pre-resolved one
+std::string_view entry_text(const ie_table* t, const Entry& e) {
   const uint8_t* a = t->h_arena.data();
   if (e.flags & EF_RAWALT) {
     uint32_t rl;
     memcpy(&rl, a + e.text_off - 4, 4);
-    out.assign((const char*)a + e.text_off - 4 - ((rl + 3u) & ~3u), rl);
-  } else {
-    out.assign((const char*)a + e.text_off, e.text_len);
+    return std::string_view((const char*)a + e.text_off - 4 - ((rl + 3u) & ~3u), rl);
   }
+  return std::string_view((const char*)a + e.text_off, e.text_len);
+}
+
+bool value_str(const ie_table* t, uint32_t tb, uint32_t vid, std::string& out) {
+  if (vid == IE_VID_CLOCK_HHMM || vid == IE_VID_CLOCK_HHMMSS) {  // (one clock for every table of a set)
+    const ie_clock c = table_clock(t);
+    char buf[16];
+    snprintf(buf, sizeof buf, vid == IE_VID_CLOCK_HHMM ? "%02d:%02d" : "%02d:%02d:%02d", c.hour, c.minute, c.second);
+    out = buf;
+    return true;
+  }
+  const uint32_t s = slot_of_vid(t, vid, tb);
+  if (s == UINT32_MAX) return false;
+  out.assign(entry_text(t, t->h_entries[s]));
   return true;
 }
 
@@ -365,6 +374,21 @@ int table_with(ie_exec* x, const ie_table* t, const std::vector<uint32_t>& owner
 }  // namespace
 
 extern "C" {
+
+// the stored value behind a value id (any table of the set: the ids are unique in a set), from the
+// host mirror: its kind and its text (a pre-resolved entry's raw text); valid until the next update
+int ie_table_value(const ie_table* t, uint32_t vid, int32_t* kind, const char** text, uint64_t* len) {
+  if (!t || !kind || !text || !len) return fail(IE_ERR_INVALID, "null argument");
+  if (vid >= IE_VID_CLOCK_HHMMSS) return fail(IE_ERR_INVALID, "a clock id has no stored value");
+  const uint32_t s = slot_of_vid(t, vid);
+  if (s == UINT32_MAX) return fail(IE_ERR_INVALID, "value id not in the table");
+  const Entry& e = t->h_entries[s];
+  const std::string_view v = entry_text(t, e);
+  *kind = (int32_t)(e.flags & EF_KIND_MASK);
+  *text = v.data();
+  *len = v.size();
+  return IE_SUCCESS;
+}
 
 void ie_map_result_free(ie_map_result* r) {
   if (!r) return;

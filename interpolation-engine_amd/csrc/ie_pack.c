@@ -391,12 +391,15 @@ fail:
   return NULL;
 }
 
-// assign(values, changes, vids, delete) -> None: values[vids[i]] = the stored value (None for a
-// delete), the list grown with None as the ids need; ids 0xFFFFFFFF are skipped
+// assign(values, changes, vids, delete[, in_table]) -> None: values[vids[i]] = the stored value (None
+// for a delete), the list grown with None as the ids need; ids 0xFFFFFFFF are skipped. With
+// in_table, a str or int value is not held: the marker goes in its place and the value is read back
+// from the table's mirror when asked for (ie_table_value), so a store does not keep (and later free)
+// the caller's KB-long texts
 static PyObject* assign(PyObject* self, PyObject* args) {
   (void)self;
-  PyObject *values, *changes, *vids, *del;
-  if (!PyArg_ParseTuple(args, "O!OOO", &PyList_Type, &values, &changes, &vids, &del)) return NULL;
+  PyObject *values, *changes, *vids, *del, *in_table = NULL;
+  if (!PyArg_ParseTuple(args, "O!OOO|O", &PyList_Type, &values, &changes, &vids, &del, &in_table)) return NULL;
   Py_buffer vb;
   if (PyObject_GetBuffer(vids, &vb, PyBUF_SIMPLE) < 0) return NULL;
   PyObject* seq = PySequence_Fast(changes, "changes must be a sequence");
@@ -416,6 +419,7 @@ static PyObject* assign(PyObject* self, PyObject* args) {
       if (PyList_Append(values, Py_None) < 0) goto fail;
     PyObject* v = PyTuple_GET_ITEM(PySequence_Fast_GET_ITEM(seq, i), 2);
     if (v == del) v = Py_None;
+    else if (in_table && (PyUnicode_CheckExact(v) || PyLong_CheckExact(v))) v = in_table;
     Py_INCREF(v);
     if (PyList_SetItem(values, (Py_ssize_t)id[i], v) < 0) goto fail;  // (steals v, drops the old value)
   }

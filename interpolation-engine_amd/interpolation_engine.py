@@ -37,6 +37,7 @@ inserts_dir = None  # py:44 — when set, get_interpdata falls back to its files
 
 
 DELETE = object()  # InsertsTableSet.update: remove the key (`del inserts[key]`)
+_IN_TABLE = object()  # InsertsTableSet.values: a str / int the table's mirror holds (value() reads it)
 
 
 class InterpolationException(Exception):
@@ -153,7 +154,14 @@ class InsertsTableSet:
             return "%02d:%02d" % self.clock[:2]
         if vid == N.VID_HHMMSS:
             return "%02d:%02d:%02d" % self.clock
-        return self.values[vid]
+        v = self.values[vid]
+        if v is _IN_TABLE:  # a str / int stored by update(): read back from the table's mirror
+            k, p, n = ctypes.c_int32(), ctypes.c_void_p(), ctypes.c_uint64()
+            N.check(N.lib().ie_table_value(self.h, vid, ctypes.byref(k), ctypes.byref(p), ctypes.byref(n)),
+                    "ie_table_value")
+            text = N.dec(ctypes.string_at(p.value, n.value)) if n.value else ""
+            return int(text) if k.value == N.KIND_INT else text
+        return v
 
     def table_keys(self, t):
         return list(self.dicts[t].keys())  # the live dict (as py:467's message reads it)
@@ -182,7 +190,7 @@ class InsertsTableSet:
         if rc == N.ERR_CAPACITY:
             return False
         N.check(rc, "ie_table_set_store")
-        P.assign(self.values, changes, vids, DELETE)
+        P.assign(self.values, changes, vids, DELETE, _IN_TABLE)
         # (where a store call's time goes: packing, the library, the value list)
         self.last_update_native_s = t1 - t0
         self.last_update_split_s = (t0 - tp, t1 - t0, time.perf_counter() - t1)

@@ -282,3 +282,33 @@ def test_update_keeps_values_by_store_ids():
                 assert res[50 + t] == {"r": rnd}
     finally:
         tset.close()
+
+
+def test_large_rewrite_batches_match_the_oracle():
+    # >= 4096 stores that only rewrite present keys take the parallel placement (per-thread arena
+    # regions): shorter texts in place, longer ones appended, a key stored twice in one call (the
+    # second wins), typed values; every string matches the oracle on the mutated states after each
+    # round, and the value ids stay those of the keys
+    rng = random.Random(9)
+    states = [{"h": "hist %d" % t, "o": "out", "n": t, "tmpl": "<{h}|{o}>"} for t in range(2000)]
+    tset = IE.InsertsTableSet(states, clock=CLOCK, mutable=True)
+    try:
+        # the first round reverts the pre-resolved templates (serial path); the next ones are rewrites only
+        for rnd in range(4):
+            changes = []
+            for t, d in enumerate(states):
+                d["h"] = d["h"] + " more %d" % rnd * rng.randrange(0, 6)
+                d["o"] = "o%d" % rng.randrange(0, 10 ** rng.randrange(1, 6))
+                d["n"] = d["n"] + rnd
+                changes += [(t, "h", d["h"]), (t, "o", "ignored"), (t, "o", d["o"]), (t, "n", d["n"])]
+            before = [tset.run(["{n}"], [t])[0][1] for t in (0, 777)]
+            assert tset.update(changes)
+            strings = ["{h}", "x{o}y", "{tmpl}", "{n}", "n={n}"] * len(states)
+            ids = [t for t in range(len(states)) for _ in range(5)]
+            bad = _check(tset, states, strings, ids)
+            assert not bad, (rnd, len(bad), bad[:3])
+            assert [tset.run(["{n}"], [t])[0][1] for t in (0, 777)] == before  # ids kept by rewrites
+            size, live, _ = tset.arena_stats()
+            assert size <= 2 * live + (64 << 10) + 64 or rnd == 0, (rnd, size, live)
+    finally:
+        tset.close()
