@@ -149,6 +149,7 @@ def parse(argv=None):
     ap.add_argument("--layout", choices=["views", "packed"], default="",
                     help="output layout (default views; config 4 views runs the fused unescape command): views = each tile claims its "
                          "output range with one atomic (no look-back), packed = input order (look-back)")
+    ap.add_argument("--no-packed", action="store_true", help="skip the packed-layout launches beside a views run")
     ap.add_argument("--reserve", type=int, default=32,
                     help="views output: IE_OPT_RESERVE (F x16: tile t writes at F x its input offset, no claim "
                          "atomic; 0 = one claim per tile on one cursor)")
@@ -447,6 +448,27 @@ def main(argv=None):
     cmd_ms = [x.elapsed(3 * k + 1, 3 * k + 2) for k in range(args.steps)] if cmd else None
     wall_max = max_over_ranks(wall, dist)
 
+    # the §8b packed layout (offsets[N+1] in input order, what ie_interpolate_device writes) timed on
+    # the same batch and build beside the views headline (untimed for `value`; 20 launches)
+    packed = None
+    if views and cfg in (2, 3) and not args.no_packed:
+        op = N.DevOut(d_out.ptr, out_cap, d_ooff.ptr, d_st.ptr, d_vid.ptr, d_tot.ptr)
+        for k in range(25):
+            if k >= 5:
+                x.mark(2 * (k - 5))
+            N.check(L.ie_interpolate_device_ids(x.h, W.table, ids, W.d_in.ptr, W.d_off.ptr, n, ctypes.byref(op)),
+                    "packed")
+            if k >= 5:
+                x.mark(2 * (k - 5) + 1)
+        x.sync()
+        pk_ms = float(np.mean([x.elapsed(2 * k, 2 * k + 1) for k in range(20)]))
+        pk_out = int(d_tot.to_numpy(np.uint64, 1)[0])
+        pk_alg = in_bytes + pk_out + 17 * n + (4 * n if ids is not None else 0)
+        packed = {"launch_ms": round(pk_ms, 4), "frac": round(pk_alg / (pk_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                  "launches": 20, "note": "packed offsets[N+1] layout (decoupled look-back), same batch and build"}
+        N.check(resolve(), "views again")  # (the views results back in the buffers for the checks below)
+        x.sync()
+
     x.set_timing(True)  # one more call with the library's own events for the telemetry
     if cmd and not views and os.environ.get("IE_DIAG_CMD_RESOLVE"):  # diagnostic: the command's second resolve instead
         N.check(L.ie_interpolate_device(x.h, W.table, d_u.ptr, d_uoff.ptr, n, ctypes.byref(o2)), "timing")
@@ -538,6 +560,8 @@ def main(argv=None):
                                        "chain_failures": int(tm.n_chain_fail), "deferred": int(tm.n_deferred)}},
             "cpu_baseline": cpu,
         }
+        if packed:
+            line["roofline"]["packed_layout"] = packed
         if nchk:
             line["shard_checks"] = checks
         if cfg == 5:

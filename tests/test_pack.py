@@ -1,0 +1,94 @@
+"""The store packer (interpolation-engine_amd/csrc/ie_pack.c, a CPython module; host only, no GPU):
+InsertsTableSet.update's (dict index, key, value) changes and a table set's dicts -> the ie_kv
+records and table ids / kv_start the C ABI takes. The records point into the str objects (ASCII) or
+into one buffer the other texts are transcoded into across threads; every key and text must equal
+_native.enc (UTF-8, 'surrogatepass') of the Python string, and the value list is filled by the ids."""
+import ctypes
+import random
+
+import pytest
+
+import __graft_entry__ as G
+
+G.build()
+PKG = G.load_package()
+N = PKG._native
+IE = PKG.interpolation_engine
+P = N.pack_module()
+
+ALPHABET = ["a", "b", " ", "{", "}", "\\", "é", "ÿ", "\x7f", "\x80", "€", "〠", "\ud800", "\udfff", "😀", "\U0010ffff"]
+
+
+def _rand_str(rng, n):
+    extra = rng.choice(ALPHABET)  # one non-ASCII kind per string, sometimes none
+    return "".join(rng.choice(["a", "b", " ", extra]) for _ in range(n))
+
+
+def _records(kv, n):
+    return (N.KV * n).from_buffer(kv)
+
+
+@pytest.mark.parametrize("threads", [1, 8])
+def test_pack_matches_enc(threads):
+    rng = random.Random(threads)
+    changes = []
+    for i in range(3000):
+        k = _rand_str(rng, rng.randrange(0, 40))
+        v = _rand_str(rng, rng.randrange(0, 2000)) if i % 7 else rng.choice([i, -i, 10 ** 30, True, None, 1.5, [1, "x"], {"a": 1}])
+        changes.append((i % 5, k, v))
+    changes.append((2, "gone", IE.DELETE))
+    kv, tids, keep = P.pack(changes, 5, IE.DELETE, IE.render, "py", threads)
+    recs = _records(kv, len(changes))
+    assert list(memoryview(tids).cast("I")) == [c[0] for c in changes]
+    for r, (t, k, v) in zip(recs, changes):
+        assert ctypes.string_at(r.key, r.key_len) == N.enc(k)
+        if v is IE.DELETE:
+            assert r.kind == -1
+            continue
+        kind, text = IE.render(v, "py")
+        assert r.kind == kind and ctypes.string_at(r.text, r.text_len) == N.enc(text), (k, v)
+
+
+def test_pack_dicts_kv_start_and_order():
+    rng = random.Random(3)
+    dicts = [{_rand_str(rng, 5) + str(j): _rand_str(rng, rng.randrange(0, 300)) for j in range(rng.randrange(0, 9))}
+             for _ in range(50)]
+    dicts[7]["typed"] = [1, 2]
+    kv, st, keep = P.pack_dicts(dicts, IE.render, "rs", 4)
+    starts = list(memoryview(st).cast("Q"))
+    assert starts[0] == 0 and starts[-1] == sum(len(d) for d in dicts)
+    recs = _records(kv, max(1, starts[-1]))
+    i = 0
+    for t, d in enumerate(dicts):
+        assert starts[t] == i
+        for k, v in d.items():
+            kind, text = IE.render(v, "rs")
+            assert ctypes.string_at(recs[i].key, recs[i].key_len) == N.enc(k)
+            assert recs[i].kind == kind and ctypes.string_at(recs[i].text, recs[i].text_len) == N.enc(text)
+            i += 1
+
+
+def test_pack_errors():
+    with pytest.raises(TypeError, match="insert keys must be str"):
+        P.pack([(0, 5, "x")], 1, IE.DELETE, IE.render, "py")
+    with pytest.raises(IndexError):
+        P.pack([(3, "k", "x")], 2, IE.DELETE, IE.render, "py")
+    with pytest.raises(TypeError):
+        P.pack([(0, "k")], 1, IE.DELETE, IE.render, "py")
+    with pytest.raises(TypeError):
+        P.pack([(0, "k", object())], 1, IE.DELETE, IE.render, "py")
+    with pytest.raises(TypeError):
+        P.pack_dicts([{1: "x"}], IE.render, "py")
+
+
+def test_assign_holds_typed_values_only():
+    marker = object()
+    values = ["v0", "v1"]
+    changes = [(0, "a", "text"), (0, "b", 7), (0, "c", [1]), (0, "d", IE.DELETE), (0, "e", True), (0, "f", "skip")]
+    vids = bytearray(memoryview(__import__("array").array("I", [0, 3, 5, 1, 2, 0xFFFFFFFF])).cast("B"))
+    P.assign(values, changes, vids, IE.DELETE, marker)
+    assert values[0] is marker and values[3] is marker  # str and int: read back from the table
+    assert values[5] == [1] and values[1] is None and values[2] is True and values[4] is None
+    values2 = []
+    P.assign(values2, changes[:3], bytearray(memoryview(__import__("array").array("I", [2, 0, 1])).cast("B")), IE.DELETE)
+    assert values2 == [7, [1], "text"]
