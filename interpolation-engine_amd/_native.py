@@ -91,8 +91,12 @@ def map_result_to_python(res_ptr):
     r = res_ptr.contents
     n = r.n
     blob = ctypes.string_at(r.bytes, r.bytes_len) if r.bytes_len else b""
-    o = [r.offsets[i] for i in range(n + 1)]
-    out = [(blob[o[i]:o[i + 1]], r.status[i], r.where[i], r.chosen[i], r.value_id[i]) for i in range(n)]
+
+    def arr(p, size, fmt):  # (one copy per array: no ctypes indexing per row)
+        return memoryview(ctypes.string_at(p, size * n)).cast(fmt).tolist() if n else []
+    o = memoryview(ctypes.string_at(r.offsets, 8 * (n + 1))).cast("Q").tolist()
+    st, wh, ch, vid = arr(r.status, 1, "B"), arr(r.where, 4, "I"), arr(r.chosen, 4, "i"), arr(r.value_id, 4, "I")
+    out = [(blob[o[i]:o[i + 1]], st[i], wh[i], ch[i], vid[i]) for i in range(n)]
     lib().ie_map_result_free(res_ptr)
     return out
 
