@@ -197,7 +197,9 @@ int ie_table_set_clock(ie_table* t, const ie_clock* now);
  * the map per task): entry i sets kv[i] (kind < 0: deletes the key) in table table_id[i], value id
  * vid[i], without a rebuild: a key the table has is rewritten in place, a new key re-places its
  * pilot group (or, when that group has no free placement, the whole table is placed again at the
- * same capacity: entries and pilots uploaded whole). Synchronous (waits for the device first, like ie_table_set_clock). A brace-bearing
+ * same capacity: entries and pilots uploaded whole). Waits for the device first (like ie_table_set_clock);
+ * the patch kernel it ends with completes asynchronously, ordered before every later batch on the
+ * table (the batches wait on its event in their own stream). A brace-bearing
  * value is not pre-resolved, and the pre-resolved values of every changed table return to their raw
  * text (both then resolve through the exact evaluator, in the reference's order). IE_ERR_CAPACITY:
  * a new key found no placement (the entries before it were applied, it and the rest were not:
