@@ -1525,6 +1525,7 @@ static int table_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
         slot_of[i] = slot;
       }
     });
+    tr.mark("(pre-pass)", n);
     const unsigned T = host_threads();
     std::vector<std::vector<uint64_t>> mine(T);
     std::vector<uint64_t> region(T + 1, 0);
@@ -1539,8 +1540,10 @@ static int table_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
     }
     const uint64_t start = (t->h_arena.size() + 3ull) & ~3ull;
     if (all_present.load() && start + region[T] + 8 <= t->arena_limit) {
+      tr.mark("(lists)", T);
       while (t->h_arena.size() & 3) t->h_arena.push_back(0);
       t->h_arena.grow(region[T]);
+      tr.mark("(grown)", region[T]);
       uint8_t* const base = t->h_arena.data();
       std::vector<int64_t> live_delta(T, 0);
       std::vector<uint64_t> maxtext(T, 0);
@@ -1549,6 +1552,9 @@ static int table_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
         for (uint64_t k = lo; k < hi; k++) {
           uint64_t cursor = start + region[k];
           int64_t dl = 0;
+          uint64_t mt = 0;
+          std::vector<uint32_t> tk;  // (thread-local: the per-thread slots of shared vectors would share lines)
+          tk.reserve(mine[k].size());
           for (uint64_t i : mine[k]) {
             const uint32_t slot = slot_of[i], tb = table_id[i];
             Entry& e = t->h_entries[slot];
@@ -1590,14 +1596,17 @@ static int table_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
               e = nb;
             }
             dirty.set_atomic(slot);
-            touched_k[k].push_back(tb);
-            maxtext[k] = std::max<uint64_t>(maxtext[k], text.size());
+            tk.push_back(tb);
+            mt = std::max<uint64_t>(mt, text.size());
             if (autov) vid_out[i] = v;
           }
           memset(base + cursor, 0, start + region[k + 1] - cursor);  // (the region's unused tail: dead)
           live_delta[k] = dl;
+          maxtext[k] = mt;
+          touched_k[k] = std::move(tk);
         }
       });
+      tr.mark("(placed)", region[T]);
       for (unsigned k = 0; k < T; k++) {
         t->arena_live = (uint64_t)((int64_t)t->arena_live + live_delta[k]);
         t->dev.maxtext = std::max<uint64_t>(t->dev.maxtext, maxtext[k]);

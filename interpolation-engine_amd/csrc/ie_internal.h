@@ -160,6 +160,12 @@ class HostArena {
   }
   void grow(uint64_t k) {  // k more bytes, written later (ie_table_set_update's deferred copies)
     reserve(n_ + k);
+#ifdef MADV_POPULATE_WRITE
+    if (k >= (1u << 20)) {  // (fresh pages faulted in by one call, not by the writers one at a time)
+      const uintptr_t lo = ((uintptr_t)(p_ + n_) + 4095) & ~(uintptr_t)4095, hi = (uintptr_t)(p_ + n_ + k) & ~(uintptr_t)4095;
+      if (hi > lo) (void)madvise((void*)lo, hi - lo, MADV_POPULATE_WRITE);
+    }
+#endif
     n_ += k;
   }
   void push_back(uint8_t b) {

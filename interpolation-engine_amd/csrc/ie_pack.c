@@ -203,7 +203,42 @@ static int utf8_of(PyObject* s, jobs_t* J, uint64_t rec, const char** p, uint64_
   return 0;
 }
 
-static void free_buf(PyObject* cap) { PyMem_RawFree(PyCapsule_GetPointer(cap, "ie_pack.buf")); }
+// The transcode buffer outlives the call only until the records are used: when its capsule goes,
+// the buffer is kept for the next call instead of freed (a store loop packs tens of MB per
+// iteration: a fresh mapping each time costs its page faults, and its unmapping, again). The GIL
+// guards the slot.
+static uint8_t* spare_buf = NULL;
+static size_t spare_cap = 0;
+
+static uint8_t* take_buf(size_t need, size_t* cap) {
+  if (spare_buf && spare_cap >= need) {
+    uint8_t* b = spare_buf;
+    *cap = spare_cap;
+    spare_buf = NULL;
+    spare_cap = 0;
+    return b;
+  }
+  *cap = need;
+  return (uint8_t*)PyMem_RawMalloc(need);
+}
+
+typedef struct {
+  uint8_t* p;
+  size_t cap;
+} held_t;
+
+static void free_buf(PyObject* capsule) {
+  held_t* h = (held_t*)PyCapsule_GetPointer(capsule, "ie_pack.buf");
+  if (!h) return;
+  if (!spare_buf || spare_cap < h->cap) {  // (keep the larger one)
+    PyMem_RawFree(spare_buf);
+    spare_buf = h->p;
+    spare_cap = h->cap;
+  } else {
+    PyMem_RawFree(h->p);
+  }
+  PyMem_RawFree(h);
+}
 
 // one record: key k, value v (the delete marker: kind -1); 0, or -1 with the Python error set
 static int pack_kv(PyObject* k, PyObject* v, kv_rec* r, uint64_t i, jobs_t* J, PyObject* keep, PyObject* del,
@@ -261,11 +296,17 @@ static int finish(kv_rec* kv, jobs_t* J, PyObject* keep, int threads) {
     J->p[k].off = total;
     total += J->p[k].out;
   }
-  uint8_t* buf = (uint8_t*)PyMem_RawMalloc(total + 16);
-  if (!buf) {
+  size_t cap = 0;
+  uint8_t* buf = take_buf(total + 16, &cap);
+  held_t* held = (held_t*)PyMem_RawMalloc(sizeof(held_t));
+  if (!buf || !held) {
+    PyMem_RawFree(buf);
+    PyMem_RawFree(held);
     PyErr_NoMemory();
     return -1;
   }
+  held->p = buf;
+  held->cap = cap;
   Py_BEGIN_ALLOW_THREADS
   run_jobs(J->p, J->n, buf, threads);
   Py_END_ALLOW_THREADS
@@ -274,13 +315,14 @@ static int finish(kv_rec* kv, jobs_t* J, PyObject* keep, int threads) {
     if (J->p[k].rec & 1) r->text = (const char*)buf + J->p[k].off, r->text_len = J->p[k].out;
     else r->key = (const char*)buf + J->p[k].off, r->key_len = J->p[k].out;
   }
-  PyObject* cap = PyCapsule_New(buf, "ie_pack.buf", free_buf);
-  if (!cap) {
+  PyObject* capsule = PyCapsule_New(held, "ie_pack.buf", free_buf);
+  if (!capsule) {
     PyMem_RawFree(buf);
+    PyMem_RawFree(held);
     return -1;
   }
-  const int rc = PyList_Append(keep, cap);
-  Py_DECREF(cap);
+  const int rc = PyList_Append(keep, capsule);
+  Py_DECREF(capsule);
   return rc;
 }
 
