@@ -1797,8 +1797,12 @@ static int table_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
   t->defer = nullptr;  // (the pre-resolved values below copy out of temporaries: no deferral)
   tr.mark("copies", t->h_arena.size() - call_start);
   // values pre-resolved against the old dict of a changed table: back to their raw text
-  std::sort(touched.begin(), touched.end());
-  touched.erase(std::unique(touched.begin(), touched.end()), touched.end());
+  if (t->rawalt.empty()) {
+    touched.clear();  // (no table holds a pre-resolved value any more: nothing to return to raw)
+  } else {
+    std::sort(touched.begin(), touched.end());
+    touched.erase(std::unique(touched.begin(), touched.end()), touched.end());
+  }
   for (uint32_t tb : touched) {
     auto it = t->rawalt.find(tb);
     if (it == t->rawalt.end()) continue;

@@ -37,10 +37,12 @@ __attribute__((used)) static const char kPackId[] = "IE_BUILD_ID:" IE_PACK_ID;  
 typedef struct {
   const void* src;
   uint64_t len;  // code units
-  int kind;      // 1, 2, 4 bytes per unit
+  int kind;      // 1, 2, 4 bytes per unit; KIND_JOB_INT: str() of ival
+  int64_t ival;
   uint64_t rec;  // record index * 2 + (0: key, 1: text)
   uint64_t off, out;
 } job_t;
+enum { KIND_JOB_INT = 8 };
 
 static inline uint8_t* put_cp(uint8_t* o, uint32_t c) {  // one code point (surrogates: 3 bytes, as 'surrogatepass')
   if (c < 0x80) {
@@ -62,6 +64,10 @@ static inline uint8_t* put_cp(uint8_t* o, uint32_t c) {  // one code point (surr
 }
 
 static uint64_t utf8_len(const job_t* j) {
+  if (j->kind == KIND_JOB_INT) {
+    char tmp[24];
+    return (uint64_t)snprintf(tmp, sizeof tmp, "%lld", (long long)j->ival);
+  }
   uint64_t n = j->len;
   if (j->kind == 1) {
     const uint8_t* d = (const uint8_t*)j->src;
@@ -77,6 +83,12 @@ static uint64_t utf8_len(const job_t* j) {
 }
 
 static void transcode(const job_t* j, uint8_t* o) {  // (runs of ASCII 8-16 units at a time)
+  if (j->kind == KIND_JOB_INT) {
+    char tmp[24];
+    const int n = snprintf(tmp, sizeof tmp, "%lld", (long long)j->ival);
+    memcpy(o, tmp, (size_t)n);
+    return;
+  }
   const uint64_t len = j->len;
   uint64_t i = 0;
   if (j->kind == 1) {
@@ -174,6 +186,22 @@ typedef struct {
   uint64_t n, cap;
 } jobs_t;
 
+static job_t* new_job(jobs_t* J) {
+  if (J->n == J->cap) {
+    const uint64_t cap = J->cap ? 2 * J->cap : 1024;
+    job_t* q = (job_t*)PyMem_RawRealloc(J->p, cap * sizeof(job_t));
+    if (!q) {
+      PyErr_NoMemory();
+      return NULL;
+    }
+    J->p = q;
+    J->cap = cap;
+  }
+  job_t* j = &J->p[J->n++];
+  j->ival = 0;
+  return j;
+}
+
 // the record's UTF-8 ('surrogatepass', as _native.enc): an ASCII str is its own UTF-8 (a pointer
 // into it); any other becomes a job
 static int utf8_of(PyObject* s, jobs_t* J, uint64_t rec, const char** p, uint64_t* n) {
@@ -183,17 +211,8 @@ static int utf8_of(PyObject* s, jobs_t* J, uint64_t rec, const char** p, uint64_
     *n = (uint64_t)PyUnicode_GET_LENGTH(s);
     return 0;
   }
-  if (J->n == J->cap) {
-    const uint64_t cap = J->cap ? 2 * J->cap : 1024;
-    job_t* q = (job_t*)PyMem_RawRealloc(J->p, cap * sizeof(job_t));
-    if (!q) {
-      PyErr_NoMemory();
-      return -1;
-    }
-    J->p = q;
-    J->cap = cap;
-  }
-  job_t* j = &J->p[J->n++];
+  job_t* j = new_job(J);
+  if (!j) return -1;
   j->src = PyUnicode_DATA(s);
   j->len = (uint64_t)PyUnicode_GET_LENGTH(s);
   j->kind = PyUnicode_KIND(s);
@@ -259,6 +278,21 @@ static int pack_kv(PyObject* k, PyObject* v, kv_rec* r, uint64_t i, jobs_t* J, P
     text = v;
   } else if (PyLong_CheckExact(v)) {
     r->kind = KIND_INT;
+    int overflow = 0;
+    const long long x = PyLong_AsLongLongAndOverflow(v, &overflow);
+    if (!overflow && !(x == -1 && PyErr_Occurred())) {  // (str(int) formatted with the texts: no str object)
+      job_t* j = new_job(J);
+      if (!j) return -1;
+      j->src = NULL;
+      j->len = 0;
+      j->ival = x;
+      j->kind = KIND_JOB_INT;
+      j->rec = 2 * i + 1;
+      r->text = NULL;
+      r->text_len = 0;
+      return 0;
+    }
+    PyErr_Clear();
     text = PyObject_Str(v);
     if (!text || PyList_Append(keep, text) < 0) {
       Py_XDECREF(text);
