@@ -3,7 +3,8 @@
 bench.py reads for `roofline.traffic`.
 
 Which dispatches count: the k_resolve dispatches of the batch (the largest grid; the table
-build's small pre-resolution dispatch is left out). In config 4 every step launches k_resolve
+build's small pre-resolution dispatch is left out). A views batch of >= 2^19 strings runs a LEAN
+first pass and a subset pass per step: the two are summed as one step (per_step_lean). In config 4 every step launches k_resolve
 twice (the interpolation, then the unescape command's second resolve): the roofline kernel is the
 first, so every other batch-sized dispatch counts, starting with the first. Both counters are in KB.
 
@@ -36,6 +37,36 @@ def fused_unescape(name):
     return bool(m and m.group(4) == "1")
 
 
+def flags(name):
+    """k_resolve's template flags (FAILC, MULTI, VIEWS, UNESC, LK, LEAN) from a kernel name."""
+    m = re.search(r"k_resolve<([^>]*)>", name)
+    if m:
+        f = [a.strip() == "true" for a in m.group(1).split(",")]
+    else:
+        f = [b == "1" for b in re.findall(r"Lb([01])E", name.split("k_resolve", 1)[-1])]
+    return (f + [False] * 6)[:6]
+
+
+def per_step_lean(big):
+    """A views batch that runs the LEAN first pass (the default at >= 2^19 strings): a step is the
+    LEAN dispatch plus the subset pass right after it (same grid, not LEAN, not the fused command);
+    packed-layout dispatches (not VIEWS) and the fused command are left out."""
+    vals, i = [], 0
+    while i < len(big):
+        v, nm = big[i]
+        f = flags(nm)
+        if f[5]:
+            tot = v
+            if i + 1 < len(big):
+                f2 = flags(big[i + 1][1])
+                if f2[2] and not f2[3] and not f2[5]:
+                    tot += big[i + 1][0]
+                    i += 1
+            vals.append(tot)
+        i += 1
+    return vals
+
+
 def per_dispatch(d, counter, cfg):
     rows = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
@@ -46,7 +77,9 @@ def per_dispatch(d, counter, cfg):
                 rows.setdefault(k, [g, 0.0, r["Kernel_Name"]])[1] += float(r["Counter_Value"])
     gmax = max(g for g, _, _ in rows.values())
     big = [(v, name) for k, (g, v, name) in sorted(rows.items()) if g == gmax]
-    if cfg == 4 and any(fused_unescape(nm) for _, nm in big):
+    if any(flags(nm)[5] for _, nm in big):
+        vals = per_step_lean(big)
+    elif cfg == 4 and any(fused_unescape(nm) for _, nm in big):
         # views: each step is the interpolation, the fused command, its deferred subset: the
         # roofline kernel is the dispatch right before each fused one
         vals = [big[i][0] for i in range(len(big) - 1) if not fused_unescape(big[i][1]) and fused_unescape(big[i + 1][1])]
