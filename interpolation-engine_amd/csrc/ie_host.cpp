@@ -17,6 +17,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <iterator>
 #include <mutex>
 #include <string>
 #include <string_view>
@@ -955,40 +956,86 @@ bool replace_all(ie_table* t, const Entry& extra) {
 }  // extern "C++"
 
 // Entries -> perfect-hash table on the device.
+// a placement to reuse (the pre-resolution's second upload: same keys, same slots)
+struct Placement {
+  uint64_t seed, m;
+  uint32_t nb;
+  std::vector<uint16_t> pilots;
+  std::vector<uint32_t> slot_of;
+};
+
 int upload_table(const std::vector<Ent>& ents, uint32_t n_tables, int32_t dialect, uint32_t flags,
-                 int32_t device, ie_table** out) {
-  HostArena arena;
-  std::vector<Entry> items;
-  items.reserve(ents.size());
+                 int32_t device, ie_table** out, const Placement* reuse = nullptr,
+                 std::vector<uint32_t>* slots_out = nullptr) {
+  // the arena's layout first (every entry's place, serially: a prefix sum), then the bytes, the
+  // entries and the key hashes across the host threads
+  const uint64_t ne = ents.size();
+  std::vector<uint64_t> at(ne + 1, 0), toffs(ne);
   uint64_t maxtext = 8;
   bool long_keys = false;
-  for (const Ent& e : ents) {
-    long_keys |= e.key.size() > kInlineKey && e.key.size() <= 2 * kInlineKey;
-    while (arena.size() & 3) arena.push_back(0);  // texts 4-byte aligned (dword copies)
-    if (e.flags & EF_RAWALT) {  // [raw text][u32 raw length] right before the splice text
-      arena.insert(arena.end(), e.raw.begin(), e.raw.end());
-      while (arena.size() & 3) arena.push_back(0);
-      const uint32_t rl = (uint32_t)e.raw.size();
-      arena.insert(arena.end(), (const uint8_t*)&rl, (const uint8_t*)&rl + 4);
-      maxtext = std::max<uint64_t>(maxtext, e.raw.size());
+  {
+    uint64_t pos = 0;
+    for (uint64_t i = 0; i < ne; i++) {
+      const Ent& e = ents[i];
+      long_keys |= e.key.size() > kInlineKey && e.key.size() <= 2 * kInlineKey;
+      if (e.key.size() >= 0xFFFFFFF0ull || e.text.size() >= 0xFFFFFFF0ull) return fail(IE_ERR_INVALID, "key or text above 4 GiB");
+      pos = (pos + 3) & ~3ull;  // texts 4-byte aligned (dword copies)
+      at[i] = pos;
+      if (e.flags & EF_RAWALT) {  // [raw text][u32 raw length] right before the splice text
+        pos = ((pos + e.raw.size() + 3) & ~3ull) + 4;
+        maxtext = std::max<uint64_t>(maxtext, e.raw.size());
+      }
+      toffs[i] = pos;
+      pos = ((pos + e.text.size() + 3) & ~3ull) + e.key.size();  // the key follows at key_off_of(toff, len)
+      maxtext = std::max<uint64_t>(maxtext, e.text.size());
+      if (pos >= 0xFFFFFFF0ull) return fail(IE_ERR_INVALID, "table arena above 4 GiB");
     }
-    const uint64_t toff = arena.size();
-    arena.insert(arena.end(), e.text.begin(), e.text.end());
-    while (arena.size() & 3) arena.push_back(0);  // the key follows at key_off_of(toff, len)
-    arena.insert(arena.end(), e.key.begin(), e.key.end());
-    if (arena.size() >= 0xFFFFFFF0ull) return fail(IE_ERR_INVALID, "table arena above 4 GiB");
-    if (e.key.size() >= 0xFFFFFFF0ull || e.text.size() >= 0xFFFFFFF0ull) return fail(IE_ERR_INVALID, "key or text above 4 GiB");
-    maxtext = std::max<uint64_t>(maxtext, e.text.size());
-    Entry b{};
-    b.key_len = (uint32_t)e.key.size();
-    b.text_len = (uint32_t)e.text.size();
-    b.vid = e.vid;
-    b.flags = e.flags | EF_OCCUPIED | (e.tid << kTidShift);
-    b.text_off = (uint32_t)toff;
-    memcpy(b.key, e.key.data(), std::min<size_t>(e.key.size(), kInlineKey));
-    memcpy(b.text, e.text.data(), std::min<size_t>(e.text.size(), kInlineText));
-    items.push_back(b);
+    at[ne] = pos;
   }
+  HostArena arena;
+  arena.grow(at[ne]);
+  std::vector<Entry> items(ne);
+  std::vector<uint64_t> hs0(ne);
+  const uint64_t seed0 = reuse ? reuse->seed : 0xA0761D6478BD642Full;
+  parallel_for(ne, at[ne] + 64 * ne, [&](uint64_t lo, uint64_t hi) {
+    uint8_t* const a = arena.data();
+    for (uint64_t i = lo; i < hi; i++) {
+      const Ent& e = ents[i];
+      uint64_t p = at[i];
+      if (e.flags & EF_RAWALT) {
+        memcpy(a + p, e.raw.data(), e.raw.size());
+        const uint64_t q = (p + e.raw.size() + 3) & ~3ull;
+        memset(a + p + e.raw.size(), 0, q - p - e.raw.size());
+        const uint32_t rl = (uint32_t)e.raw.size();
+        memcpy(a + q, &rl, 4);
+        p = q + 4;
+      }
+      memcpy(a + p, e.text.data(), e.text.size());
+      const uint64_t ko = (p + e.text.size() + 3) & ~3ull;
+      memset(a + p + e.text.size(), 0, ko - p - e.text.size());
+      memcpy(a + ko, e.key.data(), e.key.size());
+      const uint64_t end = ko + e.key.size();
+      memset(a + end, 0, at[i + 1] - end);  // (the pad before the next entry)
+      Entry b{};
+      b.key_len = (uint32_t)e.key.size();
+      b.text_len = (uint32_t)e.text.size();
+      b.vid = e.vid;
+      b.flags = e.flags | EF_OCCUPIED | (e.tid << kTidShift);
+      b.text_off = (uint32_t)toffs[i];
+      memcpy(b.key, e.key.data(), std::min<size_t>(e.key.size(), kInlineKey));
+      memcpy(b.text, e.text.data(), std::min<size_t>(e.text.size(), kInlineText));
+      items[i] = b;
+      hs0[i] = key_hash(e.key, seed0, e.tid);
+    }
+  });
+  uint64_t hs_seed = seed0;  // (the seed hs0 was computed under)
+  auto rehash = [&](uint64_t sd) {
+    if (sd == hs_seed) return;
+    parallel_for(ne, 32 * ne, [&](uint64_t lo, uint64_t hi) {
+      for (uint64_t i = lo; i < hi; i++) hs0[i] = key_hash(ents[i].key, sd, ents[i].tid);
+    });
+    hs_seed = sd;
+  };
   // perfect-hash placement: about 4 keys per pilot group at load 0.8 (entries 64 B: a 100k-key
   // table is 8 MB of entries and 50 KB of L2-resident pilots). A failed search changes the seed
   // (two keys with one 64-bit hash can never be separated) and then grows the table.
@@ -997,14 +1044,21 @@ int upload_table(const std::vector<Ent>& ents, uint32_t n_tables, int32_t dialec
   // and 4 when the table is full, so that a group can be placed again around new keys)
   const bool mut = (flags & IE_TABLE_MUTABLE) != 0;
   uint64_t m = std::max<uint64_t>(16, mut ? 2 * nk + 16 : nk + nk / 4 + 1);
-  const uint32_t nb = (uint32_t)std::max<uint64_t>(1, ((mut ? m : nk) + 3) / 4);
-  uint64_t seed = 0xA0761D6478BD642Full;
+  const uint32_t nb = reuse ? reuse->nb : (uint32_t)std::max<uint64_t>(1, ((mut ? m : nk) + 3) / 4);
+  uint64_t seed = seed0;
   std::vector<uint16_t> pilots;
   std::vector<uint32_t> slot_of;
   // the one-trip table experiment (IE_CUCKOO=1 with a k_resolve built -DIE_CUCKOO): two-choice
   // placement at load 0.4, no pilots; such a table takes no ie_table_set_update
   static const bool cuckoo = getenv("IE_CUCKOO") && atoi(getenv("IE_CUCKOO")) == 1;
-  if (cuckoo) {
+  bool placed = false;
+  if (reuse && !cuckoo && reuse->slot_of.size() == items.size()) {
+    placed = true;
+    seed = reuse->seed;
+    m = reuse->m;
+    pilots = reuse->pilots;
+    slot_of = reuse->slot_of;
+  } else if (cuckoo) {
     m = std::max<uint64_t>(16, (5 * nk) / 2 + 16);
     pilots.assign(nb, 0);
     for (int attempt = 0;; attempt++) {
@@ -1039,16 +1093,17 @@ int upload_table(const std::vector<Ent>& ents, uint32_t n_tables, int32_t dialec
       seed = fmix64_host(seed + 0x9E3779B97F4A7C15ull);
     }
   }
-  for (int attempt = 0; !cuckoo; attempt++) {
+  for (int attempt = 0; !cuckoo && !placed; attempt++) {  // (a failed ph_place leaves slot_of sized: the flag ends the loop)
     if (m > (1ull << 31)) return fail(IE_ERR_INVALID, "table too large");
-    std::vector<uint64_t> hs(items.size());
-    for (size_t i = 0; i < items.size(); i++) hs[i] = key_hash(ents[i].key, seed, ents[i].tid);
-    if (ph_place(hs, m, nb, pilots, slot_of)) break;
+    rehash(seed);
+    if ((placed = ph_place(hs0, m, nb, pilots, slot_of))) break;
     if (attempt & 1) m += m / 4;
     else seed = fmix64_host(seed + 0x9E3779B97F4A7C15ull);
   }
+  rehash(seed);  // (the groups below: the hashes under the final seed)
   std::vector<Entry> entries(m);
   for (size_t i = 0; i < items.size(); i++) entries[slot_of[i]] = items[i];
+  if (slots_out) *slots_out = slot_of;
   ie_table* t = new ie_table();
   t->groups.assign(nb, {});
   t->clock_slots.assign(2ull * n_tables, UINT32_MAX);
@@ -1056,7 +1111,7 @@ int upload_table(const std::vector<Ent>& ents, uint32_t n_tables, int32_t dialec
     if (items[i].vid == IE_VID_CLOCK_HHMM || items[i].vid == IE_VID_CLOCK_HHMMSS)
       t->clock_slots[2ull * ents[i].tid + (items[i].vid == IE_VID_CLOCK_HHMMSS)] = slot_of[i];
     if (items[i].flags & EF_RAWALT) t->rawalt[ents[i].tid].push_back(slot_of[i]);
-    t->groups[ph_group(key_hash(ents[i].key, seed, ents[i].tid), nb)].push_back(slot_of[i]);
+    t->groups[ph_group(hs0[i], nb)].push_back(slot_of[i]);
   }
   t->device = device;
   t->dialect = dialect;
@@ -1116,7 +1171,7 @@ int upload_table(const std::vector<Ent>& ents, uint32_t n_tables, int32_t dialec
 // under the build clock and under a second clock that differs in every field, and a value whose
 // status or text differs stays raw, so ie_table_set_clock never leaves a stale time behind.
 int preresolve(ie_table* t0, std::vector<Ent>& ents, uint32_t n_tables, int32_t dialect, uint32_t flags,
-               int32_t device, const ie_clock& clock, ie_table** out) {
+               int32_t device, const ie_clock& clock, ie_table** out, std::vector<uint32_t>& slots) {
   auto clean_value = [](std::string_view v, bool need_brace) {
     size_t opens = 0;
     int64_t depth = 0;
@@ -1204,8 +1259,10 @@ int preresolve(ie_table* t0, std::vector<Ent>& ents, uint32_t n_tables, int32_t 
   ie_batch_free(b);
   ie_batch_free(b2);
   if (!changed) return IE_SUCCESS;
+  // the same keys at the same slots: t0's placement, only the texts and the arena laid out again
+  const Placement P{t0->dev.seed, t0->dev.m, t0->dev.nb, t0->h_pilots, std::move(slots)};
   ie_table* t1 = nullptr;
-  rc = upload_table(ents, n_tables, dialect, flags, device, &t1);
+  rc = upload_table(ents, n_tables, dialect, flags, device, &t1, &P);
   if (rc) return rc;
   ie_table_free(t0);
   *out = t1;
@@ -1221,44 +1278,74 @@ int ie_table_set_build(const ie_kv* kv, const uint64_t* kv_start, uint32_t n_tab
     if (kv_start[t + 1] < kv_start[t]) return fail(IE_ERR_INVALID, "kv_start must be non-decreasing");
   int rc = set_device(device);
   if (rc) return rc;
+  Trace tr("build");
   char hhmm[16], hhmmss[16];
   const int h = now ? now->hour : 0, mi = now ? now->minute : 0, se = now ? now->second : 0;
   snprintf(hhmm, sizeof hhmm, "%02d:%02d", h, mi);
   snprintf(hhmmss, sizeof hhmmss, "%02d:%02d:%02d", h, mi, se);
-  std::vector<Ent> ents;
-  ents.reserve(kv_start[n_tables] - kv_start[0] + 2ull * n_tables);
-  std::unordered_map<std::string_view, uint64_t> last;
-  std::vector<uint64_t> order;
-  for (uint32_t tb = 0; tb < n_tables; tb++) {
-    // dict semantics per table: the last duplicate wins; '' is never looked up (py:446 / interp.rs:105)
-    last.clear();
-    order.clear();
-    for (uint64_t i = kv_start[tb]; i < kv_start[tb + 1]; i++) {
-      std::string_view k(kv[i].key ? kv[i].key : "", kv[i].key_len);
-      if (k.empty()) continue;
-      auto it = last.find(k);
-      if (it == last.end()) {
-        last.emplace(k, i);
-        order.push_back(i);
-      } else {
-        it->second = i;
+  // every table's entries (dict semantics per table: the last duplicate wins; '' is never looked up,
+  // py:446 / interp.rs:105), tables split over the host threads, then concatenated in table order
+  const unsigned T = (unsigned)std::min<uint64_t>(host_threads(), std::max<uint64_t>(1, n_tables / 256));
+  std::vector<std::vector<Ent>> part(T);
+  std::vector<int> part_rc(T, IE_SUCCESS);
+  parallel_for(T, T > 1 ? ~0ull : 0ull, [&](uint64_t lo, uint64_t hi) {
+    for (uint64_t k = lo; k < hi; k++) {
+      const uint32_t t_lo = (uint32_t)((uint64_t)n_tables * k / T), t_hi = (uint32_t)((uint64_t)n_tables * (k + 1) / T);
+      std::vector<Ent>& out = part[k];
+      out.reserve(kv_start[t_hi] - kv_start[t_lo] + 2ull * (t_hi - t_lo));
+      std::unordered_map<std::string_view, uint64_t> last;
+      std::vector<uint64_t> order;
+      for (uint32_t tb = t_lo; tb < t_hi && part_rc[k] == IE_SUCCESS; tb++) {
+        last.clear();
+        order.clear();
+        for (uint64_t i = kv_start[tb]; i < kv_start[tb + 1]; i++) {
+          std::string_view key(kv[i].key ? kv[i].key : "", kv[i].key_len);
+          if (key.empty()) continue;
+          auto it = last.find(key);
+          if (it == last.end()) {
+            last.emplace(key, i);
+            order.push_back(i);
+          } else {
+            it->second = i;
+          }
+        }
+        for (uint64_t i : order) {
+          std::string_view key(kv[i].key, kv[i].key_len);
+          const uint64_t j = last[key];
+          if (key == "HH:MM" || key == "HH:MM:SS") continue;  // py:433-436: the clock always wins
+          if (kv[j].kind < 0 || kv[j].kind > IE_KIND_DICT) {
+            part_rc[k] = IE_ERR_INVALID;  // (bad kind)
+            break;
+          }
+          if (j >= IE_VID_CLOCK_HHMMSS) {
+            part_rc[k] = IE_ERR_CAPACITY;  // (more inserts than value ids)
+            break;
+          }
+          std::string_view tx(kv[j].text ? kv[j].text : "", kv[j].text_len);
+          out.push_back(Ent{key, tx, kind_flags(kv[j].kind, dialect) | text_flags(tx), (uint32_t)j, tb, {}});
+        }
+        out.push_back(Ent{"HH:MM", hhmm, kind_flags(IE_KIND_STR, dialect) | text_flags(hhmm), IE_VID_CLOCK_HHMM, tb, {}});
+        out.push_back(Ent{"HH:MM:SS", hhmmss, kind_flags(IE_KIND_STR, dialect) | text_flags(hhmmss), IE_VID_CLOCK_HHMMSS,
+                          tb, {}});
       }
     }
-    for (uint64_t i : order) {
-      std::string_view k(kv[i].key, kv[i].key_len);
-      const uint64_t j = last[k];
-      if (k == "HH:MM" || k == "HH:MM:SS") continue;  // py:433-436: the clock always wins
-      if (kv[j].kind < 0 || kv[j].kind > IE_KIND_DICT) return fail(IE_ERR_INVALID, "bad kind");
-      if (j >= IE_VID_CLOCK_HHMMSS) return fail(IE_ERR_INVALID, "more inserts than value ids");
-      std::string_view t(kv[j].text ? kv[j].text : "", kv[j].text_len);
-      ents.push_back(Ent{k, t, kind_flags(kv[j].kind, dialect) | text_flags(t), (uint32_t)j, tb, {}});
-    }
-    ents.push_back(Ent{"HH:MM", hhmm, kind_flags(IE_KIND_STR, dialect) | text_flags(hhmm), IE_VID_CLOCK_HHMM, tb, {}});
-    ents.push_back(Ent{"HH:MM:SS", hhmmss, kind_flags(IE_KIND_STR, dialect) | text_flags(hhmmss), IE_VID_CLOCK_HHMMSS,
-                       tb, {}});
+  });
+  for (unsigned k = 0; k < T; k++) {
+    if (part_rc[k] == IE_ERR_INVALID) return fail(IE_ERR_INVALID, "bad kind");
+    if (part_rc[k] != IE_SUCCESS) return fail(IE_ERR_INVALID, "more inserts than value ids");
   }
+  std::vector<Ent> ents;
+  {
+    uint64_t total = 0;
+    for (const auto& v : part) total += v.size();
+    ents.reserve(total);
+    for (auto& v : part) std::move(v.begin(), v.end(), std::back_inserter(ents));
+  }
+  tr.mark("entries", ents.size());
   ie_table* t0 = nullptr;
-  rc = upload_table(ents, n_tables, dialect, flags, device, &t0);
+  std::vector<uint32_t> slots;
+  rc = upload_table(ents, n_tables, dialect, flags, device, &t0, nullptr, &slots);
+  tr.mark("upload", ents.size());
   if (rc || getenv("IE_NO_PRERESOLVE")) {  // diagnostic switch: raw splice texts only
     *out = t0;
     if (t0) t0->next_vid = (uint32_t)std::min<uint64_t>(kv_start[n_tables], IE_VID_CLOCK_HHMMSS);
@@ -1266,7 +1353,8 @@ int ie_table_set_build(const ie_kv* kv, const uint64_t* kv_start, uint32_t n_tab
   }
   *out = t0;
   const ie_clock clk{h, mi, se};
-  rc = preresolve(t0, ents, n_tables, dialect, flags, device, clk, out);
+  rc = preresolve(t0, ents, n_tables, dialect, flags, device, clk, out, slots);
+  tr.mark("pre-resolve", ents.size());
   if (rc) {
     ie_table_free(*out);
     *out = nullptr;
