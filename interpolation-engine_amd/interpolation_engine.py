@@ -723,8 +723,13 @@ def get_simple_insertkey(content):
             if c == insert_start:
                 depth += 1
         return content[1:-1]
-    if content[0] != insert_start or content[-1] != insert_stop:  # (the loop fails at once, py:487-492)
+    # (the loop's depth must be non-zero at every inner position: no brace at all fails at the second
+    # character; '{key}' with a brace-free key passes; the rest, e.g. 'b}{a' -> '}{', takes the loop)
+    if insert_start not in content and insert_stop not in content:
         return None
+    inner = content[1:-1]
+    if content[0] == insert_start and content[-1] == insert_stop and insert_start not in inner and insert_stop not in inner:
+        return inner
     b = N.enc(content)
     o, l = ctypes.c_uint64(), ctypes.c_uint64()
     if N.lib().ie_simple_insertkey(b, len(b), 0, ctypes.byref(o), ctypes.byref(l)):

@@ -166,10 +166,9 @@ def _leaves(inserts, x, out):
     """recursive_replace's walk (py:1748-1759) without the string work: whole-string keys are
     resolved with get_interpdata on the host (py:1749-1754); returns a skeleton whose str leaves
     are indices into `out` (the strings replace_str must run on)."""
-    if type(x) == str and (len(x) <= 2 or x[0] != "{"):  # (not a whole-string key: a leaf as it is)
-        if len(x) > 2 or not IE.get_simple_insertkey(x):
-            out.append(x)
-            return ("__leaf__", len(out) - 1)
+    if type(x) == str and "{" not in x and "}" not in x:  # (no brace: never a whole-string key, a leaf)
+        out.append(x)
+        return ("__leaf__", len(out) - 1)
     k = IE.get_simple_insertkey(x)
     if k:
         sub = IE.get_simple_insertkey(k)

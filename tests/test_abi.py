@@ -127,3 +127,24 @@ def test_synthetic_strings_follow_the_spec(config):
                                           ctypes.byref(total)), "window")
     assert buf2[:int(total.value)].tobytes() == blob[int(offs[500]):int(offs[510])]
     N.lib().ie_synth_free(h)
+
+
+def test_simple_insertkey_fast_paths_match_the_loop():
+    # the mirror's pure-Python shortcuts (no '{' first / '}' last; a brace-free '{key}') against the
+    # reference's loop (py:484-495) restated here, on random brace strings
+    import random
+
+    def loop(content):
+        depth = 0
+        for i, c in enumerate(content):
+            if c == "}":
+                depth -= 1
+            if (depth == 0) != (i == 0 or i == len(content) - 1):
+                return None
+            if c == "{":
+                depth += 1
+        return content[1:-1]
+    rng = random.Random(12)
+    for _ in range(20000):
+        s = "".join(rng.choice("{}ab\\") for _ in range(rng.randrange(0, 9)))
+        assert PKG.get_simple_insertkey(s) == loop(s), s
