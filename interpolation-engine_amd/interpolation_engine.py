@@ -156,6 +156,8 @@ class InsertsTableSet:
             return "%02d:%02d:%02d" % self.clock
         v = self.values[vid]
         if v is _IN_TABLE:  # a str / int stored by update(): read back from the table's mirror
+            if not getattr(self, "h", None):
+                raise RuntimeError("the table set is closed: a stored value is read back from its table")
             k, p, n = ctypes.c_int32(), ctypes.c_void_p(), ctypes.c_uint64()
             N.check(N.lib().ie_table_value(self.h, vid, ctypes.byref(k), ctypes.byref(p), ctypes.byref(n)),
                     "ie_table_value")
