@@ -668,6 +668,11 @@ def run_map_tasks(states, tasks, dialect="py", device=0):
     removed (py:1843-1868) in place on its device copy (ie_table_set_update) before the next task.
     Returns one list of per-state outcomes per task."""
     outs, tset = [], None
+    # (the cyclic collector paused for the run: the states' objects are millions, and a full
+    # collection in the middle of a step costs tens of ms; the run creates no cycles of its own)
+    import gc
+    gc_was = gc.isenabled()
+    gc.disable()
     try:
         for task in tasks:
             if tset is None:
@@ -692,6 +697,8 @@ def run_map_tasks(states, tasks, dialect="py", device=0):
                 tset.close()
                 tset = None
     finally:
+        if gc_was:
+            gc.enable()
         if tset is not None:
             tset.close()
     return outs
