@@ -21,8 +21,10 @@ host glue with the reference's exact semantics. Every string interpolation, esca
 unescape runs on the device; without libie_amd.so or a GPU the calls raise.
 """
 import copy
+import contextlib
 import ctypes
 import datetime as _dt
+import gc
 import json
 import os
 import re
@@ -38,6 +40,20 @@ inserts_dir = None  # py:44 — when set, get_interpdata falls back to its files
 
 DELETE = object()  # InsertsTableSet.update: remove the key (`del inserts[key]`)
 _IN_TABLE = object()  # InsertsTableSet.values: a str / int the table's mirror holds (value() reads it)
+
+
+@contextlib.contextmanager
+def _gc_paused():
+    """The cyclic collector off for a bulk step (a store, a build, a map run): the callers' heaps hold
+    millions of objects, and a full collection in the middle costs tens of ms; the steps create no
+    cycles of their own."""
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 
 
 class InterpolationException(Exception):
@@ -120,8 +136,9 @@ class InsertsTableSet:
         # the ie_kv records of every dict in one native pass (csrc/ie_pack.c: pointers into the
         # str objects, the texts that are not ASCII transcoded across host threads): a table set of
         # many states holds ~10^5 entries
-        kvb, stb, keep = N.pack_module().pack_dicts([d if isinstance(d, dict) else dict(d) for d in self.dicts],
-                                                     render, dialect, N.host_threads())
+        with _gc_paused():
+            kvb, stb, keep = N.pack_module().pack_dicts([d if isinstance(d, dict) else dict(d) for d in self.dicts],
+                                                         render, dialect, N.host_threads())
         cb = ctypes.c_char * len(kvb)
         h = ctypes.c_void_p()
         clk = N.Clock(*self.clock)
@@ -181,6 +198,10 @@ class InsertsTableSet:
             return True
         P = N.pack_module()
         tp = time.perf_counter()
+        with _gc_paused():  # (no cyclic collection over the caller's heap in the middle of a store)
+            return self._store(P, changes, n, tp)
+
+    def _store(self, P, changes, n, tp):
         kv, tids, keep = P.pack(changes, len(self.dicts), DELETE, render, self.dialect, N.host_threads())
         vids = bytearray(4 * n)
         cv = ctypes.c_char * (4 * n)

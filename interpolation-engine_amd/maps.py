@@ -673,7 +673,7 @@ def run_map_tasks(states, tasks, dialect="py", device=0):
     import gc
     gc_was = gc.isenabled()
     gc.disable()
-    try:
+    try:  # (interpolation_engine._gc_paused's rule, kept inline: the finally also closes the table set)
         for task in tasks:
             if tset is None:
                 tset = IE.InsertsTableSet(states, dialect=dialect, device=device, mutable=True)
