@@ -31,8 +31,8 @@ enum { KIND_STR = 0, KIND_INT = 1 };
 #endif
 __attribute__((used)) static const char kPackId[] = "IE_BUILD_ID:" IE_PACK_ID;  // (__graft_entry__.built_id)
 
-// A text that is not ASCII: transcoded into the call's buffer (its offset there found by a count
-// pass), both passes across the threads with the GIL released (the strs are immutable and the
+// A text that is not ASCII: transcoded into the call's buffer (one pass, each thread's jobs back to
+// back in a region sized by their bounds), across the threads with the GIL released (the strs are immutable and the
 // changes list keeps them alive)
 typedef struct {
   const void* src;
@@ -63,94 +63,107 @@ static inline uint8_t* put_cp(uint8_t* o, uint32_t c) {  // one code point (surr
   return o;
 }
 
-static uint64_t utf8_len(const job_t* j) {
-  if (j->kind == KIND_JOB_INT) {
-    char tmp[24];
-    return (uint64_t)snprintf(tmp, sizeof tmp, "%lld", (long long)j->ival);
-  }
-  uint64_t n = j->len;
-  if (j->kind == 1) {
-    const uint8_t* d = (const uint8_t*)j->src;
-    for (uint64_t i = 0; i < j->len; i++) n += d[i] >> 7;
-  } else if (j->kind == 2) {
-    const uint16_t* d = (const uint16_t*)j->src;
-    for (uint64_t i = 0; i < j->len; i++) n += (d[i] >= 0x80) + (d[i] >= 0x800);
-  } else {
-    const uint32_t* d = (const uint32_t*)j->src;
-    for (uint64_t i = 0; i < j->len; i++) n += (d[i] >= 0x80) + (d[i] >= 0x800) + (d[i] >= 0x10000);
-  }
-  return n;
+// the most UTF-8 bytes a job can make (the output buffer is sized by these: one pass, no count pass
+// over the source first)
+static uint64_t utf8_bound(const job_t* j) {
+  if (j->kind == KIND_JOB_INT) return 24;
+  return j->len * (j->kind == 4 ? 4u : j->kind == 2 ? 3u : 2u);
 }
 
-static void transcode(const job_t* j, uint8_t* o) {  // (runs of ASCII 8-16 units at a time)
+// the job's UTF-8 at o; returns the bytes written (16 units at a time where all are ASCII)
+static uint64_t transcode(const job_t* j, uint8_t* o) {
   if (j->kind == KIND_JOB_INT) {
     char tmp[24];
     const int n = snprintf(tmp, sizeof tmp, "%lld", (long long)j->ival);
     memcpy(o, tmp, (size_t)n);
-    return;
+    return (uint64_t)n;
   }
+  uint8_t* const o0 = o;
   const uint64_t len = j->len;
   uint64_t i = 0;
+  // 16 units at a time: the block's ASCII units packed to bytes and stored whole, `o` advanced past
+  // the ASCII prefix only; the first wider unit after it is written on its own, and the next block
+  // starts right after it (a slot's bound leaves room for the 16-byte store)
   if (j->kind == 1) {
     const uint8_t* d = (const uint8_t*)j->src;
-    while (i < len) {
-      if (i + 16 <= len) {
-        const __m128i v = _mm_loadu_si128((const __m128i*)(d + i));
-        if (!_mm_movemask_epi8(v)) {
-          _mm_storeu_si128((__m128i*)o, v);
-          o += 16;
-          i += 16;
-          continue;
-        }
+    while (i + 16 <= len) {
+      const __m128i v = _mm_loadu_si128((const __m128i*)(d + i));
+      _mm_storeu_si128((__m128i*)o, v);
+      const unsigned wide = (unsigned)_mm_movemask_epi8(v);
+      if (!wide) {
+        o += 16;
+        i += 16;
+        continue;
       }
-      o = put_cp(o, d[i++]);
+      const unsigned p = (unsigned)__builtin_ctz(wide);
+      o = put_cp(o + p, d[i + p]);
+      i += p + 1;
     }
   } else if (j->kind == 2) {
     const uint16_t* d = (const uint16_t*)j->src;
     const __m128i hi = _mm_set1_epi16((short)0xFF80);
-    while (i < len) {
-      if (i + 8 <= len) {
-        const __m128i v = _mm_loadu_si128((const __m128i*)(d + i));
-        if (_mm_movemask_epi8(_mm_cmpeq_epi16(_mm_and_si128(v, hi), _mm_setzero_si128())) == 0xFFFF) {
-          _mm_storel_epi64((__m128i*)o, _mm_packus_epi16(v, v));
-          o += 8;
-          i += 8;
-          continue;
-        }
+    while (i + 16 <= len) {
+      const __m128i v0 = _mm_loadu_si128((const __m128i*)(d + i)), v1 = _mm_loadu_si128((const __m128i*)(d + i + 8));
+      _mm_storeu_si128((__m128i*)o, _mm_packus_epi16(v0, v1));
+      const __m128i a0 = _mm_cmpeq_epi16(_mm_and_si128(v0, hi), _mm_setzero_si128());
+      const __m128i a1 = _mm_cmpeq_epi16(_mm_and_si128(v1, hi), _mm_setzero_si128());
+      const unsigned wide = ~(unsigned)_mm_movemask_epi8(_mm_packs_epi16(a0, a1)) & 0xFFFFu;
+      if (!wide) {
+        o += 16;
+        i += 16;
+        continue;
       }
-      o = put_cp(o, d[i++]);
+      const unsigned p = (unsigned)__builtin_ctz(wide);
+      o = put_cp(o + p, d[i + p]);
+      i += p + 1;
     }
   } else {
     const uint32_t* d = (const uint32_t*)j->src;
     const __m128i hi = _mm_set1_epi32((int)0xFFFFFF80u);
-    while (i < len) {
-      if (i + 8 <= len) {
-        const __m128i v0 = _mm_loadu_si128((const __m128i*)(d + i)), v1 = _mm_loadu_si128((const __m128i*)(d + i + 4));
-        const __m128i z = _mm_cmpeq_epi32(_mm_and_si128(_mm_or_si128(v0, v1), hi), _mm_setzero_si128());
-        if (_mm_movemask_epi8(z) == 0xFFFF) {
-          const __m128i w = _mm_packs_epi32(v0, v1);  // (all < 0x80: no saturation)
-          _mm_storel_epi64((__m128i*)o, _mm_packus_epi16(w, w));
-          o += 8;
-          i += 8;
-          continue;
-        }
+    while (i + 16 <= len) {
+      const __m128i v0 = _mm_loadu_si128((const __m128i*)(d + i)), v1 = _mm_loadu_si128((const __m128i*)(d + i + 4));
+      const __m128i v2 = _mm_loadu_si128((const __m128i*)(d + i + 8)), v3 = _mm_loadu_si128((const __m128i*)(d + i + 12));
+      // (an ASCII lane packs to itself; a wider one's byte is garbage, past the prefix kept)
+      _mm_storeu_si128((__m128i*)o, _mm_packus_epi16(_mm_packs_epi32(v0, v1), _mm_packs_epi32(v2, v3)));
+      const __m128i z = _mm_setzero_si128();
+      const __m128i a01 = _mm_packs_epi32(_mm_cmpeq_epi32(_mm_and_si128(v0, hi), z), _mm_cmpeq_epi32(_mm_and_si128(v1, hi), z));
+      const __m128i a23 = _mm_packs_epi32(_mm_cmpeq_epi32(_mm_and_si128(v2, hi), z), _mm_cmpeq_epi32(_mm_and_si128(v3, hi), z));
+      const unsigned wide = ~(unsigned)_mm_movemask_epi8(_mm_packs_epi16(a01, a23)) & 0xFFFFu;
+      if (!wide) {
+        o += 16;
+        i += 16;
+        continue;
       }
-      o = put_cp(o, d[i++]);
+      const unsigned p = (unsigned)__builtin_ctz(wide);
+      o = put_cp(o + p, d[i + p]);
+      i += p + 1;
     }
   }
+  if (j->kind == 1)
+    for (const uint8_t* d = (const uint8_t*)j->src; i < len; i++) o = put_cp(o, d[i]);
+  else if (j->kind == 2)
+    for (const uint16_t* d = (const uint16_t*)j->src; i < len; i++) o = put_cp(o, d[i]);
+  else
+    for (const uint32_t* d = (const uint32_t*)j->src; i < len; i++) o = put_cp(o, d[i]);
+  return (uint64_t)(o - o0);
 }
 
 typedef struct {
   job_t* jobs;
   uint64_t lo, hi;
-  uint8_t* buf;  // NULL: the count pass
+  uint8_t* buf;
+  uint64_t base;  // the span's region: the bounds of the jobs before it
 } span_t;
 
+// a span's jobs back to back from its region's start (the region holds their bounds: the used
+// part is dense, and a reused buffer is touched in about the same pages call after call)
 static void* run_span(void* arg) {
   span_t* sp = (span_t*)arg;
+  uint64_t at = sp->base;
   for (uint64_t k = sp->lo; k < sp->hi; k++) {
-    if (sp->buf) transcode(&sp->jobs[k], sp->buf + sp->jobs[k].off);
-    else sp->jobs[k].out = utf8_len(&sp->jobs[k]);
+    sp->jobs[k].off = at;
+    sp->jobs[k].out = transcode(&sp->jobs[k], sp->buf + at);
+    at += sp->jobs[k].out;
   }
   return NULL;
 }
@@ -163,13 +176,14 @@ static void run_jobs(job_t* jobs, uint64_t n, uint8_t* buf, int threads) {
   if (threads < 1 || units < (1u << 20)) threads = 1;
   span_t sp[16];
   pthread_t th[16];
-  uint64_t k = 0, acc = 0;
+  uint64_t k = 0, acc = 0, bsum = 0;
   for (int w = 0; w < threads; w++) {
     sp[w].jobs = jobs;
     sp[w].buf = buf;
     sp[w].lo = k;
+    sp[w].base = bsum;
     const uint64_t want = units * (uint64_t)(w + 1) / (uint64_t)threads;
-    while (k < n && (acc < want || w == threads - 1)) acc += jobs[k].len * (uint64_t)jobs[k].kind, k++;
+    while (k < n && (acc < want || w == threads - 1)) acc += jobs[k].len * (uint64_t)jobs[k].kind, bsum += utf8_bound(&jobs[k]), k++;
     sp[w].hi = k;
   }
   int started[16] = {0};
@@ -237,8 +251,8 @@ static uint8_t* take_buf(size_t need, size_t* cap) {
     spare_cap = 0;
     return b;
   }
-  *cap = need;
-  return (uint8_t*)PyMem_RawMalloc(need);
+  *cap = need + need / 4;  // (headroom: a loop's texts grow call by call, and a fresh buffer faults again)
+  return (uint8_t*)PyMem_RawMalloc(*cap);
 }
 
 typedef struct {
@@ -318,18 +332,12 @@ static int pack_kv(PyObject* k, PyObject* v, kv_rec* r, uint64_t i, jobs_t* J, P
   return utf8_of(text, J, 2 * i + 1, &r->text, &r->text_len);
 }
 
-// the texts that are not ASCII: counted, placed, transcoded (across the threads, the GIL released);
-// then the records point there and `keep` holds the buffer
+// the texts that are not ASCII: transcoded into one buffer sized by their bounds (across the
+// threads, the GIL released); then the records point there and `keep` holds the buffer
 static int finish(kv_rec* kv, jobs_t* J, PyObject* keep, int threads) {
   if (!J->n) return 0;
   uint64_t total = 0;
-  Py_BEGIN_ALLOW_THREADS
-  run_jobs(J->p, J->n, NULL, threads);
-  Py_END_ALLOW_THREADS
-  for (uint64_t k = 0; k < J->n; k++) {
-    J->p[k].off = total;
-    total += J->p[k].out;
-  }
+  for (uint64_t k = 0; k < J->n; k++) total += utf8_bound(&J->p[k]);
   size_t cap = 0;
   uint8_t* buf = take_buf(total + 16, &cap);
   held_t* held = (held_t*)PyMem_RawMalloc(sizeof(held_t));
@@ -342,7 +350,7 @@ static int finish(kv_rec* kv, jobs_t* J, PyObject* keep, int threads) {
   held->p = buf;
   held->cap = cap;
   Py_BEGIN_ALLOW_THREADS
-  run_jobs(J->p, J->n, buf, threads);
+  run_jobs(J->p, J->n, buf, threads);  // (each job's .off / .out: where it wrote, how many bytes)
   Py_END_ALLOW_THREADS
   for (uint64_t k = 0; k < J->n; k++) {
     kv_rec* r = &kv[J->p[k].rec / 2];

@@ -92,3 +92,19 @@ def test_assign_holds_typed_values_only():
     values2 = []
     P.assign(values2, changes[:3], bytearray(memoryview(__import__("array").array("I", [2, 0, 1])).cast("B")), IE.DELETE)
     assert values2 == [7, [1], "text"]
+
+
+@pytest.mark.parametrize("threads", [1, 8])
+def test_pack_long_mixed_texts(threads):
+    """Long texts, mostly ASCII with a sprinkling of one wider kind (1-, 2- or 4-byte units): the
+    16-unit ASCII blocks, the blocks that fall back to unit-by-unit, and the tails."""
+    rng = random.Random(5 + threads)
+    wide = [["é", "ÿ", "\x80"], ["€", "〠", "\ud800", "\udfff"], ["😀", "\U0010ffff"]]
+    changes = []
+    for i in range(4000):
+        kinds = ["a", "{", " "] + rng.choice(wide)
+        s = "".join(rng.choice(kinds) if rng.random() < 0.1 else "x" for _ in range(rng.randrange(0, 300)))
+        changes.append((0, "k%d" % i, s))
+    kv, tids, keep = P.pack(changes, 1, IE.DELETE, IE.render, "py", threads)
+    for r, (_, k, v) in zip(_records(kv, len(changes)), changes):
+        assert ctypes.string_at(r.text, r.text_len) == N.enc(v), k
