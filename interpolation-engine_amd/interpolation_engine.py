@@ -39,6 +39,7 @@ inserts_dir = None  # py:44 — when set, get_interpdata falls back to its files
 
 
 DELETE = object()  # InsertsTableSet.update: remove the key (`del inserts[key]`)
+_NOT_DONE = object()  # InsertsTableSet.run1: the string needs results() (a failure, an inserts-directory key)
 _IN_TABLE = object()  # InsertsTableSet.values: a str / int the table's mirror holds (value() reads it)
 
 
@@ -268,6 +269,27 @@ class InsertsTableSet:
             return t
         return [(st, text(o) if st == N.OK_STR else (vids[i] if st == N.OK_VALUE else None))
                 for i, (o, st) in enumerate(zip(outs, sts))]
+
+    def run1(self, s):
+        """One str against dict 0 (a scalar interpolate_inserts): its result when the device
+        resolved it (a text or a stored value), else _NOT_DONE (the caller takes results(), which
+        builds the failure or completes an inserts-directory key). The same library call as run(),
+        without the list plumbing."""
+        x = get_exec(self.device)
+        b = N.enc(s)
+        res = ctypes.POINTER(N.BatchRes)()
+        lib = N.lib()
+        N.check(lib.ie_interpolate_batch(x.h, self.h, b, (ctypes.c_uint64 * 2)(0, len(b)), 1, ctypes.byref(res)),
+                "ie_interpolate_batch")
+        r = res.contents
+        st, vid, o0, o1 = r.status[0], r.value_id[0], r.offsets[0], r.offsets[1]
+        out = ctypes.string_at(r.bytes, o1)[o0:] if st == N.OK_STR and o1 else b""
+        lib.ie_batch_free(res)
+        if st == N.OK_STR:
+            return N.dec(out)
+        if st == N.OK_VALUE:
+            return self.value(vid)
+        return _NOT_DONE
 
     def results(self, strings, table_ids=None):
         """Like interpolate_inserts on each string; failures come back as exception instances."""
@@ -767,7 +789,12 @@ def interpolate_batch(inserts, contents, dialect="py", device=0):
 
 def interpolate_inserts(inserts, content):
     """py:497-541 — the drop-in. Raises exactly where the reference raises."""
-    r = table_for(inserts).results([content])[0]
+    t = table_for(inserts)
+    if type(content) is str:
+        r = t.run1(content)
+        if r is not _NOT_DONE:
+            return r
+    r = t.results([content])[0]
     if isinstance(r, BaseException):
         raise r
     return r
