@@ -199,6 +199,8 @@ class InsertsTableSet:
             return True
         P = N.pack_module()
         tp = time.perf_counter()
+        if n < 4096:  # (a few stores: no collection to fear, and the pause costs a µs of its own)
+            return self._store(P, changes, n, tp)
         with _gc_paused():  # (no cyclic collection over the caller's heap in the middle of a store)
             return self._store(P, changes, n, tp)
 

@@ -70,6 +70,17 @@ def main():
         ins["name"] = "Tom" if ins["name"] != "Tom" else "Ann"
         tt.refresh(ins)
     out["refresh_only"] = per_call(upd_only, 1000)
+    lib_s, split = [], []
+    for _ in range(500):
+        upd_only()
+        lib_s.append(tt.last_update_native_s)
+        split.append(tt.last_update_split_s)
+    lib_s.sort()
+    out["refresh_library_us_median"] = round(1e6 * lib_s[len(lib_s) // 2], 2)
+    out["refresh_pack_us_median"] = round(1e6 * sorted(x[0] for x in split)[len(split) // 2], 2)
+    out["refresh_values_us_median"] = round(1e6 * sorted(x[2] for x in split)[len(split) // 2], 2)
+    changes = [(0, "name", "Zed")]
+    out["update_1_us"] = per_call(lambda: tt.update(changes), 1000)
     print(json.dumps(out))
 
 
