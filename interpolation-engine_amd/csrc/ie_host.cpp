@@ -269,6 +269,7 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
   rc = ensure_work(x, op, n);
   if (rc) return rc;
   x->stamp_tiles = 0;
+  x->no_emit_used = false;
   if (op == kOpInterp && !x->stamps_path.empty()) {  // diagnostic build hook, see DESIGN.md
     const uint64_t tiles = (n + kRBlock - 1) / kRBlock;
     IE_HIP(x->stamps.ensure(tiles * 128));
@@ -343,7 +344,10 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
       IE_HIP(launch_resolve_deferring(B, W, t->dev, out->bytes, cap, (uint64_t*)x->u_off.p, (uint32_t*)x->u_len.p,
                                       d_tid ? (uint32_t*)x->u_tid.p : nullptr, st));
     } else {
-      IE_HIP(wide ? launch_resolve512(B, W, t->dev, out->bytes, cap, st) : launch_resolve(B, W, t->dev, out->bytes, cap, st));
+      // (a one-string call: k_resolve alone, one launch and its emit kernel's ~5 µs fewer)
+      const bool ne = x->small_no_emit && d_out_len && !wide && !W.reserve16 && !x->opt_noeval && n <= (uint64_t)kRBlock;
+      x->no_emit_used = ne;
+      IE_HIP(wide ? launch_resolve512(B, W, t->dev, out->bytes, cap, st) : launch_resolve(B, W, t->dev, out->bytes, cap, st, ne));
     }
     if (!x->stat_pending && !x->no_stats) {
       if (!x->stat_host) {
@@ -423,10 +427,14 @@ int run_host_small(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, 
   // (the adaptive fail-commit / deferral statistics come from the larger batches)
   x->no_stats = true;
   x->ctr_override = ctr_size ? dv + in_size : nullptr;
+  x->small_no_emit = ctr_size != 0 && views;  // (the deferred-tile count comes back with the counters)
   int rc = run_device(x, op, t, dv + i_bytes, (const uint64_t*)dv, n, &o,
                       table_id ? (const uint32_t*)(dv + i_tid) : nullptr, views ? (uint32_t*)(dout + o_len) : nullptr);
   x->no_stats = false;
   x->ctr_override = nullptr;
+  x->small_no_emit = false;
+  const bool no_emit = x->no_emit_used;
+  x->no_emit_used = false;
   if (rc) return rc;
   if (ctr_size) {
     IE_HIP(hipMemcpyAsync(h + in_size, dv + in_size, ctr_size + o_err, hipMemcpyDeviceToHost, x->stream));
@@ -438,6 +446,9 @@ int run_host_small(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, 
   const uint32_t err = ctr_size ? ((const uint32_t*)(h + in_size))[1] : *(const uint32_t*)(ho + o_err);  // (check_device_error's rules)
   if (err & 2u) return fail(IE_ERR_CAPACITY, "a step's output did not fit its caller-sized buffer");
   if (err) return fail(IE_ERR_TIMEOUT, "look-back spin timed out (a predecessor tile never published)");
+  // without the emit kernel a deferred tile's bytes were never written (counters word 9): the
+  // generic path runs the batch (as for an output beyond the first-guess capacity)
+  if (no_emit && ((const uint32_t*)(h + in_size))[9] != 0) return IE_SUCCESS;
   total = *(const uint64_t*)ho;
   if (total > cap) return IE_SUCCESS;
   b = new ie_batch{};

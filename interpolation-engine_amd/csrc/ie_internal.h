@@ -275,6 +275,8 @@ struct ie_exec {
   bool fail_commit = false;
   bool stat_pending = false;
   bool no_stats = false;  // run_host_small: no statistics copy (two stream operations of a scalar call)
+  bool small_no_emit = false;  // run_host_small: a one-tile views batch may skip k_emit_windows
+  bool no_emit_used = false;   // (run_device: it did; a deferred tile then needs the full path)
   uint8_t* ctr_override = nullptr;  // run_host_small: the counters in its own block, zeroed by its input copy
   uint64_t stat_n = 0;
   uint32_t* stat_host = nullptr;  // pinned

@@ -118,8 +118,10 @@ struct WcSet {
 hipError_t launch_wildcard(const WcSet& P, const uint8_t* bytes, const uint64_t* off, uint64_t n,
                            const uint32_t* range, int32_t* match, uint8_t* ncap, uint32_t* caps, hipStream_t st);
 
+// no_emit: a one-tile views batch without the emit kernel (k_resolve writes the total; a tile it
+// had to defer is left unwritten: the caller sees defer_count and runs the batch again in full)
 hipError_t launch_resolve(const Batch& B, const Work& W, const DevTable& T, uint8_t* out,
-                          uint64_t cap, hipStream_t st);
+                          uint64_t cap, hipStream_t st, bool no_emit = false);
 // the same with 512-string tiles (ie_resolve512.hip)
 hipError_t launch_resolve512(const Batch& B, const Work& W, const DevTable& T, uint8_t* out,
                              uint64_t cap, hipStream_t st);

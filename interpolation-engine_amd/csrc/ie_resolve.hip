@@ -1637,6 +1637,10 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(LK ? IE
     B.out_off[B.n] = base + tile_total;
     *W.total = base + tile_total;
   }
+  // views, one tile: the only claim on the cursor is this tile's, so the batch's total is its end
+  // (k_emit_windows writes the same; a one-tile scalar call may skip that kernel)
+  // (not in the LEAN first pass: its emit kernel always runs, and its code stays as it was)
+  if (VIEWS && !LEAN && gridDim.x == 1u && !W.reserve16 && !(W.debug_noeval & 2u) && tid == 0) *W.total = base + tile_total;
   const bool write_bytes = base + tile_total <= cap;  // caller's buffer too small: offsets only
   // (reserved ranges: *total is the sum of lengths, not the extent, so the flag tells the caller)
   if (VIEWS && W.reserve16 && !write_bytes && tid == 0) atomicOr(W.err, 2u);
@@ -1748,7 +1752,7 @@ __global__ __launch_bounds__(kRBlock) void k_unesc_deferred(Batch B, Work W, uin
 }
 
 hipError_t launch_resolve_impl(const Batch& B, const Work& W, const DevTable& T, uint8_t* out, uint64_t cap,
-                               hipStream_t st, bool unesc = false, bool lean = false) {
+                               hipStream_t st, bool unesc = false, bool lean = false, bool no_emit = false) {
   const uint64_t tiles = (B.n + kRBlock - 1) / kRBlock;
   if (!tiles) return hipSuccess;
   if (tiles > 0xFFFFFFFFull) return hipErrorInvalidValue;
@@ -1808,7 +1812,9 @@ hipError_t launch_resolve_impl(const Batch& B, const Work& W, const DevTable& T,
 #undef IE_LAUNCH
   }
   // the deferred (oversized) tiles' bytes (exits at once when there are none); views: the total
-  if (out || B.out_len) hipLaunchKernelGGL(k_emit_windows, dim3(grid < 512u ? grid : 512u), dim3(kRBlock), 0, st, B, W, T, out);
+  // (a one-tile views batch may go without it: no_emit, see launch_resolve)
+  if ((out || B.out_len) && !(no_emit && grid == 1u && B.out_len && !W.reserve16))
+    hipLaunchKernelGGL(k_emit_windows, dim3(grid < 512u ? grid : 512u), dim3(kRBlock), 0, st, B, W, T, out);
   return hipGetLastError();
 }
 
@@ -1911,8 +1917,8 @@ hipError_t launch_resolve512(const Batch& B, const Work& W, const DevTable& T, u
 }
 #else
 hipError_t launch_resolve(const Batch& B, const Work& W, const DevTable& T, uint8_t* out, uint64_t cap,
-                          hipStream_t st) {
-  return IE_RNS::launch_resolve_impl(B, W, T, out, cap, st);
+                          hipStream_t st, bool no_emit) {
+  return IE_RNS::launch_resolve_impl(B, W, T, out, cap, st, false, false, no_emit);
 }
 hipError_t launch_debug_probe(const DevTable& T, const uint8_t* key, uint32_t klen, uint64_t* out, hipStream_t st) {
   return IE_RNS::launch_debug_probe_impl(T, key, klen, out, st);
