@@ -1200,3 +1200,30 @@ def test_unescape_command_views_table_set():
         want = (rst, rlen, rhash, rvid.astype(np.int64))
         _assert_cmd_equal(sub, got, want, True)
     tset.close()
+
+
+def test_one_string_calls_without_the_emit_kernel():
+    """A one-tile views call runs k_resolve alone (it writes the total); a tile whose output it must
+    defer (past the LDS stage: a long value, a long string) comes back with the deferred count and
+    the call runs again on the generic path. Every case equals the oracle, through run1 (the scalar
+    interpolate_inserts path) and through a batch of the same strings."""
+    x = PKG.interpolation_engine.get_exec(0)
+    x.set_option(N.OPT_VIEWS, 1)
+    try:
+        table = {"k": "v" * 70000, "s": "short", "n": "{s}-{s}", "m": "é" * 30000, "e": ""}
+        strings = ["{k}", "a{s}b", "x" * 70000 + "{s}", "{n}", "{m}{m}", "{e}", "", "{s}" * 3000, "{missing}"]
+        t = PKG.InsertsTable(table, clock=CLOCK)
+        ref = O.Oracle(table, "py", clock=CLOCK)
+        for s in strings:
+            rst, rout, _ = ref.interpolate(s)
+            got = t.run1(s)
+            if rst == "OK_STR":
+                assert got == rout, (s[:20], len(got) if isinstance(got, str) else got)
+            else:
+                assert got is PKG.interpolation_engine._NOT_DONE, s[:20]
+        for s, (st, payload) in zip(strings, t.run(strings)):
+            rst, rout, _ = ref.interpolate(s)
+            assert N.STATUS_NAMES[st] == rst and (rst != "OK_STR" or payload == rout), s[:20]
+        t.close()
+    finally:
+        x.set_option(N.OPT_VIEWS, 0)
