@@ -1211,19 +1211,23 @@ def test_one_string_calls_without_the_emit_kernel():
     x.set_option(N.OPT_VIEWS, 1)
     try:
         table = {"k": "v" * 70000, "s": "short", "n": "{s}-{s}", "m": "é" * 30000, "e": ""}
-        strings = ["{k}", "a{s}b", "x" * 70000 + "{s}", "{n}", "{m}{m}", "{e}", "", "{s}" * 3000, "{missing}"]
+        strings = ["a{k}b", "{k}", "a{s}b", "x" * 70000 + "{s}", "{n}", "{m}{m}", "{e}", "", "{s}" * 3000, "{missing}"]
         t = PKG.InsertsTable(table, clock=CLOCK)
         ref = O.Oracle(table, "py", clock=CLOCK)
         for s in strings:
-            rst, rout, _ = ref.interpolate(s)
+            rst, rout, rvid = ref.interpolate(s)
             got = t.run1(s)
             if rst == "OK_STR":
                 assert got == rout, (s[:20], len(got) if isinstance(got, str) else got)
+            elif rst == "OK_VALUE":  # a whole-string key: the stored value itself
+                assert got == t.value(rvid), s[:20]
             else:
                 assert got is PKG.interpolation_engine._NOT_DONE, s[:20]
         for s, (st, payload) in zip(strings, t.run(strings)):
-            rst, rout, _ = ref.interpolate(s)
-            assert N.STATUS_NAMES[st] == rst and (rst != "OK_STR" or payload == rout), s[:20]
+            rst, rout, rvid = ref.interpolate(s)
+            assert N.STATUS_NAMES[st] == rst, s[:20]
+            assert rst != "OK_STR" or payload == rout, s[:20]
+            assert rst != "OK_VALUE" or payload == rvid, s[:20]
         t.close()
     finally:
         x.set_option(N.OPT_VIEWS, 0)
