@@ -250,7 +250,7 @@ int ie_exec_timing(ie_exec* x, ie_timing* out); /* syncs */
                           pack the results in input order on the host; 0: packed on the device */
 #define IE_OPT_DEFER 7 /* views batches in two passes: a first pass without the exact evaluator and
                           the literal path (leaner registers and schedule), then the strings it could
-                          not finish in tiles of their own. 2 (default): batches of >= 2^21 strings,
+                          not finish in tiles of their own. 2 (default): batches of >= 2^19 strings,
                           and any batch after one with > 0.4 % such strings; 1: always; -1: only the
                           latter; 0: never (one pass, every string in its tile) */
 #define IE_OPT_RESERVE 8 /* views output of a packed batch: 0 (default): each tile claims its range on one
@@ -435,7 +435,8 @@ int ie_replace_map(ie_exec* x, const ie_table* t, const char* name, uint64_t nam
 /* delete (except_matching = 0: the keys some wildcard matches, py:1843-1855) / delete_except (1: the
  * keys no wildcard matches, py:1857-1868) in the given states (NULL: every state): wildcards packed
  * (offsets[n + 1]), as the task pre-pass left them; the keys are removed from the table set
- * (ie_table_set_update) and listed in out (bytes = the key, where = its state). */
+ * (ie_table_set_store: their value ids go back to the set's free list) and listed in out (bytes =
+ * the key, where = its state, value_id = the id it freed). */
 int ie_delete_keys(ie_exec* x, ie_table* t, const uint32_t* states, uint32_t n_states, const uint8_t* wbytes,
                    const uint64_t* woffsets, uint32_t n_wildcards, int32_t except_matching, ie_map_result** out);
 

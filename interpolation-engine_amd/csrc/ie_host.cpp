@@ -320,6 +320,15 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
     }
     W.fail_commit = forced ? (uint32_t)x->opt_fail_commit : (uint32_t)x->fail_commit;
     if (W.err_keys) W.fail_commit = 0;  // misses go through the exact evaluator to the literal path
+    // the adaptive choices' telemetry: written into pinned host words by the call's last emit kernel
+    // (no copy after it), or copied below when the call has none (a one-tile no-emit call)
+    const bool want_stats = !x->stat_pending && !x->no_stats;
+    if (want_stats && !x->stat_host) {
+      IE_HIP(hipHostMalloc((void**)&x->stat_host, 64, hipHostMallocMapped));
+      IE_HIP(hipHostGetDevicePointer((void**)&x->stat_dev, x->stat_host, 0));
+      IE_HIP(hipEventCreateWithFlags(&x->stat_ev, hipEventDisableTiming));
+    }
+    W.stat_out = want_stats ? x->stat_dev : nullptr;
     if (x->timing) IE_HIP(hipEventRecord(x->ev[1], st));
     // 512-string tiles halve the look-back hops: the unescape command's second resolve (its input
     // is interpolation output, so its evaluation is light and the look-back bounds it) takes them
@@ -347,14 +356,11 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
       // (a one-string call: k_resolve alone, one launch and its emit kernel's ~5 µs fewer)
       const bool ne = x->small_no_emit && d_out_len && !wide && !W.reserve16 && !x->opt_noeval && n <= (uint64_t)kRBlock;
       x->no_emit_used = ne;
+      if (ne) W.stat_out = nullptr;
       IE_HIP(wide ? launch_resolve512(B, W, t->dev, out->bytes, cap, st) : launch_resolve(B, W, t->dev, out->bytes, cap, st, ne));
     }
-    if (!x->stat_pending && !x->no_stats) {
-      if (!x->stat_host) {
-        IE_HIP(hipHostMalloc((void**)&x->stat_host, 64, hipHostMallocDefault));
-        IE_HIP(hipEventCreateWithFlags(&x->stat_ev, hipEventDisableTiming));
-      }
-      IE_HIP(hipMemcpyAsync(x->stat_host, W.stats, 5 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    if (want_stats) {
+      if (!W.stat_out) IE_HIP(hipMemcpyAsync(x->stat_host, W.stats, 5 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
       IE_HIP(hipEventRecord(x->stat_ev, st));
       x->stat_pending = true;
       x->stat_n = n;
@@ -1061,7 +1067,12 @@ int upload_table(const std::vector<Ent>& ents, uint32_t n_tables, int32_t dialec
   std::vector<uint32_t> slot_of;
   // the one-trip table experiment (IE_CUCKOO=1 with a k_resolve built -DIE_CUCKOO): two-choice
   // placement at load 0.4, no pilots; such a table takes no ie_table_set_update
+  // (the setting must match the kernels: a pilot-free table under kernels that read pilots would
+  // miss every key, so a library built without -DIE_CUCKOO refuses the variable instead)
   static const bool cuckoo = getenv("IE_CUCKOO") && atoi(getenv("IE_CUCKOO")) == 1;
+  if (cuckoo != kernels_cuckoo())
+    return fail(IE_ERR_INVALID, cuckoo ? "IE_CUCKOO=1 needs a library whose k_resolve was built with -DIE_CUCKOO"
+                                       : "this library's k_resolve was built with -DIE_CUCKOO: set IE_CUCKOO=1");
   bool placed = false;
   if (reuse && !cuckoo && reuse->slot_of.size() == items.size()) {
     placed = true;
@@ -1830,7 +1841,10 @@ static int table_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
         std::fill(t->occ.begin(), t->occ.end(), 0ull);
         for (size_t s2 = 0; s2 < t->h_entries.size(); s2++)
           if (t->h_entries[s2].flags & EF_OCCUPIED) occupy((uint32_t)s2, true);
-        t->vid_ok = false;
+        {
+          std::lock_guard<std::mutex> lock(t->vid_mu);
+          t->vid_ok = false;
+        }
         t->n_entries++;
         if (key.size() > kInlineKey && key.size() <= 2 * kInlineKey) t->dev.flags |= TF_LONG_KEYS;
         t->dev.maxtext = std::max<uint64_t>(t->dev.maxtext, text.size());
@@ -2004,6 +2018,7 @@ static int table_update(ie_table* t, const ie_kv* kv, const uint32_t* table_id, 
   if ((rc = apply_patches(t, pe))) return rc;
   tr.mark("patch apply", pe.dst.size());
   t->dev.n_entries = (uint32_t)t->n_entries;
+  std::lock_guard<std::mutex> vid_lock(t->vid_mu);
   if (t->vid_ok) {  // the value ids of the changed slots (a stale one is caught on use)
     for (uint32_t s2 : dirty.slots()) {
       const Entry& e = t->h_entries[s2];

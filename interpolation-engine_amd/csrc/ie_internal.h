@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <mutex>
 #include <new>
 
 #include <string>
@@ -216,7 +217,11 @@ struct ie_table {
   uint32_t next_vid = 0;
   std::vector<uint32_t> free_vids;
   std::vector<std::vector<uint32_t>> groups;
-  // value id -> slot, built on demand (ie_maps.cpp: str() of a typed result), kept by the updates
+  // value id -> slot, built on demand (ie_maps.cpp: str() of a typed result), kept by the updates.
+  // The lazy rebuild happens on the READ paths (ie_table_value, the map steps' value_str), which
+  // several host threads may run on one table at once (the header's thread contract): vid_mu
+  // guards the map and its flag
+  mutable std::mutex vid_mu;
   mutable std::vector<uint32_t> vid_slot;  // value id -> slot (UINT32_MAX: none); checked on use
   mutable bool vid_ok = false;
   // occupied slots (bitmap) for ie_table_set_update's pilot searches: cache-resident where the
@@ -279,7 +284,8 @@ struct ie_exec {
   bool no_emit_used = false;   // (run_device: it did; a deferred tile then needs the full path)
   uint8_t* ctr_override = nullptr;  // run_host_small: the counters in its own block, zeroed by its input copy
   uint64_t stat_n = 0;
-  uint32_t* stat_host = nullptr;  // pinned
+  uint32_t* stat_host = nullptr;  // pinned, mapped: the last emit kernel of a call writes it (stat_dev)
+  uint32_t* stat_dev = nullptr;
   hipEvent_t stat_ev = nullptr;
   // workspace
   DevBuf counters, pool, out_len, tile_sum, tile_base, defer_tiles, defer_desc;

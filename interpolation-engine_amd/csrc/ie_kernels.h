@@ -96,6 +96,9 @@ struct Work {
   uint64_t* res_ovf;     // 1   the overflow region's start (written by the reserved pass)
   uint32_t recurse;      // k_resolve in the unescape command (py dialect): whole-string items whose
                          // result recursive_interpolate walks again report IE_RECURSE
+  // the call's telemetry words (stats[0..4]) in host-mapped pinned memory, written by its last
+  // k_emit_windows (no copy kernel after it); null: the host copies them itself
+  uint32_t* stat_out;
   uint32_t zero_on_overflow; // escape kernels: when the output exceeds its capacity, write every
                              // offset as 0 (a step that reads these strings next then reads nothing)
   // escape pipeline
@@ -151,6 +154,9 @@ struct PatchInline {
   uint32_t n;
 };
 hipError_t launch_patch_inline(const PatchInline& a, hipStream_t st);
+// whether k_resolve (ie_resolve.hip) was compiled for the two-choice table experiment (-DIE_CUCKOO):
+// the host places keys the same way or refuses to build (ie_host.cpp, upload_table)
+bool kernels_cuckoo();
 hipError_t launch_status_carry(const uint8_t* before, uint8_t* after, uint64_t n, hipStream_t st);
 hipError_t launch_debug_probe(const DevTable& T, const uint8_t* key, uint32_t klen, uint64_t* out,
                               hipStream_t st);

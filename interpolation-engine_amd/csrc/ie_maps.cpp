@@ -102,6 +102,7 @@ ie_clock table_clock(const ie_table* t);
 
 // the slot holding value id vid (table tb, or any table when tb is UINT32_MAX), UINT32_MAX: none
 uint32_t slot_of_vid(const ie_table* t, uint32_t vid, uint32_t tb = UINT32_MAX) {
+  std::lock_guard<std::mutex> lock(t->vid_mu);  // (concurrent readers of one table)
   if (!t->vid_ok) {
     t->vid_slot.assign(t->next_vid, UINT32_MAX);
     for (uint32_t s = 0; s < (uint32_t)t->h_entries.size(); s++) {
@@ -740,13 +741,16 @@ int ie_delete_keys(ie_exec* x, ie_table* t, const uint32_t* states, uint32_t n_s
     const std::string_view key((const char*)ks.bytes.data() + ks.off[k], ks.off[k + 1] - ks.off[k]);
     o.push(key, IE_OK_STR, ks.tid[k], -1);
   }
-  // (keys copied out first: the update rewrites the mirror they point into)
+  // (keys copied out first: the update rewrites the mirror they point into). The store path
+  // (ie_table_set_store) gives each deleted key's value id back to the table's free list and
+  // reports it, so the caller drops the value it held under that id (value_id in the result)
   for (uint64_t k = 0; k < o.status.size(); k++) {
     kv.push_back(ie_kv{(const char*)o.bytes.data() + o.off[k], o.off[k + 1] - o.off[k], nullptr, 0, -1, 0});
     tids.push_back(o.where[k]);
-    vids.push_back(0);
+    vids.push_back(IE_VID_NONE);
   }
-  if (!kv.empty() && (rc = ie_table_set_update(t, kv.data(), tids.data(), vids.data(), kv.size()))) return rc;
+  if (!kv.empty() && (rc = ie_table_set_store(t, kv.data(), tids.data(), kv.size(), vids.data()))) return rc;
+  for (uint64_t k = 0; k < vids.size(); k++) o.vid[k] = vids[k];
   return emit(o, out);
 }
 

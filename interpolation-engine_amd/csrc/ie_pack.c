@@ -32,8 +32,12 @@ enum { KIND_STR = 0, KIND_INT = 1 };
 __attribute__((used)) static const char kPackId[] = "IE_BUILD_ID:" IE_PACK_ID;  // (__graft_entry__.built_id)
 
 // A text that is not ASCII: transcoded into the call's buffer (one pass, each thread's jobs back to
-// back in a region sized by their bounds), across the threads with the GIL released (the strs are immutable and the
-// changes list keeps them alive)
+// back in a region sized by their bounds), across the threads with the GIL released. The records
+// point into str objects the call OWNS a reference to (held in `keep`, which the caller holds until
+// the library has read the records): pack() takes a tuple snapshot of the changes (the change tuples
+// are immutable), pack_dicts() holds every key and value it points into. Another thread that
+// rebinds a list item or a dict value meanwhile then frees nothing the records (or the transcode
+// threads, or the library behind a ctypes call that released the GIL) still read.
 typedef struct {
   const void* src;
   uint64_t len;  // code units
@@ -376,19 +380,20 @@ static PyObject* pack(PyObject* self, PyObject* args) {
   long long n_tables;
   int threads = 1;
   if (!PyArg_ParseTuple(args, "OLOOO|i", &changes, &n_tables, &del, &render, &dialect, &threads)) return NULL;
-  PyObject* seq = PySequence_Fast(changes, "changes must be a sequence");
+  // a snapshot the call owns (a list the caller mutates later cannot free a change under us)
+  PyObject* seq = PySequence_Tuple(changes);
   if (!seq) return NULL;
-  const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+  const Py_ssize_t n = PyTuple_GET_SIZE(seq);
   PyObject* kvb = PyByteArray_FromStringAndSize(NULL, (Py_ssize_t)(n * sizeof(kv_rec)));
   PyObject* tidb = PyByteArray_FromStringAndSize(NULL, (Py_ssize_t)(n * 4));
   PyObject* keep = PyList_New(0);
   jobs_t J = {NULL, 0, 0};
-  if (!kvb || !tidb || !keep) goto fail;
+  if (!kvb || !tidb || !keep || PyList_Append(keep, seq) < 0) goto fail;
   kv_rec* kv = (kv_rec*)PyByteArray_AS_STRING(kvb);
   uint32_t* tid = (uint32_t*)PyByteArray_AS_STRING(tidb);
   for (Py_ssize_t i = 0; i < n; i++) {
-    PyObject* c = PySequence_Fast_GET_ITEM(seq, i);
-    if (!PyTuple_Check(c) || PyTuple_GET_SIZE(c) != 3) {
+    PyObject* c = PyTuple_GET_ITEM(seq, i);
+    if (!PyTuple_CheckExact(c) || PyTuple_GET_SIZE(c) != 3) {
       PyErr_SetString(PyExc_TypeError, "a change is a (dict index, key, value) tuple");
       goto fail;
     }
@@ -444,6 +449,14 @@ static PyObject* pack_dicts(PyObject* self, PyObject* args) {
   PyObject* keep = PyList_New(0);
   jobs_t J = {NULL, 0, 0};
   if (!kvb || !stb || !keep) goto fail;
+  // every key and value the records may point into, owned by the call (a dict entry rebound by
+  // another thread, or a temporary dict the caller drops, frees nothing the records still read)
+  PyObject* hold = PyTuple_New(2 * n);
+  if (!hold || PyList_Append(keep, hold) < 0) {
+    Py_XDECREF(hold);
+    goto fail;
+  }
+  Py_DECREF(hold);  // (keep owns it)
   kv_rec* kv = (kv_rec*)PyByteArray_AS_STRING(kvb);
   uint64_t* st = (uint64_t*)PyByteArray_AS_STRING(stb);
   Py_ssize_t i = 0;
@@ -457,6 +470,10 @@ static PyObject* pack_dicts(PyObject* self, PyObject* args) {
         PyErr_SetString(PyExc_RuntimeError, "a dict changed size while packing");
         goto fail;
       }
+      Py_INCREF(k);
+      Py_INCREF(v);
+      PyTuple_SET_ITEM(hold, 2 * i, k);
+      PyTuple_SET_ITEM(hold, 2 * i + 1, v);
       if (pack_kv(k, v, &kv[i], (uint64_t)i, &J, keep, NULL, render, dialect) < 0) goto fail;
       i++;
     }

@@ -1044,29 +1044,34 @@ __device__ __forceinline__ bool maybe_simple(const uint8_t* s, uint32_t n) {
 // lane rebuilds its string's pieces from the stored descriptor (template runs from the input in
 // global memory, values from the table or the literal pool) and the tile's output goes through
 // the LDS stage in windows of kRStageBytes (long pieces copied by a whole wave).
-__global__ __launch_bounds__(kRBlock) void k_emit_windows(Batch B0, Work W, DevTable T, uint8_t* out) {
+// One launch serves a whole call: the defer list holds the tiles of the batch B0 and, flagged
+// kDeferSub, those of its deferred subset B1 (a two-pass views call: one emit after both passes).
+constexpr uint32_t kDeferSub = 1u << 31;
+__global__ __launch_bounds__(kRBlock) void k_emit_windows(Batch B0, Batch B1, Work W, DevTable T, uint8_t* out) {
   __shared__ __attribute__((aligned(16))) uint8_t s_win[kRStageBytes + 48];
-  Batch B = B0;
-  if (B0.n_dev) {
-    const uint64_t nd = gld(B0.n_dev);
-    B.n = nd < B0.n ? nd : B0.n;
-  }
   const uint32_t count = __hip_atomic_load(W.defer_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t tid = threadIdx.x;
   // views output: the bytes every tile claimed are the batch's total (k_resolve has finished)
-  if (B.out_len && blockIdx.x == 0 && tid == 0) {
+  if (B0.out_len && blockIdx.x == 0 && tid == 0) {
     uint64_t t = 0;  // reserved ranges: the tiles' sums (the cursor counts the overflow region only)
     if (W.reserve16)
       for (uint32_t k = 0; k < 16; k++) t += W.shards[16u * k];
     *W.total = W.reserve16 ? t : *W.cursor;
   }
+  // the call's telemetry straight into the host's pinned words (every resolve pass has finished)
+  if (W.stat_out && blockIdx.x == 0 && tid < 5) gst(W.stat_out + tid, W.stats[tid]);
   // fewer deferred tiles than workgroups: each tile's windows are shared by `per` workgroups (a
   // tile of multi-KB outputs is hundreds of windows: one workgroup alone would take them in turn)
   const uint32_t per = count && count < gridDim.x ? gridDim.x / count : 1u;
   const uint32_t slot0 = per > 1u ? blockIdx.x / per : blockIdx.x, wk = per > 1u ? blockIdx.x % per : 0u;
   const uint32_t slot_step = per > 1u ? count : gridDim.x;  // (per > 1: one slot per workgroup)
   for (uint32_t slot = slot0; slot < count; slot += slot_step) {
-    const uint32_t tile = gld(W.defer_tiles + slot);
+    const uint32_t tword = gld(W.defer_tiles + slot), tile = tword & ~kDeferSub;
+    Batch B = (tword & kDeferSub) ? B1 : B0;  // (uniform)
+    if (B.n_dev) {
+      const uint64_t nd = gld(B.n_dev);
+      B.n = nd < B.n ? nd : B.n;
+    }
     const uint64_t first = (uint64_t)tile * kRBlock, last = min(first + (uint64_t)kRBlock, B.n), i = first + tid;
     // (a deferred subset's results sit at out_index[] of the batch)
     const uint64_t of = B.out_index ? gld(B.out_index + first) : first;
@@ -1166,6 +1171,10 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(LK ? IE
     __syncthreads();
     tile = s_misc[0];
   }
+  // a deferred subset (B0.n_dev: its string count is only known on the device) runs on a bounded
+  // grid that strides over the tiles (a subset with nothing in it costs a few workgroups, not a
+  // whole batch's); every other launch has a workgroup per tile and takes one trip
+  for (;;) {
   const TileGeo geo = load_geo(B, tile, tid);
   TilePrefetch<kStageV> pre;
   pre.nv = 0;
@@ -1664,10 +1673,15 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(LK ? IE
     gst4(dd + 1, make_uint4(d.close[0], d.close[1], d.close[2], n32));
     gst4(dd + 2, make_uint4(d.vk[0], d.vk[1], d.vk[2], 0u));
     gst4(dd + 3, make_uint4(d.vs[0], d.vs[1], d.vs[2], 0u));
-    if (tid == 0) gst(W.defer_tiles + slot, tile);
+    if (tid == 0) gst(W.defer_tiles + slot, tile | (B.out_index ? kDeferSub : 0u));  // (a subset's tile: flagged)
   }
   IE_STAMP(5);
 #undef IE_STAMP
+  }
+  if (!(VIEWS && !LEAN && !UNESC) || !B0.n_dev) break;  // (uniform)
+  tile += gridDim.x;
+  if (tile >= ntiles) break;
+  __syncthreads();  // the next tile's stage and union: every wave is done with this one's
   }
 }
 
@@ -1751,12 +1765,21 @@ __global__ __launch_bounds__(kRBlock) void k_unesc_deferred(Batch B, Work W, uin
   }
 }
 
+// the deferred subset's bounded grid (see k_resolve): 4 workgroups per CU
+constexpr uint32_t kSubsetGrid = 1024;
+
+// emit: launch k_emit_windows after the resolve (false: the caller launches one for the whole call,
+// launch_emit)
 hipError_t launch_resolve_impl(const Batch& B, const Work& W, const DevTable& T, uint8_t* out, uint64_t cap,
-                               hipStream_t st, bool unesc = false, bool lean = false, bool no_emit = false) {
+                               hipStream_t st, bool unesc = false, bool lean = false, bool no_emit = false,
+                               bool emit = true) {
   const uint64_t tiles = (B.n + kRBlock - 1) / kRBlock;
   if (!tiles) return hipSuccess;
   if (tiles > 0xFFFFFFFFull) return hipErrorInvalidValue;
-  const uint32_t grid = (uint32_t)tiles;
+  const uint32_t egrid = (uint32_t)(tiles < 512u ? tiles : 512u);
+  // (a subset views batch strides over its tiles: see k_resolve)
+  const uint32_t grid = B.n_dev && B.out_len && !unesc && !lean ? (uint32_t)(tiles < kSubsetGrid ? tiles : kSubsetGrid)
+                                                                  : (uint32_t)tiles;
   const bool multi = B.table_id != nullptr;
   if (unesc) {  // the fused unescape command (views only)
     if (!B.out_len) return hipErrorInvalidValue;
@@ -1765,7 +1788,7 @@ hipError_t launch_resolve_impl(const Batch& B, const Work& W, const DevTable& T,
     if (v == 1) hipLaunchKernelGGL((k_resolve<false, true, true, true>), dim3(grid), dim3(kRBlock), 0, st, B, W, T, out, cap);
     if (v == 2) hipLaunchKernelGGL((k_resolve<true, false, true, true>), dim3(grid), dim3(kRBlock), 0, st, B, W, T, out, cap);
     if (v == 3) hipLaunchKernelGGL((k_resolve<true, true, true, true>), dim3(grid), dim3(kRBlock), 0, st, B, W, T, out, cap);
-    hipLaunchKernelGGL(k_emit_windows, dim3(grid < 512u ? grid : 512u), dim3(kRBlock), 0, st, B, W, T, out);
+    if (emit) hipLaunchKernelGGL(k_emit_windows, dim3(egrid), dim3(kRBlock), 0, st, B, B, W, T, out);
     return hipGetLastError();
   }
   // LK: a table with 17-32 byte keys gets the instances whose chain jobs take such keys (they cost
@@ -1786,7 +1809,7 @@ hipError_t launch_resolve_impl(const Batch& B, const Work& W, const DevTable& T,
       IE_LAUNCH_LEAN(7, true, true, true)
 #undef IE_LAUNCH_LEAN
     }
-    hipLaunchKernelGGL(k_emit_windows, dim3(grid < 512u ? grid : 512u), dim3(kRBlock), 0, st, B, W, T, out);
+    if (emit) hipLaunchKernelGGL(k_emit_windows, dim3(egrid), dim3(kRBlock), 0, st, B, B, W, T, out);
     return hipGetLastError();
   }
 #endif
@@ -1813,8 +1836,17 @@ hipError_t launch_resolve_impl(const Batch& B, const Work& W, const DevTable& T,
   }
   // the deferred (oversized) tiles' bytes (exits at once when there are none); views: the total
   // (a one-tile views batch may go without it: no_emit, see launch_resolve)
-  if ((out || B.out_len) && !(no_emit && grid == 1u && B.out_len && !W.reserve16))
-    hipLaunchKernelGGL(k_emit_windows, dim3(grid < 512u ? grid : 512u), dim3(kRBlock), 0, st, B, W, T, out);
+  if (emit && (out || B.out_len) && !(no_emit && grid == 1u && B.out_len && !W.reserve16))
+    hipLaunchKernelGGL(k_emit_windows, dim3(egrid), dim3(kRBlock), 0, st, B, B, W, T, out);
+  return hipGetLastError();
+}
+
+// one k_emit_windows for a call of two passes: the batch B and its deferred subset D
+hipError_t launch_emit(const Batch& B, const Batch& D, const Work& W, const DevTable& T, uint8_t* out,
+                       hipStream_t st) {
+  const uint64_t tiles = (B.n + kRBlock - 1) / kRBlock;
+  if (!tiles) return hipSuccess;
+  hipLaunchKernelGGL(k_emit_windows, dim3((uint32_t)(tiles < 512u ? tiles : 512u)), dim3(kRBlock), 0, st, B, D, W, T, out);
   return hipGetLastError();
 }
 
@@ -1896,17 +1928,17 @@ hipError_t launch_resolve_deferring(const Batch& B, const Work& W, const DevTabl
   W1.sub_off = sub_off;
   W1.sub_len = sub_len;
   W1.sub_tid = multi ? sub_tid : nullptr;
-  hipError_t e = IE_RNS::launch_resolve_impl(B, W1, T, out, cap, st, false, true);
+  hipError_t e = IE_RNS::launch_resolve_impl(B, W1, T, out, cap, st, false, true, false, false);
   if (e != hipSuccess) return e;
-  // the second pass's windowed-tile list restarts at 0: its own counter word (counters word 13,
-  // zeroed with the rest at the call's start; the first pass's list was consumed by its
-  // k_emit_windows)
+  // the second pass appends its windowed tiles to the first's list (flagged as the subset's), and
+  // ONE k_emit_windows writes both passes' windows, the total and the telemetry
   Work W2 = W;
   W2.defer_slow = 0;
-  W2.defer_count = W.defer_count + 4;
   const Batch D{B.bytes, sub_off, B.n, B.out_off, B.status, B.value_id, multi ? sub_tid : nullptr, sub_len, B.out_len,
                 W.udefer_list, W.udefer_count};
-  return IE_RNS::launch_resolve_impl(D, W2, T, out, cap, st);
+  e = IE_RNS::launch_resolve_impl(D, W2, T, out, cap, st, false, false, false, false);
+  if (e != hipSuccess) return e;
+  return IE_RNS::launch_emit(B, D, W, T, out, st);
 }
 #endif
 
@@ -1922,6 +1954,13 @@ hipError_t launch_resolve(const Batch& B, const Work& W, const DevTable& T, uint
 }
 hipError_t launch_debug_probe(const DevTable& T, const uint8_t* key, uint32_t klen, uint64_t* out, hipStream_t st) {
   return IE_RNS::launch_debug_probe_impl(T, key, klen, out, st);
+}
+bool kernels_cuckoo() {
+#ifdef IE_CUCKOO
+  return true;
+#else
+  return false;
+#endif
 }
 #endif
 

@@ -642,10 +642,12 @@ def delete_states(states, task, dialect="py", device=0, tables=None):
             IE.N.check(IE.N.lib().ie_delete_keys(x.h, tset.h, ids.ctypes.data, len(members),
                                                  ctypes.cast(ctypes.c_char_p(blob), ctypes.c_void_p), offs.ctypes.data,
                                                  len(wild), 1 if except_ else 0, ctypes.byref(res)), "ie_delete_keys")
-            for b, _, s, _, _ in IE.N.map_result_to_python(res):
+            for b, _, s, _, vid in IE.N.map_result_to_python(res):
                 k = IE.N.dec(b)
                 states[s].pop(k, None)
                 out[s].append(k)
+                if vid < len(tset.values):  # (the id went back to the table's free list)
+                    tset.values[vid] = None
             # keys a dict holds but the table never does (the clock names, ''): the same test
             odd = [(s, k) for s in members for k in states[s] if k in ("", "HH:MM", "HH:MM:SS")]
             if odd:

@@ -108,3 +108,39 @@ def test_pack_long_mixed_texts(threads):
     kv, tids, keep = P.pack(changes, 1, IE.DELETE, IE.render, "py", threads)
     for r, (_, k, v) in zip(_records(kv, len(changes)), changes):
         assert ctypes.string_at(r.text, r.text_len) == N.enc(v), k
+
+
+def test_records_outlive_the_callers_objects():
+    """The records point into str objects the call owns (`keep`), not into the caller's list and
+    dicts: the caller drops or rebinds its list items and dict values right after pack returns (as
+    another thread could while the library reads the records with the GIL released), and every
+    record still reads the text it was packed from."""
+    import gc
+    rng = random.Random(11)
+    # fresh (unshared, refcount-1) ASCII texts: freed at once if nothing but the list held them
+    texts = ["".join(rng.choice("abcdefgh") for _ in range(200)) + str(i) for i in range(500)]
+    want = [N.enc(t) for t in texts]
+    changes = [(0, "k%d" % i, t) for i, t in enumerate(texts)]
+    del texts
+    kv, tids, keep = P.pack(changes, 1, IE.DELETE, IE.render, "py", 4)
+    for i in range(len(changes)):  # the caller rebinds every item and drops its list
+        changes[i] = (0, "x", "y" * (i % 50))
+    del changes
+    gc.collect()
+    junk = ["".join(rng.choice("zyxw") for _ in range(200)) for _ in range(2000)]  # reuse the freed memory
+    for r, w in zip(_records(kv, len(want)), want):
+        assert ctypes.string_at(r.text, r.text_len) == w
+    # pack_dicts: values rebound in the dicts, and a temporary dict the caller does not keep
+    vals = ["".join(rng.choice("abcdefgh") for _ in range(300)) + "é" * (i % 2) + str(i) for i in range(300)]
+    wantd = [N.enc(v) for v in vals]
+    d0 = {"a%d" % i: vals[i] for i in range(150)}
+    kv2, st2, keep2 = P.pack_dicts([d0, dict(("b%d" % i, vals[i]) for i in range(150, 300))], IE.render, "py", 4)
+    del vals
+    for k in list(d0):
+        d0[k] = "rebound"
+    d0.clear()
+    gc.collect()
+    junk2 = ["".join(rng.choice("zyxw") for _ in range(300)) for _ in range(2000)]
+    for r, w in zip(_records(kv2, len(wantd)), wantd):
+        assert ctypes.string_at(r.text, r.text_len) == w
+    del junk, junk2, keep, keep2
