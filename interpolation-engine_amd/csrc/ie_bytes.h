@@ -241,63 +241,16 @@ __device__ __forceinline__ uint32_t cr_first_close(uint32_t r) { return (r & kLo
 __device__ __forceinline__ uint32_t cr_inner_open(uint32_t r) { return (r & kLongRec) ? r & 0x3FFFu : (r >> 16) & 0xFFu; }
 __device__ __forceinline__ uint32_t cr_last_close(uint32_t r) { return (r & kLongRec) ? (r >> 14) & 0x3FFFu : r >> 24; }
 
-// the string's chains (<= kMaxTop, depth <= kChainDepth; records as in ChainJobs::crec). False:
-// the string is not a chain-only clean string (the exact evaluator decides it).
-__device__ __forceinline__ bool parse_chains(const lds_u8* tile, uint32_t p0, uint32_t n, const lds_u32* cm,
-                                             const lds_u32* oddbits, const lds_u32* escbits, bool active,
-                                             uint32_t (&crec)[kMaxTop], uint32_t (&cdep)[kMaxTop], uint32_t& nch,
-                                             Ev& Om_out, Ev& Cm_out, uint32_t& maxd_out, bool& whole_out) {
-  whole_out = false;
-  if (active && n > kChainMax) {
-    // A long string (a prompt template): copied verbatim when none of its bytes is a brace and its
-    // chunks hold no U+3020 lead byte (py:505-540 leave it unchanged). One with up to kMaxTop FLAT
-    // pairs ({key} with no brace inside, no '\\' near any of them) is chain-shaped too: each pair is
-    // a one-level chain whose record holds 14-bit positions (kLongRec). Anything else: the exact
-    // evaluator.
-    nch = 0;
-#pragma unroll
-    for (int c = 0; c < kMaxTop; c++) crec[c] = cdep[c] = 0;
-    const uint32_t c0 = p0 >> 4, cl = (p0 + n - 1) >> 4;
-    bool ok = n < (1u << 14), braces = false, esc = false, inside = false;
-    uint32_t a = 0;
-    for (uint32_t c = c0; c <= cl && ok; c++) {
-      const uint32_t b_lo = c == c0 ? (p0 & 15u) : 0u, b_hi = c == cl ? ((p0 + n - 1) & 15u) : 15u;
-      const uint32_t bm = ((2u << b_hi) - 1u) & ~((1u << b_lo) - 1u);  // the string's bytes in the chunk
-      uint32_t op = cm[c] & bm, cls = (cm[c] >> 16) & bm;  // '{' / '}' bytes of the chunk
-      if ((oddbits[c >> 5] >> (c & 31u)) & 1u) ok = false;
-      esc |= ((escbits[c >> 5] >> (c & 31u)) & 1u) != 0u;
-      braces |= (op | cls) != 0u;
-      while ((op | cls) && ok) {  // the chunk's events in byte order
-        const uint32_t k = (uint32_t)__builtin_ctz(op | cls), pos = 16u * c + k - p0;
-        if ((op >> k) & 1u) {
-          ok = !inside;  // a brace inside a pair: nesting (the exact evaluator)
-          inside = true;
-          a = pos;
-          op &= op - 1u;
-        } else {
-          ok = inside && nch < (uint32_t)kMaxTop;  // a '}' before its '{', or too many pairs
-          if (ok) {
-            crec[nch] = kLongRec | a | (pos << 14);
-            cdep[nch] = 1u;
-            nch++;
-          }
-          inside = false;
-          cls &= cls - 1u;
-        }
-      }
-    }
-    ok = ok && !inside && !(braces && esc);
-    // a single pair that is the whole string: get_simple_insertkey's typed result (exact evaluator)
-    ok = ok && !(nch == 1u && (crec[0] & 0x3FFFu) == 0u && ((crec[0] >> 14) & 0x3FFFu) == n - 1u);
-    if (!ok) nch = 0;
-    Om_out = Cm_out = Ev{0ull, 0ull};
-    maxd_out = ok && nch ? 1u : 0u;
-    return ok;
-  }
-  bool ok = active && n <= kChainMax;
-  // ---- 1. the string's open / close events as 128-bit windows ----
+// The open / close events of a string of <= kChainMax bytes at p0 of the staged tile, as 128-bit
+// windows (bit i = byte i), from the chunk masks: braces right after a '\\' are not events (escapes,
+// py:505-508). ok in: the string is a candidate; out: false when a chunk of it holds a U+3020 lead
+// byte or an escape that the restore may misread (the exact evaluator's strings). parse_chains'
+// first step; the LEAN k_resolve also recomputes it for a chain's middle levels.
+__device__ __forceinline__ void string_events(const lds_u8* tile, uint32_t p0, uint32_t n, const lds_u32* cm,
+                                              const lds_u32* oddbits, const lds_u32* escbits, bool& ok, bool& any_esc,
+                                              Ev& Om, Ev& Cm) {
   uint32_t O[4], C[4];
-  bool any_esc = false;
+  any_esc = false;
   {
     const uint32_t c0 = ok ? p0 >> 4 : 0u, o = p0 & 15u;
     const uint32_t cl = ok && n ? (p0 + n - 1) >> 4 : c0;
@@ -362,8 +315,68 @@ __device__ __forceinline__ bool parse_chains(const lds_u8* tile, uint32_t p0, ui
       if (hazard) ok = false;
     }
   }
-  const Ev Om{O[0] | ((uint64_t)O[1] << 32), O[2] | ((uint64_t)O[3] << 32)};
-  const Ev Cm{C[0] | ((uint64_t)C[1] << 32), C[2] | ((uint64_t)C[3] << 32)};
+  Om = Ev{O[0] | ((uint64_t)O[1] << 32), O[2] | ((uint64_t)O[3] << 32)};
+  Cm = Ev{C[0] | ((uint64_t)C[1] << 32), C[2] | ((uint64_t)C[3] << 32)};
+}
+
+// the string's chains (<= kMaxTop, depth <= kChainDepth; records as in ChainJobs::crec). False:
+// the string is not a chain-only clean string (the exact evaluator decides it).
+__device__ __forceinline__ bool parse_chains(const lds_u8* tile, uint32_t p0, uint32_t n, const lds_u32* cm,
+                                             const lds_u32* oddbits, const lds_u32* escbits, bool active,
+                                             uint32_t (&crec)[kMaxTop], uint32_t (&cdep)[kMaxTop], uint32_t& nch,
+                                             Ev& Om_out, Ev& Cm_out, uint32_t& maxd_out, bool& whole_out) {
+  whole_out = false;
+  if (active && n > kChainMax) {
+    // A long string (a prompt template): copied verbatim when none of its bytes is a brace and its
+    // chunks hold no U+3020 lead byte (py:505-540 leave it unchanged). One with up to kMaxTop FLAT
+    // pairs ({key} with no brace inside, no '\\' near any of them) is chain-shaped too: each pair is
+    // a one-level chain whose record holds 14-bit positions (kLongRec). Anything else: the exact
+    // evaluator.
+    nch = 0;
+#pragma unroll
+    for (int c = 0; c < kMaxTop; c++) crec[c] = cdep[c] = 0;
+    const uint32_t c0 = p0 >> 4, cl = (p0 + n - 1) >> 4;
+    bool ok = n < (1u << 14), braces = false, esc = false, inside = false;
+    uint32_t a = 0;
+    for (uint32_t c = c0; c <= cl && ok; c++) {
+      const uint32_t b_lo = c == c0 ? (p0 & 15u) : 0u, b_hi = c == cl ? ((p0 + n - 1) & 15u) : 15u;
+      const uint32_t bm = ((2u << b_hi) - 1u) & ~((1u << b_lo) - 1u);  // the string's bytes in the chunk
+      uint32_t op = cm[c] & bm, cls = (cm[c] >> 16) & bm;  // '{' / '}' bytes of the chunk
+      if ((oddbits[c >> 5] >> (c & 31u)) & 1u) ok = false;
+      esc |= ((escbits[c >> 5] >> (c & 31u)) & 1u) != 0u;
+      braces |= (op | cls) != 0u;
+      while ((op | cls) && ok) {  // the chunk's events in byte order
+        const uint32_t k = (uint32_t)__builtin_ctz(op | cls), pos = 16u * c + k - p0;
+        if ((op >> k) & 1u) {
+          ok = !inside;  // a brace inside a pair: nesting (the exact evaluator)
+          inside = true;
+          a = pos;
+          op &= op - 1u;
+        } else {
+          ok = inside && nch < (uint32_t)kMaxTop;  // a '}' before its '{', or too many pairs
+          if (ok) {
+            crec[nch] = kLongRec | a | (pos << 14);
+            cdep[nch] = 1u;
+            nch++;
+          }
+          inside = false;
+          cls &= cls - 1u;
+        }
+      }
+    }
+    ok = ok && !inside && !(braces && esc);
+    // a single pair that is the whole string: get_simple_insertkey's typed result (exact evaluator)
+    ok = ok && !(nch == 1u && (crec[0] & 0x3FFFu) == 0u && ((crec[0] >> 14) & 0x3FFFu) == n - 1u);
+    if (!ok) nch = 0;
+    Om_out = Cm_out = Ev{0ull, 0ull};
+    maxd_out = ok && nch ? 1u : 0u;
+    return ok;
+  }
+  bool ok = active && n <= kChainMax;
+  // ---- 1. the string's open / close events as 128-bit windows ----
+  bool any_esc = false;
+  Ev Om, Cm;
+  string_events(tile, p0, n, cm, oddbits, escbits, ok, any_esc, Om, Cm);
   // ---- 2. chains: the events of a chain-only string are blocks O^d C^d (each pair has at most
   //      one child), so chain c is located by a few mask scans: its first '{' (a), its first '}'
   //      (c1), the opens in [a, c1) (its depth), the closes before the next '{' (as many). ----

@@ -175,9 +175,10 @@ int ensure_work(ie_exec* x, int op, uint64_t n) {
   if (op == kOpInterp) {
     IE_HIP(x->pool.ensure(x->pool_request));
     // room for every tile to be deferred (64 B of descriptor per string; grow-only, never read
-    // unless written, so only HBM capacity is spent)
-    IE_HIP(x->defer_tiles.ensure(tiles * sizeof(uint32_t)));
-    IE_HIP(x->defer_desc.ensure(tiles * 128 * 64));  // whole tiles of kRBlock >= 128 strings
+    // unless written, so only HBM capacity is spent), twice: a two-pass views call appends its
+    // deferred subset's tiles to the first pass's list (one k_emit_windows for both)
+    IE_HIP(x->defer_tiles.ensure(2 * tiles * 32));  // (a 32-byte record per deferred tile)
+    IE_HIP(x->defer_desc.ensure(2 * tiles * 128 * 64));  // whole tiles of kRBlock >= 128 strings
   } else {
     IE_HIP(x->out_len.ensure((n + 1) * sizeof(uint32_t)));
     IE_HIP(x->tile_sum.ensure(tiles * sizeof(uint64_t)));

@@ -65,7 +65,7 @@ struct Work {
   uint32_t fail_commit;  // 1: chain failures commit in the chain evaluator (k_resolve<true>)
   // tiles whose output does not fit the LDS stage: k_emit_windows writes their bytes
   uint32_t* defer_count; // 1
-  uint32_t* defer_tiles; // tiles
+  uint32_t* defer_tiles; // 8 words per deferred tile: {tile | kDeferSub, 0, base (u64), total (u64), 0, 0}
   uint4* defer_desc;     // tiles * kBlock * 4: each string's descriptor
   uint64_t* cursor;      // 1   views output: bytes claimed so far (zeroed per call)
   // the fused unescape command (k_resolve<.., UNESC>): strings it cannot finish in the stage (not

@@ -47,10 +47,27 @@
 #define IE_RNS r256
 #endif
 
+// LEAN5 (an experiment, off: profiles/r06/lean5/README.md): the LEAN first pass in <= 32 KB of LDS
+// and <= 96 VGPRs per 256-string tile, i.e. five workgroups (waves) per CU (SIMD) instead of four:
+// the chunk masks stay through the chain jobs (a middle level's braces are found from them again, no
+// 8 KB of event columns), the job results overwrite their records, one chain job per lane, and the
+// output goes to a 13 KB stage, the bytes past it stored straight to HBM by each lane. Measured
+// slower than the 4-wave LEAN (config 3 1.38 vs 0.82 ms; the window-loop and two-part variants
+// 0.98 / 1.15 ms): every scheme lengthens a tile's life more than the fifth wave adds tiles
+#ifndef IE_LEAN5
+#define IE_LEAN5 0
+#endif
+#ifndef IE_WAVES_PER_EU_LEAN
+#define IE_WAVES_PER_EU_LEAN 5
+#endif
+
 // issue the first value text's loads before the output scan (config 4 first resolve 1.80 -> 1.76 ms,
 // configs 2 and 3 unchanged: profiles/r03/early_text/)
 #ifndef IE_EARLY_TEXT
 #define IE_EARLY_TEXT 1
+#endif
+#if IE_LEAN5 && !IE_EARLY_TEXT
+#error "LEAN5 keeps the entry texts the early loads put in registers (IE_EARLY_TEXT)"
 #endif
 
 // chain jobs with wave-uniform skips (empty job slots, no template after the child, short keys):
@@ -429,6 +446,10 @@ struct ChainJobs {  // LDS views, tile-wide
   lds_u16* p0;      // kRBlock: each string's first byte in the stage
   lds_u32* tbl;     // kRBlock: each string's table in the set
   lds_u64* ev;      // kRBlock x 4 columns: the event masks of strings with chains deeper than 2
+  // (LEAN5: no event columns; a middle level's braces come from the classification, kept alive)
+  const lds_u32* cm;
+  const lds_u32* odd;
+  const lds_u32* esc;
 };
 constexpr uint32_t kJobCap = kMaxTop * kRBlock;
 constexpr uint32_t kResFail = 1u << 29, kResReject = 1u << 28;
@@ -452,11 +473,20 @@ constexpr uint32_t kResWhole = 1u << 27;  // a whole-string '{key}' (res_s: the 
 #endif
 template <bool LK>
 constexpr int kJobsPerLane = LK ? IE_LK_JOBS : 2;
+// the LEAN5 instances (96 VGPRs)
+#ifndef IE_EXP_NOEVM
+#define IE_EXP_NOEVM 0
+#endif
+#ifndef IE_LEAN_JOBS
+#define IE_LEAN_JOBS 1
+#endif
+template <bool LK, bool L5>
+constexpr int kJobsPerLaneOf = L5 ? (LK ? 1 : IE_LEAN_JOBS) : kJobsPerLane<LK>;
 
-template <bool FAILC, bool LK>
+template <bool FAILC, bool LK, bool EVM = false>
 __device__ void resolve_jobs(const DevTable& T, const lds_u8* tile, const ChainJobs J, uint32_t j0, uint32_t njobs,
                              bool& chain_fail, uint64_t* stamp) {
-  constexpr int NJ = kJobsPerLane<LK>;
+  constexpr int NJ = kJobsPerLaneOf<LK, EVM>;
   const uint32_t tid = threadIdx.x;
   bool on[NJ], done[NJ], wh[NJ];
   uint32_t job[NJ], cr[NJ], dep[NJ], ls[NJ], tb[NJ], res_k[NJ], res_s[NJ];
@@ -498,7 +528,17 @@ __device__ void resolve_jobs(const DevTable& T, const lds_u8* tile, const ChainJ
       uint32_t c = r == 0 ? cr_first_close(cr[q]) : top ? cr_last_close(cr[q]) : 0u;
       const bool mid = on[q] && r != 0 && !top;
       if (__any(mid)) {
-        if (mid) {
+        if (EVM && !IE_EXP_NOEVM) {
+          // the string's events again, from the tile's chunk masks (up to the chain's last close:
+          // every level of the chain lies before it)
+          bool evok = mid, evesc;
+          Ev Om, Cm;
+          string_events(tile, (uint32_t)(s[q] - tile), cr_last_close(cr[q]) + 1u, J.cm, J.odd, J.esc, evok, evesc, Om, Cm);
+          if (mid) {
+            o = ev_last(ev_below(Om, co_[q]));
+            c = ev_first(ev_from(Cm, cl_[q] + 1u));
+          }
+        } else if (mid) {
           const lds_u64* e = J.ev + ls[q];
           o = ev_last(ev_below(Ev{e[0], e[kRBlock]}, co_[q]));
           c = ev_first(ev_from(Ev{e[2 * kRBlock], e[3 * kRBlock]}, cl_[q] + 1u));
@@ -833,6 +873,22 @@ constexpr uint32_t kOutStage = (kUnionLds - 32) & ~15u;
 static_assert(4 * kRBlock + 13 * 4 * kRBlock <= kUnionLds, "parked descriptors fit the union");
 static_assert(kKeyCap >= 32 && kMaxDepth <= 8, "evaluator scratch");
 
+// LEAN5 union, by phase: classification (chunk masks, odd / escape bits) from the staging through the
+// chain jobs | the job arrays (records, overwritten by their results; meta; result sources; string
+// starts); then the output's first kLWin bytes over all of it (the rest over the input stage)
+constexpr uint32_t kLCmOff = 0;
+constexpr uint32_t kLOddOff = kLCmOff + 4 * (kChunks + 10);
+constexpr uint32_t kLEscOff = kLOddOff + 4 * kOddWords;
+constexpr uint32_t kLCrecOff = (kLEscOff + 4 * kOddWords + 15) & ~15u;
+constexpr uint32_t kLMetaOff = kLCrecOff + 4 * kJobCap;
+constexpr uint32_t kLResSOff = kLMetaOff + 2 * kJobCap;
+constexpr uint32_t kLP0Off = kLResSOff + 4 * kJobCap;
+constexpr uint32_t kUnionLean = (kLP0Off + 2 * kRBlock + 15) & ~15u;
+constexpr uint32_t kLWin = kUnionLean - 16;  // the output window (a multiple of 16; the unaligned
+                                             // stream-out reads one block past it)
+// the most output a LEAN5 tile writes itself (the window, then straight stores); more: k_emit_windows
+constexpr uint32_t kLDirectMax = 2 * kLWin;
+
 // where a tile's strings lie: [lo, hi) for the tile, this lane's string at so (sn bytes)
 struct TileGeo {
   uint64_t lo, hi, so, sn;
@@ -906,6 +962,8 @@ __device__ __forceinline__ uint4 bytes_at(u32x4 x, u32x4 y, uint32_t r) {
 
 // stream the LDS stage [0, len) to g (any alignment): 16-byte stores at 16-byte aligned
 // addresses, each assembled from the two stage blocks it straddles; byte stores at the ends
+// (STAGE: the stage's capacity, which bounds the blocks per lane)
+template <uint32_t STAGE = kOutStage>
 __device__ __forceinline__ void stream_stage(uint8_t* g, const uint8_t* stage, uint32_t len, uint32_t tid) {
   const uintptr_t pg = (uintptr_t)g, pe = pg + len;
   const uintptr_t a_up = (pg + 15) & ~(uintptr_t)15, b_down = pe & ~(uintptr_t)15;
@@ -920,7 +978,7 @@ __device__ __forceinline__ void stream_stage(uint8_t* g, const uint8_t* stage, u
     gst(g + k, ((const lds_u8*)stage)[k]);
   }
   const uint32_t nv = (uint32_t)((b_down - a_up) >> 4);
-  constexpr int kOutV = (kOutStage + kRBlock * 16 - 1) / (kRBlock * 16);
+  constexpr int kOutV = (STAGE + kRBlock * 16 - 1) / (kRBlock * 16);
   uint4 v[kOutV];
   if (head == 0) {  // (uniform) a 16-aligned destination, e.g. reserved ranges: the stage's blocks as they are
 #pragma unroll
@@ -1005,6 +1063,26 @@ __device__ __forceinline__ void window_piece(lds_u8* win, int64_t rel, const uin
   }
 }
 
+// len (<= 28) bytes held as 8 little-endian words (zero past the text) to any global address: head
+// bytes until 4-aligned, then dwords realigned in registers, then the tail bytes (put_words' twin)
+__device__ __forceinline__ void put_words_g(uint8_t* dst, const uint32_t (&t)[8], uint32_t len) {
+  const uint32_t h0 = (0u - (uint32_t)(uintptr_t)dst) & 3u, h = h0 < len ? h0 : len;
+  if (h > 0) gst(dst, (uint8_t)t[0]);
+  if (h > 1) gst(dst + 1, (uint8_t)(t[0] >> 8));
+  if (h > 2) gst(dst + 2, (uint8_t)(t[0] >> 16));
+  const uint32_t rest = len - h, nfull = rest >> 2, r = rest & 3u;
+  uint32_t* q = (uint32_t*)(dst + h);
+  uint32_t last = 0;
+#pragma unroll
+  for (int k = 0; k < 7; k++) {
+    const uint32_t a = __builtin_amdgcn_alignbyte(t[k + 1], t[k], h);  // text bytes h+4k .. h+4k+3
+    if ((uint32_t)k < nfull) gst(q + k, a);
+    last = (uint32_t)k == nfull ? a : last;
+  }
+  uint8_t* b = dst + h + 4u * nfull;
+  for (uint32_t k = 0; k < r; k++) gst(b + k, (uint8_t)(last >> (8u * k)));
+}
+
 // len bytes at src (global memory) -> stage + off, by this lane; pieces over 96 bytes (multi-KB
 // values such as a state's history) by the whole wave instead, so that one lane's long copy does
 // not hold up its tile (and with it every later tile's look-back). Uniform control flow.
@@ -1066,19 +1144,19 @@ __global__ __launch_bounds__(kRBlock) void k_emit_windows(Batch B0, Batch B1, Wo
   const uint32_t slot0 = per > 1u ? blockIdx.x / per : blockIdx.x, wk = per > 1u ? blockIdx.x % per : 0u;
   const uint32_t slot_step = per > 1u ? count : gridDim.x;  // (per > 1: one slot per workgroup)
   for (uint32_t slot = slot0; slot < count; slot += slot_step) {
-    const uint32_t tword = gld(W.defer_tiles + slot), tile = tword & ~kDeferSub;
-    Batch B = (tword & kDeferSub) ? B1 : B0;  // (uniform)
+    // the tile's record {tile | kDeferSub, -, base, total} and each lane's descriptor {.., local,
+    // length}, as its k_resolve left them: a later pass of the same call may have rewritten the
+    // batch's offsets / lengths / statuses of strings it deferred (its own results)
+    const uint4 rec = gld4((const uint4*)(W.defer_tiles + 8ull * slot)), rec2 = gld4((const uint4*)(W.defer_tiles + 8ull * slot) + 1);
+    const uint32_t tile = rec.x & ~kDeferSub;
+    Batch B = (rec.x & kDeferSub) ? B1 : B0;  // (uniform)
     if (B.n_dev) {
       const uint64_t nd = gld(B.n_dev);
       B.n = nd < B.n ? nd : B.n;
     }
-    const uint64_t first = (uint64_t)tile * kRBlock, last = min(first + (uint64_t)kRBlock, B.n), i = first + tid;
-    // (a deferred subset's results sit at out_index[] of the batch)
-    const uint64_t of = B.out_index ? gld(B.out_index + first) : first;
-    const uint64_t ol = B.out_index ? gld(B.out_index + last - 1) : last - 1;
-    const uint64_t base = gld(B.out_off + of);
-    const uint64_t tile_total =
-        (B.out_len ? gld(B.out_off + ol) + gld(B.out_len + ol) : gld(B.out_off + last)) - base;
+    const uint64_t first = (uint64_t)tile * kRBlock, i = first + tid;
+    const uint64_t base = ((uint64_t)rec.w << 32) | rec.z;
+    const uint64_t tile_total = ((uint64_t)rec2.y << 32) | rec2.x;
     const uint4* dd = W.defer_desc + ((uint64_t)slot * kRBlock + tid) * 4;
     Desc d;
     uint32_t olen = 0, n32 = 0;
@@ -1090,10 +1168,8 @@ __global__ __launch_bounds__(kRBlock) void k_emit_windows(Batch B0, Batch B1, Wo
       d.close[0] = b.x, d.close[1] = b.y, d.close[2] = b.z, n32 = b.w;
       d.vk[0] = c.x, d.vk[1] = c.y, d.vk[2] = c.z;
       d.vs[0] = e.x, d.vs[1] = e.y, d.vs[2] = e.z;
-      const uint64_t oi = B.out_index ? gld(B.out_index + i) : i;
-      const uint64_t o = gld(B.out_off + oi);
-      local = o - base;
-      olen = gld(B.status + oi) != IE_OK_STR ? 0u : B.out_len ? gld(B.out_len + oi) : (uint32_t)(gld(B.out_off + i + 1) - o);
+      local = c.w;
+      olen = e.w;
       s = B.bytes + gld(B.in_off + i);
     } else {
       d.ntop = 0;
@@ -1140,8 +1216,10 @@ __global__ __launch_bounds__(kRBlock) void k_emit_windows(Batch B0, Batch B1, Wo
 // classified again) and then resolved; strings that cannot be finished there (not staged, or
 // needing the literal path) go to W.udefer_list for the deferred pass.
 template <bool FAILC, bool MULTI, bool VIEWS, bool UNESC = false, bool LK = false, bool LEAN = false>
-__global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(LK ? IE_WAVES_PER_EU_LK : IE_WAVES_PER_EU))) void k_resolve(Batch B0, Work W, DevTable T, uint8_t* out,
+__global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(
+    LEAN && IE_LEAN5 ? IE_WAVES_PER_EU_LEAN : LK ? IE_WAVES_PER_EU_LK : IE_WAVES_PER_EU))) void k_resolve(Batch B0, Work W, DevTable T, uint8_t* out,
                                                     uint64_t cap) {
+  constexpr bool L5 = LEAN && IE_LEAN5 != 0;
   // a deferred subset counts its strings on the device (the grid is sized for B0.n)
   Batch B = B0;
   if (B0.n_dev) {
@@ -1149,15 +1227,15 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(LK ? IE
     B.n = nd < B0.n ? nd : B0.n;
   }
   __shared__ __attribute__((aligned(16))) uint8_t s_in[kRTileBytes + 48];
-  __shared__ __attribute__((aligned(16))) uint8_t s_u[kUnionLds];
+  __shared__ __attribute__((aligned(16))) uint8_t s_u[L5 ? kUnionLean : kUnionLds];
   __shared__ uint32_t s_olen[kRBlock];  // output length; the value id for IE_OK_VALUE strings
   __shared__ uint8_t s_st[kRBlock];
-  __shared__ uint16_t s_pend[kRBlock];
+  __shared__ uint16_t s_pend[LEAN ? 1 : kRBlock];  // (no literal path in a LEAN pass)
   __shared__ uint32_t s_misc[4];  // tile, pending count, defer slot
   __shared__ uint64_t s_red[kRBlock / 64 + 2];
-  lds_u32* const s_cm = (lds_u32*)(lds_u8*)(s_u + kCmOff);    // event masks of the staged chunks (+ pad)
-  lds_u32* const s_odd = (lds_u32*)(lds_u8*)(s_u + kOddOff);  // one bit per chunk: 0xE3 inside
-  lds_u32* const s_esc = (lds_u32*)(lds_u8*)(s_u + kEscOff);  // one bit per chunk: '\' inside
+  lds_u32* const s_cm = (lds_u32*)(lds_u8*)(s_u + (L5 ? kLCmOff : kCmOff));    // event masks of the staged chunks (+ pad)
+  lds_u32* const s_odd = (lds_u32*)(lds_u8*)(s_u + (L5 ? kLOddOff : kOddOff));  // one bit per chunk: 0xE3 inside
+  lds_u32* const s_esc = (lds_u32*)(lds_u8*)(s_u + (L5 ? kLEscOff : kEscOff));  // one bit per chunk: '\' inside
   lds_u32* const s_lit = (lds_u32*)(lds_u8*)s_u;              // literal-path results: pool offset >> 4
 
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
@@ -1325,14 +1403,14 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(LK ? IE
       // chains: parse per string, resolve per chain job (tile-wide), gather per string. The job
       // arrays live in the union (results and string starts in the exact evaluator's key area,
       // records in the chunk masks once every string has read its event windows).
-      lds_u64* const ev = (lds_u64*)(lds_u8*)(s_u + kKbufLds) + tid;
       uint32_t crec[kMaxTop], cdep[kMaxTop], nch = 0;
       Ev Om, Cm;
       uint32_t maxd;
       bool whole1;
       const bool pok = parse_chains((const lds_u8*)s_in, p0, (uint32_t)sn, s_cm, s_odd, s_esc, active && lane_staged,
                                     crec, cdep, nch, Om, Cm, maxd, whole1);
-      if (__any(maxd > 2u)) {  // middle levels are found from these masks in their round
+      if (!L5 && __any(maxd > 2u)) {  // middle levels are found from these masks in their round
+        lds_u64* const ev = (lds_u64*)(lds_u8*)(s_u + kKbufLds) + tid;
         ev[0] = Om.lo, ev[kRBlock] = Om.hi, ev[2 * kRBlock] = Cm.lo, ev[3 * kRBlock] = Cm.hi;
       }
       uint64_t njobs64;
@@ -1341,10 +1419,15 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(LK ? IE
       const uint32_t jb = (uint32_t)block_scan<IE_FEWER_BARRIERS == 0>(pok ? nch : 0u, s_red, &njobs64);
       const uint32_t njobs = (uint32_t)njobs64;
       IE_STAMP(8);
-      const ChainJobs J{(lds_u32*)(lds_u8*)(s_u + kCmOff), (lds_u16*)(lds_u8*)(s_u + 8 * kJobCap),
-                        (lds_u32*)(lds_u8*)s_u, (lds_u32*)(lds_u8*)(s_u + 4 * kJobCap),
-                        (lds_u16*)(lds_u8*)(s_u + 10 * kJobCap), (lds_u32*)(lds_u8*)s_olen,
-                        (lds_u64*)(lds_u8*)(s_u + kKbufLds)};
+      const ChainJobs J =
+          L5 ? ChainJobs{(lds_u32*)(lds_u8*)(s_u + kLCrecOff), (lds_u16*)(lds_u8*)(s_u + kLMetaOff),
+                         (lds_u32*)(lds_u8*)(s_u + kLCrecOff),  // (a job's result over its record)
+                         (lds_u32*)(lds_u8*)(s_u + kLResSOff), (lds_u16*)(lds_u8*)(s_u + kLP0Off),
+                         (lds_u32*)(lds_u8*)s_olen, nullptr, s_cm, s_odd, s_esc}
+             : ChainJobs{(lds_u32*)(lds_u8*)(s_u + kCmOff), (lds_u16*)(lds_u8*)(s_u + 8 * kJobCap),
+                         (lds_u32*)(lds_u8*)s_u, (lds_u32*)(lds_u8*)(s_u + 4 * kJobCap),
+                         (lds_u16*)(lds_u8*)(s_u + 10 * kJobCap), (lds_u32*)(lds_u8*)s_olen,
+                         (lds_u64*)(lds_u8*)(s_u + kKbufLds), nullptr, nullptr, nullptr};
       if (pok) {
 #pragma unroll
         for (int c = 0; c < kMaxTop; c++) {
@@ -1358,7 +1441,7 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(LK ? IE
       J.tbl[tid] = tid_s;
       __syncthreads();
       IE_STAMP(9);
-      for (uint32_t j0 = 0; j0 < njobs; j0 += kJobsPerLane<LK> * kRBlock) resolve_jobs<FAILC, LK>(T, (const lds_u8*)s_in, J, j0, njobs, chain_fail, j0 == 0 ? stamp_row : nullptr);
+      for (uint32_t j0 = 0; j0 < njobs; j0 += kJobsPerLaneOf<LK, L5> * kRBlock) resolve_jobs<FAILC, LK, L5>(T, (const lds_u8*)s_in, J, j0, njobs, chain_fail, j0 == 0 ? stamp_row : nullptr);
       IE_STAMP(10);
       __syncthreads();
       IE_STAMP(11);
@@ -1418,7 +1501,7 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(LK ? IE
         }
       }
     }
-    pend = i < B.n && st == kStatusPending;
+    pend = !LEAN && i < B.n && st == kStatusPending;
     if (pend) s_pend[atomicAdd(&s_misc[1], 1u)] = (uint16_t)tid;
     s_st[tid] = st;
     s_olen[tid] = st == IE_OK_STR ? olen : (st == IE_OK_VALUE || st == IE_RECURSE ? vid : 0u);
@@ -1569,11 +1652,98 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(LK ? IE
 
   // ---- 5. the tile's output bytes into the LDS stage (tile-relative offsets) while the
   //      look-back is pending; tiles whose output does not fit store straight to HBM later ----
-  const bool in_stage = tile_total <= (uint64_t)kOutStage;
+  // (LEAN5: the output's first kLWin bytes go to the window stage (the union), the rest straight to
+  // HBM; a tile of more than kLDirectMax bytes is deferred)
+  const bool in_stage = L5 ? tile_total <= (uint64_t)kLDirectMax : tile_total <= (uint64_t)kOutStage;
 #if !IE_EARLY_TEXT
   const bool mine = i < B.n && st == IE_OK_STR && olen;
 #endif
-  if (in_stage) {
+  // LEAN5: the tile's place first (its bytes past the window are stored during the build)
+  if (L5) {
+    if (tid == 0) s_red[kRBlock / 64] = lb_early;
+    __syncthreads();
+  }
+  const uint64_t base5 = L5 ? s_red[kRBlock / 64] : 0ull;
+  // LEAN5: this lane's output in one pass over its pieces: the bytes in the window [0, kLWin) of
+  // the tile's output to the window stage (template runs from the input stage, entry texts from
+  // registers, arena texts by lane or by wave), the bytes past it stored straight to their place in
+  // HBM by the lane (a piece across the edge: in part each way), so that no second build follows
+  // the window's stream-out
+  const uint32_t local_w = (uint32_t)local;
+  uint8_t* const gout = out + base5;
+  auto build_direct = [&]() {
+    const lds_u8* const ls = (const lds_u8*)s;
+    const uint32_t ntop = mine ? d.ntop : 0u;
+    const bool in_win = mine && local_w < kLWin;              // (bytes in the window)
+    const bool past = mine && local_w + olen > kLWin;         // (bytes past it)
+    uint32_t w = local_w;  // the next piece's place in the tile's output
+    // 1. the window's bytes, and the entry texts wholly past it (from the registers)
+#pragma unroll
+    for (int j = 0; j <= kMaxTop; j++) {
+      // template run j
+      const uint32_t t_lo = j == 0 ? 0u : d.close[j - 1] + 1;
+      const uint32_t t_hi = (uint32_t)j < ntop ? d.open[j] : n32;
+      const uint32_t tl = mine && (uint32_t)j <= ntop ? t_hi - t_lo : 0u;
+      const uint32_t tb = w + tl < kLWin ? w + tl : kLWin;
+      const uint32_t tn = in_win && w < tb ? tb - w : 0u;
+      if (__any(tn != 0)) {
+        lds_u8* const dst = (lds_u8*)s_u + (tn ? w : 0u);
+        if (lane_staged) lds_copy(dst, tn ? ls + t_lo : (const lds_u8*)s_in, tn);
+        else if (tn) copy_bytes<true, false>((uint8_t*)dst, s + t_lo, tn);  // a string past the stage
+      }
+      w += tl;
+      if (j == kMaxTop) break;
+      // value j
+      if (j + 1 < kMaxTop) load_text(j + 1, tt[(j + 1) & 1]);
+      const bool von = mine && (uint32_t)j < ntop;
+      const uint32_t kind = d.vk[j] >> 30, len = von ? d.vk[j] & kLenMask : 0u;
+      const bool ent = von && kind == kValEntry;
+      const uint32_t vb = w + len < kLWin ? w + len : kLWin;
+      const bool vin = von && w < vb;
+      const bool ewhole = ent && vin && vb == w + len;
+      if (__any(ewhole) && ewhole) put_words((lds_u8*)s_u + w, tt[j & 1], len);
+      if (ent && vin && !ewhole) {  // (an entry text across the edge: its window part, byte by byte)
+        const uint8_t* tx = T.entries[d.vs[j]].text;
+        for (uint32_t k = w; k < vb; k++) ((lds_u8*)s_u)[k] = gld(tx + (k - w));
+      }
+      const bool far = vin && kind != kValEntry;  // an arena text
+      if (__any(far))
+        stage_piece((lds_u8*)s_u, far, far ? w : 0u, kind == kValArena ? T.arena + d.vs[j] : W.pool + ((uint64_t)d.vs[j] << 4),
+                    far ? vb - w : 0u);
+      const bool eg = ent && w >= kLWin;
+      if (__any(eg) && eg) put_words_g(gout + w, tt[j & 1], len);
+      w += len;
+    }
+    // 2. the rest past the window, by the lane (not unrolled: one copy loop of each kind): template
+    //    runs from the input stage, arena texts and entry texts across the edge from the table
+    if (__any(past)) {
+      uint32_t pw = local_w;
+#pragma unroll 1
+      for (uint32_t j = 0; past && j <= ntop; j++) {
+        const uint32_t t_lo = j == 0 ? 0u : d.close[j - 1] + 1;
+        const uint32_t t_hi = j < ntop ? d.open[j] : n32;
+        const uint32_t tl = t_hi - t_lo, ga = pw > kLWin ? pw : kLWin;
+        if (ga < pw + tl) {
+          if (lane_staged) copy_bytes<false, true>(gout + ga, (const uint8_t*)(ls + t_lo + (ga - pw)), pw + tl - ga);
+          else copy_bytes<false, false>(gout + ga, s + t_lo + (ga - pw), pw + tl - ga);
+        }
+        pw += tl;
+        if (j == ntop) break;
+        const uint32_t vk = j == 0 ? d.vk[0] : j == 1 ? d.vk[1] : d.vk[2];
+        const uint32_t vs = j == 0 ? d.vs[0] : j == 1 ? d.vs[1] : d.vs[2];
+        const uint32_t kind = vk >> 30, len = vk & kLenMask, va = pw > kLWin ? pw : kLWin;
+        if (va < pw + len && !(kind == kValEntry && pw >= kLWin))  // (not an entry text wholly past: step 1's)
+          copy_bytes<false, false>(gout + va,
+                                   (kind == kValEntry ? (const uint8_t*)T.entries[vs].text
+                                    : kind == kValArena ? T.arena + vs : W.pool + ((uint64_t)vs << 4)) + (va - pw),
+                                   pw + len - va);
+        pw += len;
+      }
+    }
+  };
+  if (L5) {
+    if (in_stage && base5 + tile_total <= cap) build_direct();
+  } else if (in_stage) {
     // entry texts of the values (inline, <= kInlineText bytes): into registers, value j's loads
     // issued one value ahead of its use
 #if !IE_EARLY_TEXT
@@ -1621,7 +1791,7 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(LK ? IE
   }
   IE_STAMP(4);
   if (VIEWS) {
-    if (tid == 0) s_red[kRBlock / 64] = lb_early;
+    if (!L5 && tid == 0) s_red[kRBlock / 64] = lb_early;
   } else if (wave == 0) {
     const uint64_t b = look_back(W.tile_state, tile, tile_total, W.err, W.stamps ? W.stats + 2 : nullptr, lb_early);
     if (tid == 0) s_red[kRBlock / 64] = b;
@@ -1657,7 +1827,13 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(LK ? IE
   // ---- 6. stream out: 16-byte stores at 16-byte aligned addresses, each assembled from the
   //      two stage blocks it straddles (the shift is uniform over the tile) ----
   uint8_t* const g = out + base;
-  if (write_bytes && in_stage) {
+  if (L5 && write_bytes && in_stage) {
+    // the window (the bytes past it are out already)
+    uint32_t tid_w;  // (opaque: the stream-out's per-block addresses computed here, not kept from before)
+    asm volatile("v_mov_b32 %0, %1" : "=v"(tid_w) : "v"(tid_t));
+    if (!(W.debug_noeval & 4u))  // (diagnostic bit 2: no bytes)
+      stream_stage<kLWin>(g, s_u, (uint32_t)min((uint64_t)kLWin, tile_total), tid_w);
+  } else if (!L5 && write_bytes && in_stage) {
     if (!(W.debug_noeval & 4u)) stream_stage(g, s_u, (uint32_t)tile_total, tid_t);  // (diagnostic bit 2: no bytes)
   } else if (write_bytes) {
     // a tile whose output exceeds the stage (long strings, large expansions) or whose input was
@@ -1671,9 +1847,13 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(LK ? IE
     const uint32_t nt = mine ? d.ntop : 0u;
     gst4(dd, make_uint4(nt, d.open[0], d.open[1], d.open[2]));
     gst4(dd + 1, make_uint4(d.close[0], d.close[1], d.close[2], n32));
-    gst4(dd + 2, make_uint4(d.vk[0], d.vk[1], d.vk[2], 0u));
-    gst4(dd + 3, make_uint4(d.vs[0], d.vs[1], d.vs[2], 0u));
-    if (tid == 0) gst(W.defer_tiles + slot, tile | (B.out_index ? kDeferSub : 0u));  // (a subset's tile: flagged)
+    gst4(dd + 2, make_uint4(d.vk[0], d.vk[1], d.vk[2], mine ? (uint32_t)local : 0u));
+    gst4(dd + 3, make_uint4(d.vs[0], d.vs[1], d.vs[2], mine ? olen : 0u));
+    if (tid == 0) {  // the tile's record (a subset's tile: flagged)
+      uint4* r = (uint4*)(W.defer_tiles + 8ull * slot);
+      gst4(r, make_uint4(tile | (B.out_index ? kDeferSub : 0u), 0u, (uint32_t)base, (uint32_t)(base >> 32)));
+      gst4(r + 1, make_uint4((uint32_t)tile_total, (uint32_t)(tile_total >> 32), 0u, 0u));
+    }
   }
   IE_STAMP(5);
 #undef IE_STAMP
@@ -1781,6 +1961,7 @@ hipError_t launch_resolve_impl(const Batch& B, const Work& W, const DevTable& T,
   const uint32_t grid = B.n_dev && B.out_len && !unesc && !lean ? (uint32_t)(tiles < kSubsetGrid ? tiles : kSubsetGrid)
                                                                   : (uint32_t)tiles;
   const bool multi = B.table_id != nullptr;
+#ifndef IE_EXP_ONLY_LEAN  // (experiments: -DIE_EXP_ONLY_LEAN compiles the LEAN instances alone, tools/resusage.sh)
   if (unesc) {  // the fused unescape command (views only)
     if (!B.out_len) return hipErrorInvalidValue;
     const int v = (W.fail_commit ? 2 : 0) | (multi ? 1 : 0);
@@ -1791,6 +1972,7 @@ hipError_t launch_resolve_impl(const Batch& B, const Work& W, const DevTable& T,
     if (emit) hipLaunchKernelGGL(k_emit_windows, dim3(egrid), dim3(kRBlock), 0, st, B, B, W, T, out);
     return hipGetLastError();
   }
+#endif
   // LK: a table with 17-32 byte keys gets the instances whose chain jobs take such keys (they cost
   // config 3 3 %: their registers; config 5 -32 %: its long keys leave the exact evaluator)
   const int variant = ((T.flags & TF_LONG_KEYS) ? 8 : 0) | (W.fail_commit ? 4 : 0) | (multi ? 2 : 0) | (B.out_len ? 1 : 0);
@@ -1813,6 +1995,7 @@ hipError_t launch_resolve_impl(const Batch& B, const Work& W, const DevTable& T,
     return hipGetLastError();
   }
 #endif
+#ifndef IE_EXP_ONLY_LEAN
   switch (variant) {
 #define IE_LAUNCH(V, F, M, S, L) \
   case V: hipLaunchKernelGGL((k_resolve<F, M, S, false, L>), dim3(grid), dim3(kRBlock), 0, st, B, W, T, out, cap); break;
@@ -1834,6 +2017,7 @@ hipError_t launch_resolve_impl(const Batch& B, const Work& W, const DevTable& T,
     IE_LAUNCH(15, true, true, true, true)
 #undef IE_LAUNCH
   }
+#endif
   // the deferred (oversized) tiles' bytes (exits at once when there are none); views: the total
   // (a one-tile views batch may go without it: no_emit, see launch_resolve)
   if (emit && (out || B.out_len) && !(no_emit && grid == 1u && B.out_len && !W.reserve16))

@@ -1231,3 +1231,91 @@ def test_one_string_calls_without_the_emit_kernel():
         t.close()
     finally:
         x.set_option(N.OPT_VIEWS, 0)
+
+
+def _window_table(rng):
+    """Values of every size class the output windows meet: inline entry texts (<= 28 B), arena
+    texts of tens to hundreds of bytes, and multi-KB texts (a tile of those spans many windows or
+    goes to the windowed emit kernel)."""
+    t = {}
+    for j in range(200):
+        t["s%d" % j] = "".join(rng.choice("abcdefé€") for _ in range(rng.randint(0, 26)))
+        t["m%d" % j] = "".join(rng.choice("mnopq rs") for _ in range(rng.randint(29, 300)))
+        t["l%d" % j] = "".join(rng.choice("LMNOP-") for _ in range(rng.randint(900, 5000)))
+        t["i%d" % j] = "s%d" % rng.randrange(200)  # {q-{iN}}-style chains: the inner value is a key
+        t["q-s%d" % j] = "".join(rng.choice("xyz") for _ in range(rng.randint(1, 40)))
+    return t
+
+
+def _window_strings(rng, n, p_long):
+    out = []
+    for _ in range(n):
+        parts = []
+        for _ in range(rng.randint(1, 3)):
+            r = rng.random()
+            if r < p_long:
+                k = "{l%d}" % rng.randrange(200)
+            elif r < 0.35:
+                k = "{m%d}" % rng.randrange(200)
+            elif r < 0.6:
+                k = "{q-{i%d}}" % rng.randrange(200)
+            else:
+                k = "{s%d}" % rng.randrange(200)
+            parts.append("".join(rng.choice("ab cd") for _ in range(rng.randint(1, 30))) + k)
+        out.append("".join(parts) + "z" * rng.randint(0, 9))
+    return out
+
+
+@pytest.mark.parametrize("p_long", [0.0, 0.004, 0.05])
+def test_output_windows_vs_oracle(p_long, fail_commit):
+    """Tile outputs from a fraction of the LDS stage to ~40 times it (values of every size class):
+    a tile over the stage is deferred to k_emit_windows, which a two-pass views call (the 'defer'
+    fixture variants: the LEAN pass, then its deferred subset) launches ONCE for both passes, from
+    per-tile records (the subset pass rewrites the first pass's rows of the strings it takes). With
+    -DIE_LEAN5=1 the LEAN pass's 13 KB stage and its direct stores past it. Every fixture layout,
+    against the oracle."""
+    rng = random.Random(int(p_long * 1000) + 5)
+    table = _window_table(rng)
+    strings = _window_strings(rng, 6000, p_long)
+    bad = compare_with_oracle(table, strings)
+    assert not bad, [b[:2] for b in bad[:3]]
+
+
+@pytest.mark.parametrize("reserve", [0, 32])
+def test_output_windows_device_views_lean(reserve):
+    """The same through ie_interpolate_device_views with the two-pass LEAN path forced and reserved
+    output ranges on and off (16-aligned vs unaligned stream-outs), a batch of many tiles, deferred
+    tiles in both passes."""
+    rng = random.Random(77 + reserve)
+    tdict = _window_table(rng)
+    strings = _window_strings(rng, 40_000, 0.01)
+    x = N.Exec(0)
+    x.set_option(N.OPT_VIEWS, 1)
+    x.set_option(N.OPT_DEFER, 1)
+    x.set_option(N.OPT_RESERVE, reserve)
+    table = PKG.InsertsTable(tdict, clock=CLOCK)
+    blob, offs = N.pack(strings)
+    n = len(strings)
+    d_bytes = N.DeviceBuffer.from_numpy(x, np.frombuffer(blob + b"\0" * 16, np.uint8))
+    d_off = N.DeviceBuffer.from_numpy(x, np.asarray(offs, np.uint64))
+    cap = 64 * len(blob) + (1 << 20)
+    r = DevResult(x, n, cap)
+    lens = N.DeviceBuffer(x, 4 * n + 4)
+    v = N.DevViews(r.bytes.ptr, cap, r.off.ptr, lens.ptr, r.status.ptr, r.vid.ptr, r.total_d.ptr)
+    N.check(N.lib().ie_interpolate_device_views(x.h, table.h, None, d_bytes.ptr, d_off.ptr, None, n, ctypes.byref(v)),
+            "ie_interpolate_device_views")
+    x.sync()
+    st = r.status.to_numpy(np.uint8, n)
+    starts = r.off.to_numpy(np.uint64, n)
+    ln = lens.to_numpy(np.uint32, n).astype(np.uint64)
+    ext = int((starts + ln).max())
+    out = r.bytes.to_numpy(np.uint8, ext).tobytes()
+    assert_views_disjoint(starts, ln, ext)
+    ref = O.Oracle(tdict, "py", clock=CLOCK)
+    bad = []
+    for i, s in enumerate(strings):
+        rst, rout, _ = ref.interpolate(s)
+        got = out[int(starts[i]):int(starts[i] + ln[i])].decode("utf-8", "surrogatepass") if st[i] == 0 else None
+        if N.STATUS_NAMES[st[i]] != rst or (rst == "OK_STR" and got != rout):
+            bad.append((i, s[:60], N.STATUS_NAMES[st[i]], rst))
+    assert not bad, bad[:3]
