@@ -267,7 +267,10 @@ int ie_exec_timing(ie_exec* x, ie_timing* out); /* syncs */
                           no keys, misses stay on the fast evaluators) */
 int ie_exec_set_option(ie_exec* x, int32_t option, int64_t value);
 /* Literal-path scratch pool size. Setting it makes ie_interpolate_device fully asynchronous: it no
- * longer waits to check the pool's demand, and strings that ran out of it report IE_E_OVERFLOW. */
+ * longer waits to check the pool's demand, and strings that ran out of it report IE_E_OVERFLOW.
+ * Without it the device calls wait only for the demand, which the call's last kernel publishes to
+ * host memory as it starts (not for the stream): read their results through the exec's stream
+ * (ie_copy_d2h) or after ie_exec_sync, as with the asynchronous form. */
 int ie_exec_set_scratch(ie_exec* x, uint64_t bytes);
 /* Keys only the host can look up (get_interpdata's file fallback for a key that is not a canonical
  * relative file name under the inserts directory, py:452-461): for every string of the exec's last

@@ -167,11 +167,18 @@ int set_device(int32_t dev) {
 constexpr uint64_t kLeanMinN = 1ull << 19;
 constexpr uint32_t kSumShards = 16;  // reserved-range tile sums (IE_OPT_RESERVE), 128 B apart after the counters
 constexpr uint64_t kCounterBytes = 64 + kSumShards * 128;
+// Two counter sets, used in turn: a two-pass views call's last kernel (k_emit_windows) zeroes the set
+// it did not use, so the next call starts on a clean set without a fill of its own; every other call
+// fills its set first. The look-back words of a packed interpolation follow both sets.
+constexpr uint64_t kLookbackOff = 2 * kCounterBytes;
+inline uint8_t* ctr_base(ie_exec* x) { return (uint8_t*)x->counters.p + x->ctr_cur * kCounterBytes; }
 int ensure_work(ie_exec* x, int op, uint64_t n) {
   // (k_resolve tiles of 128 strings or more: enough look-back words and deferred-tile slots)
   const uint64_t tiles = (n + 127) / 128 + 1;
-  // counters, then (interpolation) the look-back words: one buffer, zeroed by one memset per call
-  IE_HIP(x->counters.ensure(kCounterBytes + (op == kOpInterp ? tiles * sizeof(uint64_t) : 0)));
+  // the counter sets, then (interpolation) the look-back words: one buffer (a new one is not clean)
+  const void* const before = x->counters.p;
+  IE_HIP(x->counters.ensure(kLookbackOff + (op == kOpInterp ? tiles * sizeof(uint64_t) : 0)));
+  if (x->counters.p != before) x->ctr_next_clean = false;
   if (op == kOpInterp) {
     IE_HIP(x->pool.ensure(x->pool_request));
     // room for every tile to be deferred (64 B of descriptor per string; grow-only, never read
@@ -189,7 +196,7 @@ int ensure_work(ie_exec* x, int op, uint64_t n) {
 
 Work make_work(ie_exec* x, uint64_t* total) {
   Work W{};
-  void* const C = x->ctr_override ? (void*)x->ctr_override : x->counters.p;
+  void* const C = x->ctr_override ? (void*)x->ctr_override : (void*)ctr_base(x);
   W.total = total;
   W.tile_ticket = (uint32_t*)C;
   W.err = (uint32_t*)C + 1;
@@ -201,7 +208,8 @@ Work make_work(ie_exec* x, uint64_t* total) {
   W.defer_count = (uint32_t*)C + 9;
   W.defer_tiles = (uint32_t*)x->defer_tiles.p;
   W.defer_desc = (uint4*)x->defer_desc.p;
-  W.tile_state = (uint64_t*)((uint8_t*)C + kCounterBytes);
+  // (the small host path's own block: its look-back words right after its counters)
+  W.tile_state = (uint64_t*)(x->ctr_override ? (uint8_t*)C + kCounterBytes : (uint8_t*)x->counters.p + kLookbackOff);
   W.shards = (uint64_t*)((uint8_t*)C + 64);
   W.n_shards = kSumShards;
   W.cursor = (uint64_t*)C + 5;  // words 10-11
@@ -269,6 +277,15 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
   }
   rc = ensure_work(x, op, n);
   if (rc) return rc;
+  x->pool_pub = false;
+  // the counter set of this call: the clean one the last two-pass call left, else the current one
+  // (filled below)
+  bool ctr_clean = false;
+  if (!x->ctr_override && x->ctr_next_clean) {
+    x->ctr_cur ^= 1u;
+    x->ctr_next_clean = false;
+    ctr_clean = true;
+  }
   x->stamp_tiles = 0;
   x->no_emit_used = false;
   if (op == kOpInterp && !x->stamps_path.empty()) {  // diagnostic build hook, see DESIGN.md
@@ -300,7 +317,11 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
   if (x->timing) IE_HIP(hipEventRecord(x->ev[0], st));
   // the counters and, for a packed interpolation, the look-back words (one fill instead of two)
   const uint64_t zero_tiles = (op == kOpInterp && n && !d_out_len) ? (n + 127) / 128 : 0;  // (ensure_work)
-  if (!x->ctr_override) IE_HIP(hipMemsetAsync(x->counters.p, 0, kCounterBytes + zero_tiles * sizeof(uint64_t), st));
+  if (!x->ctr_override && (!ctr_clean || zero_tiles)) {  // (one fill: from the set through the look-back words)
+    uint8_t* const c0 = ctr_base(x);
+    const uint64_t to = zero_tiles ? kLookbackOff + zero_tiles * sizeof(uint64_t) : (uint64_t)(c0 - (uint8_t*)x->counters.p) + kCounterBytes;
+    IE_HIP(hipMemsetAsync(c0, 0, to - (uint64_t)(c0 - (uint8_t*)x->counters.p), st));
+  }
   if (n == 0) {
     if (!d_out_len) IE_HIP(hipMemsetAsync(out->offsets, 0, sizeof(uint64_t), st));
     IE_HIP(hipMemsetAsync(out->total, 0, sizeof(uint64_t), st));
@@ -318,18 +339,33 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
       const uint64_t heavy = (uint64_t)x->stat_host[3] + x->stat_host[0];
       if (heavy * 256 > x->stat_n) x->defer_slow = true;
       else if (heavy * 4096 < x->stat_n) x->defer_slow = false;
+      // the next two-pass call's grids, from the last two-pass call's telemetry: as many subset
+      // workgroups as the strings it deferred need (8 per XCD when none), and a small emit grid
+      // when no tile had to be windowed
+      if (x->stat_two_pass) {
+        const uint64_t need = (x->stat_host[3] + 255) / 256;
+        x->hint_sub_grid = (uint32_t)std::min<uint64_t>(1024, std::max<uint64_t>(64, need));
+        x->hint_emit_grid = x->stat_host[5] ? 512u : 32u;
+      }
     }
     W.fail_commit = forced ? (uint32_t)x->opt_fail_commit : (uint32_t)x->fail_commit;
     if (W.err_keys) W.fail_commit = 0;  // misses go through the exact evaluator to the literal path
     // the adaptive choices' telemetry: written into pinned host words by the call's last emit kernel
     // (no copy after it), or copied below when the call has none (a one-tile no-emit call)
     const bool want_stats = !x->stat_pending && !x->no_stats;
-    if (want_stats && !x->stat_host) {
+    bool two_pass = false;
+    if (!x->stat_host) {  // (words 0-5 the telemetry, 8-9 the pool demand word)
       IE_HIP(hipHostMalloc((void**)&x->stat_host, 64, hipHostMallocMapped));
       IE_HIP(hipHostGetDevicePointer((void**)&x->stat_dev, x->stat_host, 0));
       IE_HIP(hipEventCreateWithFlags(&x->stat_ev, hipEventDisableTiming));
+      memset(x->stat_host, 0, 64);
     }
     W.stat_out = want_stats ? x->stat_dev : nullptr;
+    // the literal pool's demand, published to the host by the call's last emit kernel (the device
+    // APIs wait for that word instead of synchronising the stream: pool_demand)
+    W.pool_out = (uint64_t*)(x->stat_dev + 8);
+    W.pool_seq = (uint32_t)(++x->pool_seq & 0xFFFFFFu);
+    x->pool_pub = true;
     if (x->timing) IE_HIP(hipEventRecord(x->ev[1], st));
     // 512-string tiles halve the look-back hops: the unescape command's second resolve (its input
     // is interpolation output, so its evaluation is light and the look-back bounds it) takes them
@@ -351,23 +387,33 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
       IE_HIP(x->u_len.ensure(n * 4 + 4));
       if (d_tid) IE_HIP(x->u_tid.ensure(n * 4 + 4));
       W.udefer_list = (uint32_t*)x->u_list.p;
+      W.sub_grid = x->hint_sub_grid;
+      W.emit_grid = x->hint_emit_grid;
+      two_pass = true;
+      if (!x->ctr_override) {  // (the call's emit kernel zeroes the other counter set for the next call)
+        W.zero_next = (uint32_t*)((uint8_t*)x->counters.p + (x->ctr_cur ^ 1u) * kCounterBytes);
+        W.zero_words = (uint32_t)(kCounterBytes / 4);
+      }
       IE_HIP(launch_resolve_deferring(B, W, t->dev, out->bytes, cap, (uint64_t*)x->u_off.p, (uint32_t*)x->u_len.p,
                                       d_tid ? (uint32_t*)x->u_tid.p : nullptr, st));
+      if (W.zero_next) x->ctr_next_clean = true;
     } else {
       // (a one-string call: k_resolve alone, one launch and its emit kernel's ~5 µs fewer)
       const bool ne = x->small_no_emit && d_out_len && !wide && !W.reserve16 && !x->opt_noeval && n <= (uint64_t)kRBlock;
       x->no_emit_used = ne;
-      if (ne) W.stat_out = nullptr;
+      if (ne) W.stat_out = nullptr, W.pool_out = nullptr, x->pool_pub = false;
       IE_HIP(wide ? launch_resolve512(B, W, t->dev, out->bytes, cap, st) : launch_resolve(B, W, t->dev, out->bytes, cap, st, ne));
     }
     if (want_stats) {
-      if (!W.stat_out) IE_HIP(hipMemcpyAsync(x->stat_host, W.stats, 5 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+      if (!W.stat_out) IE_HIP(hipMemcpyAsync(x->stat_host, W.stats, 6 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
       IE_HIP(hipEventRecord(x->stat_ev, st));
       x->stat_pending = true;
       x->stat_n = n;
+      x->stat_two_pass = two_pass;
     }
   } else {
     if (x->timing) IE_HIP(hipEventRecord(x->ev[1], st));
+    x->pool_pub = false;
     IE_HIP(launch_escape(op, B, W, out->bytes, cap, st));
   }
   if (x->timing) {
@@ -381,7 +427,7 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
 // look-back timeout flag of the last call (after a sync)
 int check_device_error(ie_exec* x) {
   uint32_t err = 0;
-  if (x->counters.p) IE_HIP(hipMemcpy(&err, (uint32_t*)x->counters.p + 1, 4, hipMemcpyDeviceToHost));
+  if (x->counters.p) IE_HIP(hipMemcpy(&err, (uint32_t*)ctr_base(x) + 1, 4, hipMemcpyDeviceToHost));
   if (err & 2u) return fail(IE_ERR_CAPACITY, "a step's output did not fit its caller-sized buffer");
   if (err) return fail(IE_ERR_TIMEOUT, "look-back spin timed out (a predecessor tile never published)");
   return IE_SUCCESS;
@@ -447,7 +493,7 @@ int run_host_small(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, 
     IE_HIP(hipMemcpyAsync(h + in_size, dv + in_size, ctr_size + o_err, hipMemcpyDeviceToHost, x->stream));
   } else {
     IE_HIP(hipMemcpyAsync(ho, dout, o_err, hipMemcpyDeviceToHost, x->stream));
-    IE_HIP(hipMemcpyAsync(ho + o_err, (uint32_t*)x->counters.p + 1, 4, hipMemcpyDeviceToHost, x->stream));
+    IE_HIP(hipMemcpyAsync(ho + o_err, (uint32_t*)ctr_base(x) + 1, 4, hipMemcpyDeviceToHost, x->stream));
   }
   IE_HIP(hipStreamSynchronize(x->stream));
   const uint32_t err = ctr_size ? ((const uint32_t*)(h + in_size))[1] : *(const uint32_t*)(ho + o_err);  // (check_device_error's rules)
@@ -2157,13 +2203,13 @@ int ie_exec_timing(ie_exec* x, ie_timing* out) {
   out->complex_ms = 0.0f;   // literal strings are resolved inside k_resolve
   out->total_ms = setup + kern;
   uint32_t st[6] = {0, 0, 0, 0, 0, 0};
-  if (x->counters.p) IE_HIP(hipMemcpy(st, (uint32_t*)x->counters.p + 4, 24, hipMemcpyDeviceToHost));
+  if (x->counters.p) IE_HIP(hipMemcpy(st, (uint32_t*)ctr_base(x) + 4, 24, hipMemcpyDeviceToHost));
   out->n_complex = st[0];
   out->n_direct = st[5];  // tiles deferred to the windowed emit (counter word 9)
   out->n_polls = st[2];
   out->n_exact = st[3];
   uint32_t nd = 0;
-  if (x->counters.p) IE_HIP(hipMemcpy(&nd, (uint32_t*)x->counters.p + 12, 4, hipMemcpyDeviceToHost));
+  if (x->counters.p) IE_HIP(hipMemcpy(&nd, (uint32_t*)ctr_base(x) + 12, 4, hipMemcpyDeviceToHost));
   out->n_deferred = nd;
   out->n_chain_fail = st[4];
   return check_device_error(x);
@@ -2294,6 +2340,30 @@ int ie_exec_elapsed(ie_exec* x, uint32_t a, uint32_t b, float* ms) {
   return IE_SUCCESS;
 }
 
+// the literal pool's demand of the last interpolation call: the word its last emit kernel published
+// to pinned host memory (a wait of about a microsecond after the device wrote it, and the stream's
+// later work already queued behind it), else a copy and a synchronisation
+int pool_demand(ie_exec* x, uint64_t* used) {
+  if (x->pool_pub) {
+    const volatile uint64_t* w = (const volatile uint64_t*)(x->stat_host + 8);
+    const uint64_t want = x->pool_seq & 0xFFFFFFu;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t k = 1;; k++) {
+      const uint64_t v = *w;
+      if ((v >> 40) == want) {
+        *used = v & ((1ull << 40) - 1);
+        return IE_SUCCESS;
+      }
+      // (bounded: a call that never gets there, e.g. a fault, is reported by the synchronisation)
+      if ((k & 4095u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
+      __builtin_ia32_pause();
+    }
+  }
+  IE_HIP(hipMemcpyAsync(used, (uint64_t*)ctr_base(x) + 1, 8, hipMemcpyDeviceToHost, x->stream));
+  IE_HIP(hipStreamSynchronize(x->stream));
+  return IE_SUCCESS;
+}
+
 int ie_interpolate_device_ids(ie_exec* x, const ie_table* t, const uint32_t* d_table_id, const uint8_t* d_bytes,
                               const uint64_t* d_offsets, uint64_t n, const ie_dev_out* out) {
   if (!x) return fail(IE_ERR_INVALID, "null exec");
@@ -2307,8 +2377,7 @@ int ie_interpolate_device_ids(ie_exec* x, const ie_table* t, const uint32_t* d_t
   // fixed every later offset, so a partial fix-up is impossible). Strings over their own
   // single-pass budget stay IE_E_OVERFLOW here; ie_interpolate_batch re-runs those in max mode.
   uint64_t used = 0;
-  IE_HIP(hipMemcpyAsync(&used, (uint64_t*)x->counters.p + 1, 8, hipMemcpyDeviceToHost, x->stream));
-  IE_HIP(hipStreamSynchronize(x->stream));
+  if ((rc = pool_demand(x, &used))) return rc;
   if (used <= x->pool.bytes) return IE_SUCCESS;
   x->pool_request = std::max<uint64_t>(x->pool_request, used + used / 8 + (1ull << 20));
   if ((rc = reset_host_keys(x))) return rc;
@@ -2332,8 +2401,7 @@ int ie_interpolate_device_views(ie_exec* x, const ie_table* t, const uint32_t* d
   if (rc || !n || x->pool_fixed) return rc;
   // the literal path's scratch demand, as ie_interpolate_device_ids
   uint64_t used = 0;
-  IE_HIP(hipMemcpyAsync(&used, (uint64_t*)x->counters.p + 1, 8, hipMemcpyDeviceToHost, x->stream));
-  IE_HIP(hipStreamSynchronize(x->stream));
+  if ((rc = pool_demand(x, &used))) return rc;
   if (used <= x->pool.bytes) return IE_SUCCESS;
   x->pool_request = std::max<uint64_t>(x->pool_request, used + used / 8 + (1ull << 20));
   if ((rc = reset_host_keys(x))) return rc;
@@ -2374,7 +2442,7 @@ int ie_unescape_cmd_device(ie_exec* x, const ie_table* t, const uint32_t* d_tabl
   rc = ie_interpolate_device_ids(x, t, d_table_id, tmp->bytes, tmp->offsets, n, out);
   x->in_cmd = false;
   if (rc) return rc;
-  IE_HIP(launch_cap_check(tmp->total, tmp->bytes_cap, (uint32_t*)x->counters.p + 1, x->stream));
+  IE_HIP(launch_cap_check(tmp->total, tmp->bytes_cap, (uint32_t*)ctr_base(x) + 1, x->stream));
   if (d_status_in) IE_HIP(launch_status_carry(d_status_in, out->status, n, x->stream));
   return IE_SUCCESS;
 }
@@ -2399,8 +2467,7 @@ int ie_unescape_cmd_device_views(ie_exec* x, const ie_table* t, const uint32_t* 
   if (rc) return rc;
   if (n && !x->pool_fixed) {  // the pool's demand (deferred strings + literal path), as ie_interpolate_device
     uint64_t used = 0;
-    IE_HIP(hipMemcpyAsync(&used, (uint64_t*)x->counters.p + 1, 8, hipMemcpyDeviceToHost, x->stream));
-    IE_HIP(hipStreamSynchronize(x->stream));
+    if ((rc = pool_demand(x, &used))) return rc;
     if (used > x->pool.bytes) {
       x->pool_request = std::max<uint64_t>(x->pool_request, used + used / 8 + (1ull << 20));
       if ((rc = run())) return rc;

@@ -286,6 +286,12 @@ struct ie_exec {
   uint64_t stat_n = 0;
   uint32_t* stat_host = nullptr;  // pinned, mapped: the last emit kernel of a call writes it (stat_dev)
   uint32_t* stat_dev = nullptr;
+  uint32_t hint_sub_grid = 0, hint_emit_grid = 0;  // (0: the defaults until a call's telemetry is in)
+  bool stat_two_pass = false;                        // (the pending telemetry is a two-pass call's)
+  uint32_t ctr_cur = 0;        // the counter set of the last call (ie_host.cpp, kCounterBytes)
+  uint64_t pool_seq = 0;       // the last interpolation call's number (its published pool word)
+  bool pool_pub = false;       // its last emit kernel publishes the pool demand (pool_demand)
+  bool ctr_next_clean = false; // the other set was zeroed by the last call's emit kernel
   hipEvent_t stat_ev = nullptr;
   // workspace
   DevBuf counters, pool, out_len, tile_sum, tile_base, defer_tiles, defer_desc;

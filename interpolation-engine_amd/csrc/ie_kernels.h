@@ -99,6 +99,18 @@ struct Work {
   // the call's telemetry words (stats[0..4]) in host-mapped pinned memory, written by its last
   // k_emit_windows (no copy kernel after it); null: the host copies them itself
   uint32_t* stat_out;
+  // grid hints from the exec's last completed call (0: the defaults): a deferred subset's bounded
+  // grid and the emit kernel's (both stride over their work: any size is correct, a small one is
+  // cheap when there is little to do)
+  uint32_t sub_grid, emit_grid;
+  // a two-pass call's emit kernel zeroes the exec's other counter set (zero_words words) for the next
+  // call (no fill before it)
+  uint32_t* zero_next;
+  uint32_t zero_words;
+  // the literal pool's demand (pool_used) with the call's number, seq << 40 | used, to host-mapped
+  // memory by the call's last k_emit_windows (null: not this kernel)
+  uint64_t* pool_out;
+  uint32_t pool_seq;
   uint32_t zero_on_overflow; // escape kernels: when the output exceeds its capacity, write every
                              // offset as 0 (a step that reads these strings next then reads nothing)
   // escape pipeline

@@ -450,7 +450,16 @@ struct ChainJobs {  // LDS views, tile-wide
   const lds_u32* cm;
   const lds_u32* odd;
   const lds_u32* esc;
+  // a small table's pilots staged in LDS (the LEAN instances, T.nb <= kLdsPilots), or null
+  const lds_u16* pil;
 };
+// pilot groups a LEAN workgroup stages in LDS with IE_LDS_PILOTS (tables of up to ~1.4k keys, e.g.
+// config 2's 1k-key dict: a lookup is then one memory round trip, the entry's, instead of two); what
+// the 4-workgroup LDS budget has left (40,960 B per workgroup). Measured slower (config 2 0.1036 vs
+// 0.0994 ms, config 3 0.792 vs 0.774 ms: the second branch costs the kernel 32 B of scratch, and the
+// pilots were L2 hits, not the tile's bound), so off by default
+
+constexpr uint32_t kLdsPilots = 352;
 constexpr uint32_t kJobCap = kMaxTop * kRBlock;
 constexpr uint32_t kResFail = 1u << 29, kResReject = 1u << 28;
 constexpr uint32_t kResWhole = 1u << 27;  // a whole-string '{key}' (res_s: the value id; kind bits 0-2)
@@ -628,11 +637,20 @@ __device__ void resolve_jobs(const DevTable& T, const lds_u8* tile, const ChainJ
       slot2[q] = b;
     }
 #else
-    // pilots, then entries: two memory latencies per round, every job's in flight together
+    // pilots, then entries: two memory latencies per round, every job's in flight together (a
+    // small table's pilots: from LDS, one memory latency per round)
+    if (J.pil) {
 #pragma unroll
-    for (int q = 0; q < NJ; q++) {
-      const uint32_t pilot = on[q] ? (uint32_t)gld(T.pilots + ph_group(h[q], T.nb)) : 0u;
-      slot[q] = on[q] ? ph_slot(h[q], pilot, T.m) : 0u;
+      for (int q = 0; q < NJ; q++) {
+        const uint32_t pilot = on[q] ? (uint32_t)J.pil[ph_group(h[q], T.nb)] : 0u;
+        slot[q] = on[q] ? ph_slot(h[q], pilot, T.m) : 0u;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < NJ; q++) {
+        const uint32_t pilot = on[q] ? (uint32_t)gld(T.pilots + ph_group(h[q], T.nb)) : 0u;
+        slot[q] = on[q] ? ph_slot(h[q], pilot, T.m) : 0u;
+      }
     }
 #endif
     if (stamp && threadIdx.x == 0 && r == 0) {  // diagnostic: pilots arrived
@@ -1137,7 +1155,16 @@ __global__ __launch_bounds__(kRBlock) void k_emit_windows(Batch B0, Batch B1, Wo
     *W.total = W.reserve16 ? t : *W.cursor;
   }
   // the call's telemetry straight into the host's pinned words (every resolve pass has finished)
-  if (W.stat_out && blockIdx.x == 0 && tid < 5) gst(W.stat_out + tid, W.stats[tid]);
+  // (words 4-9: the five telemetry words and the windowed-tile count)
+  if (W.stat_out && blockIdx.x == 0 && tid < 6) gst(W.stat_out + tid, tid < 5 ? W.stats[tid] : count);
+  // the pool's demand: every resolve pass of the call has finished
+  if (W.pool_out && blockIdx.x == 0 && tid == 0) {
+    const uint64_t u = __hip_atomic_load(W.pool_used, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    gst(W.pool_out, (uint64_t)(((uint64_t)W.pool_seq << 40) | (u < (1ull << 40) ? u : (1ull << 40) - 1)));
+  }
+  // the next call's counters (the set this call did not use)
+  if (W.zero_next && blockIdx.x == gridDim.x - 1)
+    for (uint32_t k = tid; k < W.zero_words; k += kRBlock) gst(W.zero_next + k, 0u);
   // fewer deferred tiles than workgroups: each tile's windows are shared by `per` workgroups (a
   // tile of multi-KB outputs is hundreds of windows: one workgroup alone would take them in turn)
   const uint32_t per = count && count < gridDim.x ? gridDim.x / count : 1u;
@@ -1231,6 +1258,12 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(
   __shared__ uint32_t s_olen[kRBlock];  // output length; the value id for IE_OK_VALUE strings
   __shared__ uint8_t s_st[kRBlock];
   __shared__ uint16_t s_pend[LEAN ? 1 : kRBlock];  // (no literal path in a LEAN pass)
+  __shared__ uint16_t s_pil[LEAN && !L5 ? kLdsPilots : 1];  // a small table's pilots (LEAN)
+// (measured slower, off: profiles/r06/lds_pilots/README.md)
+#ifndef IE_LDS_PILOTS
+#define IE_LDS_PILOTS 0
+#endif
+  const bool pil_lds = IE_LDS_PILOTS && LEAN && !L5 && T.nb <= kLdsPilots;
   __shared__ uint32_t s_misc[4];  // tile, pending count, defer slot
   __shared__ uint64_t s_red[kRBlock / 64 + 2];
   lds_u32* const s_cm = (lds_u32*)(lds_u8*)(s_u + (L5 ? kLCmOff : kCmOff));    // event masks of the staged chunks (+ pad)
@@ -1257,6 +1290,12 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(
   TilePrefetch<kStageV> pre;
   pre.nv = 0;
   if (tile < ntiles) pre.issue(B, geo, tid);
+  // a small table's pilots, loaded with the tile's input (in flight together; stored to LDS with it)
+  uint32_t pil0 = 0, pil1 = 0;
+  if (pil_lds && tile < ntiles) {
+    if (tid < T.nb) pil0 = gld(T.pilots + tid);
+    if (tid + kRBlock < T.nb) pil1 = gld(T.pilots + tid + kRBlock);
+  }
   if (tile < ntiles) {
   uint64_t t_start = 0;
   if (tid == 0) {
@@ -1290,6 +1329,10 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(
   const bool lane_staged = p0 + sn <= 16ull * nv;
   {
     pre.commit((uint4*)s_in, tid);
+    if (pil_lds) {  // (uniform; their first reader is behind the classification's barriers)
+      s_pil[tid] = (uint16_t)pil0;
+      if (tid + kRBlock < kLdsPilots) s_pil[tid + kRBlock] = (uint16_t)pil1;
+    }
     if (UNESC) {
       // the fused unescape command: per staged chunk, the bytes that are '\\' (bits 0-15) and the
       // braces (bits 16-31), from the prefetch registers, in the chunk-mask array (the
@@ -1423,11 +1466,12 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(
           L5 ? ChainJobs{(lds_u32*)(lds_u8*)(s_u + kLCrecOff), (lds_u16*)(lds_u8*)(s_u + kLMetaOff),
                          (lds_u32*)(lds_u8*)(s_u + kLCrecOff),  // (a job's result over its record)
                          (lds_u32*)(lds_u8*)(s_u + kLResSOff), (lds_u16*)(lds_u8*)(s_u + kLP0Off),
-                         (lds_u32*)(lds_u8*)s_olen, nullptr, s_cm, s_odd, s_esc}
+                         (lds_u32*)(lds_u8*)s_olen, nullptr, s_cm, s_odd, s_esc, nullptr}
              : ChainJobs{(lds_u32*)(lds_u8*)(s_u + kCmOff), (lds_u16*)(lds_u8*)(s_u + 8 * kJobCap),
                          (lds_u32*)(lds_u8*)s_u, (lds_u32*)(lds_u8*)(s_u + 4 * kJobCap),
                          (lds_u16*)(lds_u8*)(s_u + 10 * kJobCap), (lds_u32*)(lds_u8*)s_olen,
-                         (lds_u64*)(lds_u8*)(s_u + kKbufLds), nullptr, nullptr, nullptr};
+                         (lds_u64*)(lds_u8*)(s_u + kKbufLds), nullptr, nullptr, nullptr,
+                         pil_lds ? (const lds_u16*)s_pil : nullptr};
       if (pok) {
 #pragma unroll
         for (int c = 0; c < kMaxTop; c++) {
@@ -1956,9 +2000,10 @@ hipError_t launch_resolve_impl(const Batch& B, const Work& W, const DevTable& T,
   const uint64_t tiles = (B.n + kRBlock - 1) / kRBlock;
   if (!tiles) return hipSuccess;
   if (tiles > 0xFFFFFFFFull) return hipErrorInvalidValue;
-  const uint32_t egrid = (uint32_t)(tiles < 512u ? tiles : 512u);
+  const uint32_t emax = W.emit_grid ? W.emit_grid : 512u, smax = W.sub_grid ? W.sub_grid : kSubsetGrid;
+  const uint32_t egrid = (uint32_t)(tiles < emax ? tiles : emax);
   // (a subset views batch strides over its tiles: see k_resolve)
-  const uint32_t grid = B.n_dev && B.out_len && !unesc && !lean ? (uint32_t)(tiles < kSubsetGrid ? tiles : kSubsetGrid)
+  const uint32_t grid = B.n_dev && B.out_len && !unesc && !lean ? (uint32_t)(tiles < smax ? tiles : smax)
                                                                   : (uint32_t)tiles;
   const bool multi = B.table_id != nullptr;
 #ifndef IE_EXP_ONLY_LEAN  // (experiments: -DIE_EXP_ONLY_LEAN compiles the LEAN instances alone, tools/resusage.sh)
@@ -2030,7 +2075,8 @@ hipError_t launch_emit(const Batch& B, const Batch& D, const Work& W, const DevT
                        hipStream_t st) {
   const uint64_t tiles = (B.n + kRBlock - 1) / kRBlock;
   if (!tiles) return hipSuccess;
-  hipLaunchKernelGGL(k_emit_windows, dim3((uint32_t)(tiles < 512u ? tiles : 512u)), dim3(kRBlock), 0, st, B, D, W, T, out);
+  const uint32_t emax = W.emit_grid ? W.emit_grid : 512u;
+  hipLaunchKernelGGL(k_emit_windows, dim3((uint32_t)(tiles < emax ? tiles : emax)), dim3(kRBlock), 0, st, B, D, W, T, out);
   return hipGetLastError();
 }
 
@@ -2042,7 +2088,10 @@ hipError_t launch_emit(const Batch& B, const Batch& D, const Work& W, const DevT
 // at their places in the batch, bytes claimed from the same cursor). Asynchronous.
 hipError_t launch_unescape_cmd(const Batch& B, const Work& W, const DevTable& T, uint8_t* out, uint64_t cap,
                                uint64_t* sub_off, uint32_t* sub_len, uint32_t* sub_tid, hipStream_t st) {
-  hipError_t e = IE_RNS::launch_resolve_impl(B, W, T, out, cap, st, true);
+  Work W0 = W;  // (the fused pass's emit: neither the telemetry nor the pool word, the call goes on)
+  W0.stat_out = nullptr;
+  W0.pool_out = nullptr;
+  hipError_t e = IE_RNS::launch_resolve_impl(B, W0, T, out, cap, st, true);
   if (e != hipSuccess) return e;
   // the windowed-tile list is the deferred resolve's again
   e = hipMemsetAsync(W.defer_count, 0, sizeof(uint32_t), st);

@@ -193,3 +193,18 @@ def test_c_program_against_the_header(tmp_path):
     assert r.returncode == 0, r.stderr
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout + r.stderr
+
+
+def test_rust_shim_constants_match_header():
+    """The shim's status and flag constants (its IE_NEEDS_HOST completion branches on them) equal the
+    header's enumerators and macros, and the completion's entry point is declared."""
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    consts = {m.group(1): int(m.group(2), 0) for m in re.finditer(r"pub const (IE_\w+): \w+ = (\w+);", text)}
+    src = open(os.path.join(ROOT, "include", "ie_amd.h")).read()
+    hdr = {m.group(1): int(m.group(2), 0) for m in re.finditer(r"\b(IE_\w+)\s*=\s*(\d+)", src)}
+    hdr.update({m.group(1): int(m.group(2), 0) for m in re.finditer(r"#define (IE_\w+) (0x[0-9A-Fa-f]+|\d+)u?\b", src)})
+    for name in ("IE_OK_STR", "IE_OK_VALUE", "IE_E_RS_PANIC", "IE_NEEDS_HOST", "IE_TABLE_HAS_INSERTS_DIR",
+                 "IE_DIALECT_RS"):
+        assert name in consts, name
+        assert consts[name] == hdr[name], (name, consts[name], hdr[name])
+    assert "ie_exec_host_keys" in rust_shim_prototypes()
