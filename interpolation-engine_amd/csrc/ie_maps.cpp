@@ -80,6 +80,11 @@ struct Strs {
     tid.push_back(t);
   }
   uint64_t size() const { return tid.size(); }
+  void reserve(uint64_t n, uint64_t nbytes) {  // (no regrowth copies of a batch of KB-long texts)
+    bytes.reserve(nbytes);
+    off.reserve(n + 1);
+    tid.reserve(n);
+  }
 };
 
 // the results of a batch: str() of each (py:1692, 1698-1699, 1722, 1738: a whole-string key's
@@ -290,10 +295,10 @@ bool substitutable(std::string_view v) {
   return depth == 0;
 }
 
-// the value text with every unescaped `{N}` pair of a capture index replaced by that capture
-std::string substitute(std::string_view v, const std::vector<std::string_view>& caps) {
-  std::string out;
-  out.reserve(v.size() + 32);
+// the value text with every unescaped `{N}` pair of a capture index replaced by that capture,
+// appended to out (a batch's bytes: no intermediate string)
+template <class Out>
+void substitute(Out& out, std::string_view v, const std::vector<std::string_view>& caps) {
   size_t i = 0;
   while (i < v.size()) {
     if (v[i] == '{' && !(i > 0 && v[i - 1] == '\\')) {
@@ -302,16 +307,15 @@ std::string substitute(std::string_view v, const std::vector<std::string_view>& 
       if (j < v.size() && v[j] == '}' && j > i + 1 && v[i + 1] != '0' && j - i - 1 <= 6) {
         const uint64_t k = strtoull(std::string(v.substr(i + 1, j - i - 1)).c_str(), nullptr, 10);
         if (k >= 1 && k <= caps.size()) {
-          out.append(caps[k - 1]);
+          out.insert(out.end(), caps[k - 1].begin(), caps[k - 1].end());
           i = j + 1;
           continue;
         }
       }
     }
-    out.push_back(v[i]);
+    out.push_back((typename Out::value_type)v[i]);
     i++;
   }
-  return out;
 }
 
 // the clock a table was last given (its 'HH:MM:SS' entry)
@@ -560,6 +564,11 @@ int ie_replace_map(ie_exec* x, const ie_table* t, const char* name, uint64_t nam
     }
     // 1. interpolate (py:1722); the keys of this pass (py:1728); on the first pass output_name (py:1715)
     Strs in;
+    {
+      uint64_t nb = 0;
+      for (uint64_t i : active) nb += cur[i].size();
+      in.reserve(active.size() + (uint64_t)nt * m + (name ? nt : 0), nb + 64 * (uint64_t)nt * m);
+    }
     for (uint64_t i : active) in.add(cur[i], table_id[i]);
     std::vector<uint32_t> kst;
     if (pass == 1 || live_keys) {
@@ -598,6 +607,7 @@ int ie_replace_map(ie_exec* x, const ie_table* t, const char* name, uint64_t nam
       }
     }
     std::vector<uint64_t> alive;
+    uint64_t alive_bytes = 0;
     for (size_t q = 0; q < active.size(); q++) {
       const uint64_t i = active[q];
       if (!ok(r.st[q])) {
@@ -606,11 +616,14 @@ int ie_replace_map(ie_exec* x, const ie_table* t, const char* name, uint64_t nam
       }
       cur[i].assign(r.text[q]);
       alive.push_back(i);
+      alive_bytes += cur[i].size();
     }
     // 2. the first map whose key matches (py:1725-1735), every leaf in one launch
     Blocks blocks;
     Strs mstr;
+    mstr.reserve(alive.size(), alive_bytes);
     std::vector<uint32_t> range;
+    range.reserve(2 * alive.size());
     std::unordered_map<uint32_t, std::pair<uint32_t, uint32_t>> rg_of;  // (a state's leaves share its block)
     for (uint64_t i : alive) {
       const uint32_t s = table_id[i];
@@ -652,7 +665,13 @@ int ie_replace_map(ie_exec* x, const ie_table* t, const char* name, uint64_t nam
         inert &= (text_flags(caps[c]) & EF_INERT) != 0;
       }
       if (inert && substitutable(rv[j])) {
-        vin.add(caps.empty() ? std::string(rv[j]) : substitute(rv[j], caps), s);
+        if (caps.empty()) {
+          vin.add(rv[j], s);
+        } else {  // (the substituted value straight into the batch)
+          substitute(vin.bytes, rv[j], caps);
+          vin.off.push_back(vin.bytes.size());
+          vin.tid.push_back(s);
+        }
         vleaf.push_back(i);
       } else {
         std::vector<std::pair<std::string, std::string>> ex;

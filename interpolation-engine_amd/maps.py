@@ -663,6 +663,14 @@ def delete_states(states, task, dialect="py", device=0, tables=None):
     return out
 
 
+REBUILDS = []  # (task, stores, the library's reason) of every table-set rebuild run_map_tasks made
+
+
+def N_last_error():
+    e = IE.N.lib().ie_last_error()
+    return e.decode("utf-8", "replace") if e else ""
+
+
 def run_map_tasks(states, tasks, dialect="py", device=0):
     """goto_map / replace_map / delete / delete_except tasks in order over many states (the
     reference's loop applies them one state at a time): one table set for the whole run, a
@@ -696,6 +704,7 @@ def run_map_tasks(states, tasks, dialect="py", device=0):
             # the same stores on the device copy (ie_table_set_update), or a rebuild when a new
             # key found no placement
             if changes and not tset.update(changes):
+                REBUILDS.append((task.get("label") or task["cmd"], len(changes), N_last_error()))
                 tset.close()
                 tset = None
     finally:

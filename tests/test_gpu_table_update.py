@@ -312,3 +312,59 @@ def test_large_rewrite_batches_match_the_oracle():
             assert size <= 2 * live + (64 << 10) + 64 or rnd == 0, (rnd, size, live)
     finally:
         tset.close()
+
+
+def test_value_reads_from_two_threads():
+    """ie_table_value's value-id -> slot map is rebuilt lazily after an update, on the read path;
+    ctypes releases the GIL, so two threads reading one table's values at once both reach that
+    rebuild (the header: a table may be read by several threads). Every read must still return
+    the stored value."""
+    import threading
+    states = [{"k%d" % j: "v%d-%d" % (t, j) for j in range(40)} for t in range(200)]
+    tset = IE.InsertsTableSet(states, clock=CLOCK, mutable=True)
+    try:
+        errors = []
+        for rnd in range(5):
+            changes = [(t, "k%d" % ((t + rnd) % 40), "w%d-%d" % (rnd, t)) for t in range(200)]
+            assert tset.update(changes)
+            for t, k, v in changes:
+                states[t][k] = v
+            vids = [(tset.keys.index(k, tset.starts[t], tset.starts[t + 1]), states[t][k])
+                    for t in range(200) for k in ("k%d" % ((t + rnd) % 40), "k%d" % ((t + rnd + 1) % 40))]
+
+            def read(part):
+                try:
+                    for vid, want in part:
+                        got = tset.value(vid)
+                        if got != want:
+                            errors.append((vid, got, want))
+                except Exception as e:  # noqa: BLE001 (reported below)
+                    errors.append(repr(e))
+            ths = [threading.Thread(target=read, args=(vids[i::2],)) for i in range(2)]
+            for th in ths:
+                th.start()
+            for th in ths:
+                th.join()
+        assert not errors, errors[:3]
+    finally:
+        tset.close()
+
+
+def test_deleted_keys_give_their_value_ids_back():
+    """delete / delete_except through ie_delete_keys (the store path): each deleted key's value id
+    is reported, goes back to the set's free list (the next new key takes it) and the mirror drops
+    the value it held under it."""
+    from interpolation_engine_amd import maps as M
+    states = [{"keep": "a", "drop_1": "b", "drop_2": [1, 2]} for _ in range(30)]
+    tset = IE.InsertsTableSet(states, clock=CLOCK, mutable=True)
+    try:
+        got = M.delete_states(states, {"cmd": "delete", "wildcards": ["drop_*"]}, tables=tset)
+        assert all(sorted(g) == ["drop_1", "drop_2"] for g in got)
+        assert all(set(s) == {"keep"} for s in states)
+        freed = [i for i, v in enumerate(tset.values) if v is None]
+        assert len(freed) == 60  # (the typed list values are no longer held)
+        assert tset.update([(0, "new", [3])])
+        r = tset.run(["{new}"], [0])[0]
+        assert r[0] == N.OK_VALUE and r[1] in freed and tset.value(r[1]) == [3]
+    finally:
+        tset.close()

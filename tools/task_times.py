@@ -62,6 +62,8 @@ def main():
                 pstats.Stats(prof, stream=buf).sort_stats("tottime").print_stats(40)
                 sys.stderr.write(buf.getvalue())
             best = dt if best is None else min(best, dt)
+        out.setdefault("rebuilds", {})["states_%d" % n] = list(M.REBUILDS)
+        M.REBUILDS.clear()
         out["states_%d" % n] = {"us_per_state_task": [round(1e6 * x / n, 2) for x in per_task],
                                 "us_per_state_program_task_by_task": round(1e6 * sum(per_task) / n, 2),
                                 "us_per_state_program": round(1e6 * best / n, 2)}
