@@ -742,6 +742,9 @@ __device__ void resolve_jobs(const DevTable& T, const lds_u8* tile, const ChainJ
 // a string's descriptor from its jobs [jb, jb + nch): false when any job needs the exact evaluator;
 // a failed job (FAILC) makes the string fail with the status of the failing pair with the largest
 // opening offset (the reference resolves the rightmost chain first and stops at its first failure)
+// (RECS_LDS: the chain records are read from the job array, not kept in registers across the jobs;
+// the LEAN5 layout overwrites them with the results, so it passes them in registers)
+template <bool RECS_LDS>
 __device__ bool combine_chains(const ChainJobs J, uint32_t jb, uint32_t nch, const uint32_t (&crec)[kMaxTop],
                                uint32_t n, Desc& d, uint32_t& out_len, uint8_t& status, uint32_t& vid,
                                uint32_t& vflags) {
@@ -762,7 +765,8 @@ __device__ bool combine_chains(const ChainJobs J, uint32_t jb, uint32_t nch, con
   for (int c = 0; c < kMaxTop; c++) {
     if ((uint32_t)c >= nch) continue;
     const uint32_t rk = J.res_k[jb + c], rs = J.res_s[jb + c];
-    const uint32_t a = cr_first_open(crec[c]), e = cr_last_close(crec[c]);
+    const uint32_t rec = RECS_LDS ? J.crec[jb + c] : crec[c];
+    const uint32_t a = cr_first_open(rec), e = cr_last_close(rec);
     if (rk & kResReject) {
       ok = false;
     } else if ((rk >> 30) == 0u) {  // failed at the pair opening at (rk >> 8) & 0xFF
@@ -1489,7 +1493,9 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(
       IE_STAMP(10);
       __syncthreads();
       IE_STAMP(11);
-      const bool fast = pok && combine_chains(J, jb, nch, crec, (uint32_t)sn, d, olen, r, vid, vflags);
+      // (the fail-commit LEAN instances read the records back from LDS: they spilled otherwise, 20-24 B
+      // per lane, config 4 1.420 -> 1.378 ms; the others keep them in registers, 1 % faster)
+      const bool fast = pok && combine_chains<!L5 && LEAN && FAILC>(J, jb, nch, crec, (uint32_t)sn, d, olen, r, vid, vflags);
       __syncthreads();  // the job arrays are free (the exact evaluator's scratch)
       IE_STAMP(12);
       slow = active && !fast;
@@ -1539,7 +1545,9 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(
         const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
         if (dfr) W.udefer_list[pos] = (uint32_t)i;
         if (LEAN && dfr) {  // (the second pass's view of the string: no gather kernel)
-          W.sub_off[pos] = so;
+          // (the string's offset read again here, not held in registers across the chain jobs: the
+          // fail-commit LEAN instance spilled it)
+          W.sub_off[pos] = gld(B.in_off + i);
           W.sub_len[pos] = (uint32_t)min(sn, (uint64_t)0xFFFFFFFFu);
           if (MULTI) W.sub_tid[pos] = tid_s;
         }
@@ -1696,6 +1704,9 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(
 
   // ---- 5. the tile's output bytes into the LDS stage (tile-relative offsets) while the
   //      look-back is pending; tiles whose output does not fit store straight to HBM later ----
+  // (a fail-commit LEAN pass: the string's pointer made again here, not held in registers across
+  // the chain jobs; a string past the stage reads its offset again)
+  const uint8_t* const sx = !(LEAN && FAILC) ? s : i < B.n ? (lane_staged ? s_in + p0 : B.bytes + gld(B.in_off + i)) : nullptr;
   // (LEAN5: the output's first kLWin bytes go to the window stage (the union), the rest straight to
   // HBM; a tile of more than kLDirectMax bytes is deferred)
   const bool in_stage = L5 ? tile_total <= (uint64_t)kLDirectMax : tile_total <= (uint64_t)kOutStage;
@@ -1716,7 +1727,7 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(
   const uint32_t local_w = (uint32_t)local;
   uint8_t* const gout = out + base5;
   auto build_direct = [&]() {
-    const lds_u8* const ls = (const lds_u8*)s;
+    const lds_u8* const ls = (const lds_u8*)sx;
     const uint32_t ntop = mine ? d.ntop : 0u;
     const bool in_win = mine && local_w < kLWin;              // (bytes in the window)
     const bool past = mine && local_w + olen > kLWin;         // (bytes past it)
@@ -1733,7 +1744,7 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(
       if (__any(tn != 0)) {
         lds_u8* const dst = (lds_u8*)s_u + (tn ? w : 0u);
         if (lane_staged) lds_copy(dst, tn ? ls + t_lo : (const lds_u8*)s_in, tn);
-        else if (tn) copy_bytes<true, false>((uint8_t*)dst, s + t_lo, tn);  // a string past the stage
+        else if (tn) copy_bytes<true, false>((uint8_t*)dst, sx + t_lo, tn);  // a string past the stage
       }
       w += tl;
       if (j == kMaxTop) break;
@@ -1769,7 +1780,7 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(
         const uint32_t tl = t_hi - t_lo, ga = pw > kLWin ? pw : kLWin;
         if (ga < pw + tl) {
           if (lane_staged) copy_bytes<false, true>(gout + ga, (const uint8_t*)(ls + t_lo + (ga - pw)), pw + tl - ga);
-          else copy_bytes<false, false>(gout + ga, s + t_lo + (ga - pw), pw + tl - ga);
+          else copy_bytes<false, false>(gout + ga, sx + t_lo + (ga - pw), pw + tl - ga);
         }
         pw += tl;
         if (j == ntop) break;
@@ -1804,7 +1815,7 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(
     load_text(0, tt[0]);
 #endif
     lds_u8* const dd = (lds_u8*)(s_u + (mine ? local : 0));
-    const lds_u8* const ls = (const lds_u8*)s;
+    const lds_u8* const ls = (const lds_u8*)sx;
     const uint32_t ntop = mine ? d.ntop : 0u;
     uint32_t w = 0;
 #pragma unroll
@@ -1816,7 +1827,7 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(
       const uint32_t tl = ton ? t_hi - t_lo : 0u;
       if (__any(tl != 0)) {
         if (lane_staged) lds_copy(dd + w, tl ? ls + t_lo : (const lds_u8*)s_in, tl);
-        else if (tl) copy_bytes<true, false>((uint8_t*)(dd + w), s + t_lo, tl);  // a string past the stage
+        else if (tl) copy_bytes<true, false>((uint8_t*)(dd + w), sx + t_lo, tl);  // a string past the stage
       }
       w += tl;
       if (j == kMaxTop) break;
