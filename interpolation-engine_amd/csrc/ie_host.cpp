@@ -346,13 +346,17 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
         const uint64_t need = (x->stat_host[3] + 255) / 256;
         x->hint_sub_grid = (uint32_t)std::min<uint64_t>(1024, std::max<uint64_t>(64, need));
         x->hint_emit_grid = x->stat_host[5] ? 512u : 32u;
+        x->hint_fc = x->stat_fc;
       }
     }
     W.fail_commit = forced ? (uint32_t)x->opt_fail_commit : (uint32_t)x->fail_commit;
     if (W.err_keys) W.fail_commit = 0;  // misses go through the exact evaluator to the literal path
     // the adaptive choices' telemetry: written into pinned host words by the call's last emit kernel
-    // (no copy after it), or copied below when the call has none (a one-tile no-emit call)
-    const bool want_stats = !x->stat_pending && !x->no_stats;
+    // (no copy after it), or copied below when the call has none (a one-tile no-emit call). The
+    // unescape command's calls publish none: their counts (the deferred subset's, the interpolation
+    // of unescaped output) misled the next plain batch (config 4: a step after a command took the
+    // evaluator without fail commit, 3.3 ms instead of 1.4); the command takes the plain batches' choice
+    const bool want_stats = !x->stat_pending && !x->no_stats && !x->in_cmd && !x->cmd_fused;
     bool two_pass = false;
     if (!x->stat_host) {  // (words 0-5 the telemetry, 8-9 the pool demand word)
       IE_HIP(hipHostMalloc((void**)&x->stat_host, 64, hipHostMallocMapped));
@@ -387,8 +391,11 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
       IE_HIP(x->u_len.ensure(n * 4 + 4));
       if (d_tid) IE_HIP(x->u_tid.ensure(n * 4 + 4));
       W.udefer_list = (uint32_t*)x->u_list.p;
-      W.sub_grid = x->hint_sub_grid;
-      W.emit_grid = x->hint_emit_grid;
+      // (a grid measured under the other fail-commit mode would be wrong by the failing strings: the
+      // evaluator defers them without it, 490 tiles in config 4, and 64 workgroups took 1.1 ms)
+      const bool hint_ok = x->hint_fc == (W.fail_commit != 0);
+      W.sub_grid = hint_ok ? x->hint_sub_grid : 0u;
+      W.emit_grid = hint_ok ? x->hint_emit_grid : 0u;
       two_pass = true;
       if (!x->ctr_override) {  // (the call's emit kernel zeroes the other counter set for the next call)
         W.zero_next = (uint32_t*)((uint8_t*)x->counters.p + (x->ctr_cur ^ 1u) * kCounterBytes);
@@ -401,7 +408,7 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
       // (a one-string call: k_resolve alone, one launch and its emit kernel's ~5 µs fewer)
       const bool ne = x->small_no_emit && d_out_len && !wide && !W.reserve16 && !x->opt_noeval && n <= (uint64_t)kRBlock;
       x->no_emit_used = ne;
-      if (ne) W.stat_out = nullptr, W.pool_out = nullptr, x->pool_pub = false;
+      if (ne) W.stat_out = nullptr, W.pool_out = nullptr, x->pool_pub = false, W.ctr_host = x->zc_ctr_host;
       IE_HIP(wide ? launch_resolve512(B, W, t->dev, out->bytes, cap, st) : launch_resolve(B, W, t->dev, out->bytes, cap, st, ne));
     }
     if (want_stats) {
@@ -410,6 +417,7 @@ int run_device(ie_exec* x, int op, const ie_table* t, const uint8_t* d_bytes, co
       x->stat_pending = true;
       x->stat_n = n;
       x->stat_two_pass = two_pass;
+      x->stat_fc = W.fail_commit != 0;
     }
   } else {
     if (x->timing) IE_HIP(hipEventRecord(x->ev[1], st));
@@ -441,6 +449,91 @@ int check_device_error(ie_exec* x) {
 constexpr uint64_t kSmallN = 1024, kSmallBytes = 1ull << 16;
 inline uint64_t al256(uint64_t v) { return (v + 255) & ~255ull; }
 
+// the exec's zero-copy block (pinned, mapped into the device's address space, coherent: the kernel
+// reads what the host has just written and the host what the kernel wrote, with no cache between)
+int ensure_zc(ie_exec* x, uint64_t need) {
+  if (x->zc_bytes >= need) return IE_SUCCESS;
+  if (x->zc_host) (void)hipHostFree(x->zc_host);
+  x->zc_host = x->zc_dev = nullptr;
+  x->zc_bytes = 0;
+  const uint64_t want = std::max<uint64_t>(need, 1ull << 19);
+  IE_HIP(hipHostMalloc((void**)&x->zc_host, want, hipHostMallocMapped | hipHostMallocCoherent));
+  IE_HIP(hipHostGetDevicePointer((void**)&x->zc_dev, x->zc_host, 0));
+  x->zc_bytes = want;
+  return IE_SUCCESS;
+}
+
+// A one-tile views interpolation (the mirror's scalar call, py:497-541) without copies: the input
+// written into the zero-copy block, k_resolve reading it there and writing its results there, the
+// call's counters in device memory that k_resolve itself leaves zeroed after putting their words in
+// the block (Work::ctr_host). One launch and one wait; run_host_small's two block copies (and the
+// waits between the three stream operations) are gone. Same contract as run_host_small.
+int run_host_small_zc(ie_exec* x, const ie_table* t, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                      const uint32_t* table_id, ie_batch*& b, std::vector<uint32_t>& lens, uint64_t& total) {
+  const uint64_t base = offsets[0], in_bytes = offsets[n] - base, cap = 2 * in_bytes + 4096;
+  const uint64_t i_tid = al256((n + 1) * 8), i_bytes = i_tid + al256(table_id ? n * 4 : 0);
+  const uint64_t in_size = i_bytes + al256(in_bytes + 64);
+  // outputs: total | offsets | lengths | statuses | value ids | bytes | the counter words
+  const uint64_t o_off = 256, o_len = o_off + al256((n + 1) * 8), o_st = o_len + al256(n * 4),
+                 o_vid = o_st + al256(n + 1), o_bytes = o_vid + al256((n + 1) * 4), o_ctr = o_bytes + al256(cap);
+  int rc = ensure_zc(x, in_size + o_ctr + 256);
+  if (rc) return rc;
+  if (x->zc_dirty || !x->zc_ctr.p) {
+    IE_HIP(x->zc_ctr.ensure(kCounterBytes + 256));  // (the counters, then the one-tile look-back words)
+    IE_HIP(hipMemsetAsync(x->zc_ctr.p, 0, kCounterBytes + 256, x->stream));
+    x->zc_dirty = false;
+  }
+  uint8_t* const h = x->zc_host;
+  uint8_t* const dv = x->zc_dev;
+  uint64_t* const hoff = (uint64_t*)h;
+  for (uint64_t i = 0; i <= n; i++) hoff[i] = offsets[i] - base;
+  if (table_id) memcpy(h + i_tid, table_id, n * 4);
+  if (in_bytes) memcpy(h + i_bytes, bytes + base, in_bytes);
+  uint8_t* const ho = h + in_size;
+  uint8_t* const dout = dv + in_size;
+  ie_dev_out o{dout + o_bytes, cap, (uint64_t*)(dout + o_off), dout + o_st, (uint32_t*)(dout + o_vid), (uint64_t*)dout};
+  x->no_stats = true;
+  x->ctr_override = (uint8_t*)x->zc_ctr.p;
+  x->small_no_emit = true;
+  x->zc_ctr_host = (uint32_t*)(dout + o_ctr);
+  rc = run_device(x, kOpInterp, t, dv + i_bytes, (const uint64_t*)dv, n, &o,
+                  table_id ? (const uint32_t*)(dv + i_tid) : nullptr, (uint32_t*)(dout + o_len));
+  x->no_stats = false;
+  x->ctr_override = nullptr;
+  x->small_no_emit = false;
+  x->zc_ctr_host = nullptr;
+  const bool no_emit = x->no_emit_used;
+  x->no_emit_used = false;
+  if (rc) {
+    x->zc_dirty = true;
+    return rc;
+  }
+  if (!no_emit) {  // (another path ran, e.g. two passes: the counters stayed as it left them)
+    IE_HIP(hipMemcpyAsync(ho + o_ctr, x->zc_ctr.p, 64, hipMemcpyDeviceToHost, x->stream));
+    x->zc_dirty = true;
+  }
+  IE_HIP(hipStreamSynchronize(x->stream));
+  const uint32_t* const ctr = (const uint32_t*)(ho + o_ctr);
+  if (ctr[1] & 2u) return fail(IE_ERR_CAPACITY, "a step's output did not fit its caller-sized buffer");
+  if (ctr[1]) return fail(IE_ERR_TIMEOUT, "look-back spin timed out (a predecessor tile never published)");
+  if (no_emit && ctr[9] != 0) return IE_SUCCESS;  // a deferred tile: the generic path (run_host_small)
+  total = *(const uint64_t*)ho;
+  if (total > cap) return IE_SUCCESS;
+  b = new ie_batch{};
+  b->n = n;
+  b->bytes_len = total;
+  b->bytes = new uint8_t[total + 1];
+  b->offsets = new uint64_t[n + 1];
+  b->status = new uint8_t[n + 1];
+  b->value_id = new uint32_t[n + 1];
+  if (total) memcpy(b->bytes, ho + o_bytes, total);
+  memcpy(b->offsets, ho + o_off, n * 8);
+  lens.assign((const uint32_t*)(ho + o_len), (const uint32_t*)(ho + o_len) + n);
+  memcpy(b->status, ho + o_st, n);
+  memcpy(b->value_id, ho + o_vid, n * 4);
+  return IE_SUCCESS;
+}
+
 int run_host_small(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, const uint64_t* offsets,
                    uint64_t n, const uint32_t* table_id, bool views, ie_batch*& b, std::vector<uint32_t>& lens,
                    uint64_t& total) {
@@ -457,6 +550,8 @@ int run_host_small(ie_exec* x, int op, const ie_table* t, const uint8_t* bytes, 
   const uint64_t o_off = 256, o_len = o_off + al256((n + 1) * 8), o_st = o_len + al256(views ? n * 4 : 0),
                  o_vid = o_st + al256(n + 1), o_bytes = o_vid + al256((n + 1) * 4), o_err = o_bytes + al256(cap);
   const uint64_t need = in_size + ctr_size + o_err + 256;
+  if (x->opt_zc && own_ctr && views && op == kOpInterp && n <= (uint64_t)kRBlock && !x->in_cmd && !x->cmd_fused)
+    return run_host_small_zc(x, t, bytes, offsets, n, table_id, b, lens, total);
   IE_HIP(x->sm_dev.ensure(std::max<uint64_t>(need, 1ull << 19)));
   if (x->sm_host_bytes < need) {
     if (x->sm_host) (void)hipHostFree(x->sm_host);
@@ -2138,6 +2233,7 @@ int ie_exec_create(int32_t device, void* hip_stream, ie_exec** out) {
     x->opt_reserve = v >= 16 && v <= 1024 ? (uint32_t)v : 0u;
   }
   if (const char* e = getenv("IE_SMALL_HOST")) x->opt_small = atoi(e) != 0;
+  if (const char* e = getenv("IE_SMALL_ZC")) x->opt_zc = atoi(e) != 0;
   if (const char* e = getenv("IE_DEFER")) x->opt_defer = atoi(e) < 0 ? -1 : atoi(e) >= 2 ? 2 : atoi(e) != 0 ? 1 : 0;
   if (const char* e = getenv("IE_DEBUG_STAMPS")) x->stamps_path = e;
   if (hip_stream) {
@@ -2580,28 +2676,34 @@ int ie_wildcard_match_batch(ie_exec* x, const ie_wildcards* w, const uint8_t* by
   const uint64_t o_ncap = al256(n * 4), o_caps = o_ncap + al256(n), out_size = o_caps + al256(n * 8 * IE_WC_MAX_CAP);
   if (in_size + out_size <= (4ull << 20)) {
     const uint64_t need = in_size + out_size;
-    IE_HIP(x->sm_dev.ensure(std::max<uint64_t>(need, 1ull << 19)));
-    if (x->sm_host_bytes < need) {
-      if (x->sm_host) (void)hipHostFree(x->sm_host);
-      x->sm_host = nullptr;
-      x->sm_host_bytes = 0;
-      const uint64_t want = std::max<uint64_t>(need, 1ull << 19);
-      IE_HIP(hipHostMalloc((void**)&x->sm_host, want, hipHostMallocDefault));
-      x->sm_host_bytes = want;
+    // zero-copy (IE_SMALL_ZC): k_wildcard reads the block and writes its results into it, no copies
+    const bool zc = x->opt_zc != 0;
+    if (zc) {
+      if ((rc = ensure_zc(x, need))) return rc;
+    } else {
+      IE_HIP(x->sm_dev.ensure(std::max<uint64_t>(need, 1ull << 19)));
+      if (x->sm_host_bytes < need) {
+        if (x->sm_host) (void)hipHostFree(x->sm_host);
+        x->sm_host = nullptr;
+        x->sm_host_bytes = 0;
+        const uint64_t want = std::max<uint64_t>(need, 1ull << 19);
+        IE_HIP(hipHostMalloc((void**)&x->sm_host, want, hipHostMallocDefault));
+        x->sm_host_bytes = want;
+      }
     }
-    uint8_t* const h = x->sm_host;
-    uint8_t* const dv = (uint8_t*)x->sm_dev.p;
+    uint8_t* const h = zc ? x->zc_host : x->sm_host;
+    uint8_t* const dv = zc ? x->zc_dev : (uint8_t*)x->sm_dev.p;
     uint64_t* const hoff = (uint64_t*)h;
     for (uint64_t i = 0; i <= n; i++) hoff[i] = offsets[i] - base;
     if (range) memcpy(h + i_rng, range, n * 8);
     if (nb) memcpy(h + i_bytes, bytes + base, nb);
     memset(h + i_bytes + nb, 0, 64);
-    IE_HIP(hipMemcpyAsync(dv, h, in_size, hipMemcpyHostToDevice, x->stream));
+    if (!zc) IE_HIP(hipMemcpyAsync(dv, h, in_size, hipMemcpyHostToDevice, x->stream));
     uint8_t* const dout = dv + in_size;
     rc = ie_wildcard_match_device(x, w, dv + i_bytes, (const uint64_t*)dv, n, range ? (const uint32_t*)(dv + i_rng) : nullptr,
                                   (int32_t*)dout, dout + o_ncap, (uint32_t*)(dout + o_caps));
     if (rc) return rc;
-    IE_HIP(hipMemcpyAsync(h + in_size, dout, out_size, hipMemcpyDeviceToHost, x->stream));
+    if (!zc) IE_HIP(hipMemcpyAsync(h + in_size, dout, out_size, hipMemcpyDeviceToHost, x->stream));
     IE_HIP(hipStreamSynchronize(x->stream));
     memcpy(match, h + in_size, n * 4);
     memcpy(ncap, h + in_size + o_ncap, n);

@@ -288,6 +288,7 @@ struct ie_exec {
   uint32_t* stat_dev = nullptr;
   uint32_t hint_sub_grid = 0, hint_emit_grid = 0;  // (0: the defaults until a call's telemetry is in)
   bool stat_two_pass = false;                        // (the pending telemetry is a two-pass call's)
+  bool stat_fc = false, hint_fc = false;             // (the fail-commit mode they were measured in)
   uint32_t ctr_cur = 0;        // the counter set of the last call (ie_host.cpp, kCounterBytes)
   uint64_t pool_seq = 0;       // the last interpolation call's number (its published pool word)
   bool pool_pub = false;       // its last emit kernel publishes the pool demand (pool_demand)
@@ -313,10 +314,22 @@ struct ie_exec {
   DevBuf sm_dev;
   uint8_t* sm_host = nullptr;
   uint64_t sm_host_bytes = 0;
+  // small calls without copies (IE_SMALL_ZC, default on): one pinned block, mapped and coherent, the
+  // kernels read their inputs from and write their outputs to; the counters of such a call in
+  // device memory, left zeroed by its k_resolve (zc_dirty: a call that took another path did not)
+  int32_t opt_zc = 1;
+  uint8_t* zc_host = nullptr;
+  uint8_t* zc_dev = nullptr;  // (the block's device address)
+  uint64_t zc_bytes = 0;
+  DevBuf zc_ctr;
+  bool zc_dirty = true;
+  uint32_t* zc_ctr_host = nullptr;  // (run_device: a one-tile no-emit call's counter words go here)
   ~ie_exec() {
     for (auto& kv : wc_cache) ie_wildcards_free(kv.second);
     sm_dev.release();
+    zc_ctr.release();
     if (sm_host) (void)hipHostFree(sm_host);
+    if (zc_host) (void)hipHostFree(zc_host);
     for (DevBuf* b : {&u_list, &u_off, &u_len, &u_tid, &host_keys}) b->release();
     for (DevBuf* b : {&counters, &pool, &out_len, &tile_sum, &tile_base, &defer_tiles, &defer_desc, &in_bytes,
                       &in_off, &in_tid, &o_bytes, &o_off, &o_len, &o_status, &o_vid, &o_total, &wc_range, &wc_match, &wc_ncap, &wc_caps,

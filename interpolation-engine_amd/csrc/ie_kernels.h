@@ -111,6 +111,9 @@ struct Work {
   // memory by the call's last k_emit_windows (null: not this kernel)
   uint64_t* pool_out;
   uint32_t pool_seq;
+  // a one-tile views call without copies (ie_host.cpp, run_host_small_zc): k_resolve's last
+  // instructions put counter words 0-15 here (host-mapped) and zero them on the device (null: not)
+  uint32_t* ctr_host;
   uint32_t zero_on_overflow; // escape kernels: when the output exceeds its capacity, write every
                              // offset as 0 (a step that reads these strings next then reads nothing)
   // escape pipeline

@@ -1246,7 +1246,10 @@ __global__ __launch_bounds__(kRBlock) void k_emit_windows(Batch B0, Batch B1, Wo
 // staged string is unescaped in place in the LDS stage (after the classification; its chunks are
 // classified again) and then resolved; strings that cannot be finished there (not staged, or
 // needing the literal path) go to W.udefer_list for the deferred pass.
-template <bool FAILC, bool MULTI, bool VIEWS, bool UNESC = false, bool LK = false, bool LEAN = false>
+// SUB: a views deferred subset's instance, the only one with the grid-stride loop over tiles (in the
+// others the loop's back edge made the compiler keep the prefetch and the entry-text registers in
+// scratch: 53 spill stores and 80 reloads per tile in the views instance of scalar calls)
+template <bool FAILC, bool MULTI, bool VIEWS, bool UNESC = false, bool LK = false, bool LEAN = false, bool SUB = false>
 __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(
     LEAN && IE_LEAN5 ? IE_WAVES_PER_EU_LEAN : LK ? IE_WAVES_PER_EU_LK : IE_WAVES_PER_EU))) void k_resolve(Batch B0, Work W, DevTable T, uint8_t* out,
                                                     uint64_t cap) {
@@ -1275,21 +1278,26 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(
   lds_u32* const s_esc = (lds_u32*)(lds_u8*)(s_u + (L5 ? kLEscOff : kEscOff));  // one bit per chunk: '\' inside
   lds_u32* const s_lit = (lds_u32*)(lds_u8*)s_u;              // literal-path results: pool offset >> 4
 
-  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
+  const uint32_t tid0 = threadIdx.x;
   const uint32_t ntiles = (uint32_t)((B.n + kRBlock - 1) / kRBlock);
   // Views: tile = workgroup index (no tile waits on another). Packed output: the tile index is a
   // ticket taken when the workgroup starts, so every tile a look-back waits on has started (HIP
   // promises no dispatch order; one atomic per tile, on the packed path only)
   uint32_t tile = blockIdx.x;
   if (!VIEWS) {
-    if (tid == 0) s_misc[0] = atomicAdd(W.tile_ticket, 1u);
+    if (tid0 == 0) s_misc[0] = atomicAdd(W.tile_ticket, 1u);
     __syncthreads();
     tile = s_misc[0];
   }
   // a deferred subset (B0.n_dev: its string count is only known on the device) runs on a bounded
   // grid that strides over the tiles (a subset with nothing in it costs a few workgroups, not a
-  // whole batch's); every other launch has a workgroup per tile and takes one trip
+  // whole batch's: the SUB instances); every other launch has a workgroup per tile, one trip
   for (;;) {
+  // (SUB: the lane index opaque per tile, so that nothing derived from it is kept in registers (or
+  // scratch) across the loop's back edge; a no-op for the one-trip instances)
+  uint32_t tid_l;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(tid_l) : "v"(tid0));
+  const uint32_t tid = SUB ? tid_l : tid0, wave = tid >> 6, lane = tid & 63u;
   const TileGeo geo = load_geo(B, tile, tid);
   TilePrefetch<kStageV> pre;
   pre.nv = 0;
@@ -1913,10 +1921,21 @@ __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(
   IE_STAMP(5);
 #undef IE_STAMP
   }
-  if (!(VIEWS && !LEAN && !UNESC) || !B0.n_dev) break;  // (uniform)
+  if (!SUB || !B0.n_dev) break;  // (uniform)
   tile += gridDim.x;
   if (tile >= ntiles) break;
   __syncthreads();  // the next tile's stage and union: every wave is done with this one's
+  }
+  // a one-tile host call without copies (W.ctr_host, ie_host.cpp run_host_small_zc; the launch is
+  // this workgroup alone): the call's counter words to the host, then zeroed for its next call
+  if (VIEWS && !LEAN && !SUB && !UNESC && W.ctr_host) {
+    __threadfence();
+    __syncthreads();  // (every access of this call to the counters is done)
+    if (tid0 < 16u) {
+      const uint32_t v = __hip_atomic_load(W.tile_ticket + tid0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      gst(W.ctr_host + tid0, v);
+      __hip_atomic_store(W.tile_ticket + tid0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -2013,9 +2032,13 @@ hipError_t launch_resolve_impl(const Batch& B, const Work& W, const DevTable& T,
   if (tiles > 0xFFFFFFFFull) return hipErrorInvalidValue;
   const uint32_t emax = W.emit_grid ? W.emit_grid : 512u, smax = W.sub_grid ? W.sub_grid : kSubsetGrid;
   const uint32_t egrid = (uint32_t)(tiles < emax ? tiles : emax);
-  // (a subset views batch strides over its tiles: see k_resolve)
-  const uint32_t grid = B.n_dev && B.out_len && !unesc && !lean ? (uint32_t)(tiles < smax ? tiles : smax)
-                                                                  : (uint32_t)tiles;
+  // (a subset views batch strides over its tiles: the SUB instances of k_resolve)
+#if !defined(IE_RESOLVE_WIDE)
+  const bool sub = B.n_dev && B.out_len && !unesc && !lean;
+#else
+  const bool sub = false;  // (the 512-string kernels never run a views subset: a whole grid if one did)
+#endif
+  const uint32_t grid = sub ? (uint32_t)(tiles < smax ? tiles : smax) : (uint32_t)tiles;
   const bool multi = B.table_id != nullptr;
 #ifndef IE_EXP_ONLY_LEAN  // (experiments: -DIE_EXP_ONLY_LEAN compiles the LEAN instances alone, tools/resusage.sh)
   if (unesc) {  // the fused unescape command (views only)
@@ -2048,6 +2071,25 @@ hipError_t launch_resolve_impl(const Batch& B, const Work& W, const DevTable& T,
 #undef IE_LAUNCH_LEAN
     }
     if (emit) hipLaunchKernelGGL(k_emit_windows, dim3(egrid), dim3(kRBlock), 0, st, B, B, W, T, out);
+    return hipGetLastError();
+  }
+#endif
+#if !defined(IE_EXP_ONLY_LEAN) && !defined(IE_RESOLVE_WIDE)
+  if (sub) {
+    switch (variant >> 1) {  // (views: bit 0 set)
+#define IE_LAUNCH_SUB(V, F, M, L) \
+  case V: hipLaunchKernelGGL((k_resolve<F, M, true, false, L, false, true>), dim3(grid), dim3(kRBlock), 0, st, B, W, T, out, cap); break;
+      IE_LAUNCH_SUB(0, false, false, false)
+      IE_LAUNCH_SUB(1, false, true, false)
+      IE_LAUNCH_SUB(2, true, false, false)
+      IE_LAUNCH_SUB(3, true, true, false)
+      IE_LAUNCH_SUB(4, false, false, true)
+      IE_LAUNCH_SUB(5, false, true, true)
+      IE_LAUNCH_SUB(6, true, false, true)
+      IE_LAUNCH_SUB(7, true, true, true)
+#undef IE_LAUNCH_SUB
+    }
+    if (emit && (out || B.out_len)) hipLaunchKernelGGL(k_emit_windows, dim3(egrid), dim3(kRBlock), 0, st, B, B, W, T, out);
     return hipGetLastError();
   }
 #endif

@@ -185,6 +185,28 @@ def _leaves(inserts, x, out):
     return x
 
 
+class _StateDependent(Exception):
+    pass
+
+
+def _static_leaves(x, out):
+    """_leaves for an item with no whole-string key anywhere (the walk then reads no state: one
+    skeleton and leaf list serve every state); raises _StateDependent otherwise."""
+    if type(x) == str and "{" not in x and "}" not in x:
+        out.append(x)
+        return ("__leaf__", len(out) - 1)
+    if IE.get_simple_insertkey(x):
+        raise _StateDependent()
+    if type(x) == str:
+        out.append(x)
+        return ("__leaf__", len(out) - 1)
+    if type(x) == list:
+        return [_static_leaves(xx, out) for xx in x]
+    if type(x) == dict:
+        return {("__key__", _static_leaves(xk, out)): _static_leaves(xv, out) for xk, xv in x.items()}
+    return x
+
+
 def _rebuild(skel, done):
     if type(skel) == tuple and len(skel) == 2 and skel[0] == "__leaf__":
         return done[skel[1]]
@@ -492,18 +514,29 @@ def replace_map_states(states, task, dialect="py", device=0, tables=None):
         if tset.has_dir or pairs is None or type(name) is not str:
             return _replace_map_states_host(states, task, dialect, device, tables=tset)
         out = [None] * n
-        skels, leaves, owner = [None] * n, [], []
-        for s in range(n):
-            mine = []
-            try:
-                skels[s] = (_leaves(states[s], task["item"], mine), len(leaves))
-            except (IE.InterpolationException, AssertionError, TypeError) as e:
-                out[s] = e
-                continue
-            leaves.extend(mine)
-            owner.extend([s] * len(mine))
         import ctypes
         import numpy as np
+        try:  # an item without whole-string keys: one walk for all states (its leaves repeated)
+            lv0 = []
+            skel0 = _static_leaves(task["item"], lv0)
+        except _StateDependent:
+            skel0 = None
+        if skel0 is not None:
+            k0 = len(lv0)
+            skels = [(skel0, s * k0) for s in range(n)]
+            leaves = lv0 * n
+            owner = [s for s in range(n) for _ in range(k0)]
+        else:
+            skels, leaves, owner = [None] * n, [], []
+            for s in range(n):
+                mine = []
+                try:
+                    skels[s] = (_leaves(states[s], task["item"], mine), len(leaves))
+                except (IE.InterpolationException, AssertionError, TypeError) as e:
+                    out[s] = e
+                    continue
+                leaves.extend(mine)
+                owner.extend([s] * len(mine))
         arr, keep = IE.N.map_pairs(pairs)
         blob, offs = IE.N.pack(leaves)
         ids = np.asarray(owner, np.uint32)

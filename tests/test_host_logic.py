@@ -37,3 +37,20 @@ def test_value_dict_keeps_the_captures_and_what_the_value_reaches():
     assert M._value_dict(nested_value, "{e}", [], "py") == nested_value
     # keys the state does not hold stay out (the device reports the miss, as the reference raises)
     assert M._value_dict(state, "{zz}", [], "py") == {}
+
+
+def test_static_walk_is_the_state_walk_for_items_without_whole_string_keys():
+    """replace_map_states walks an item once for all states when no node is a whole-string key
+    (recursive_replace, py:1748-1759, then reads no state): the same skeleton and leaves as the
+    per-state walk; an item with one raises, and the per-state walk runs."""
+    state = {"a": "A", "k": "v{a}"}
+    for item in ["plain", "x {a} y", ["{a} and {b}", "z", {"{a}-x": ["w", 3, None]}], {"k": {"n": 1.5}}, 7]:
+        lv0, lv1 = [], []
+        assert M._static_leaves(item, lv0) == M._leaves(state, item, lv1)
+        assert lv0 == lv1
+    for item in ["{a}", ["x", "{k}"], {"{a}": "y"}]:
+        try:
+            M._static_leaves(item, [])
+        except M._StateDependent:
+            continue
+        raise AssertionError("%r holds a whole-string key" % (item,))
