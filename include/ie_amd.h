@@ -265,6 +265,10 @@ int ie_exec_timing(ie_exec* x, ie_timing* out); /* syncs */
                           missing key its message names (py:467, "Could not find variable '<key>'")
                           in ie_exec_host_keys; such strings take the literal path (0, the default:
                           no keys, misses stay on the fast evaluators) */
+#define IE_OPT_SMALL_ZC 10 /* host calls of one tile (<= 256 strings, views) and small wildcard batches
+                          without copies: 1: inputs and outputs in one mapped, coherent pinned block the
+                          kernels read and write; 2: the outputs only; 0 (default; env IE_SMALL_ZC):
+                          one pinned block copy each way (the same latency) */
 int ie_exec_set_option(ie_exec* x, int32_t option, int64_t value);
 /* Literal-path scratch pool size. Setting it makes ie_interpolate_device fully asynchronous: it no
  * longer waits to check the pool's demand, and strings that ran out of it report IE_E_OVERFLOW.

@@ -22,6 +22,7 @@ TABLE_HAS_INSERTS_DIR = 1
 TABLE_MUTABLE = 2
 OPT_FAIL_COMMIT, OPT_FAST, OPT_DEBUG_NOEVAL, OPT_TILE, OPT_VIEWS, OPT_DEFER, OPT_RESERVE = 1, 2, 3, 4, 5, 7, 8
 OPT_ERROR_KEYS = 9
+OPT_SMALL_ZC = 10
 
 # every symbol include/ie_amd.h declares (tests check the .so exports exactly these)
 EXPORTS = [

@@ -484,13 +484,20 @@ int run_host_small_zc(ie_exec* x, const ie_table* t, const uint8_t* bytes, const
     x->zc_dirty = false;
   }
   uint8_t* const h = x->zc_host;
-  uint8_t* const dv = x->zc_dev;
   uint64_t* const hoff = (uint64_t*)h;
   for (uint64_t i = 0; i <= n; i++) hoff[i] = offsets[i] - base;
   if (table_id) memcpy(h + i_tid, table_id, n * 4);
   if (in_bytes) memcpy(h + i_bytes, bytes + base, in_bytes);
+  // IE_SMALL_ZC=2: the input still goes over in one copy (device-memory reads in the kernel), only
+  // the outputs are written straight to the host
+  uint8_t* dv = x->zc_dev;
+  if (x->opt_zc == 2) {
+    IE_HIP(x->sm_dev.ensure(std::max<uint64_t>(in_size, 1ull << 19)));
+    dv = (uint8_t*)x->sm_dev.p;
+    IE_HIP(hipMemcpyAsync(dv, h, i_bytes + in_bytes, hipMemcpyHostToDevice, x->stream));
+  }
   uint8_t* const ho = h + in_size;
-  uint8_t* const dout = dv + in_size;
+  uint8_t* const dout = x->zc_dev + in_size;
   ie_dev_out o{dout + o_bytes, cap, (uint64_t*)(dout + o_off), dout + o_st, (uint32_t*)(dout + o_vid), (uint64_t*)dout};
   x->no_stats = true;
   x->ctr_override = (uint8_t*)x->zc_ctr.p;
@@ -2233,7 +2240,7 @@ int ie_exec_create(int32_t device, void* hip_stream, ie_exec** out) {
     x->opt_reserve = v >= 16 && v <= 1024 ? (uint32_t)v : 0u;
   }
   if (const char* e = getenv("IE_SMALL_HOST")) x->opt_small = atoi(e) != 0;
-  if (const char* e = getenv("IE_SMALL_ZC")) x->opt_zc = atoi(e) != 0;
+  if (const char* e = getenv("IE_SMALL_ZC")) x->opt_zc = atoi(e);
   if (const char* e = getenv("IE_DEFER")) x->opt_defer = atoi(e) < 0 ? -1 : atoi(e) >= 2 ? 2 : atoi(e) != 0 ? 1 : 0;
   if (const char* e = getenv("IE_DEBUG_STAMPS")) x->stamps_path = e;
   if (hip_stream) {
@@ -2373,6 +2380,10 @@ int ie_exec_set_option(ie_exec* x, int32_t option, int64_t value) {
       return IE_SUCCESS;
     case IE_OPT_ERROR_KEYS:
       x->opt_err_keys = value ? 1 : 0;
+      return IE_SUCCESS;
+    case IE_OPT_SMALL_ZC:
+      if (value < 0 || value > 2) return fail(IE_ERR_INVALID, "small zero-copy must be 0, 1 or 2");
+      x->opt_zc = (int32_t)value;
       return IE_SUCCESS;
     default:
       return fail(IE_ERR_INVALID, "unknown exec option");

@@ -314,10 +314,13 @@ struct ie_exec {
   DevBuf sm_dev;
   uint8_t* sm_host = nullptr;
   uint64_t sm_host_bytes = 0;
-  // small calls without copies (IE_SMALL_ZC, default on): one pinned block, mapped and coherent, the
-  // kernels read their inputs from and write their outputs to; the counters of such a call in
-  // device memory, left zeroed by its k_resolve (zc_dirty: a call that took another path did not)
-  int32_t opt_zc = 1;
+  // small calls without copies (IE_SMALL_ZC=1; 2: the outputs only): one pinned block, mapped and
+  // coherent, the kernels read their inputs from and write their outputs to; the counters of such a
+  // call in device memory, left zeroed by its k_resolve (zc_dirty: a call that took another path did
+  // not). Off by default: the scalar call measured the same with and without it (32.2-33.3 µs in
+  // every mode, profiles/r06/scalar_zc/): what the two copies saved, the kernel's reads and writes
+  // across the host link cost
+  int32_t opt_zc = 0;
   uint8_t* zc_host = nullptr;
   uint8_t* zc_dev = nullptr;  // (the block's device address)
   uint64_t zc_bytes = 0;

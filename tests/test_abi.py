@@ -44,7 +44,8 @@ def test_header_constants_match_the_binding():
     assert {k: int(v) for k, v in defs.items()} == {
         "IE_OPT_FAIL_COMMIT": N.OPT_FAIL_COMMIT, "IE_OPT_FAST": N.OPT_FAST,
         "IE_OPT_DEBUG_NOEVAL": N.OPT_DEBUG_NOEVAL, "IE_OPT_TILE": N.OPT_TILE, "IE_OPT_VIEWS": N.OPT_VIEWS,
-        "IE_OPT_DEFER": N.OPT_DEFER, "IE_OPT_RESERVE": N.OPT_RESERVE, "IE_OPT_ERROR_KEYS": N.OPT_ERROR_KEYS}
+        "IE_OPT_DEFER": N.OPT_DEFER, "IE_OPT_RESERVE": N.OPT_RESERVE, "IE_OPT_ERROR_KEYS": N.OPT_ERROR_KEYS,
+        "IE_OPT_SMALL_ZC": N.OPT_SMALL_ZC}
 
 
 def test_abi_version():

@@ -91,3 +91,47 @@ def test_small_path_table_ids(monkeypatch):
         assert N.STATUS_NAMES[st] == rst, (s, i)
         if rst == "OK_STR":
             assert payload == rout, (s, i)
+
+
+@pytest.mark.parametrize("zc", [1, 2])
+def test_small_path_without_copies(monkeypatch, zc):
+    """IE_OPT_SMALL_ZC (run_host_small_zc): one-tile views calls read and write a mapped host block
+    and k_resolve leaves the call's counters zeroed for the next one; calls in a row, between them
+    calls on the other paths (a 300-string batch, an output past the first-guess capacity, which
+    leave the zero-copy counters to the host), each equal to the copying path and the oracle."""
+    rng = random.Random(77 + zc)
+    t = PKG.InsertsTable(TABLE, clock=CLOCK)
+    x = _exec(monkeypatch, True, 1)
+    x.set_option(N.OPT_SMALL_ZC, zc)
+    ref_x = _exec(monkeypatch, True, 1)
+    ref = O.Oracle(TABLE, "py", clock=CLOCK)
+    for k, n in enumerate([1, 1, 7, 256, 300, 1, ("{big}" * 12,), 3, 200, 1]):
+        strings = list(n) if isinstance(n, tuple) else _batch(rng, n)
+        got = t.run(strings, exec_=x)
+        assert got == t.run(strings, exec_=ref_x), k
+        for s, (st, payload) in zip(strings, got):
+            rst, rout, _ = ref.interpolate(s)
+            assert N.STATUS_NAMES[st] == rst, (k, s)
+            if rst == "OK_STR":
+                assert payload == rout, (k, s)
+    with pytest.raises(RuntimeError):
+        x.set_option(N.OPT_SMALL_ZC, 3)
+
+
+def test_small_wildcard_batch_without_copies(monkeypatch):
+    """ie_wildcard_match_batch's small batch in the mapped block (IE_OPT_SMALL_ZC): the same matches
+    and captures as with the block copies."""
+    from interpolation_engine_amd.wildcard import Wildcards
+    pats = ["go *", "take * from *", "*"]
+    texts = ["go north", "take lamp from table", "look", "take x from y", "go  "] * 9
+    w = Wildcards(pats)
+    try:
+        got = []
+        for zc in (0, 1):
+            x = _exec(monkeypatch, True, 1)
+            x.set_option(N.OPT_SMALL_ZC, zc)
+            got.append([a.tolist() for a in w.match_raw(texts, None, exec_=x)])
+    finally:
+        w.close()
+    assert got[0] == got[1]
+    assert got[0][0][:3] == [0, 1, 2]
