@@ -102,6 +102,29 @@ def map_result_to_python(res_ptr):
     return out
 
 
+def map_result_columns(res_ptr):
+    """Copy an ie_map_result into Python and free it, as columns: (texts as str, statuses, where,
+    chosen, value ids). An ASCII result (the common case) is decoded once and sliced."""
+    r = res_ptr.contents
+    n = r.n
+    blob = ctypes.string_at(r.bytes, r.bytes_len) if r.bytes_len else b""
+    if n:
+        o = memoryview(ctypes.string_at(r.offsets, 8 * (n + 1))).cast("Q").tolist()
+        if blob.isascii():
+            txt = blob.decode("ascii")
+            texts = [txt[a:b] for a, b in zip(o, o[1:])]
+        else:
+            texts = [dec(blob[a:b]) for a, b in zip(o, o[1:])]
+
+        def arr(p, size, fmt):
+            return memoryview(ctypes.string_at(p, size * n)).cast(fmt).tolist()
+        cols = (texts, arr(r.status, 1, "B"), arr(r.where, 4, "I"), arr(r.chosen, 4, "i"), arr(r.value_id, 4, "I"))
+    else:
+        cols = ([], [], [], [], [])
+    lib().ie_map_result_free(res_ptr)
+    return cols
+
+
 def map_pairs(pairs):
     """[(key str, value str)] -> (ctypes array of MapPair, the encoded bytes kept alive)"""
     keep = [(enc(k), enc(v)) for k, v in pairs]

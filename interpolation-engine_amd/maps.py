@@ -472,27 +472,28 @@ def goto_map_states(states, task, dialect="py", device=0, tables=None):
         x = IE.get_exec(tset.device)
         IE.N.check(IE.N.lib().ie_goto_map(x.h, tset.h, text, len(text), arr, len(pairs), ctypes.byref(res)),
                    "ie_goto_map")
-        rows = IE.N.map_result_to_python(res)
+        g_text, g_st, g_wh, _, _ = IE.N.map_result_columns(res)
         m = len(pairs)
         src = lambda w: task["text"] if w == 0 else pairs[w - 1][0] if w <= m else pairs[w - 1 - m][1]  # noqa: E731
-        errs = _errors_of(tset, [(s, src(w)) for s, (_, st, w, _, _) in enumerate(rows)
-                                 if st not in (IE.N.OK_STR, IE.N.E_NO_MATCH, IE.N.E_NO_NULL)])
+        OK_STR, E_NO_MATCH, E_NO_NULL = IE.N.OK_STR, IE.N.E_NO_MATCH, IE.N.E_NO_NULL
+        errs = _errors_of(tset, [(s, src(g_wh[s])) for s, st in enumerate(g_st)
+                                 if st != OK_STR and st != E_NO_MATCH and st != E_NO_NULL])
     finally:
         if tables is None:
             tset.close()
     out = []
     label = task.get("traceback_label")
-    for s, (b, st, w, _, _) in enumerate(rows):
-        if st == IE.N.OK_STR:
-            target = IE.N.dec(b)
+    for s, st in enumerate(g_st):
+        if st == OK_STR:
+            target = g_text[s]
             out.append({"goto_target": target} if target != "CONTINUE" else None)
-        elif st == IE.N.E_NO_MATCH:  # py:1708
-            out.append(AssertionError("Order Index %s: goto_map has no matches for '%s'." % (label, IE.N.dec(b))))
-        elif st == IE.N.E_NO_NULL:  # py:1703
+        elif st == E_NO_MATCH:  # py:1708
+            out.append(AssertionError("Order Index %s: goto_map has no matches for '%s'." % (label, g_text[s])))
+        elif st == E_NO_NULL:  # py:1703
             out.append(AssertionError("Order Index %s: value text '%s' could not be resolved but 'NULL' is not a "
                                       "key in target_maps." % (label, task["text"])))
         else:
-            out.append(errs[(s, src(w))])
+            out.append(errs[(s, src(g_wh[s]))])
     return out
 
 
@@ -547,26 +548,24 @@ def replace_map_states(states, task, dialect="py", device=0, tables=None):
                                              offs.ctypes.data, ids.ctypes.data, len(leaves), arr, m,
                                              1 if task.get("repeat_until_done", False) else 0, ctypes.byref(nres),
                                              ctypes.byref(res)), "ie_replace_map")
-        names = IE.N.map_result_to_python(nres)
-        rows = IE.N.map_result_to_python(res) if leaves else []
+        OK_STR, OK_VALUE = IE.N.OK_STR, IE.N.OK_VALUE
+        n_text, n_st, _, _, n_vid = IE.N.map_result_columns(nres)
+        r_text, r_st, r_wh, _, _ = IE.N.map_result_columns(res) if leaves else ([], [], [], [], [])
         # the exceptions of the failed strings (rare): names, leaves, keys; a failed value with the
         # captures its key took (its message lists inserts | extra_inserts, py:467)
-        want, vfail = [], []
-        for s, (b, st, _, _, _) in enumerate(names):
-            if st not in (IE.N.OK_STR, IE.N.OK_VALUE):
-                want.append((s, name))
-        for i, (b, st, w, ch, _) in enumerate(rows):
-            if st == IE.N.OK_STR:
-                continue
+        want = [(s, name) for s, st in enumerate(n_st) if st != OK_STR and st != OK_VALUE]
+        vfail = []
+        for i in [i for i, st in enumerate(r_st) if st != OK_STR]:
+            w = r_wh[i]
             if w == 0:
-                want.append((owner[i], IE.N.dec(b)))
+                want.append((owner[i], r_text[i]))
             elif w <= m:
                 want.append((owner[i], pairs[w - 1][0]))
             else:
                 vfail.append(i)
         errs = _errors_of(tset, want)
         # the interpolated keys whose captures a failed value took
-        kwant = list(dict.fromkeys((owner[i], pairs[rows[i][2] - 1 - m][0]) for i in vfail))
+        kwant = list(dict.fromkeys((owner[i], pairs[r_wh[i] - 1 - m][0]) for i in vfail))
         kgot = dict(zip(kwant, _str_results(tset, [k for _, k in kwant], [t for t, _ in kwant])))
     finally:
         if tables is None:
@@ -577,8 +576,8 @@ def replace_map_states(states, task, dialect="py", device=0, tables=None):
     verr = {}
     if vfail:
         from .wildcard import Wildcards
-        keys_v = [kgot[(owner[i], pairs[rows[i][2] - 1 - m][0])] for i in vfail]
-        texts_v = [IE.N.dec(rows[i][0]) for i in vfail]
+        keys_v = [kgot[(owner[i], pairs[r_wh[i] - 1 - m][0])] for i in vfail]
+        texts_v = [r_text[i] for i in vfail]
         ok_q = [q for q, k in enumerate(keys_v) if not isinstance(k, BaseException)]
         caps_v = [[] for _ in vfail]
         if ok_q:
@@ -594,36 +593,43 @@ def replace_map_states(states, task, dialect="py", device=0, tables=None):
         fulls = [dict(states[owner[i]], **{str(k + 1): c for k, c in enumerate(caps_v[q])}) for q, i in enumerate(vfail)]
         xs = IE.InsertsTableSet(fulls, dialect=dialect, device=device)
         try:
-            got = xs.results([pairs[rows[i][2] - 1 - m][1] for i in vfail], list(range(len(vfail))))
+            got = xs.results([pairs[r_wh[i] - 1 - m][1] for i in vfail], list(range(len(vfail))))
         finally:
             xs.close()
         verr = dict(zip(vfail, got))
     no_value = object()
     value_if_error = ([v for k, v in pairs if k == "NULL"] + [no_value])[0]  # py:1761
     label = task.get("traceback_label")
-    count = [0] * n
-    for o in owner:
-        count[o] += 1
+    if skel0 is not None:
+        count = [k0] * n
+    else:
+        count = [0] * n
+        for o in owner:
+            count[o] += 1
     for s in range(n):
-        b, st, _, _, vid = names[s]
-        if st not in (IE.N.OK_STR, IE.N.OK_VALUE):
+        st = n_st[s]
+        if st != OK_STR and st != OK_VALUE:
             # output_name is interpolated before the reference's try (py:1715, 1762): its error
             # reaches the caller as it is, whatever 'NULL' says
             out[s] = errs[(s, name)]
             continue
-        nm = IE.N.dec(b) if st == IE.N.OK_STR else tset.value(vid)  # (a typed output_name, py:1715)
+        nm = n_text[s] if st == OK_STR else tset.value(n_vid[s])  # (a typed output_name, py:1715)
         if out[s] is not None:
             e = out[s]
         else:
             skel, base = skels[s]
-            e, done = None, []
-            for k in range(base, base + count[s]):
-                bb, lst, w, _, _ = rows[k]
-                if lst == IE.N.OK_STR:
-                    done.append(IE.N.dec(bb))
-                    continue
-                e = verr[k] if k in verr else errs[(s, IE.N.dec(bb) if w == 0 else pairs[w - 1][0])]
-                break
+            e, c = None, count[s]
+            if r_st[base:base + c].count(OK_STR) == c:  # (every leaf resolved: the common case)
+                done = r_text[base:base + c]
+            else:
+                done = []
+                for k in range(base, base + c):
+                    if r_st[k] == OK_STR:
+                        done.append(r_text[k])
+                        continue
+                    w = r_wh[k]
+                    e = verr[k] if k in verr else errs[(s, r_text[k] if w == 0 else pairs[w - 1][0])]
+                    break
         if e is None:
             out[s] = (nm, _rebuild(skel, done))
         elif isinstance(e, IE.InterpolationException):
