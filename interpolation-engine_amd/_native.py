@@ -396,9 +396,19 @@ def batch_to_python(res_ptr):
     return outs, st.tolist(), vid.tolist()
 
 
+_PY_PACK = os.environ.get("IE_PY_PACK") == "1"  # (A/B: the Python packing)
+
+
 def pack(strings):
-    """list[str|bytes] -> (bytes blob, uint64 offsets array)"""
+    """list[str|bytes] -> (bytes blob, uint64 offsets array); in C (_ie_pack.pack_strs) when the
+    packer is built"""
     import numpy as np
+    if not _PY_PACK:
+        try:
+            blob, o = pack_module().pack_strs(strings)
+            return blob, np.frombuffer(o, dtype=np.uint64).copy()
+        except (RuntimeError, TypeError):  # (the packer not built, or items other than str / bytes)
+            pass
     memo = {}  # batches repeat strings (a task's texts once per state): each encoded once
 
     def one(s):

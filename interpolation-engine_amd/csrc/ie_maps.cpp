@@ -535,8 +535,9 @@ int ie_replace_map(ie_exec* x, const ie_table* t, const char* name, uint64_t nam
     rv[j] = std::string_view(maps[j].value, maps[j].value_len);
     live_keys |= rk[j].find('{') != std::string_view::npos;
   }
-  std::vector<std::string> cur(n), last(n);
-  for (uint64_t i = 0; i < n; i++) cur[i] = last[i] = std::string((const char*)bytes + offsets[i], offsets[i + 1] - offsets[i]);
+  // each leaf's text between passes (a pass reads it into its batch, and writes it once at its end)
+  std::vector<std::string> cur(n);
+  for (uint64_t i = 0; i < n; i++) cur[i] = std::string((const char*)bytes + offsets[i], offsets[i + 1] - offsets[i]);
   // the owners' interpolated keys (per state: the keys before the first that fails, and its status)
   std::vector<std::vector<std::string>> keys(nt);
   std::vector<uint32_t> key_ok(nt, m), key_at(nt, UINT32_MAX);
@@ -606,17 +607,24 @@ int ie_replace_map(ie_exec* x, const ie_table* t, const char* name, uint64_t nam
         keys[s][j].assign(r.text[k]);
       }
     }
-    std::vector<uint64_t> alive;
+    // the strings that interpolated: their batch position (the pass's starting text, for the fixed
+    // point) and their text, as views (of this pass's batch and results, alive until its end)
+    std::vector<uint64_t> alive, alive_q;
+    std::vector<std::string_view> iv;
     uint64_t alive_bytes = 0;
+    alive.reserve(active.size());
+    alive_q.reserve(active.size());
+    iv.reserve(active.size());
     for (size_t q = 0; q < active.size(); q++) {
       const uint64_t i = active[q];
       if (!ok(r.st[q])) {
         st[i] = r.st[q];  // (cur[i]: the string that failed)
         continue;
       }
-      cur[i].assign(r.text[q]);
       alive.push_back(i);
-      alive_bytes += cur[i].size();
+      alive_q.push_back(q);
+      iv.push_back(r.text[q]);
+      alive_bytes += r.text[q].size();
     }
     // 2. the first map whose key matches (py:1725-1735), every leaf in one launch
     Blocks blocks;
@@ -625,14 +633,14 @@ int ie_replace_map(ie_exec* x, const ie_table* t, const char* name, uint64_t nam
     std::vector<uint32_t> range;
     range.reserve(2 * alive.size());
     std::unordered_map<uint32_t, std::pair<uint32_t, uint32_t>> rg_of;  // (a state's leaves share its block)
-    for (uint64_t i : alive) {
-      const uint32_t s = table_id[i];
+    for (size_t k = 0; k < alive.size(); k++) {
+      const uint32_t s = table_id[alive[k]];
       auto it = rg_of.find(s);
       if (it == rg_of.end()) it = rg_of.emplace(s, blocks.range(keys[s], key_ok[s])).first;
       const auto rg = it->second;
       range.push_back(rg.first);
       range.push_back(rg.second);
-      mstr.add(cur[i], table_id[i]);
+      mstr.add(iv[k], s);
     }
     tr.mark("blocks", blocks.pats.size());
     Match mt;
@@ -640,7 +648,7 @@ int ie_replace_map(ie_exec* x, const ie_table* t, const char* name, uint64_t nam
     tr.mark("match", mstr.size());
     // 3. the matched maps' values against inserts | {'1': capture, ...} (py:1732-1738)
     Strs vin;                                // captures spliced in, on the states' own tables
-    std::vector<uint64_t> vleaf;
+    std::vector<uint64_t> vleaf;             // (positions in `alive`)
     std::vector<uint32_t> slow_owner;        // the rest: a table of their own
     std::vector<std::vector<std::pair<std::string, std::string>>> slow_extra;
     std::vector<uint64_t> slow_leaf;
@@ -661,7 +669,7 @@ int ie_replace_map(ie_exec* x, const ie_table* t, const char* name, uint64_t nam
       bool inert = true;
       for (uint32_t c = 0; c < mt.ncap[q]; c++) {
         const uint32_t a = mt.caps[(q * IE_WC_MAX_CAP + c) * 2], l = mt.caps[(q * IE_WC_MAX_CAP + c) * 2 + 1];
-        caps[c] = std::string_view(cur[i]).substr(a, l);
+        caps[c] = iv[q].substr(a, l);
         inert &= (text_flags(caps[c]) & EF_INERT) != 0;
       }
       if (inert && substitutable(rv[j])) {
@@ -672,45 +680,51 @@ int ie_replace_map(ie_exec* x, const ie_table* t, const char* name, uint64_t nam
           vin.off.push_back(vin.bytes.size());
           vin.tid.push_back(s);
         }
-        vleaf.push_back(i);
+        vleaf.push_back(q);
       } else {
         std::vector<std::pair<std::string, std::string>> ex;
         for (uint32_t c = 0; c < caps.size(); c++) ex.emplace_back(std::to_string(c + 1), std::string(caps[c]));
         sin.add(rv[j], (uint32_t)slow_owner.size());
         slow_owner.push_back(s);
         slow_extra.push_back(std::move(ex));
-        slow_leaf.push_back(i);
+        slow_leaf.push_back(q);
       }
     }
     tr.mark("captures", vin.size());
     Res vr;
     if ((rc = interp(x, t, vin, vr))) return rc;
     tr.mark("values", vin.size());
+    // each alive string's text at the end of the pass: its value's, or (no match, a failed value:
+    // the matched text) the interpolated one
+    std::vector<std::string_view> nv(iv);
     for (size_t q = 0; q < vleaf.size(); q++) {
-      const uint64_t i = vleaf[q];
-      if (!ok(vr.st[q])) st[i] = vr.st[q], wh[i] = 1 + m + (uint32_t)ch[i];  // (cur[i]: the matched text)
-      else cur[i].assign(vr.text[q]);
+      const uint64_t i = alive[vleaf[q]];
+      if (!ok(vr.st[q])) st[i] = vr.st[q], wh[i] = 1 + m + (uint32_t)ch[i];
+      else nv[vleaf[q]] = vr.text[q];
     }
+    Res sr;
     if (!slow_owner.empty()) {
       ie_table* xt = nullptr;
       if ((rc = table_with(x, t, slow_owner, slow_extra, &xt))) return rc;
-      Res sr;
       rc = interp(x, xt, sin, sr);
       ie_table_free(xt);
       if (rc) return rc;
       for (size_t q = 0; q < slow_leaf.size(); q++) {
-        const uint64_t i = slow_leaf[q];
+        const uint64_t i = alive[slow_leaf[q]];
         if (!ok(sr.st[q])) st[i] = sr.st[q], wh[i] = 1 + m + (uint32_t)ch[i];
-        else cur[i].assign(sr.text[q]);
+        else nv[slow_leaf[q]] = sr.text[q];
       }
       tr.mark("slow values", sin.size());
     }
-    // 4. a fixed point, or one pass without repeat_until_done (py:1742-1745)
+    // 4. the pass's texts kept; a fixed point (against the text the pass started from, still in its
+    // batch), or one pass without repeat_until_done (py:1742-1745)
     std::vector<uint64_t> next;
-    for (uint64_t i : alive) {
-      if (st[i] != IE_OK_STR || !repeat_until_done || last[i] == cur[i]) continue;
-      last[i] = cur[i];
-      next.push_back(i);
+    for (size_t k = 0; k < alive.size(); k++) {
+      const uint64_t i = alive[k], q = alive_q[k];
+      cur[i].assign(nv[k]);
+      if (st[i] != IE_OK_STR || !repeat_until_done) continue;
+      const std::string_view start((const char*)in.bytes.data() + in.off[q], in.off[q + 1] - in.off[q]);
+      if (start != std::string_view(cur[i])) next.push_back(i);
     }
     active.swap(next);
   }

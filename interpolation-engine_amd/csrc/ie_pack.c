@@ -533,7 +533,72 @@ fail:
   return NULL;
 }
 
+// A batch of strings -> (one bytes blob of their UTF-8, one bytes object of uint64 offsets[n+1]):
+// _native.pack's work without a Python-level encode and join per string (a map step's KB-long
+// leaves). ASCII strs are copied from their own buffer; the others encoded as _native.enc does
+// (utf-8, surrogatepass); bytes objects taken as they are.
+static PyObject* pack_strs(PyObject* self, PyObject* arg) {
+  (void)self;
+  PyObject* seq = PySequence_Fast(arg, "pack_strs takes a sequence");
+  if (!seq) return NULL;
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+  PyObject** items = PySequence_Fast_ITEMS(seq);
+  PyObject* enc = PyList_New(n);  // (the encoded form of each non-ASCII str, else None)
+  PyObject* offs = enc ? PyBytes_FromStringAndSize(NULL, (Py_ssize_t)((n + 1) * sizeof(uint64_t))) : NULL;
+  if (!offs) {
+    Py_XDECREF(enc);
+    Py_DECREF(seq);
+    return NULL;
+  }
+  uint64_t* o = (uint64_t*)PyBytes_AS_STRING(offs);
+  uint64_t total = 0;
+  o[0] = 0;
+  for (Py_ssize_t i = 0; i < n; i++) {
+    PyObject* s = items[i];
+    PyObject* e = Py_None;
+    Py_ssize_t len;
+    if (PyUnicode_Check(s) && PyUnicode_IS_ASCII(s)) {
+      len = PyUnicode_GET_LENGTH(s);
+    } else if (PyUnicode_Check(s)) {
+      e = PyUnicode_AsEncodedString(s, "utf-8", "surrogatepass");
+      if (!e) goto fail;
+      len = PyBytes_GET_SIZE(e);
+    } else if (PyBytes_Check(s)) {
+      len = PyBytes_GET_SIZE(s);
+    } else {
+      PyErr_SetString(PyExc_TypeError, "pack_strs takes str or bytes items");
+      goto fail;
+    }
+    if (e == Py_None) Py_INCREF(e);
+    PyList_SET_ITEM(enc, i, e);
+    total += (uint64_t)len;
+    o[i + 1] = total;
+  }
+  PyObject* blob = PyBytes_FromStringAndSize(NULL, (Py_ssize_t)total);
+  if (!blob) goto fail;
+  char* w = PyBytes_AS_STRING(blob);
+  for (Py_ssize_t i = 0; i < n; i++) {
+    PyObject* s = items[i];
+    PyObject* e = PyList_GET_ITEM(enc, i);
+    const uint64_t len = o[i + 1] - o[i];
+    const char* src = e != Py_None ? PyBytes_AS_STRING(e) : PyUnicode_Check(s) ? (const char*)PyUnicode_DATA(s) : PyBytes_AS_STRING(s);
+    if (len) memcpy(w + o[i], src, len);
+  }
+  Py_DECREF(enc);
+  Py_DECREF(seq);
+  PyObject* r = PyTuple_Pack(2, blob, offs);
+  Py_DECREF(blob);
+  Py_DECREF(offs);
+  return r;
+fail:
+  Py_DECREF(enc);
+  Py_DECREF(offs);
+  Py_DECREF(seq);
+  return NULL;
+}
+
 static PyMethodDef methods[] = {
+    {"pack_strs", pack_strs, METH_O, "strings -> (UTF-8 blob, uint64 offsets[n+1] as bytes)"},
     {"pack", pack, METH_VARARGS, "changes -> (ie_kv records, table ids, keep-alive list)"},
     {"assign", assign, METH_VARARGS, "store the values under the ids the library handed out"},
     {"pack_dicts", pack_dicts, METH_VARARGS, "dicts -> (ie_kv records, kv_start, keep-alive list)"},

@@ -144,3 +144,17 @@ def test_records_outlive_the_callers_objects():
     for r, w in zip(_records(kv2, len(wantd)), wantd):
         assert ctypes.string_at(r.text, r.text_len) == w
     del junk, junk2, keep, keep2
+
+
+def test_pack_strs_matches_the_python_packing():
+    """_ie_pack.pack_strs (behind _native.pack): the blob and offsets _native.enc and a join give,
+    for ASCII, non-ASCII, lone-surrogate and bytes items; other items fall back to the Python
+    packing."""
+    import numpy as np
+    strs = ["abc", "", "héllo", "\ud800x", b"raw", "x" * 5000, "日本"] * 3
+    blob, offs = N.pack(strs)
+    want = [N.enc(s) if isinstance(s, str) else s for s in strs]
+    assert blob == b"".join(want)
+    assert offs.tolist() == np.cumsum([0] + [len(w) for w in want]).tolist()
+    assert N.pack([])[0] == b"" and N.pack([])[1].tolist() == [0]
+    assert N.pack([bytearray(b"ab"), "c"])[0] == b"abc"
