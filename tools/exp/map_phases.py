@@ -38,11 +38,23 @@ def main():
         st = [make_state(g["defaults"], j % 240) for j in range(n)]
         tset = IE.InsertsTableSet(st)
         rows = []
-        for task in g["tasks"]:
+        for ti, task in enumerate(g["tasks"]):
             fn = M.goto_map_states if task["cmd"] == "goto_map" else M.replace_map_states
             spent["lib"] = 0.0
+            prof = None
+            if rep and str(ti) in os.environ.get("PROFILE_TASKS", "").split(","):  # cProfile of chosen steps
+                import cProfile
+                prof = cProfile.Profile()
+                prof.enable()
             t0 = time.perf_counter()
             fn(st, task, tables=tset)
+            if prof:
+                prof.disable()
+                import io
+                import pstats
+                buf = io.StringIO()
+                pstats.Stats(prof, stream=buf).sort_stats("tottime").print_stats(25)
+                sys.stderr.write("== task %d\n" % ti + buf.getvalue())
             rows.append((task["cmd"][:4], round(1e3 * (time.perf_counter() - t0), 2), round(1e3 * spent["lib"], 2)))
         tset.close()
         out = rows
