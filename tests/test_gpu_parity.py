@@ -1319,3 +1319,46 @@ def test_output_windows_device_views_lean(reserve):
         if N.STATUS_NAMES[st[i]] != rst or (rst == "OK_STR" and got != rout):
             bad.append((i, s[:60], N.STATUS_NAMES[st[i]], rst))
     assert not bad, bad[:3]
+
+
+def test_deferred_subset_grid_from_a_stale_hint():
+    """The deferred subset's grid comes from the exec's previous two-pass call (64 workgroups when
+    it deferred nothing) and strides over however many tiles this call defers: a call that defers
+    nothing, then one that defers ~100 tiles' worth (keys past 32 bytes leave the LEAN pass), then
+    the first again, on one exec, each against the oracle."""
+    tdict = dict({"k%d" % i: "v%d" % i for i in range(100)},
+                 **{"long_key_number_%030d" % i: "L%d" % i for i in range(50)})
+    rng = random.Random(4242)
+    light = ["x {k%d} y" % rng.randrange(100) for _ in range(20_000)]
+    heavy = [("<{long_key_number_%030d}>" % rng.randrange(50)) if rng.random() < 0.8 else "{k%d}" % rng.randrange(100)
+             for _ in range(30_000)]
+    x = N.Exec(0)
+    x.set_option(N.OPT_VIEWS, 1)
+    x.set_option(N.OPT_DEFER, 1)
+    table = PKG.InsertsTable(tdict, clock=CLOCK)
+    ref = O.Oracle(tdict, "py", clock=CLOCK)
+    for k, strings in enumerate([light, heavy, light, heavy]):
+        blob, offs = N.pack(strings)
+        n = len(strings)
+        d_bytes = N.DeviceBuffer.from_numpy(x, np.frombuffer(blob + b"\0" * 16, np.uint8))
+        d_off = N.DeviceBuffer.from_numpy(x, np.asarray(offs, np.uint64))
+        cap = 4 * len(blob) + (1 << 20)
+        r = DevResult(x, n, cap)
+        lens = N.DeviceBuffer(x, 4 * n + 4)
+        v = N.DevViews(r.bytes.ptr, cap, r.off.ptr, lens.ptr, r.status.ptr, r.vid.ptr, r.total_d.ptr)
+        N.check(N.lib().ie_interpolate_device_views(x.h, table.h, None, d_bytes.ptr, d_off.ptr, None, n,
+                                                    ctypes.byref(v)), "ie_interpolate_device_views")
+        x.sync()  # (the call's telemetry lands: the next call's grid comes from it)
+        st = r.status.to_numpy(np.uint8, n)
+        starts = r.off.to_numpy(np.uint64, n)
+        ln = lens.to_numpy(np.uint32, n).astype(np.uint64)
+        ext = int((starts + ln).max())
+        out = r.bytes.to_numpy(np.uint8, ext).tobytes()
+        assert_views_disjoint(starts, ln, ext)
+        bad = []
+        for i, s in enumerate(strings):
+            rst, rout, _ = ref.interpolate(s)
+            got = out[int(starts[i]):int(starts[i] + ln[i])].decode("utf-8", "surrogatepass") if st[i] == 0 else None
+            if N.STATUS_NAMES[st[i]] != rst or (rst == "OK_STR" and got != rout):
+                bad.append((i, s[:60], N.STATUS_NAMES[st[i]], rst))
+        assert not bad, (k, bad[:3])
